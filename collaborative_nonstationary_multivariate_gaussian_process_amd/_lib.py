@@ -1,0 +1,160 @@
+"""ctypes binding of libnmgp_hip.so (the C ABI declared in include/nmgp_hip.h).
+
+The library is built in-tree (``make -C collaborative_nonstationary_multivariate_gaussian_process_amd/csrc``
+or ``python -c "import __graft_entry__ as g; g.build()"``).  There is NO fallback: if the .so is missing
+or a device call fails, the calls raise.  torch is imported first so that the process's HIP runtime
+is torch's own libamdhip64 (same SONAME), which the .so then binds to.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads the HIP runtime the library binds to)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libnmgp_hip.so")
+
+c_int, c_i64, c_dbl, c_vp, c_u64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p, ctypes.c_uint64
+
+
+class HipError(RuntimeError):
+    pass
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [("A", c_vp), ("B", c_vp), ("C", c_vp), ("kscale", c_vp), ("epi_E", c_vp), ("epi_rs", c_vp),
+                ("sA_i", c_i64), ("sA_k", c_i64), ("sA_kb", c_i64),
+                ("sB_k", c_i64), ("sB_j", c_i64), ("sB_kb", c_i64),
+                ("sC_i", c_i64), ("sC_j", c_i64), ("sE_i", c_i64), ("sE_j", c_i64),
+                ("m", c_int), ("n", c_int), ("k", c_int), ("kbA", c_int), ("kbB", c_int), ("flags", c_int),
+                ("row_seg", c_int), ("k_seg", c_int),
+                ("alpha", c_dbl), ("beta", c_dbl), ("gamma", c_dbl), ("diag_add", c_dbl),
+                ("tiles_m", c_int), ("tiles_n", c_int), ("tile_start", c_int), ("seg_span", c_int)]
+
+
+class PairwiseDesc(ctypes.Structure):
+    _fields_ = [("X", c_vp), ("Z", c_vp), ("ellX", c_vp), ("ellZ", c_vp), ("sigX", c_vp), ("sigZ", c_vp),
+                ("hyp", c_vp), ("K", c_vp), ("ldk", c_i64),
+                ("n", c_int), ("m", c_int), ("p", c_int), ("mode", c_int), ("dist", c_int), ("flags", c_int),
+                ("scale2", c_dbl), ("length_scale", c_dbl), ("diag_add", c_dbl),
+                ("tiles", c_int), ("tile_start", c_int)]
+
+
+class PairwiseBwdDesc(ctypes.Structure):
+    _fields_ = [("X", c_vp), ("Z", c_vp), ("ellX", c_vp), ("ellZ", c_vp), ("hyp", c_vp),
+                ("K", c_vp), ("Rbar", c_vp), ("Pm", c_vp), ("rowcoef", c_vp),
+                ("row_part", c_vp), ("col_part", c_vp), ("scal_part", c_vp), ("ld", c_i64),
+                ("n", c_int), ("m", c_int), ("p", c_int), ("mode", c_int), ("flags", c_int), ("tiles", c_int),
+                ("tile_start", c_int), ("pad_", c_int), ("scale2", c_dbl), ("length_scale", c_dbl)]
+
+
+class DsviArgs(ctypes.Structure):
+    _fields_ = [("D", c_int), ("M", c_int), ("B", c_int), ("Q", c_int), ("NF", c_int), ("elbo_mode", c_int),
+                ("frozen_mask", c_int), ("pad0_", c_int), ("N_over_B", c_dbl), ("jitter", c_dbl),
+                ("theta", c_vp), ("grad", c_vp),
+                ("off_muW", c_i64), ("off_sW", c_i64), ("off_muv", c_i64), ("off_sv", c_i64), ("off_muU", c_i64),
+                ("off_sU", c_i64), ("off_hyp", c_i64),
+                ("x", c_vp), ("y", c_vp), ("row_out", c_vp), ("seg", c_vp), ("Z", c_vp), ("noise", c_vp),
+                ("Afac", c_vp), ("Cinv", c_vp), ("Ainv", c_vp), ("K12", c_vp), ("P", c_vp), ("Pbar", c_vp),
+                ("R", c_vp), ("Abar", c_vp), ("WG", c_vp), ("WP", c_vp), ("Y", c_vp), ("Xs", c_vp),
+                ("v", c_vp), ("vbar", c_vp), ("ellZ", c_vp), ("ellX", c_vp), ("var_t", c_vp),
+                ("rowbuf", c_vp), ("facbuf", c_vp), ("red", c_vp), ("out", c_vp),
+                ("gib_row", c_vp), ("gib_col", c_vp), ("scal_part", c_vp), ("phi", c_vp),
+                ("info", c_vp), ("n_ct", c_int), ("n_rt", c_int), ("n_rt22", c_int), ("nblk_rows", c_int),
+                ("scal_off", c_i64 * 8)]
+
+
+# flags (include/nmgp_hip.h)
+A_LOWER, A_UPPER, B_LOWER, B_UPPER = 1, 2, 4, 8
+OUT_LOWER, OUT_TRIL, KSCALE, EPI, EPI_E_LOWER, DIAG_ADD, EPI_RS_NEG = 16, 32, 64, 128, 256, 512, 1024
+RBF, GIBBS = 0, 1
+DIST_DIFF, DIST_EXPAND = 0, 1
+HYP_LOG = 1
+
+_SIGS = {
+    "nmgp_version": (c_int, []),
+    "nmgp_sizeof_gemm_desc": (c_i64, []),
+    "nmgp_sizeof_pairwise_desc": (c_i64, []),
+    "nmgp_sizeof_pairwise_bwd_desc": (c_i64, []),
+    "nmgp_sizeof_dsvi_args": (c_i64, []),
+    "nmgp_gemm_grouped_f64": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
+    "nmgp_gemm_grouped_f32": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
+    "nmgp_gemm_f64": (c_int, [ctypes.POINTER(GemmDesc), c_vp, c_vp]),
+    "nmgp_gemm_f32": (c_int, [ctypes.POINTER(GemmDesc), c_vp, c_vp]),
+    "nmgp_potrf_batched_f64": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "nmgp_potrf_batched_f32": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "nmgp_trtri_batched_f64": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp]),
+    "nmgp_trtri_batched_f32": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp]),
+    "nmgp_pairwise_f64": (c_int, [c_vp, c_int, c_int, c_vp]),
+    "nmgp_pairwise_f32": (c_int, [c_vp, c_int, c_int, c_vp]),
+    "nmgp_pairwise_single_f64": (c_int, [ctypes.POINTER(PairwiseDesc), c_vp]),
+    "nmgp_pairwise_single_f32": (c_int, [ctypes.POINTER(PairwiseDesc), c_vp]),
+    "nmgp_pairwise_bwd_f64": (c_int, [c_vp, c_int, c_int, c_vp]),
+    "nmgp_pairwise_bwd_f32": (c_int, [c_vp, c_int, c_int, c_vp]),
+    "nmgp_pairwise_bwd_single_f64": (c_int, [ctypes.POINTER(PairwiseBwdDesc), c_vp]),
+    "nmgp_colsum_f64": (c_int, [c_vp, c_i64, c_i64, c_dbl, c_vp, c_vp]),
+    "nmgp_kron_product_f64": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "nmgp_kron_product_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "nmgp_kron_product_diag_f64": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    "nmgp_kron_mv_f64": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "nmgp_kron_mv_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "nmgp_dsvi_hyper_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_trow_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_recon_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_kl_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_tbwd_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_vbwd_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_finalize_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_adam_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_dbl, c_dbl, c_dbl, c_dbl, c_vp]),
+    "nmgp_adam_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_dbl, c_dbl, c_dbl, c_dbl, c_vp]),
+    "nmgp_normal_f64": (c_int, [c_vp, c_i64, c_u64, c_vp, c_i64, c_vp]),
+    "nmgp_counter_add": (c_int, [c_vp, c_i64, c_vp]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the ctypes library; raises if it is missing or mismatched."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `make -C {os.path.join(_HERE, 'csrc')}` "
+                          "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    for cls, fn in [(GemmDesc, "nmgp_sizeof_gemm_desc"), (PairwiseDesc, "nmgp_sizeof_pairwise_desc"),
+                    (PairwiseBwdDesc, "nmgp_sizeof_pairwise_bwd_desc"), (DsviArgs, "nmgp_sizeof_dsvi_args")]:
+        if ctypes.sizeof(cls) != getattr(L, fn)():
+            raise ImportError(f"ABI mismatch: ctypes {cls.__name__} is {ctypes.sizeof(cls)} bytes, "
+                              f"library says {getattr(L, fn)()}")
+    _lib = L
+    return L
+
+
+def exported_symbols():
+    return list(_SIGS.keys())
+
+
+def check(rc, what):
+    if rc != 0:
+        raise HipError(f"{what} failed with status {rc}")
+
+
+def stream_handle(device=None):
+    """The raw hipStream_t of torch's current stream on `device`."""
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t, offset_elems=0):
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr() + offset_elems * t.element_size())
+
+
+def require_device(t, name="tensor"):
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device (HIP) tensor; there is no CPU fallback")

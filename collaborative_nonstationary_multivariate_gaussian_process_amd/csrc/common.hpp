@@ -1,0 +1,67 @@
+// Shared device helpers for libnmgp_hip.so (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/nmgp_hip.h"
+
+#define NMGP_CHECK_LAUNCH()                                      \
+  do {                                                           \
+    if (hipGetLastError() != hipSuccess) return NMGP_ERR_LAUNCH; \
+  } while (0)
+
+namespace nmgp {
+
+constexpr int kWave = 64;
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// 16x16x4 MFMA, one A and one B element per lane:
+//   A operand lane l : A[i = l & 15][k = l >> 4]      B operand lane l : B[k = l >> 4][j = l & 15]
+//   C/D register r   : col = l & 15, row = row(l, r)  (f64 and f32 differ, MI355X guide §3)
+template <typename T> struct Mfma;
+template <> struct Mfma<double> {
+  using acc_t = f64x4;
+  __device__ static inline acc_t mma(double a, double b, acc_t c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+  }
+  __device__ static inline int row(int lane, int r) { return (lane >> 4) + 4 * r; }
+};
+template <> struct Mfma<float> {
+  using acc_t = f32x4;
+  __device__ static inline acc_t mma(float a, float b, acc_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  __device__ static inline int row(int lane, int r) { return ((lane >> 4) << 2) + r; }
+};
+
+template <typename T> __device__ inline T shfl(T v, int src) { return __shfl(v, src, 64); }
+
+template <typename T> __device__ inline T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-wide deterministic sum (blockDim.x multiple of 64, <= 1024). Result valid in all threads.
+template <typename T> __device__ inline T block_sum(T v, T* scratch /* >= 16 */) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) scratch[w] = v;
+  __syncthreads();
+  T s = 0;
+  for (int i = 0; i < nw; ++i) s += scratch[i];
+  __syncthreads();
+  return s;
+}
+
+template <typename T> __device__ inline T dexp(T x) { return exp(x); }
+template <> __device__ inline float dexp<float>(float x) { return expf(x); }
+template <typename T> __device__ inline T dlog(T x) { return log(x); }
+template <> __device__ inline float dlog<float>(float x) { return logf(x); }
+template <typename T> __device__ inline T dsqrt(T x) { return sqrt(x); }
+template <> __device__ inline float dsqrt<float>(float x) { return sqrtf(x); }
+
+}  // namespace nmgp

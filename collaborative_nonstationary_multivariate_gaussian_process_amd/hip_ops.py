@@ -1,0 +1,284 @@
+"""Thin Python wrappers over the libnmgp_hip.so C ABI (device tensors in, device tensors out).
+
+Everything here enqueues HIP kernels on torch's current stream; nothing falls back to CPU math.
+"""
+import ctypes
+import math
+
+import torch
+
+from . import _lib as L
+
+_F64 = torch.float64
+_F32 = torch.float32
+
+
+def _sfx(dtype):
+    if dtype == _F64:
+        return "f64"
+    if dtype == _F32:
+        return "f32"
+    raise TypeError(f"unsupported dtype {dtype}")
+
+
+def _addr(t, off=0):
+    return 0 if t is None else t.data_ptr() + off * t.element_size()
+
+
+# ------------------------------------------------------------------------------------ GEMM
+def gemm_desc(C, A, B, m, n, k, sA, sB, sC, *, flags=0, alpha=1.0, beta=0.0, kb=(0, 0), kscale=None,
+              epi=None, diag_add=0.0, row_seg=-1, k_seg=-1, seg_span=1, offs=(0, 0, 0)):
+    """Describe C(i,j) = alpha sum_k op(A)(i,k) s(k) op(B)(k,j) + beta C + gamma rs(i) E(i,j).
+
+    sA = (sA_i, sA_k, sA_kb), sB = (sB_k, sB_j, sB_kb), sC = (sC_i, sC_j) element strides;
+    offs = element offsets into A, B, C; epi = (E, E_off, (sE_i, sE_j), rs or None, gamma).
+    """
+    d = L.GemmDesc()
+    d.A, d.B, d.C = _addr(A, offs[0]), _addr(B, offs[1]), _addr(C, offs[2])
+    d.kscale = _addr(kscale[0], kscale[1]) if kscale is not None else 0
+    d.sA_i, d.sA_k, d.sA_kb = sA
+    d.sB_k, d.sB_j, d.sB_kb = sB
+    d.sC_i, d.sC_j = sC
+    d.m, d.n, d.k = int(m), int(n), int(k)
+    d.kbA, d.kbB = kb
+    d.flags = flags | (L.KSCALE if kscale is not None else 0)
+    d.row_seg, d.k_seg, d.seg_span = row_seg, k_seg, seg_span
+    d.alpha, d.beta, d.diag_add = alpha, beta, diag_add
+    if epi is not None:
+        E, eoff, (se_i, se_j), rs, gamma = epi
+        d.epi_E = _addr(E, eoff)
+        d.sE_i, d.sE_j = se_i, se_j
+        d.epi_rs = _addr(rs[0], rs[1]) if rs is not None else 0
+        d.gamma = gamma
+        d.flags |= L.EPI
+    if diag_add:
+        d.flags |= L.DIAG_ADD
+    d.tiles_m = (d.m + 63) // 64
+    d.tiles_n = (d.n + 63) // 64
+    return d
+
+
+class GemmGroup:
+    """A fixed list of GEMM problems launched as ONE grouped kernel (descriptors uploaded once)."""
+
+    def __init__(self, descs, device, dtype, seg=None):
+        self.dtype = dtype
+        self.seg = seg
+        arr = (L.GemmDesc * len(descs))()
+        t = 0
+        for i, d in enumerate(descs):
+            d.tile_start = t
+            t += d.tiles_m * d.tiles_n
+            arr[i] = d
+        self.total = t
+        self.n = len(descs)
+        raw = bytes(memoryview(arr).cast("B"))
+        self.dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+
+    def __call__(self, stream=None):
+        if self.n == 0 or self.total == 0:
+            return
+        s = stream if stream is not None else L.stream_handle()
+        fn = getattr(L.lib(), "nmgp_gemm_grouped_" + _sfx(self.dtype))
+        L.check(fn(ctypes.c_void_p(self.dev.data_ptr()), self.n, self.total,
+                   ctypes.c_void_p(self.seg.data_ptr()) if self.seg is not None else None, s), "gemm_grouped")
+
+
+def gemm_single(desc, dtype, seg=None):
+    fn = getattr(L.lib(), "nmgp_gemm_" + _sfx(dtype))
+    L.check(fn(ctypes.byref(desc), ctypes.c_void_p(seg.data_ptr()) if seg is not None else None,
+               L.stream_handle()), "gemm")
+
+
+def matmul(A, B, transA=False, transB=False, maskA=0, maskB=0, out=None, alpha=1.0):
+    """C = alpha op(A) op(B) for 2-D device tensors (op = transpose when requested)."""
+    L.require_device(A, "A")
+    A = A.contiguous()
+    B = B.contiguous()
+    m, k = (A.shape[1], A.shape[0]) if transA else A.shape
+    k2, n = (B.shape[1], B.shape[0]) if transB else B.shape
+    assert k == k2, (A.shape, B.shape)
+    if out is None:
+        out = torch.empty(m, n, dtype=A.dtype, device=A.device)
+    sA = (1, A.shape[1], 0) if transA else (A.shape[1], 1, 0)
+    sB = (1, B.shape[1], 0) if transB else (B.shape[1], 1, 0)
+    d = gemm_desc(out, A, B, m, n, k, sA, sB, (n, 1), flags=maskA | maskB, alpha=alpha)
+    gemm_single(d, A.dtype)
+    return out
+
+
+# ------------------------------------------------------------------------------------ Cholesky
+def potrf_(A, info=None):
+    """In-place lower Cholesky of a (batch, n, n) or (n, n) contiguous device tensor."""
+    L.require_device(A, "A")
+    assert A.is_contiguous()
+    n = A.shape[-1]
+    batch = A.numel() // (n * n) if n else 0
+    if info is None:
+        info = torch.zeros(max(batch, 1), dtype=torch.int32, device=A.device)
+    fn = getattr(L.lib(), "nmgp_potrf_batched_" + _sfx(A.dtype))
+    L.check(fn(ctypes.c_void_p(A.data_ptr()), n, n, n * n, batch, ctypes.c_void_p(info.data_ptr()),
+               L.stream_handle()), "potrf")
+    return info
+
+
+def trtri(Lm, out=None):
+    L.require_device(Lm, "L")
+    Lm = Lm.contiguous()
+    n = Lm.shape[-1]
+    batch = Lm.numel() // (n * n) if n else 0
+    if out is None:
+        out = torch.empty_like(Lm)
+    fn = getattr(L.lib(), "nmgp_trtri_batched_" + _sfx(Lm.dtype))
+    L.check(fn(ctypes.c_void_p(Lm.data_ptr()), n, n, n * n, ctypes.c_void_p(out.data_ptr()), n, n * n, batch,
+               L.stream_handle()), "trtri")
+    return out
+
+
+# ------------------------------------------------------------------------------------ pairwise
+def pairwise_desc(K, X, Z, *, mode, dist=L.DIST_DIFF, scale2=1.0, length_scale=1.0, ellX=None, ellZ=None,
+                  sigX=None, sigZ=None, hyp=None, hyp_off=0, hyp_log=False, diag_add=0.0):
+    d = L.PairwiseDesc()
+    d.X, d.Z = _addr(X), _addr(Z)
+    d.ellX, d.ellZ = _addr(ellX), _addr(ellZ)
+    d.sigX, d.sigZ = _addr(sigX), _addr(sigZ)
+    d.hyp = _addr(hyp, hyp_off) if hyp is not None else 0
+    d.K = _addr(K)
+    n, p = X.shape[0], (X.shape[1] if X.dim() > 1 else 1)
+    m = Z.shape[0]
+    d.ldk = K.shape[-1]
+    d.n, d.m, d.p, d.mode, d.dist = n, m, p, mode, dist
+    d.flags = L.HYP_LOG if hyp_log else 0
+    d.scale2, d.length_scale, d.diag_add = float(scale2), float(length_scale), float(diag_add)
+    d.tiles = ((n + 31) // 32) * ((m + 63) // 64)
+    return d
+
+
+def pairwise(X, Z, *, mode, dist=L.DIST_DIFF, scale2=1.0, length_scale=1.0, ellX=None, ellZ=None, sigX=None,
+             sigZ=None, diag_add=0.0, out=None):
+    L.require_device(X, "X")
+    X = X.contiguous()
+    Z = Z.contiguous()
+    if out is None:
+        out = torch.empty(X.shape[0], Z.shape[0], dtype=X.dtype, device=X.device)
+    d = pairwise_desc(out, X, Z, mode=mode, dist=dist, scale2=scale2, length_scale=length_scale, ellX=ellX,
+                      ellZ=ellZ, sigX=sigX, sigZ=sigZ, diag_add=diag_add)
+    fn = getattr(L.lib(), "nmgp_pairwise_single_" + _sfx(X.dtype))
+    L.check(fn(ctypes.byref(d), L.stream_handle()), "pairwise")
+    return out
+
+
+class PairwiseGroup:
+    def __init__(self, descs, device):
+        arr = (L.PairwiseDesc * len(descs))()
+        t = 0
+        for i, d in enumerate(descs):
+            d.tile_start = t
+            t += d.tiles
+            arr[i] = d
+        self.total, self.n = t, len(descs)
+        self.dev = torch.frombuffer(bytearray(bytes(memoryview(arr).cast("B"))), dtype=torch.uint8).to(device)
+
+    def __call__(self, dtype, stream=None):
+        fn = getattr(L.lib(), "nmgp_pairwise_" + _sfx(dtype))
+        L.check(fn(ctypes.c_void_p(self.dev.data_ptr()), self.n, self.total,
+                   stream if stream is not None else L.stream_handle()), "pairwise group")
+
+
+def pairwise_bwd_desc(X, Z, K, Rbar, *, mode, ld, Pm=None, rowcoef=None, ellX=None, ellZ=None, hyp=None,
+                      hyp_off=0, hyp_log=False, scale2=1.0, length_scale=1.0, row_part=None, col_part=None,
+                      scal_part=None, offs=(0, 0, 0, 0, 0, 0)):
+    """offs = element offsets into (K, Rbar, Pm, row_part, col_part, scal_part)."""
+    d = L.PairwiseBwdDesc()
+    d.X, d.Z = _addr(X), _addr(Z)
+    d.ellX, d.ellZ = _addr(ellX), _addr(ellZ)
+    d.hyp = _addr(hyp, hyp_off) if hyp is not None else 0
+    d.K, d.Rbar, d.Pm = _addr(K, offs[0]), _addr(Rbar, offs[1]), _addr(Pm, offs[2])
+    d.rowcoef = _addr(rowcoef[0], rowcoef[1]) if rowcoef is not None else 0
+    d.row_part = _addr(row_part, offs[3]) if row_part is not None else 0
+    d.col_part = _addr(col_part, offs[4]) if col_part is not None else 0
+    d.scal_part = _addr(scal_part, offs[5]) if scal_part is not None else 0
+    n = X.shape[0]
+    m = Z.shape[0]
+    d.ld = ld
+    d.n, d.m, d.p, d.mode = n, m, (X.shape[1] if X.dim() > 1 else 1), mode
+    d.flags = L.HYP_LOG if hyp_log else 0
+    d.scale2, d.length_scale = float(scale2), float(length_scale)
+    d.tiles = ((n + 31) // 32) * ((m + 63) // 64)
+    return d
+
+
+class PairwiseBwdGroup:
+    def __init__(self, descs, device):
+        arr = (L.PairwiseBwdDesc * len(descs))()
+        t = 0
+        self.starts = []
+        for i, d in enumerate(descs):
+            d.tile_start = t
+            self.starts.append(t)
+            t += d.tiles
+            arr[i] = d
+        self.total, self.n = t, len(descs)
+        self.dev = torch.frombuffer(bytearray(bytes(memoryview(arr).cast("B"))), dtype=torch.uint8).to(device)
+
+    def __call__(self, dtype, stream=None):
+        fn = getattr(L.lib(), "nmgp_pairwise_bwd_" + _sfx(dtype))
+        L.check(fn(ctypes.c_void_p(self.dev.data_ptr()), self.n, self.total,
+                   stream if stream is not None else L.stream_handle()), "pairwise bwd group")
+
+
+def bwd_tiles(n, m):
+    return ((n + 31) // 32) * ((m + 63) // 64), (m + 63) // 64, (n + 31) // 32
+
+
+def colsum(a2d, out, beta=0.0):
+    L.check(L.lib().nmgp_colsum_f64(ctypes.c_void_p(a2d.data_ptr()), a2d.shape[0], a2d.shape[1], beta,
+                                    ctypes.c_void_p(out.data_ptr()), L.stream_handle()), "colsum")
+    return out
+
+
+# ------------------------------------------------------------------------------------ Kronecker
+def kron_product(t1, t2):
+    L.require_device(t1, "t1")
+    t1, t2 = t1.contiguous(), t2.contiguous()
+    r1, c1 = t1.shape
+    r2, c2 = t2.shape
+    out = torch.empty(r1 * r2, c1 * c2, dtype=t1.dtype, device=t1.device)
+    fn = getattr(L.lib(), "nmgp_kron_product_" + _sfx(t1.dtype))
+    L.check(fn(ctypes.c_void_p(t1.data_ptr()), r1, c1, ctypes.c_void_p(t2.data_ptr()), r2, c2,
+               ctypes.c_void_p(out.data_ptr()), L.stream_handle()), "kron_product")
+    return out
+
+
+def kron_mv(B, K, y):
+    L.require_device(B, "B")
+    B, K, y = B.contiguous(), K.contiguous(), y.contiguous()
+    P1, P2 = B.shape
+    N1, N2 = K.shape
+    assert y.numel() == P2 * N2
+    out = torch.empty(P1 * N1, dtype=B.dtype, device=B.device)
+    work = torch.empty(N1 * P2, dtype=B.dtype, device=B.device)
+    fn = getattr(L.lib(), "nmgp_kron_mv_" + _sfx(B.dtype))
+    L.check(fn(ctypes.c_void_p(B.data_ptr()), P1, P2, ctypes.c_void_p(K.data_ptr()), N1, N2,
+               ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(work.data_ptr()),
+               L.stream_handle()), "kron_mv")
+    return out
+
+
+# ------------------------------------------------------------------------------------ optimiser / rng
+def adam_(theta, grad, m, v, step, lr, betas=(0.9, 0.999), eps=1e-8):
+    fn = getattr(L.lib(), "nmgp_adam_" + _sfx(theta.dtype))
+    L.check(fn(ctypes.c_void_p(theta.data_ptr()), ctypes.c_void_p(grad.data_ptr()), ctypes.c_void_p(m.data_ptr()),
+               ctypes.c_void_p(v.data_ptr()), theta.numel(), ctypes.c_void_p(step.data_ptr()), float(lr),
+               float(betas[0]), float(betas[1]), float(eps), L.stream_handle()), "adam")
+
+
+def normal_(out, seed, counter=None, offset=0):
+    L.check(L.lib().nmgp_normal_f64(ctypes.c_void_p(out.data_ptr()), out.numel(), ctypes.c_uint64(seed),
+                                    ctypes.c_void_p(counter.data_ptr()) if counter is not None else None,
+                                    int(offset), L.stream_handle()), "normal")
+    return out
+
+
+def counter_add_(counter, inc):
+    L.check(L.lib().nmgp_counter_add(ctypes.c_void_p(counter.data_ptr()), int(inc), L.stream_handle()), "counter")

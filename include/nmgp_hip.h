@@ -1,0 +1,220 @@
+/*
+ * nmgp_hip.h -- C ABI of libnmgp_hip.so, the MI355X (gfx950) kernels of the DSVI hot path of
+ * Collaborative Nonstationary Multivariate GP inference (reference: code/nmgp_dsvi.py).
+ *
+ * Conventions:
+ *   - plain pointers + sizes, no torch types; every buffer is caller-owned device memory;
+ *   - every call only ENQUEUES work on the given hipStream_t (no implicit device sync, no
+ *     allocation), so a caller may capture any sequence of calls into a hipGraph;
+ *   - return 0 on success, <0 = index of the offending argument (argument error),
+ *     NMGP_ERR_LAUNCH on a launch failure.  Numerical failures (non-PD matrix) are reported
+ *     LAPACK-style through a device `info` array: info[b] = first failing column (1-based).
+ *   - matrices are row-major; T = double (_f64) or float (_f32).
+ *
+ * Each entry point cites the reference interface it replaces.
+ */
+#ifndef NMGP_HIP_H
+#define NMGP_HIP_H
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NMGP_OK 0
+#define NMGP_ERR_LAUNCH (-1000)
+
+/* ------------------------------------------------------------------ library info */
+int nmgp_version(void);
+/* sizeof of the descriptor structs below (host code checks its own layout against these) */
+int64_t nmgp_sizeof_gemm_desc(void);
+int64_t nmgp_sizeof_pairwise_desc(void);
+int64_t nmgp_sizeof_pairwise_bwd_desc(void);
+int64_t nmgp_sizeof_dsvi_args(void);
+
+/* ------------------------------------------------------------------ grouped GEMM (MFMA)
+ * C(i,j) = alpha * sum_k op(A)(i,k) * s(k) * op(B)(k,j) + beta*C(i,j) + gamma*rs(i)*E(i,j)
+ *          (+ diag_add on i==j)
+ * Operands are addressed through strides, which covers transposes, k-concatenated blocks
+ * (A(i,k) = A[i*sA_i + (k%kbA)*sA_k + (k/kbA)*sA_kb]) and row / k ranges taken at run time from
+ * a device segment table (row_seg / k_seg >= 0: rows or k in [seg[s], seg[s+1])).
+ * Replaces every torch.matmul / torch.solve(...)-product in code/utils.py:117-157 and
+ * code/nmgp_dsvi.py:172-177 (Sigma = tril(S) tril(S)^T).                                  */
+enum {
+  NMGP_A_LOWER = 1,      /* op(A)(i,k) = 0 for k > i     */
+  NMGP_A_UPPER = 2,      /* op(A)(i,k) = 0 for k < i     */
+  NMGP_B_LOWER = 4,      /* op(B)(k,j) = 0 for j > k     */
+  NMGP_B_UPPER = 8,      /* op(B)(k,j) = 0 for j < k     */
+  NMGP_OUT_LOWER = 16,   /* store only j <= i            */
+  NMGP_OUT_TRIL = 32,    /* store j <= i, zero for j > i */
+  NMGP_KSCALE = 64,      /* multiply by s(k) = kscale[k] */
+  NMGP_EPI = 128,        /* + gamma * rs(i) * E(i,j)     */
+  NMGP_EPI_E_LOWER = 256,/* E(i,j) = 0 for j > i         */
+  NMGP_DIAG_ADD = 512,   /* + diag_add on i == j         */
+  NMGP_EPI_RS_NEG = 1024 /* rs(i) taken with a minus sign */
+};
+
+typedef struct nmgp_gemm_desc {
+  const void* A; const void* B; void* C;
+  const void* kscale; const void* epi_E; const void* epi_rs;
+  int64_t sA_i, sA_k, sA_kb;
+  int64_t sB_k, sB_j, sB_kb;
+  int64_t sC_i, sC_j;
+  int64_t sE_i, sE_j;
+  int32_t m, n, k, kbA, kbB, flags, row_seg, k_seg;
+  double alpha, beta, gamma, diag_add;
+  int32_t tiles_m, tiles_n, tile_start;
+  int32_t seg_span;      /* row_seg / k_seg cover seg[s] .. seg[s + max(seg_span,1)] */
+} nmgp_gemm_desc;
+
+/* d_desc: device array of nprob descriptors (tiles_m/tiles_n/tile_start filled by the host,
+ * tiles = ceil(m/64)*ceil(n/64)); total_tiles = sum of tiles; d_seg may be NULL if unused.  */
+int nmgp_gemm_grouped_f64(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles,
+                          const int32_t* d_seg, hipStream_t stream);
+int nmgp_gemm_grouped_f32(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles,
+                          const int32_t* d_seg, hipStream_t stream);
+/* one problem passed by value (host descriptor; tiles fields are filled internally)          */
+int nmgp_gemm_f64(const nmgp_gemm_desc* h_desc, const int32_t* d_seg, hipStream_t stream);
+int nmgp_gemm_f32(const nmgp_gemm_desc* h_desc, const int32_t* d_seg, hipStream_t stream);
+
+/* ------------------------------------------------------------------ batched Cholesky
+ * In place lower Cholesky of `batch` n x n SPD matrices (A + b*strideA), upper triangle zeroed.
+ * Replaces torch.cholesky in code/utils.py:46,54,276,347-348.  info[b] = 0 or the first
+ * non-positive pivot column (1-based), as LAPACK potrf.                                     */
+int nmgp_potrf_batched_f64(double* A, int64_t n, int64_t lda, int64_t strideA, int64_t batch,
+                           int32_t* info, hipStream_t stream);
+int nmgp_potrf_batched_f32(float* A, int64_t n, int64_t lda, int64_t strideA, int64_t batch,
+                           int32_t* info, hipStream_t stream);
+/* Out-of-place inverse of lower-triangular L: X = L^{-1} (upper triangle of X zeroed).
+ * Used for K22^{-1} = L^{-T} L^{-1} (replaces torch.solve, code/utils.py:119) and the
+ * Cholesky / log-det backward of KL_Gaussian (code/utils.py:332-351).                        */
+int nmgp_trtri_batched_f64(const double* L, int64_t n, int64_t ldl, int64_t strideL,
+                           double* X, int64_t ldx, int64_t strideX, int64_t batch, hipStream_t stream);
+int nmgp_trtri_batched_f32(const float* L, int64_t n, int64_t ldl, int64_t strideL,
+                           float* X, int64_t ldx, int64_t strideX, int64_t batch, hipStream_t stream);
+
+/* ------------------------------------------------------------------ pairwise kernel builder
+ * mode RBF:   K = scale2 * exp(-0.5 * ||x/ls - z/ls||^2)          (code/utils.py:91-94)
+ *             EXPAND distance: ||x||^2+||z||^2-2x.z on x/ls, z/ls (SIM_code/Utility/kernels.py:24-43)
+ * mode GIBBS: K = scale2 * [sigX sigZ] * sqrt(2 lx lz / (lx^2+lz^2)) * exp(-r2/(lx^2+lz^2))
+ *             (code/utils.py:97-103; SIM_code/Utility/kernels.py:46-73 with sigma, EXPAND)
+ * + diag_add on i == j (the 1e-4 / 1e-6 jitters).                                            */
+enum { NMGP_RBF = 0, NMGP_GIBBS = 1 };
+enum { NMGP_DIST_DIFF = 0, NMGP_DIST_EXPAND = 1 };
+enum { NMGP_HYP_LOG = 1 };     /* hyp[] holds log(scale2), log(ls): exponentiate on device */
+
+typedef struct nmgp_pairwise_desc {
+  const void* X; const void* Z;          /* (n x p), (m x p) row-major                  */
+  const void* ellX; const void* ellZ;    /* GIBBS per-point length scales               */
+  const void* sigX; const void* sigZ;    /* optional per-point sigma (legacy), or NULL  */
+  const void* hyp;                       /* device [scale2, ls] (RBF) / [scale2] (GIBBS), or NULL */
+  void* K;
+  int64_t ldk;
+  int32_t n, m, p, mode, dist, flags;
+  double scale2, length_scale, diag_add;
+  int32_t tiles, tile_start;
+} nmgp_pairwise_desc;
+
+int nmgp_pairwise_f64(const nmgp_pairwise_desc* d_desc, int ndesc, int total_tiles, hipStream_t stream);
+int nmgp_pairwise_f32(const nmgp_pairwise_desc* d_desc, int ndesc, int total_tiles, hipStream_t stream);
+int nmgp_pairwise_single_f64(const nmgp_pairwise_desc* h_desc, hipStream_t stream);
+int nmgp_pairwise_single_f32(const nmgp_pairwise_desc* h_desc, hipStream_t stream);
+
+/* Backward of the builder for Kbar = Rbar - rowcoef(i) * Pm (Pm / rowcoef optional):
+ *   RBF:   scal_part[t*2+0] += sum Kbar*K, scal_part[t*2+1] += sum Kbar*K*r2   (per tile t)
+ *   GIBBS: row_part[ct*n + i] = sum_j Kbar*K*dlogK/dlx_i over column tile ct,
+ *          col_part[rt*m + j] = sum_i Kbar*K*dlogK/dlz_j over row tile rt,
+ *          scal_part[t*2+0]  = sum Kbar*K
+ * Tiles are 32 rows x 64 columns; partial sums are deterministic (no atomics).              */
+typedef struct nmgp_pairwise_bwd_desc {
+  const void* X; const void* Z; const void* ellX; const void* ellZ; const void* hyp;
+  const void* K; const void* Rbar; const void* Pm; const void* rowcoef;
+  void* row_part; void* col_part; void* scal_part;
+  int64_t ld;
+  int32_t n, m, p, mode, flags, tiles, tile_start, pad_;
+  double scale2, length_scale;
+} nmgp_pairwise_bwd_desc;
+
+int nmgp_pairwise_bwd_f64(const nmgp_pairwise_bwd_desc* d_desc, int ndesc, int total_tiles, hipStream_t stream);
+int nmgp_pairwise_bwd_f32(const nmgp_pairwise_bwd_desc* d_desc, int ndesc, int total_tiles, hipStream_t stream);
+int nmgp_pairwise_bwd_single_f64(const nmgp_pairwise_bwd_desc* h_desc, hipStream_t stream);
+
+/* Deterministic column sums of a (rows x cols) row-major array: out[j] = beta*out[j] + sum_i a[i*cols+j] */
+int nmgp_colsum_f64(const double* a, int64_t rows, int64_t cols, double beta, double* out, hipStream_t stream);
+
+/* ------------------------------------------------------------------ Kronecker kernels
+ * kronecker_product (SIM_code/Utility/kronecker_operation.py:5-22): out[(i*r2+k)*(c1*c2)+j*c2+l] =
+ *   t1[i,j]*t2[k,l]  (one multiply per element: bit-exact)
+ * kronecker_product_diag (:25-33): out[i*n2+k] = d1[i]*d2[k]
+ * kron_mv (:72-85): out = (B kron K) y, B (P1 x P2), K (N1 x N2), y (P2*N2) -> (P1*N1)       */
+int nmgp_kron_product_f64(const double* t1, int64_t r1, int64_t c1, const double* t2, int64_t r2, int64_t c2,
+                          double* out, hipStream_t stream);
+int nmgp_kron_product_diag_f64(const double* d1, int64_t n1, const double* d2, int64_t n2, double* out,
+                               hipStream_t stream);
+int nmgp_kron_mv_f64(const double* B, int64_t P1, int64_t P2, const double* K, int64_t N1, int64_t N2,
+                     const double* y, double* out, double* work, hipStream_t stream);
+int nmgp_kron_product_f32(const float* t1, int64_t r1, int64_t c1, const float* t2, int64_t r2, int64_t c2,
+                          float* out, hipStream_t stream);
+int nmgp_kron_mv_f32(const float* B, int64_t P1, int64_t P2, const float* K, int64_t N1, int64_t N2,
+                     const float* y, float* out, float* work, hipStream_t stream);
+
+/* ------------------------------------------------------------------ DSVI step kernels
+ * The fused, closed-form DSVI objective and gradients (NMGP.forward + autograd backward,
+ * code/nmgp_dsvi.py:157-301) are assembled by the host from the primitives above plus the
+ * row / reduction kernels below, all reading one argument block.  See DESIGN.md §4.       */
+typedef struct nmgp_dsvi_args {
+  /* sizes */
+  int32_t D, M, B, Q, NF, elbo_mode, frozen_mask, pad0_;
+  double N_over_B, jitter;
+  /* parameters: flat theta in the registration order of code/nmgp_dsvi.py:117-155 */
+  const void* theta; void* grad;
+  int64_t off_muW, off_sW, off_muv, off_sv, off_muU, off_sU, off_hyp;
+  /* minibatch: rows grouped by output; seg[o]..seg[o+1] = rows of output o */
+  const void* x; const void* y; const int32_t* row_out; const int32_t* seg; const void* Z;
+  const void* noise;          /* z_v (M) | z_t (B) | z_pairs (Q x B), reference call order */
+  /* factor storage (see DESIGN.md §3 for the layout) */
+  void* Afac;                 /* (NF+4, M, M): A1 -> C1 (variational), then priors t,0,1,G -> C2 */
+  void* Cinv;                 /* (NF+4, M, M) inverses of the factors                          */
+  void* Ainv;                 /* (4, M, M) prior inverses t,0,1,G                              */
+  void* K12; void* P; void* Pbar; void* R;   /* (4, B, M) each, order t,0,1,G           */
+  void* Abar;                 /* (4, M, M) prior adjoints                                      */
+  void* WG; void* WP;         /* (D, B, M) quadratic-form factors                              */
+  void* Y;                    /* Ainv * mu : G (D x M) | t (1 x M) | 0 (D*D x M) | 1 (D*D x M)   */
+  void* Xs;                   /* (NF, M, M) scratch: Cinv_f * L_f                              */
+  void* v; void* vbar; void* ellZ; void* ellX; void* var_t;   /* (M),(M),(M),(B),(B)          */
+  void* rowbuf;               /* (2D+5, B) per-row adjoints                                     */
+  void* facbuf;               /* KL (NF) | delta (4,M) | wvec (4,M) | sel (4, D*D)             */
+  void* red;                  /* per-block partial sums                                        */
+  void* out;                  /* [0] loss [1] SELBO_R [2] KL_W [3] KL_v [4] KL_U               */
+  void* gib_row; void* gib_col; void* scal_part; void* phi;
+  int32_t* info;
+  int32_t n_ct, n_rt, n_rt22, nblk_rows;
+  int64_t scal_off[8];        /* tile offsets of the RBF backward problems L0_12,L0_22,L1_12,L1_22,t12,t22 */
+} nmgp_dsvi_args;
+
+int nmgp_dsvi_hyper_f64(const nmgp_dsvi_args* a, hipStream_t s);      /* hyper values + v sample   */
+int nmgp_dsvi_trow_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* t-row forward             */
+int nmgp_dsvi_recon_f64(const nmgp_dsvi_args* a, hipStream_t s);      /* recon + per-row adjoints  */
+int nmgp_dsvi_kl_f64(const nmgp_dsvi_args* a, hipStream_t s);         /* KL per factor + e-vectors */
+int nmgp_dsvi_tbwd_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* t-row backward            */
+int nmgp_dsvi_vbwd_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* v backward -> Phi         */
+int nmgp_dsvi_finalize_f64(const nmgp_dsvi_args* a, hipStream_t s);   /* loss + scalar gradients   */
+
+/* ------------------------------------------------------------------ optimiser / RNG
+ * torch.optim.Adam update (code/nmgp_dsvi.py:777,854) on a flat parameter vector; step is a
+ * device counter (incremented by the kernel's last block) so the call can be graph-replayed.  */
+int nmgp_adam_f64(double* theta, const double* grad, double* m, double* v, int64_t n,
+                  int64_t* step, double lr, double beta1, double beta2, double eps, hipStream_t stream);
+int nmgp_adam_f32(float* theta, const float* grad, float* m, float* v, int64_t n,
+                  int64_t* step, double lr, double beta1, double beta2, double eps, hipStream_t stream);
+/* Counter-based Philox4x32-10 standard normals: out[i] = N(0,1) for stream (seed, *counter + i) */
+int nmgp_normal_f64(double* out, int64_t n, uint64_t seed, const int64_t* counter, int64_t offset,
+                    hipStream_t stream);
+int nmgp_counter_add(int64_t* counter, int64_t inc, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NMGP_HIP_H */
