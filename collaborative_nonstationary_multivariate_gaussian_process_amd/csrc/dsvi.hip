@@ -245,6 +245,12 @@ __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
           wp[c] *= fp;
         }
       }
+      // rows of the latent functions s > o are not computed by the W GEMM (l_s = 0 there) but the
+      // k-concatenated P-bar GEMM reads them: store exact zeros
+      for (int s = o + 1; s < D; ++s) {
+        T* wg = WG + (int64_t)s * BM + (int64_t)r * M;
+        for (int c = lane; c < M; c += 64) wg[c] = (T)0;
+      }
       // P-bar initial rows (the rank-<=D mean terms and the -c*K12 diagonal term)
       T* acc = rowacc_all + (int64_t)w * M;
       T* PbG = (T*)a.Pbar + 3 * BM + (int64_t)r * M;

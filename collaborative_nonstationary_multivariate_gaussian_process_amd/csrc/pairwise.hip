@@ -123,8 +123,7 @@ __global__ __launch_bounds__(256) void pairwise_kernel(PwArgs args) {
       const T lx = ellX[i];
       const T S = lx * lx + lz * lz;
       const T C = dsqrt((T)2 * (lx * lz) / S);
-      k = s2 * C * dexp(-r2 / S);
-      if (sigX) k = (sigX[i] * sz) * (C * dexp(-r2 / S));
+      k = sigX ? ((sigX[i] * sz) * C) * dexp(-r2 / S) : s2 * C * dexp(-r2 / S);
     }
     if (i == j) k += dadd;
     K[(int64_t)i * d.ldk + j] = k;
@@ -166,14 +165,19 @@ __global__ __launch_bounds__(256) void pairwise_bwd_kernel(PwBwdArgs args) {
       const int64_t idx = (int64_t)i * d.ld + j;
       T kb = Rb[idx];
       if (rc) kb -= rc[i] * Pm[idx];
-      const T wv = kb * K[idx];
-      s0 += wv;
       if (!gibbs) {
-        s1 += wv * sqdist_div(X, Z, i, j, p, NMGP_DIST_DIFF, ls);
+        const T r2 = sqdist_div(X, Z, i, j, p, NMGP_DIST_DIFF, ls);
+        const T kv = K ? K[idx] : dexp((T)-0.5 * r2) * s2;   // K == NULL: recompute (K22 was factored in place)
+        const T wv = kb * kv;
+        s0 += wv;
+        s1 += wv * r2;
       } else {
         const T r2 = sqdist_div(X, Z, i, j, p, NMGP_DIST_DIFF, (T)1);
         const T lx = ellX[i];
         const T S = lx * lx + lz * lz;
+        const T kv = K ? K[idx] : s2 * dsqrt((T)2 * (lx * lz) / S) * dexp(-r2 / S);
+        const T wv = kb * kv;
+        s0 += wv;
         const T r2s = (T)2 * r2 / (S * S);
         gx = wv * ((T)0.5 / lx - lx / S + lx * r2s);
         gzacc += wv * ((T)0.5 / lz - lz / S + lz * r2s);

@@ -1,0 +1,415 @@
+"""The DSVI step engine: closed-form -SELBO and all 13 gradients on the MI355X (fp64).
+
+One engine instance owns the device workspace for a fixed (D outputs, M inducing points,
+B minibatch rows) and enqueues the ~30 HIP launches of one step on torch's
+current stream.  Nothing in a step allocates, synchronises or touches the host, so a whole step
+(noise -> forward -> backward -> Adam) can be captured once in a HIP graph and replayed.
+
+Reference path replaced: NMGP.forward + loss.backward() (code/nmgp_dsvi.py:157-301, 839-847),
+NMGP.compute_ELBO (code/nmgp_dsvi.py:303-404) and the Adam step (:777, :854).
+"""
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from . import hip_ops as H
+
+F64 = torch.float64
+JITTER = 1e-4   # code/utils.py:7
+
+PARAM_NAMES = ["mu_W", "sqrt_W", "mu_v", "sqrt_v", "mu_U", "sqrt_U",
+               "sigma2_tildeell_log", "length_scales_tildeell_log", "sigma2_L0_log",
+               "length_scales_L0_log", "sigma2_L1_log", "length_scales_L1_log", "sigma2_err_log"]
+HYPER_NAMES = PARAM_NAMES[6:]
+
+
+def param_layout(D, M):
+    """Offsets (elements) of the 13 parameters inside the flat theta vector, registration order."""
+    shapes = [(D, M), (D, M, M), (M,), (M, M), (D, D, M), (D, D, M, M)] + [()] * 7
+    offs, o = {}, 0
+    for name, shp in zip(PARAM_NAMES, shapes):
+        n = int(np.prod(shp)) if shp else 1
+        offs[name] = (o, shp)
+        o += n
+    return offs, o
+
+
+def pair_list(D):
+    return [(i, j) for i in range(D) for j in range(i + 1)]
+
+
+class DsviEngine:
+    """Workspace + launch schedule of one DSVI step for fixed (D, M, B)."""
+
+    def __init__(self, D, M, B, z, device="cuda", jitter=JITTER):
+        if not torch.cuda.is_available():
+            raise RuntimeError("DsviEngine needs a HIP device; there is no CPU fallback")
+        L.lib()
+        self.D, self.M, self.B = D, M, B
+        self.Q = D * (D + 1) // 2
+        self.NF = D + 1 + self.Q
+        self.dev = torch.device(device)
+        self.jitter = jitter
+        self.offs, self.nparam = param_layout(D, M)
+        Q, NF = self.Q, self.NF
+        e = lambda *shape: torch.zeros(*shape, dtype=F64, device=self.dev)
+        self.Z = torch.as_tensor(np.asarray(z, np.float64).reshape(-1, 1), device=self.dev).contiguous()
+        assert self.Z.shape[0] == M
+        # minibatch (rows grouped by output) + noise
+        self.x = e(B)
+        self.y = e(B)
+        self.row_out = torch.zeros(B, dtype=torch.int32, device=self.dev)
+        self.seg = torch.zeros(D + 1, dtype=torch.int32, device=self.dev)
+        self.noise = e(M + B + Q * B)
+        # factors
+        self.Afac = e(NF + 4, M, M)
+        self.Cinv = e(NF + 4, M, M)
+        self.Ainv = e(4, M, M)
+        self.K12 = e(4, B, M)
+        self.P = e(4, B, M)
+        self.Pbar = e(4, B, M)
+        self.R = e(4, B, M)
+        self.Abar = e(4, M, M)
+        self.WG = e(D, B, M)
+        self.WP = e(D, B, M)
+        self.Y = e(D + 1 + 2 * D * D, M)
+        self.Xs = e(NF, M, M)
+        self.T2 = e(M, M)
+        self.v, self.vbar, self.ellZ = e(M), e(M), e(M)
+        self.ellX, self.var_t = e(B), e(B)
+        self.rowbuf = e(2 * D + 5, B)
+        self.facbuf = e(NF + 8 * M + 4 * D * D)
+        self.nblk = (B + 3) // 4
+        self.red = e(5 * self.nblk)
+        self.out = e(8)
+        self.n_ct = (M + 63) // 64
+        self.n_rt = (B + 31) // 32
+        self.n_rt22 = (M + 31) // 32
+        self.gib_row = e(self.n_ct * B + self.n_ct * M)
+        self.gib_col = e(self.n_rt * M + self.n_rt22 * M)
+        tb = H.bwd_tiles(B, M)[0]
+        tm = H.bwd_tiles(M, M)[0]
+        scal_tiles = [tb, tm, tb, tm, tb, tm]          # L0_12, L0_22, L1_12, L1_22, t12, t22
+        self.scal_off = [0] + list(np.cumsum(scal_tiles))
+        self.scal_part = e(2 * int(self.scal_off[-1]))
+        self.phi = e(M, M)
+        self.info = torch.zeros(NF + 4, dtype=torch.int32, device=self.dev)
+        # selection weights for the -1/2 Y diag(sel) Y^T prior adjoint (static)
+        sel = np.zeros((4, D * D))
+        for i in range(D):
+            for j in range(i + 1):
+                sel[2 if i == j else 1, i * D + j] = 1.0
+        base = NF + 8 * M
+        self.facbuf[base:base + 4 * D * D] = torch.from_numpy(sel.reshape(-1)).to(self.dev)
+        self._theta = None
+        self._plans = {}
+
+    # ------------------------------------------------------------------------------------ binding
+    def bind(self, theta, grad, frozen_mask=0, N=None):
+        """Attach the flat parameter / gradient vectors (device, fp64) and build the launch plans."""
+        assert theta.dtype == F64 and theta.is_cuda and theta.numel() == self.nparam
+        if self._theta is not None and theta.data_ptr() == self._theta.data_ptr() and \
+                grad.data_ptr() == self._grad.data_ptr() and frozen_mask == self.frozen_mask:
+            if N is not None:
+                self.N = N
+            return
+        self._theta, self._grad = theta, grad
+        self.frozen_mask = frozen_mask
+        self.N = N if N is not None else self.B
+        self._plans = {}
+
+    def _args(self, elbo_mode=0):
+        a = L.DsviArgs()
+        D, M, B = self.D, self.M, self.B
+        a.D, a.M, a.B, a.Q, a.NF = D, M, B, self.Q, self.NF
+        a.elbo_mode, a.frozen_mask = elbo_mode, self.frozen_mask
+        a.N_over_B = float(self.N) / float(B)
+        a.jitter = self.jitter
+        a.theta, a.grad = self._theta.data_ptr(), self._grad.data_ptr()
+        o = self.offs
+        a.off_muW, a.off_sW, a.off_muv, a.off_sv = o["mu_W"][0], o["sqrt_W"][0], o["mu_v"][0], o["sqrt_v"][0]
+        a.off_muU, a.off_sU, a.off_hyp = o["mu_U"][0], o["sqrt_U"][0], o["sigma2_tildeell_log"][0]
+        for name in ["x", "y", "row_out", "seg", "Z", "noise", "Afac", "Cinv", "Ainv", "K12", "P", "Pbar", "R",
+                     "Abar", "WG", "WP", "Y", "Xs", "v", "vbar", "ellZ", "ellX", "var_t", "rowbuf", "facbuf",
+                     "red", "out", "gib_row", "gib_col", "scal_part", "phi", "info"]:
+            setattr(a, name, getattr(self, name).data_ptr())
+        a.n_ct, a.n_rt, a.n_rt22, a.nblk_rows = self.n_ct, self.n_rt, self.n_rt22, self.nblk
+        for i, v in enumerate(self.scal_off):
+            a.scal_off[i] = int(v)
+        return a
+
+    # ------------------------------------------------------------------------------------ plans
+    def _plan(self, elbo_mode):
+        if elbo_mode in self._plans:
+            return self._plans[elbo_mode]
+        D, M, B, NF, Q = self.D, self.M, self.B, self.NF, self.Q
+        MM, BM = M * M, B * M
+        th, gr = self._theta, self._grad
+        o = self.offs
+        sW, sv, sU = o["sqrt_W"][0], o["sqrt_v"][0], o["sqrt_U"][0]
+        muW, muv, muU, hyp = o["mu_W"][0], o["mu_v"][0], o["mu_U"][0], o["sigma2_tildeell_log"][0]
+        pairs = pair_list(D)
+        fac_off = [sW + d * MM for d in range(D)] + [sv] + [sU + (i * D + j) * MM for (i, j) in pairs]
+        prior_of = [3] * D + [0] + [2 if i == j else 1 for (i, j) in pairs]
+        dev, seg = self.dev, self.seg
+        G = lambda descs: H.GemmGroup(descs, dev, F64, seg=seg)
+        g = H.gemm_desc
+        rows_all = dict(row_seg=0, seg_span=D)          # all rows of the minibatch via the segment table
+        p = {}
+        # F1: RBF builders (K_t12, K_t22 + lam I, K_L0_*, K_L1_*)
+        bl = []
+        for k, hoff in [(0, hyp + 0), (1, hyp + 2), (2, hyp + 4)]:
+            K12v = self.K12[k]
+            bl.append(H.pairwise_desc(K12v, self.x, self.Z, mode=L.RBF, hyp=th, hyp_off=hoff, hyp_log=True))
+            bl.append(H.pairwise_desc(self.Afac[NF + k], self.Z, self.Z, mode=L.RBF, hyp=th, hyp_off=hoff,
+                                      hyp_log=True, diag_add=self.jitter))
+        p["build_rbf"] = H.PairwiseGroup(bl, dev)
+        # F2: A1_f = tril(S_f) tril(S_f)^T + lam I (lower part)
+        p["syrk"] = G([g(self.Afac, th, th, M, M, M, (M, 1, 0), (1, M, 0), (M, 1),
+                         flags=L.A_LOWER | L.B_UPPER | L.OUT_LOWER, diag_add=self.jitter,
+                         offs=(fac_off[f], fac_off[f], f * MM)) for f in range(NF)])
+        # F5: prior inverses t,0,1 and Xs_f = Cinv_f L_f
+        d5 = [g(self.Ainv, self.Cinv, self.Cinv, M, M, M, (1, M, 0), (M, 1, 0), (M, 1), flags=L.A_UPPER | L.B_LOWER,
+                offs=((NF + k) * MM, (NF + k) * MM, k * MM)) for k in range(3)]
+        if not elbo_mode:
+            d5 += [g(self.Xs, self.Cinv, th, M, M, M, (M, 1, 0), (M, 1, 0), (M, 1),
+                     flags=L.A_LOWER | L.B_LOWER | L.OUT_TRIL, offs=(f * MM, fac_off[f], f * MM)) for f in range(NF)]
+        p["inv3"] = G(d5)
+        # F6: P_k = K12_k Ainv_k (k = t,0,1) ; Y_t, Y_0, Y_1
+        d6 = [g(self.P, self.K12, self.Ainv, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), offs=(k * BM, k * MM, k * BM),
+                **rows_all) for k in range(3)]
+        d6 += [g(self.Y, self.Ainv, th, M, 1, M, (M, 1, 0), (1, M, 0), (1, M), offs=(0, muv, D * M)),
+               g(self.Y, self.Ainv, th, M, D * D, M, (M, 1, 0), (1, M, 0), (1, M), offs=(MM, muU, (D + 1) * M)),
+               g(self.Y, self.Ainv, th, M, D * D, M, (M, 1, 0), (1, M, 0), (1, M),
+                 offs=(2 * MM, muU, (D + 1 + D * D) * M))]
+        p["proj3"] = G(d6)
+        # F9: Gibbs builders (K_G22 + lam I into the G prior slot, K_G12)
+        p["build_gibbs"] = H.PairwiseGroup([
+            H.pairwise_desc(self.Afac[NF + 3], self.Z, self.Z, mode=L.GIBBS, ellX=self.ellZ, ellZ=self.ellZ,
+                            diag_add=self.jitter),
+            H.pairwise_desc(self.K12[3], self.x, self.Z, mode=L.GIBBS, ellX=self.ellX, ellZ=self.ellZ)], dev)
+        p["invG"] = G([g(self.Ainv, self.Cinv, self.Cinv, M, M, M, (1, M, 0), (M, 1, 0), (M, 1),
+                         flags=L.A_UPPER | L.B_LOWER, offs=((NF + 3) * MM, (NF + 3) * MM, 3 * MM))])
+        p["projG"] = G([g(self.P, self.K12, self.Ainv, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1),
+                          offs=(3 * BM, 3 * MM, 3 * BM), **rows_all),
+                        g(self.Y, self.Ainv, th, M, D, M, (M, 1, 0), (1, M, 0), (1, M), offs=(3 * MM, muW, 0))])
+        # F14: quadratic-form factors W = P L on the rows that use them
+        d14 = []
+        for d in range(D):
+            rs = dict(row_seg=d, seg_span=D - d) if not elbo_mode else dict(row_seg=0, seg_span=d + 1)
+            d14.append(g(self.WG, self.P, th, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), flags=L.B_LOWER,
+                         offs=(3 * BM, sW + d * MM, d * BM), **rs))
+        for (i, j) in pairs:
+            typ = 2 if i == j else 1
+            slot, rseg = (j, i) if not elbo_mode else (i, j)
+            d14.append(g(self.WP, self.P, th, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), flags=L.B_LOWER,
+                         offs=(typ * BM, sU + (i * D + j) * MM, slot * BM), row_seg=rseg))
+        p["quad"] = G(d14)
+        if elbo_mode:
+            self._plans[elbo_mode] = p
+            return p
+        # B2: P-bar += W-hat L^T ; L-bar = P^T W-hat ; mu-bar = P^T adjoints
+        d17 = [g(self.Pbar, self.WG, th, B, M, D * M, (M, 1, BM), (1, M, MM), (M, 1), flags=L.B_UPPER, kb=(M, M),
+                 beta=1.0, offs=(0, sW, 3 * BM), **rows_all)]
+        for i in range(D):
+            d17.append(g(self.Pbar, self.WP, th, B, M, M, (M, 1, 0), (1, M, 0), (M, 1), flags=L.B_UPPER, beta=1.0,
+                         offs=(i * BM, sU + (i * D + i) * MM, 2 * BM), row_seg=i))
+            if i > 0:
+                d17.append(g(self.Pbar, self.WP, th, B, M, i * M, (M, 1, BM), (1, M, MM), (M, 1), flags=L.B_UPPER,
+                             kb=(M, M), beta=1.0, offs=(0, sU + (i * D) * MM, 1 * BM), row_seg=i))
+        for d in range(D):
+            d17.append(g(gr, self.P, self.WG, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_TRIL, beta=1.0,
+                         offs=(3 * BM, d * BM, sW + d * MM), k_seg=d, seg_span=D - d))
+            d17.append(g(gr, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1), beta=1.0,
+                         offs=(3 * BM, d * B, muW + d * M), k_seg=d, seg_span=D - d))
+        for (i, j) in pairs:
+            typ = 2 if i == j else 1
+            d17.append(g(gr, self.P, self.WP, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_TRIL, beta=1.0,
+                         offs=(typ * BM, j * BM, sU + (i * D + j) * MM), k_seg=i))
+            d17.append(g(gr, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1), beta=1.0,
+                         offs=(typ * BM, (D + j) * B, muU + (i * D + j) * M), k_seg=i))
+        p["bwd_w"] = G(d17)
+        # B3: R_k = Pbar_k Ainv_k (G,0,1) ; Abar_k = Cinv^T diag(delta) Cinv ; KL L-bar
+        d18 = [g(self.R, self.Pbar, self.Ainv, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), offs=(k * BM, k * MM, k * BM),
+                 **rows_all) for k in (3, 1, 2)]
+        fb = self.facbuf
+        for k in range(4):
+            d18.append(g(self.Abar, self.Cinv, self.Cinv, M, M, M, (1, M, 0), (M, 1, 0), (M, 1),
+                         flags=L.A_UPPER | L.B_LOWER, kscale=(fb, NF + k * M),
+                         offs=((NF + k) * MM, (NF + k) * MM, k * MM)))
+        for f in range(NF):
+            k = prior_of[f]
+            d18.append(g(gr, self.Cinv, self.Xs, M, M, M, (1, M, 0), (M, 1, 0), (M, 1),
+                         flags=L.A_UPPER | L.B_LOWER | L.OUT_TRIL | L.EPI_E_LOWER, alpha=-1.0, beta=1.0,
+                         epi=(th, fac_off[f], (M, 1), (fb, NF + 4 * M + k * M), 1.0),
+                         offs=(f * MM, f * MM, fac_off[f])))
+        p["bwd_solve"] = G(d18)
+        # B4: Abar_k -= 1/2 Y_k diag(sel_k) Y_k^T
+        ybase = [D * M, (D + 1) * M, (D + 1 + D * D) * M, 0]
+        ncol = [1, D * D, D * D, D]
+        sel_base = NF + 8 * M
+        d19 = []
+        for k in range(4):
+            ks = (fb, sel_base + k * D * D) if k in (1, 2) else None
+            d19.append(g(self.Abar, self.Y, self.Y, M, M, ncol[k], (1, M, 0), (M, 1, 0), (M, 1), alpha=-0.5,
+                         beta=1.0, kscale=ks, offs=(ybase[k], ybase[k], k * MM)))
+        p["bwd_kly"] = G(d19)
+        # B5: Abar_k -= P_k^T R_k (G,0,1)
+        p["bwd_pr"] = G([g(self.Abar, self.P, self.R, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), alpha=-1.0, beta=1.0,
+                           offs=(k * BM, k * BM, k * MM), k_seg=0, seg_span=D) for k in (3, 1, 2)])
+        # B6: builder backward for G12, G22, L0_*, L1_*
+        rbd = self.rowbuf
+        so = self.scal_off
+        bw = [H.pairwise_bwd_desc(self.x, self.Z, self.K12, self.R, mode=L.GIBBS, ld=M, Pm=self.P,
+                                  rowcoef=(rbd, 2 * D * B), ellX=self.ellX, ellZ=self.ellZ, row_part=self.gib_row,
+                                  col_part=self.gib_col, offs=(3 * BM, 3 * BM, 3 * BM, 0, 0, 0)),
+              H.pairwise_bwd_desc(self.Z, self.Z, None, self.Abar, mode=L.GIBBS, ld=M, ellX=self.ellZ,
+                                  ellZ=self.ellZ, row_part=self.gib_row, col_part=self.gib_col,
+                                  offs=(0, 3 * MM, 0, self.n_ct * B, self.n_rt * M, 0))]
+        for q, (k, hoff, rc) in enumerate([(1, hyp + 2, 2 * D + 1), (2, hyp + 4, 2 * D + 2)]):
+            bw.append(H.pairwise_bwd_desc(self.x, self.Z, self.K12, self.R, mode=L.RBF, ld=M, Pm=self.P,
+                                          rowcoef=(rbd, rc * B), hyp=th, hyp_off=hoff, hyp_log=True,
+                                          scal_part=self.scal_part,
+                                          offs=(k * BM, k * BM, k * BM, 0, 0, 2 * int(so[2 * q]))))
+            bw.append(H.pairwise_bwd_desc(self.Z, self.Z, None, self.Abar, mode=L.RBF, ld=M, hyp=th, hyp_off=hoff,
+                                          hyp_log=True, scal_part=self.scal_part,
+                                          offs=(0, k * MM, 0, 0, 0, 2 * int(so[2 * q + 1]))))
+        p["bwd_build"] = H.PairwiseBwdGroup(bw, dev)
+        # B7: t chain
+        p["bwd_t1"] = G([g(self.R, self.Pbar, self.Ainv, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), offs=(0, 0, 0),
+                           **rows_all),
+                         g(self.vbar, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1),
+                           offs=(0, (2 * D + 3) * B, 0), k_seg=0, seg_span=D)])
+        p["bwd_t2"] = G([g(self.Abar, self.P, self.R, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), alpha=-1.0, beta=1.0,
+                           offs=(0, 0, 0), k_seg=0, seg_span=D)])
+        p["bwd_tbuild"] = H.PairwiseBwdGroup([
+            H.pairwise_bwd_desc(self.x, self.Z, self.K12, self.R, mode=L.RBF, ld=M, Pm=self.P,
+                                rowcoef=(rbd, (2 * D + 4) * B), hyp=th, hyp_off=hyp, hyp_log=True,
+                                scal_part=self.scal_part, offs=(0, 0, 0, 0, 0, 2 * int(so[4]))),
+            H.pairwise_bwd_desc(self.Z, self.Z, None, self.Abar, mode=L.RBF, ld=M, hyp=th, hyp_off=hyp,
+                                hyp_log=True, scal_part=self.scal_part, offs=(0, 0, 0, 0, 0, 2 * int(so[5])))], dev)
+        # B9: v Cholesky backward: grad_sv += Cinv_v^T (Psi Xs_v)
+        p["bwd_v1"] = G([g(self.T2, self.phi, self.Xs, M, M, M, (M, 1, 0), (M, 1, 0), (M, 1), flags=L.B_LOWER,
+                           offs=(0, D * MM, 0))])
+        p["bwd_v2"] = G([g(gr, self.Cinv, self.T2, M, M, M, (1, M, 0), (M, 1, 0), (M, 1),
+                           flags=L.A_UPPER | L.OUT_TRIL, beta=1.0, offs=(D * MM, 0, sv))])
+        self._plans[elbo_mode] = p
+        return p
+
+    # ------------------------------------------------------------------------------------ data
+    def load_batch(self, x, y, sizes, noise=None, index=None):
+        """Copy one minibatch (rows grouped by output, `sizes` rows per list entry) to the device."""
+        D, B = self.D, self.B
+        sizes = [int(s) for s in sizes]
+        assert sum(sizes) == B, (sum(sizes), B)
+        ids = list(range(len(sizes))) if index is None else [int(i) for i in index]
+        order = sorted(range(len(sizes)), key=lambda k: ids[k])
+        if ids != sorted(ids) or len(set(ids)) != len(ids):
+            raise NotImplementedError("index must list distinct outputs in increasing order")
+        seg = np.zeros(D + 1, np.int32)
+        for k, n in zip(ids, sizes):
+            seg[k + 1] = n
+        seg = np.cumsum(seg).astype(np.int32)
+        row_out = np.repeat(np.arange(D, dtype=np.int32), np.diff(seg))
+        self.x.copy_(torch.as_tensor(np.asarray(x, np.float64).reshape(-1)))
+        self.y.copy_(torch.as_tensor(np.asarray(y, np.float64).reshape(-1)))
+        self.seg.copy_(torch.from_numpy(seg))
+        self.row_out.copy_(torch.from_numpy(row_out))
+        if noise is not None:
+            self.noise.copy_(torch.as_tensor(noise, dtype=F64).reshape(-1))
+
+    def device_noise(self, seed, counter):
+        H.normal_(self.noise, seed, counter=counter)
+
+    # ------------------------------------------------------------------------------------ step
+    def _call(self, fn, a, s):
+        L.check(fn(ctypes.byref(a), s), fn.__name__)
+
+    def forward_backward(self, stream=None):
+        """Enqueue -SELBO (self.out[0]) and all gradients (into the bound grad vector)."""
+        s = stream if stream is not None else L.stream_handle()
+        lib = L.lib()
+        D, M, NF = self.D, self.M, self.NF
+        MM = M * M
+        p = self._plan(0)
+        a = self._args(0)
+        self._grad.zero_()
+        p["build_rbf"](F64, s)
+        p["syrk"](s)
+        L.check(lib.nmgp_potrf_batched_f64(ctypes.c_void_p(self.Afac.data_ptr()), M, M, MM, NF + 3,
+                                           ctypes.c_void_p(self.info.data_ptr()), s), "potrf")
+        L.check(lib.nmgp_trtri_batched_f64(ctypes.c_void_p(self.Afac.data_ptr()), M, M, MM,
+                                           ctypes.c_void_p(self.Cinv.data_ptr()), M, MM, NF + 3, s), "trtri")
+        p["inv3"](s)
+        p["proj3"](s)
+        self._call(lib.nmgp_dsvi_hyper_f64, a, s)
+        self._call(lib.nmgp_dsvi_trow_f64, a, s)
+        p["build_gibbs"](F64, s)
+        gslot = (NF + 3) * MM
+        L.check(lib.nmgp_potrf_batched_f64(ctypes.c_void_p(self.Afac.data_ptr() + gslot * 8), M, M, MM, 1,
+                                           ctypes.c_void_p(self.info.data_ptr() + (NF + 3) * 4), s), "potrf G")
+        L.check(lib.nmgp_trtri_batched_f64(ctypes.c_void_p(self.Afac.data_ptr() + gslot * 8), M, M, MM,
+                                           ctypes.c_void_p(self.Cinv.data_ptr() + gslot * 8), M, MM, 1, s), "trtri G")
+        p["invG"](s)
+        p["projG"](s)
+        p["quad"](s)
+        self._call(lib.nmgp_dsvi_kl_f64, a, s)
+        self._call(lib.nmgp_dsvi_recon_f64, a, s)
+        p["bwd_w"](s)
+        p["bwd_solve"](s)
+        p["bwd_kly"](s)
+        p["bwd_pr"](s)
+        p["bwd_build"](F64, s)
+        self._call(lib.nmgp_dsvi_tbwd_f64, a, s)
+        p["bwd_t1"](s)
+        p["bwd_t2"](s)
+        p["bwd_tbuild"](F64, s)
+        self._call(lib.nmgp_dsvi_vbwd_f64, a, s)
+        p["bwd_v1"](s)
+        p["bwd_v2"](s)
+        self._call(lib.nmgp_dsvi_finalize_f64, a, s)
+        return self.out
+
+    def elbo_sample(self, stream=None, with_kl=False):
+        """Enqueue one Monte-Carlo sample of compute_ELBO's reconstruction term (self.out[1]);
+        with_kl also evaluates the KL terms from THIS sample's K_G22 (out[2..4])."""
+        s = stream if stream is not None else L.stream_handle()
+        lib = L.lib()
+        M, NF = self.M, self.NF
+        MM = M * M
+        p = self._plan(1)
+        a = self._args(1)
+        p["build_rbf"](F64, s)
+        p["syrk"](s)
+        L.check(lib.nmgp_potrf_batched_f64(ctypes.c_void_p(self.Afac.data_ptr()), M, M, MM, NF + 3,
+                                           ctypes.c_void_p(self.info.data_ptr()), s), "potrf")
+        L.check(lib.nmgp_trtri_batched_f64(ctypes.c_void_p(self.Afac.data_ptr()), M, M, MM,
+                                           ctypes.c_void_p(self.Cinv.data_ptr()), M, MM, NF + 3, s), "trtri")
+        p["inv3"](s)
+        p["proj3"](s)
+        self._call(lib.nmgp_dsvi_hyper_f64, a, s)
+        self._call(lib.nmgp_dsvi_trow_f64, a, s)
+        p["build_gibbs"](F64, s)
+        gslot = (NF + 3) * MM
+        L.check(lib.nmgp_potrf_batched_f64(ctypes.c_void_p(self.Afac.data_ptr() + gslot * 8), M, M, MM, 1,
+                                           ctypes.c_void_p(self.info.data_ptr() + (NF + 3) * 4), s), "potrf G")
+        L.check(lib.nmgp_trtri_batched_f64(ctypes.c_void_p(self.Afac.data_ptr() + gslot * 8), M, M, MM,
+                                           ctypes.c_void_p(self.Cinv.data_ptr() + gslot * 8), M, MM, 1, s), "trtri G")
+        p["invG"](s)
+        p["projG"](s)
+        p["quad"](s)
+        if with_kl:
+            self._call(lib.nmgp_dsvi_kl_f64, a, s)
+        self._call(lib.nmgp_dsvi_recon_f64, a, s)
+        self._call(lib.nmgp_dsvi_finalize_f64, a, s)
+        return self.out
+
+    def check_info(self):
+        info = self.info.cpu()
+        if int(info.abs().sum()) != 0:
+            bad = int(torch.nonzero(info)[0])
+            raise torch.linalg.LinAlgError(f"cholesky: matrix {bad} is not positive-definite "
+                                           f"(leading minor of order {int(info[bad])})")

@@ -176,11 +176,13 @@ def test_pairwise_bwd(ops):
     lls = torch.tensor(np.log(0.2), requires_grad=True)
     Kc = O.create_RBF(X, Z, torch.exp(ls2), torch.exp(lls))
     (Kc * Kbar).sum().backward()
-    Kd = ops.pairwise(X.to(DEV), Z.to(DEV), mode=L.RBF, scale2=1.3, length_scale=0.2)
+    # descriptors hold raw pointers: every device tensor they name must stay referenced
+    Xd, Zd, Rbd, Pmd, rcd = X.to(DEV), Z.to(DEV), Rb.to(DEV), Pm.to(DEV), rc.to(DEV)
+    Kd = ops.pairwise(Xd, Zd, mode=L.RBF, scale2=1.3, length_scale=0.2)
     tiles, nct, nrt = ops.bwd_tiles(n, m)
     sp = torch.zeros(tiles * 2, dtype=F64, device=DEV)
-    d = ops.pairwise_bwd_desc(X.to(DEV), Z.to(DEV), Kd, Rb.to(DEV), mode=L.RBF, ld=m, Pm=Pm.to(DEV),
-                              rowcoef=(rc.to(DEV), 0), scale2=1.3, length_scale=0.2, scal_part=sp)
+    d = ops.pairwise_bwd_desc(Xd, Zd, Kd, Rbd, mode=L.RBF, ld=m, Pm=Pmd,
+                              rowcoef=(rcd, 0), scale2=1.3, length_scale=0.2, scal_part=sp)
     ops.PairwiseBwdGroup([d], DEV)(F64)
     s = sp.view(tiles, 2).sum(0).cpu()
     assert float(s[0]) == pytest.approx(float(ls2.grad), rel=1e-12)
@@ -190,12 +192,12 @@ def test_pairwise_bwd(ops):
     eZ = torch.from_numpy(np.exp(g.normal(-2, .3, m))).requires_grad_()
     Gc = O.create_Gibbs(X, Z, eX, eZ)
     (Gc * Kbar).sum().backward()
-    Gd = ops.pairwise(X.to(DEV), Z.to(DEV), mode=L.GIBBS, ellX=eX.detach().to(DEV), ellZ=eZ.detach().to(DEV))
+    eXd, eZd = eX.detach().to(DEV), eZ.detach().to(DEV)
+    Gd = ops.pairwise(Xd, Zd, mode=L.GIBBS, ellX=eXd, ellZ=eZd)
     rp = torch.zeros(nct, n, dtype=F64, device=DEV)
     cp = torch.zeros(nrt, m, dtype=F64, device=DEV)
-    d = ops.pairwise_bwd_desc(X.to(DEV), Z.to(DEV), Gd, Rb.to(DEV), mode=L.GIBBS, ld=m, Pm=Pm.to(DEV),
-                              rowcoef=(rc.to(DEV), 0), ellX=eX.detach().to(DEV), ellZ=eZ.detach().to(DEV),
-                              row_part=rp, col_part=cp)
+    d = ops.pairwise_bwd_desc(Xd, Zd, Gd, Rbd, mode=L.GIBBS, ld=m, Pm=Pmd,
+                              rowcoef=(rcd, 0), ellX=eXd, ellZ=eZd, row_part=rp, col_part=cp)
     ops.PairwiseBwdGroup([d], DEV)(F64)
     gx = torch.zeros(n, dtype=F64, device=DEV)
     gz = torch.zeros(m, dtype=F64, device=DEV)
