@@ -291,6 +291,7 @@ __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
       }
     }
   }
+  if ((threadIdx.x & 63) != 0) Rrow = epart = c0p = c1p = 0;   // every lane holds the row's value
   Rrow = block_sum(Rrow, red);
   epart = block_sum(epart, red);
   c0p = block_sum(c0p, red);
