@@ -1,0 +1,259 @@
+"""Benchmark: DSVI iterations/s on the PM2.5-shaped config (BASELINE.json configs[1]).
+
+One step = one DSVI iteration of the reference training loop (code/nmgp_dsvi.py:829-863):
+device Philox noise -> fused closed-form forward/backward (all 13 gradients) -> Adam, on a
+minibatch of B = 2000 rows drawn from N = 10,000 synthetic observations (2,000 locations x
+D = 5 outputs, M = 256 inducing points, fp64).  The step is replayed as one HIP graph.
+Multi-GPU (torchrun): each rank draws its own minibatch from its own shard, gradients are
+averaged with one RCCL all-reduce, every rank applies the same Adam update (weak scaling:
+value = minibatch iterations per second summed over ranks).
+
+Prints ONE JSON line (rank 0).  Also reports the per-phase breakdown, the roofline of the
+dominant kernel (the grouped MFMA GEMM) and the CPU baseline (the oracle, op for op the
+reference's torch-CPU path, timed on this host's cores).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+D, M, N_LOC, B = 5, 256, 2000, 2000
+FP64_MFMA_PEAK_TFLOPS = 78.6          # MI355X dense FP64 matrix peak (spec)
+HBM_PEAK_GBS = 8000.0
+
+
+def synth_data(rank):
+    """PM2.5-shaped synthetic data: all 5 outputs observed at 2,000 locations."""
+    rng = np.random.default_rng(1000 + rank)
+    xs = [np.sort(rng.uniform(0, 1, N_LOC)) for _ in range(D)]
+    ys = [rng.standard_normal(N_LOC) for _ in range(D)]
+    return xs, ys
+
+
+def epoch_batches(xs, ys, rng):
+    """One epoch of DataLoader(shuffle=True) minibatches, each split per output like vec2list."""
+    X = np.concatenate(xs)
+    Y = np.concatenate(ys)
+    I = np.concatenate([np.full(len(x), d) for d, x in enumerate(xs)])
+    perm = rng.permutation(len(X))
+    out = []
+    for s in range(0, len(X) - B + 1, B):
+        idx = perm[s:s + B]
+        idx = idx[np.argsort(I[idx], kind="stable")]        # vec2list order: grouped by output
+        seg = np.concatenate([[0], np.cumsum(np.bincount(I[idx], minlength=D))]).astype(np.int32)
+        out.append((X[idx], Y[idx], I[idx].astype(np.int32), seg))
+    return out
+
+
+class PhaseTimer:
+    """HIP events around every launch of an eager step (same stream as the kernels)."""
+
+    def __init__(self):
+        self.rec = []
+        self.cur = None
+
+    def start(self, name, kind):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.cur = e
+
+    def stop(self, name, kind):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.rec.append((name, kind, self.cur, e))
+
+    def summary(self, nsteps):
+        torch.cuda.synchronize()
+        per_name, per_kind = {}, {}
+        for name, kind, a, b in self.rec:
+            ms = a.elapsed_time(b)
+            per_name[name] = per_name.get(name, 0.0) + ms / nsteps
+            per_kind[kind] = per_kind.get(kind, 0.0) + ms / nsteps
+        return per_name, per_kind
+
+
+def cpu_baseline(seconds, xs, ys, z):
+    """The oracle (reference op for op: per-pair LU solves, dense D x D Sigma_U, torch autograd,
+    Adam) on the same PM2.5-shaped minibatch, on this host's cores; bounded to ~`seconds`."""
+    from oracle import nmgp_oracle as O
+    nthreads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(nthreads)
+    p = O.new_params(D, M, seed=22)
+    for k in ["length_scales_tildeell_log", "length_scales_L0_log", "length_scales_L1_log"]:
+        p[k] = torch.tensor(-1.0, dtype=torch.float64)
+    p = {k: v.clone().requires_grad_() for k, v in p.items()}
+    frozen = {"length_scales_tildeell_log", "length_scales_L0_log", "length_scales_L1_log"}
+    rng = np.random.default_rng(7)
+    batches = epoch_batches(xs, ys, rng)
+    state = {}
+    times = []
+    t_start = time.time()
+    it = 0
+    while True:
+        x, y, I, seg = batches[it % len(batches)]
+        xl = [x[seg[d]:seg[d + 1]] for d in range(D)]
+        yl = [y[seg[d]:seg[d + 1]] for d in range(D)]
+        t0 = time.time()
+        for v in p.values():
+            v.grad = None
+        loss, _ = O.forward(p, xl, yl, z, float(D * N_LOC), O.TorchNoise())
+        loss.backward()
+        O.adam_step(p, {k: v.grad for k, v in p.items() if k not in frozen}, state, 0.01)
+        times.append(time.time() - t0)
+        it += 1
+        if it >= 2 and (time.time() - t_start > seconds or it >= 40):
+            break
+    steady = times[1:]
+    return {"value": round(1.0 / float(np.mean(steady)), 4), "unit": "it/s", "cores": nthreads, "kind": "port",
+            "sample": f"{len(steady)} timed DSVI iterations (after 1 warm-up) of the oracle "
+                      f"(torch-CPU fp64 restatement of code/nmgp_dsvi.py:157-301 + autograd + Adam) on the same "
+                      f"D=5, M=256, B=2000 config; mean {1000 * float(np.mean(steady)):.1f} ms/it"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-breakdown", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="no HIP graph (launch every kernel from Python)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP, DsviTrainer
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.engine import param_layout
+
+    xs, ys = synth_data(rank)
+    z = np.linspace(0, 1, M)
+    model = NMGP(number_observations=D * N_LOC, dim_outputs=D, Z=z, minibatch_size=B, seed=22, device=dev,
+                 noise="device")
+    model._noise_seed = 22 + 7919 * rank
+    for k in ["length_scales_tildeell_log", "length_scales_L0_log", "length_scales_L1_log"]:
+        getattr(model, k).data.fill_(-1.0)
+        getattr(model, k).requires_grad = False
+    trainer = DsviTrainer(model, lr=0.01)
+    eng = model.engine(B)
+    rng = np.random.default_rng(55 + rank)
+    host_batches = epoch_batches(xs, ys, rng)
+    nb = len(host_batches)
+    Xb = torch.tensor(np.stack([b[0] for b in host_batches]), dtype=torch.float64, device=dev)
+    Yb = torch.tensor(np.stack([b[1] for b in host_batches]), dtype=torch.float64, device=dev)
+    Ib = torch.tensor(np.stack([b[2] for b in host_batches]), dtype=torch.int32, device=dev)
+    Sb = torch.tensor(np.stack([b[3] for b in host_batches]), dtype=torch.int32, device=dev)
+
+    def load(bi):
+        eng.x.copy_(Xb[bi], non_blocking=True)
+        eng.y.copy_(Yb[bi], non_blocking=True)
+        eng.row_out.copy_(Ib[bi], non_blocking=True)
+        eng.seg.copy_(Sb[bi], non_blocking=True)
+
+    load(0)
+    if world > 1:
+        dist.broadcast(model._theta, 0)
+    graph = None
+    if not args.eager:
+        graph = trainer.capture(eng, include_update=(world == 1))
+
+    def step(i):
+        load(i % nb)
+        if graph is not None:
+            graph.replay()
+        else:
+            trainer.grad_step(eng)
+        if world > 1:
+            dist.all_reduce(model._grad, op=dist.ReduceOp.AVG)
+            trainer.update()
+        elif graph is None:
+            trainer.update()
+
+    for i in range(args.warmup):
+        step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.time() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    loss_val = float(eng.out[0])
+    ms_per_step = 1000.0 * elapsed / args.steps
+    value = world * args.steps / elapsed
+
+    # ---------------------------------------------------------------- per-phase breakdown (eager)
+    breakdown, roofline, chol = None, None, None
+    if not args.no_breakdown:
+        nrep = 10
+        timer = PhaseTimer()
+        for i in range(nrep):
+            load(i % nb)
+            trainer.grad_step(eng, timer=timer)
+        per_name, per_kind = timer.summary(nrep)
+        seg_host = host_batches[(nrep - 1) % nb][3]
+        gemm_flops = 2.0 * sum(g.macs(seg_host) for _, g in eng.gemm_groups())
+        gemm_ms = per_kind.get("gemm", 0.0)
+        n_gemm = sum(1 for _, k, _ in eng._sched if k == "gemm")
+        achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12
+        roofline = {"kernel": "gemm_kernel<double> (grouped MFMA f64 GEMM)", "bound": "mfma",
+                    "achieved": round(achieved, 4), "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / FP64_MFMA_PEAK_TFLOPS, 5), "traffic": None,
+                    "launches_per_step": n_gemm, "avg_launch_us": round(1000 * gemm_ms / n_gemm, 2),
+                    "algorithmic_gflop_per_step": round(gemm_flops / 1e9, 4)}
+        nchol = eng.NF + 4
+        chol_ms = per_kind.get("potrf", 0.0)
+        chol = {"matrices_per_step": nchol, "n": M, "ms_per_step": round(chol_ms, 4),
+                "gflops": round(nchol * M ** 3 / 3.0 / (chol_ms * 1e-3) / 1e9, 2)}
+        breakdown = {k: round(v, 4) for k, v in sorted(per_kind.items(), key=lambda kv: -kv[1])}
+        breakdown_names = {k: round(v, 4) for k, v in sorted(per_name.items(), key=lambda kv: -kv[1])}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds, xs, ys, z)
+
+    if rank == 0:
+        rec = {"metric": "DSVI ELBO iterations/sec (PM2.5-shaped, fp64, 1 iteration = fwd+bwd+Adam on B=2000)",
+               "value": round(value, 3), "unit": "it/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+               "config": {"workload": "PM2.5-shaped synthetic DSVI step (BASELINE.json configs[1])",
+                          "D_outputs": D, "M_inducing": M, "minibatch_rows": B, "N_observations": D * N_LOC,
+                          "global_batch": B * world, "parallelism": f"dp{world}" if world > 1 else "single",
+                          "hip_graph": graph is not None},
+               "roofline": roofline, "cpu_baseline": cpu, "cholesky": chol, "phase_ms": breakdown,
+               "final_loss": loss_val}
+        if cpu is not None:
+            rec["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
+        if breakdown is not None:
+            rec["phase_ms_by_launch"] = breakdown_names
+        print(json.dumps(rec))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -328,84 +328,98 @@ class DsviEngine:
     def _call(self, fn, a, s):
         L.check(fn(ctypes.byref(a), s), fn.__name__)
 
-    def forward_backward(self, stream=None):
-        """Enqueue -SELBO (self.out[0]) and all gradients (into the bound grad vector)."""
-        s = stream if stream is not None else L.stream_handle()
+    def _schedule(self, elbo_mode, with_kl=True):
+        """The ordered launch list of one step: [(name, kind, callable(stream)), ...]."""
         lib = L.lib()
         D, M, NF = self.D, self.M, self.NF
         MM = M * M
-        p = self._plan(0)
-        a = self._args(0)
+        p = self._plan(elbo_mode)
+        a = self._args(elbo_mode)
+        self._keep_args = getattr(self, "_keep_args", {})
+        self._keep_args[elbo_mode] = a
+        Af, Ci, info = self.Afac.data_ptr(), self.Cinv.data_ptr(), self.info.data_ptr()
+        gslot = (NF + 3) * MM * 8
+        vp = ctypes.c_void_p
+
+        def row(fn):
+            return lambda s: L.check(fn(ctypes.byref(a), s), fn.__name__)
+
+        def gemm(name):
+            return lambda s: p[name](s)
+
+        def pw(name):
+            return lambda s: p[name](F64, s)
+
+        steps = [
+            ("build_rbf", "pairwise", pw("build_rbf")),
+            ("syrk", "gemm", gemm("syrk")),
+            ("potrf", "potrf", lambda s: L.check(lib.nmgp_potrf_batched_f64(vp(Af), M, M, MM, NF + 3, vp(info), s), "potrf")),
+            ("trtri", "trtri", lambda s: L.check(lib.nmgp_trtri_batched_f64(vp(Af), M, M, MM, vp(Ci), M, MM, NF + 3, s), "trtri")),
+            ("inv3", "gemm", gemm("inv3")),
+            ("proj3", "gemm", gemm("proj3")),
+            ("v", "row", row(lib.nmgp_dsvi_hyper_f64)),
+            ("trow", "row", row(lib.nmgp_dsvi_trow_f64)),
+            ("build_gibbs", "pairwise", pw("build_gibbs")),
+            ("potrf_G", "potrf", lambda s: L.check(lib.nmgp_potrf_batched_f64(vp(Af + gslot), M, M, MM, 1, vp(info + (NF + 3) * 4), s), "potrf G")),
+            ("trtri_G", "trtri", lambda s: L.check(lib.nmgp_trtri_batched_f64(vp(Af + gslot), M, M, MM, vp(Ci + gslot), M, MM, 1, s), "trtri G")),
+            ("invG", "gemm", gemm("invG")),
+            ("projG", "gemm", gemm("projG")),
+            ("quad", "gemm", gemm("quad")),
+        ]
+        if elbo_mode:
+            if with_kl:
+                steps.append(("kl", "row", row(lib.nmgp_dsvi_kl_f64)))
+            steps += [("recon", "row", row(lib.nmgp_dsvi_recon_f64)),
+                      ("finalize", "row", row(lib.nmgp_dsvi_finalize_f64))]
+            return steps
+        steps += [
+            ("kl", "row", row(lib.nmgp_dsvi_kl_f64)),
+            ("recon", "row", row(lib.nmgp_dsvi_recon_f64)),
+            ("bwd_w", "gemm", gemm("bwd_w")),
+            ("bwd_solve", "gemm", gemm("bwd_solve")),
+            ("bwd_kly", "gemm", gemm("bwd_kly")),
+            ("bwd_pr", "gemm", gemm("bwd_pr")),
+            ("bwd_build", "pairwise_bwd", pw("bwd_build")),
+            ("tbwd", "row", row(lib.nmgp_dsvi_tbwd_f64)),
+            ("bwd_t1", "gemm", gemm("bwd_t1")),
+            ("bwd_t2", "gemm", gemm("bwd_t2")),
+            ("bwd_tbuild", "pairwise_bwd", pw("bwd_tbuild")),
+            ("vbwd", "row", row(lib.nmgp_dsvi_vbwd_f64)),
+            ("bwd_v1", "gemm", gemm("bwd_v1")),
+            ("bwd_v2", "gemm", gemm("bwd_v2")),
+            ("finalize", "row", row(lib.nmgp_dsvi_finalize_f64)),
+        ]
+        return steps
+
+    def _run(self, steps, stream, timer):
+        s = stream if stream is not None else L.stream_handle()
+        for name, kind, fn in steps:
+            if timer is not None:
+                timer.start(name, kind)
+            fn(s)
+            if timer is not None:
+                timer.stop(name, kind)
+
+    def forward_backward(self, stream=None, timer=None):
+        """Enqueue -SELBO (self.out[0]) and all gradients (into the bound grad vector)."""
+        key = ("fb", self._theta.data_ptr(), self._grad.data_ptr(), self.frozen_mask, self.N)
+        if getattr(self, "_sched_key", None) != key:
+            self._sched = self._schedule(0)
+            self._sched_key = key
         self._grad.zero_()
-        p["build_rbf"](F64, s)
-        p["syrk"](s)
-        L.check(lib.nmgp_potrf_batched_f64(ctypes.c_void_p(self.Afac.data_ptr()), M, M, MM, NF + 3,
-                                           ctypes.c_void_p(self.info.data_ptr()), s), "potrf")
-        L.check(lib.nmgp_trtri_batched_f64(ctypes.c_void_p(self.Afac.data_ptr()), M, M, MM,
-                                           ctypes.c_void_p(self.Cinv.data_ptr()), M, MM, NF + 3, s), "trtri")
-        p["inv3"](s)
-        p["proj3"](s)
-        self._call(lib.nmgp_dsvi_hyper_f64, a, s)
-        self._call(lib.nmgp_dsvi_trow_f64, a, s)
-        p["build_gibbs"](F64, s)
-        gslot = (NF + 3) * MM
-        L.check(lib.nmgp_potrf_batched_f64(ctypes.c_void_p(self.Afac.data_ptr() + gslot * 8), M, M, MM, 1,
-                                           ctypes.c_void_p(self.info.data_ptr() + (NF + 3) * 4), s), "potrf G")
-        L.check(lib.nmgp_trtri_batched_f64(ctypes.c_void_p(self.Afac.data_ptr() + gslot * 8), M, M, MM,
-                                           ctypes.c_void_p(self.Cinv.data_ptr() + gslot * 8), M, MM, 1, s), "trtri G")
-        p["invG"](s)
-        p["projG"](s)
-        p["quad"](s)
-        self._call(lib.nmgp_dsvi_kl_f64, a, s)
-        self._call(lib.nmgp_dsvi_recon_f64, a, s)
-        p["bwd_w"](s)
-        p["bwd_solve"](s)
-        p["bwd_kly"](s)
-        p["bwd_pr"](s)
-        p["bwd_build"](F64, s)
-        self._call(lib.nmgp_dsvi_tbwd_f64, a, s)
-        p["bwd_t1"](s)
-        p["bwd_t2"](s)
-        p["bwd_tbuild"](F64, s)
-        self._call(lib.nmgp_dsvi_vbwd_f64, a, s)
-        p["bwd_v1"](s)
-        p["bwd_v2"](s)
-        self._call(lib.nmgp_dsvi_finalize_f64, a, s)
+        self._run(self._sched, stream, timer)
         return self.out
 
     def elbo_sample(self, stream=None, with_kl=False):
         """Enqueue one Monte-Carlo sample of compute_ELBO's reconstruction term (self.out[1]);
         with_kl also evaluates the KL terms from THIS sample's K_G22 (out[2..4])."""
-        s = stream if stream is not None else L.stream_handle()
-        lib = L.lib()
-        M, NF = self.M, self.NF
-        MM = M * M
-        p = self._plan(1)
-        a = self._args(1)
-        p["build_rbf"](F64, s)
-        p["syrk"](s)
-        L.check(lib.nmgp_potrf_batched_f64(ctypes.c_void_p(self.Afac.data_ptr()), M, M, MM, NF + 3,
-                                           ctypes.c_void_p(self.info.data_ptr()), s), "potrf")
-        L.check(lib.nmgp_trtri_batched_f64(ctypes.c_void_p(self.Afac.data_ptr()), M, M, MM,
-                                           ctypes.c_void_p(self.Cinv.data_ptr()), M, MM, NF + 3, s), "trtri")
-        p["inv3"](s)
-        p["proj3"](s)
-        self._call(lib.nmgp_dsvi_hyper_f64, a, s)
-        self._call(lib.nmgp_dsvi_trow_f64, a, s)
-        p["build_gibbs"](F64, s)
-        gslot = (NF + 3) * MM
-        L.check(lib.nmgp_potrf_batched_f64(ctypes.c_void_p(self.Afac.data_ptr() + gslot * 8), M, M, MM, 1,
-                                           ctypes.c_void_p(self.info.data_ptr() + (NF + 3) * 4), s), "potrf G")
-        L.check(lib.nmgp_trtri_batched_f64(ctypes.c_void_p(self.Afac.data_ptr() + gslot * 8), M, M, MM,
-                                           ctypes.c_void_p(self.Cinv.data_ptr() + gslot * 8), M, MM, 1, s), "trtri G")
-        p["invG"](s)
-        p["projG"](s)
-        p["quad"](s)
-        if with_kl:
-            self._call(lib.nmgp_dsvi_kl_f64, a, s)
-        self._call(lib.nmgp_dsvi_recon_f64, a, s)
-        self._call(lib.nmgp_dsvi_finalize_f64, a, s)
+        self._run(self._schedule(1, with_kl), stream, None)
         return self.out
+
+    def gemm_groups(self):
+        """(name, GemmGroup) of the training step, for FLOP accounting."""
+        p = self._plan(0)
+        return [(n, p[n]) for n, k, _ in self._schedule(0) if k == "gemm"]
 
     def check_info(self):
         info = self.info.cpu()

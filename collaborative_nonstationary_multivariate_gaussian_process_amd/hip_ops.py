@@ -72,8 +72,12 @@ class GemmGroup:
             arr[i] = d
         self.total = t
         self.n = len(descs)
+        self.descs = list(descs)
         raw = bytes(memoryview(arr).cast("B"))
         self.dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+
+    def macs(self, seg=None):
+        return sum(desc_macs(d, seg) for d in self.descs)
 
     def __call__(self, stream=None):
         if self.n == 0 or self.total == 0:
@@ -82,6 +86,38 @@ class GemmGroup:
         fn = getattr(L.lib(), "nmgp_gemm_grouped_" + _sfx(self.dtype))
         L.check(fn(ctypes.c_void_p(self.dev.data_ptr()), self.n, self.total,
                    ctypes.c_void_p(self.seg.data_ptr()) if self.seg is not None else None, s), "gemm_grouped")
+
+
+def desc_macs(d, seg=None):
+    """Algorithmic multiply-adds of one problem: structural zeros of triangular operands and the
+    skipped upper half of OUT_LOWER / OUT_TRIL outputs are not counted; row / k ranges resolved
+    from the host copy of the segment table."""
+    import numpy as np
+    span = d.seg_span if d.seg_span > 0 else 1
+    m = d.m if d.row_seg < 0 else int(seg[d.row_seg + span] - seg[d.row_seg])
+    K = d.k if d.k_seg < 0 else int(seg[d.k_seg + span] - seg[d.k_seg])
+    n = d.n
+    if m <= 0 or n <= 0 or K <= 0:
+        return 0
+    kb = d.kbA if 0 < d.kbA < K else K
+    nblk = K // kb
+    f = d.flags
+    i = np.arange(m)[:, None]
+    j = np.arange(n)[None, :]
+    lo = np.zeros((m, n), np.int64)
+    hi = np.full((m, n), kb - 1, np.int64)
+    if f & L.A_UPPER:
+        lo = np.maximum(lo, i)
+    if f & L.B_LOWER:
+        lo = np.maximum(lo, j)
+    if f & L.A_LOWER:
+        hi = np.minimum(hi, i)
+    if f & L.B_UPPER:
+        hi = np.minimum(hi, j)
+    cnt = np.clip(hi - lo + 1, 0, None)
+    if f & (L.OUT_LOWER | L.OUT_TRIL):
+        cnt = np.where(j <= i, cnt, 0)
+    return int(cnt.sum()) * nblk
 
 
 def gemm_single(desc, dtype, seg=None):

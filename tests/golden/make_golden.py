@@ -462,7 +462,8 @@ def case_inference():
                                                   itnum=2, show_ELBO=False, seed=22)
     TAPE.off()
     R.NMGP.forward = orig_fwd
-    d = {"z": z, "lr": 0.005}
+    d = {"z": z, "lr": 0.005, "x": np.concatenate(X_list).reshape(-1), "y": np.concatenate(Y_list).reshape(-1),
+         "sizes": np.array([len(x) for x in X_list])}
     for it, ((xs, ys), nz) in enumerate(zip(rec_batches, rec_noise)):
         d[f"it{it}_x"] = np.concatenate(xs); d[f"it{it}_y"] = np.concatenate(ys)
         d[f"it{it}_sizes"] = np.array([len(x) for x in xs]); d[f"it{it}_noise"] = np.concatenate([a.reshape(-1) for a in nz])
@@ -483,6 +484,10 @@ def case_inference():
 
 if __name__ == "__main__":
     torch.set_num_threads(8)
+    if len(sys.argv) > 1:
+        for name in sys.argv[1:]:
+            globals()["case_" + name]()
+        sys.exit(0)
     case_toy()
     case_modelpt()
     case_mid()
