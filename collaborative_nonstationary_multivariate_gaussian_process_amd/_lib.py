@@ -28,7 +28,8 @@ class GemmDesc(ctypes.Structure):
                 ("m", c_int), ("n", c_int), ("k", c_int), ("kbA", c_int), ("kbB", c_int), ("flags", c_int),
                 ("row_seg", c_int), ("k_seg", c_int),
                 ("alpha", c_dbl), ("beta", c_dbl), ("gamma", c_dbl), ("diag_add", c_dbl),
-                ("tiles_m", c_int), ("tiles_n", c_int), ("tile_start", c_int), ("seg_span", c_int)]
+                ("tiles_m", c_int), ("tiles_n", c_int), ("tile_start", c_int), ("seg_span", c_int),
+                ("ksplit", c_int), ("pad2_", c_int), ("ws", c_vp), ("counters", c_vp)]
 
 
 class PairwiseDesc(ctypes.Structure):
@@ -101,6 +102,7 @@ _SIGS = {
     "nmgp_dsvi_trow_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_recon_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_kl_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_delta_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_tbwd_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_vbwd_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_finalize_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),

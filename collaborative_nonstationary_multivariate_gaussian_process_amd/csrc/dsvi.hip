@@ -29,12 +29,15 @@ __device__ inline void pair_ij(int q, int& i, int& j) {
   i = r;
   j = q - r * (r + 1) / 2;
 }
-// prior slot of variational factor f: 0 = t (f == D), 1 = L0, 2 = L1, 3 = G (f < D)
+// Variational factor order: f < D latent functions W_f | D <= f < D+Q coefficient pairs (i,j) in
+// (i, j<=i) order | f = D+Q (= NF-1) the length-scale process v.  Prior slot of factor f:
+// 0 = t (v), 1 = L0 (off-diagonal pairs), 2 = L1 (diagonal pairs), 3 = G (W).
 __device__ inline int prior_of(int f, int D) {
+  const int Q = D * (D + 1) / 2;
   if (f < D) return 3;
-  if (f == D) return 0;
+  if (f == D + Q) return 0;
   int i, j;
-  pair_ij(f - D - 1, i, j);
+  pair_ij(f - D, i, j);
   return i == j ? 2 : 1;
 }
 
@@ -75,7 +78,7 @@ __global__ __launch_bounds__(256) void dsvi_v_kernel(Args a) {
   const int M = a.M, lane = threadIdx.x & 63;
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= M) return;
-  const T* Cv = (const T*)a.Afac + (int64_t)a.D * M * M;   // C1 of factor D (Sigma_v)
+  const T* Cv = (const T*)a.Afac + (int64_t)(a.NF - 1) * M * M;   // C1 of the v factor (Sigma_v)
   const T* zv = (const T*)a.noise;
   T s = 0;
   for (int k = lane; k <= c; k += 64) s += Cv[(int64_t)c * M + k] * zv[k];
@@ -310,26 +313,26 @@ template <typename T> __device__ inline const T* fac_S(const Args& a, int f) {
   const T* th = (const T*)a.theta;
   const int64_t MM = (int64_t)a.M * a.M;
   if (f < a.D) return th + a.off_sW + f * MM;
-  if (f == a.D) return th + a.off_sv;
+  if (f == a.NF - 1) return th + a.off_sv;
   int i, j;
-  pair_ij(f - a.D - 1, i, j);
+  pair_ij(f - a.D, i, j);
   return th + a.off_sU + ((int64_t)i * a.D + j) * MM;
 }
 template <typename T> __device__ inline const T* fac_mu(const Args& a, int f) {
   const T* th = (const T*)a.theta;
   if (f < a.D) return th + a.off_muW + (int64_t)f * a.M;
-  if (f == a.D) return th + a.off_muv;
+  if (f == a.NF - 1) return th + a.off_muv;
   int i, j;
-  pair_ij(f - a.D - 1, i, j);
+  pair_ij(f - a.D, i, j);
   return th + a.off_muU + ((int64_t)i * a.D + j) * a.M;
 }
 template <typename T> __device__ inline const T* fac_y(const Args& a, int f) {
   const T* Y = (const T*)a.Y;
   const int D = a.D, M = a.M;
   if (f < D) return Y + (int64_t)f * M;
-  if (f == D) return Y + (int64_t)D * M;
+  if (f == a.NF - 1) return Y + (int64_t)D * M;
   int i, j;
-  pair_ij(f - D - 1, i, j);
+  pair_ij(f - D, i, j);
   const int64_t base = (int64_t)(D + 1) * M + (i == j ? (int64_t)D * D * M : 0);
   return Y + base + ((int64_t)i * D + j) * M;
 }
@@ -353,50 +356,49 @@ __global__ __launch_bounds__(256) void dsvi_kl_kernel(Args a) {
   const T* Af = (const T*)a.Afac;
   T* fb = (T*)a.facbuf;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int b = blockIdx.x;
-  if (b < NF) {
-    const int f = b, k = prior_of(f, D);
-    const T* S = fac_S<T>(a, f);
-    const T* C1 = Af + (int64_t)f * MM;
-    const T* C2 = Af + (int64_t)(NF + k) * MM;
-    const T* mu = fac_mu<T>(a, f);
-    const T* y = fac_y<T>(a, f);
-    T ld1 = 0, ld2 = 0, t2 = 0, t3 = 0;
-    for (int i = w; i < M; i += 4) {
-      const T a1 = row_sq(S, M, i, lane) + lam;
-      if (lane == 0) {
-        const T c2 = C2[(int64_t)i * M + i];
-        ld1 += dlog(C1[(int64_t)i * M + i]);
-        ld2 += dlog(c2);
-        t2 += a1 / (c2 * c2);
-        t3 += mu[i] * y[i];
-      }
-    }
-    ld1 = block_sum(ld1, red);
-    ld2 = block_sum(ld2, red);
-    t2 = block_sum(t2, red);
-    t3 = block_sum(t3, red);
-    if (threadIdx.x == 0) fb[f] = ld2 - ld1 + (T)0.5 * (t2 + t3 - (T)M);
-  } else {
-    const int k = b - NF;
-    const T* C2 = Af + (int64_t)(NF + k) * MM;
-    T* delta = fb + NF + (int64_t)k * M;
-    T* wvec = fb + NF + 4 * (int64_t)M + (int64_t)k * M;
-    for (int i = w; i < M; i += 4) {
+  const int f = blockIdx.x, k = prior_of(f, D);
+  const T* S = fac_S<T>(a, f);
+  const T* C1 = Af + (int64_t)f * MM;
+  const T* C2 = Af + (int64_t)(NF + k) * MM;
+  const T* mu = fac_mu<T>(a, f);
+  const T* y = fac_y<T>(a, f);
+  T* ev = fb + NF + 8 * (int64_t)M + 4 * (int64_t)D * D + (int64_t)f * M;
+  T ld1 = 0, ld2 = 0, t2 = 0, t3 = 0;
+  for (int i = w; i < M; i += 4) {
+    const T a1 = row_sq(S, M, i, lane) + lam;
+    if (lane == 0) {
       const T c2 = C2[(int64_t)i * M + i];
-      const T ic = (T)1 / (c2 * c2);
-      T dl = 0;
-      for (int f = 0; f < NF; ++f) {
-        if (prior_of(f, D) != k) continue;
-        const T a1 = row_sq(fac_S<T>(a, f), M, i, lane) + lam;
-        dl += (T)0.5 - (T)0.5 * a1 * ic;
-      }
-      if (lane == 0) {
-        delta[i] = dl;
-        wvec[i] = ic;
-      }
+      ld1 += dlog(C1[(int64_t)i * M + i]);
+      ld2 += dlog(c2);
+      t2 += a1 / (c2 * c2);
+      t3 += mu[i] * y[i];
+      ev[i] = (T)0.5 - (T)0.5 * a1 / (c2 * c2);   // d KL / d C2_ii * C2_ii / 2 + 1/2
     }
   }
+  ld1 = block_sum(ld1, red);
+  ld2 = block_sum(ld2, red);
+  t2 = block_sum(t2, red);
+  t3 = block_sum(t3, red);
+  if (threadIdx.x == 0) fb[f] = ld2 - ld1 + (T)0.5 * (t2 + t3 - (T)M);
+}
+
+// delta_k[i] = sum over the factors of prior k of e_f[i];  wvec_k[i] = 1 / C2_ii^2
+template <typename T>
+__global__ __launch_bounds__(256) void dsvi_delta_kernel(Args a) {
+  const int M = a.M, D = a.D, NF = a.NF;
+  const int64_t MM = (int64_t)M * M;
+  const int k = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  T* fb = (T*)a.facbuf;
+  const T* C2 = (const T*)a.Afac + (int64_t)(NF + k) * MM;
+  const T* ev = fb + NF + 8 * (int64_t)M + 4 * (int64_t)D * D;
+  T dl = 0;
+  for (int f = 0; f < NF; ++f)
+    if (prior_of(f, D) == k) dl += ev[(int64_t)f * M + i];
+  const T c2 = C2[(int64_t)i * M + i];
+  fb[NF + (int64_t)k * M + i] = dl;
+  fb[NF + 4 * (int64_t)M + (int64_t)k * M + i] = (T)1 / (c2 * c2);
 }
 
 // ------------------------------------------------------------------------------------ t backward
@@ -452,7 +454,7 @@ __global__ __launch_bounds__(1024) void dsvi_vbwd_kernel(Args a) {
     vbs[c] = vb;
   }
   __syncthreads();
-  const T* Cv = (const T*)a.Afac + (int64_t)a.D * M * M;
+  const T* Cv = (const T*)a.Afac + (int64_t)(a.NF - 1) * M * M;
   for (int i = threadIdx.x; i < M; i += blockDim.x) {
     T s = 0;
     for (int k = i; k < M; ++k) s += Cv[(int64_t)k * M + i] * vbs[k];
@@ -491,7 +493,7 @@ __global__ __launch_bounds__(256) void dsvi_finalize_kernel(Args a) {
   T klw = 0, klv = 0, klu = 0;
   for (int f = threadIdx.x; f < NF; f += blockDim.x) {
     const T v = fb[f];
-    if (f < D) klw += v; else if (f == D) klv += v; else klu += v;
+    if (f < D) klw += v; else if (f == NF - 1) klv += v; else klu += v;
   }
   klw = block_sum(klw, red);
   klv = block_sum(klv, red);
@@ -651,7 +653,13 @@ int nmgp_dsvi_recon_f64(const Args* a, hipStream_t s) {
 }
 int nmgp_dsvi_kl_f64(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
-  hipLaunchKernelGGL(nmgp::dsvi_kl_kernel<double>, dim3(a->NF + 4), dim3(256), 0, s, *a);
+  hipLaunchKernelGGL(nmgp::dsvi_kl_kernel<double>, dim3(a->NF), dim3(256), 0, s, *a);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
+int nmgp_dsvi_delta_f64(const Args* a, hipStream_t s) {
+  CHECK_ARGS(a);
+  hipLaunchKernelGGL(nmgp::dsvi_delta_kernel<double>, dim3((unsigned)((a->M + 255) / 256), 4), dim3(256), 0, s, *a);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }

@@ -36,7 +36,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
     dp = &args.descs[lo];
   }
   const nmgp_gemm_desc& d = *dp;
+  __shared__ int s_last;
   tile -= d.tile_start;
+  const int ksplit = d.ksplit > 1 ? d.ksplit : 1;
+  const int ks = tile % ksplit;
+  tile /= ksplit;
   const int tn = tile % d.tiles_n, tm = tile / d.tiles_n;
   int64_t r0 = 0;
   int m = d.m;
@@ -69,11 +73,20 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
     if ((flags & NMGP_B_UPPER) && kbB >= K) kend = min(kend, j0 + GBN);
   }
   kbeg = (kbeg / GBK) * GBK;
-  if (zero_tile) kend = kbeg;
+  if (zero_tile) {
+    if (ks != 0) return;          // one chunk writes the zero tile directly
+    kend = kbeg;
+  } else if (ksplit > 1) {        // this workgroup's k chunk (multiple of GBK)
+    int chunk = (kend - kbeg + ksplit - 1) / ksplit;
+    chunk = ((chunk + GBK - 1) / GBK) * GBK;
+    const int cb = kbeg + ks * chunk;
+    kend = max(cb, min(kend, cb + chunk));
+    kbeg = cb;
+  }
 
   const T* __restrict__ A = (const T*)d.A;
   const T* __restrict__ Bm = (const T*)d.B;
-  const T* __restrict__ ks = (const T*)d.kscale;
+  const T* __restrict__ ksc = (const T*)d.kscale;
   const int t = threadIdx.x;
   const int lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
   const bool a_kc = (d.sA_k == 1);
@@ -111,7 +124,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
         const bool z = ((flags & NMGP_B_LOWER) && gj > kk) || ((flags & NMGP_B_UPPER) && gj < kk);
         if (!z) {
           val = Bm[(k0 + kk) * d.sB_k + (int64_t)gj * d.sB_j + (int64_t)kb * d.sB_kb];
-          if (flags & NMGP_KSCALE) val *= ks[k0 + gk];
+          if (flags & NMGP_KSCALE) val *= ksc[k0 + gk];
         }
       }
       Bs[kl][jl] = val;
@@ -130,6 +143,47 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
       acc11 = Mfma<T>::mma(a1, b1, acc11);
     }
     __syncthreads();
+  }
+
+  if (ksplit > 1 && !zero_tile) {
+    // deterministic split-K: publish this chunk's partial, the last arriver sums all chunks in order
+    T* ws = (T*)d.ws + (int64_t)(tm * d.tiles_n + tn) * ksplit * 4096;
+    T* mine = ws + (int64_t)ks * 4096 + t * 16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      mine[r] = acc00[r];
+      mine[4 + r] = acc01[r];
+      mine[8 + r] = acc10[r];
+      mine[12 + r] = acc11[r];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      int32_t* ctr = d.counters + tm * d.tiles_n + tn;
+      const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (old == ksplit - 1);
+      if (last) {
+        __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    acc00 = acc01 = acc10 = acc11 = acc_t{0, 0, 0, 0};
+    for (int c = 0; c < ksplit; ++c) {
+      const T* src = ws + (int64_t)c * 4096 + t * 16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        acc00[r] += src[r];
+        acc01[r] += src[4 + r];
+        acc10[r] += src[8 + r];
+        acc11[r] += src[12 + r];
+      }
+    }
   }
 
   T* __restrict__ C = (T*)d.C;
@@ -194,6 +248,7 @@ static int launch_single(const nmgp_gemm_desc* h, const int32_t* d_seg, hipStrea
   d.tiles_m = (d.m + GBM - 1) / GBM;
   d.tiles_n = (d.n + GBN - 1) / GBN;
   d.tile_start = 0;
+  d.ksplit = 1;
   GemmArgs a;
   a.descs = nullptr;
   a.nprob = 1;

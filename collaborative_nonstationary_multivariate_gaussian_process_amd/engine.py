@@ -81,7 +81,7 @@ class DsviEngine:
         self.v, self.vbar, self.ellZ = e(M), e(M), e(M)
         self.ellX, self.var_t = e(B), e(B)
         self.rowbuf = e(2 * D + 5, B)
-        self.facbuf = e(NF + 8 * M + 4 * D * D)
+        self.facbuf = e(NF + 8 * M + 4 * D * D + NF * M)
         self.nblk = (B + 3) // 4
         self.red = e(5 * self.nblk)
         self.out = e(8)
@@ -152,8 +152,10 @@ class DsviEngine:
         sW, sv, sU = o["sqrt_W"][0], o["sqrt_v"][0], o["sqrt_U"][0]
         muW, muv, muU, hyp = o["mu_W"][0], o["mu_v"][0], o["mu_U"][0], o["sigma2_tildeell_log"][0]
         pairs = pair_list(D)
-        fac_off = [sW + d * MM for d in range(D)] + [sv] + [sU + (i * D + j) * MM for (i, j) in pairs]
-        prior_of = [3] * D + [0] + [2 if i == j else 1 for (i, j) in pairs]
+        # factor order: W (D) | pairs (Q) | v  -> v and the 3 static priors are contiguous slots NF-1..NF+2
+        fac_off = [sW + d * MM for d in range(D)] + [sU + (i * D + j) * MM for (i, j) in pairs] + [sv]
+        prior_of = [3] * D + [2 if i == j else 1 for (i, j) in pairs] + [0]
+        FV = NF - 1
         dev, seg = self.dev, self.seg
         G = lambda descs: H.GemmGroup(descs, dev, F64, seg=seg)
         g = H.gemm_desc
@@ -167,16 +169,20 @@ class DsviEngine:
             bl.append(H.pairwise_desc(self.Afac[NF + k], self.Z, self.Z, mode=L.RBF, hyp=th, hyp_off=hoff,
                                       hyp_log=True, diag_add=self.jitter))
         p["build_rbf"] = H.PairwiseGroup(bl, dev)
-        # F2: A1_f = tril(S_f) tril(S_f)^T + lam I (lower part)
-        p["syrk"] = G([g(self.Afac, th, th, M, M, M, (M, 1, 0), (1, M, 0), (M, 1),
-                         flags=L.A_LOWER | L.B_UPPER | L.OUT_LOWER, diag_add=self.jitter,
-                         offs=(fac_off[f], fac_off[f], f * MM)) for f in range(NF)])
-        # F5: prior inverses t,0,1 and Xs_f = Cinv_f L_f
+        # F2: A1_f = tril(S_f) tril(S_f)^T + lam I (lower part); v on the main path, the rest on the side stream
+        syrk = lambda f: g(self.Afac, th, th, M, M, M, (M, 1, 0), (1, M, 0), (M, 1),
+                           flags=L.A_LOWER | L.B_UPPER | L.OUT_LOWER, diag_add=self.jitter,
+                           offs=(fac_off[f], fac_off[f], f * MM))
+        xs = lambda f: g(self.Xs, self.Cinv, th, M, M, M, (M, 1, 0), (M, 1, 0), (M, 1),
+                         flags=L.A_LOWER | L.B_LOWER | L.OUT_TRIL, offs=(f * MM, fac_off[f], f * MM))
+        p["syrk"] = G([syrk(FV)])
+        p["syrk_side"] = G([syrk(f) for f in range(FV)])
+        # F5: prior inverses t,0,1 and Xs_f = Cinv_f L_f (KL gradient)
         d5 = [g(self.Ainv, self.Cinv, self.Cinv, M, M, M, (1, M, 0), (M, 1, 0), (M, 1), flags=L.A_UPPER | L.B_LOWER,
                 offs=((NF + k) * MM, (NF + k) * MM, k * MM)) for k in range(3)]
         if not elbo_mode:
-            d5 += [g(self.Xs, self.Cinv, th, M, M, M, (M, 1, 0), (M, 1, 0), (M, 1),
-                     flags=L.A_LOWER | L.B_LOWER | L.OUT_TRIL, offs=(f * MM, fac_off[f], f * MM)) for f in range(NF)]
+            d5.append(xs(FV))
+            p["xs_side"] = G([xs(f) for f in range(FV)])
         p["inv3"] = G(d5)
         # F6: P_k = K12_k Ainv_k (k = t,0,1) ; Y_t, Y_0, Y_1
         d6 = [g(self.P, self.K12, self.Ainv, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), offs=(k * BM, k * MM, k * BM),
@@ -293,9 +299,9 @@ class DsviEngine:
                                 hyp_log=True, scal_part=self.scal_part, offs=(0, 0, 0, 0, 0, 2 * int(so[5])))], dev)
         # B9: v Cholesky backward: grad_sv += Cinv_v^T (Psi Xs_v)
         p["bwd_v1"] = G([g(self.T2, self.phi, self.Xs, M, M, M, (M, 1, 0), (M, 1, 0), (M, 1), flags=L.B_LOWER,
-                           offs=(0, D * MM, 0))])
+                           offs=(0, FV * MM, 0))])
         p["bwd_v2"] = G([g(gr, self.Cinv, self.T2, M, M, M, (1, M, 0), (M, 1, 0), (M, 1),
-                           flags=L.A_UPPER | L.OUT_TRIL, beta=1.0, offs=(D * MM, 0, sv))])
+                           flags=L.A_UPPER | L.OUT_TRIL, beta=1.0, offs=(FV * MM, 0, sv))])
         self._plans[elbo_mode] = p
         return p
 
@@ -329,16 +335,18 @@ class DsviEngine:
         L.check(fn(ctypes.byref(a), s), fn.__name__)
 
     def _schedule(self, elbo_mode, with_kl=True):
-        """The ordered launch list of one step: [(name, kind, callable(stream)), ...]."""
+        """The ordered launch list of one step.  Items are (name, kind, callable(stream), where) with
+        where in {"main", "side"}, plus ("fork",) / ("join",) markers: the D+Q variational factors that
+        only the KL terms need are factored on a side stream, overlapping the forward chain."""
         lib = L.lib()
         D, M, NF = self.D, self.M, self.NF
         MM = M * M
+        FV = NF - 1
         p = self._plan(elbo_mode)
         a = self._args(elbo_mode)
         self._keep_args = getattr(self, "_keep_args", {})
-        self._keep_args[elbo_mode] = a
+        self._keep_args[(elbo_mode, with_kl)] = a
         Af, Ci, info = self.Afac.data_ptr(), self.Cinv.data_ptr(), self.info.data_ptr()
-        gslot = (NF + 3) * MM * 8
         vp = ctypes.c_void_p
 
         def row(fn):
@@ -350,55 +358,93 @@ class DsviEngine:
         def pw(name):
             return lambda s: p[name](F64, s)
 
-        steps = [
-            ("build_rbf", "pairwise", pw("build_rbf")),
-            ("syrk", "gemm", gemm("syrk")),
-            ("potrf", "potrf", lambda s: L.check(lib.nmgp_potrf_batched_f64(vp(Af), M, M, MM, NF + 3, vp(info), s), "potrf")),
-            ("trtri", "trtri", lambda s: L.check(lib.nmgp_trtri_batched_f64(vp(Af), M, M, MM, vp(Ci), M, MM, NF + 3, s), "trtri")),
-            ("inv3", "gemm", gemm("inv3")),
-            ("proj3", "gemm", gemm("proj3")),
-            ("v", "row", row(lib.nmgp_dsvi_hyper_f64)),
-            ("trow", "row", row(lib.nmgp_dsvi_trow_f64)),
-            ("build_gibbs", "pairwise", pw("build_gibbs")),
-            ("potrf_G", "potrf", lambda s: L.check(lib.nmgp_potrf_batched_f64(vp(Af + gslot), M, M, MM, 1, vp(info + (NF + 3) * 4), s), "potrf G")),
-            ("trtri_G", "trtri", lambda s: L.check(lib.nmgp_trtri_batched_f64(vp(Af + gslot), M, M, MM, vp(Ci + gslot), M, MM, 1, s), "trtri G")),
-            ("invG", "gemm", gemm("invG")),
-            ("projG", "gemm", gemm("projG")),
-            ("quad", "gemm", gemm("quad")),
+        def potrf(first, count):
+            return lambda s: L.check(lib.nmgp_potrf_batched_f64(vp(Af + first * MM * 8), M, M, MM, count,
+                                                                vp(info + first * 4), s), "potrf")
+
+        def trtri(first, count):
+            return lambda s: L.check(lib.nmgp_trtri_batched_f64(vp(Af + first * MM * 8), M, M, MM,
+                                                                vp(Ci + first * MM * 8), M, MM, count, s), "trtri")
+
+        need_side = (not elbo_mode) or with_kl
+        steps = []
+        if need_side:
+            steps += [("fork",),
+                      ("syrk_side", "gemm", gemm("syrk_side"), "side"),
+                      ("potrf_side", "potrf", potrf(0, FV), "side"),
+                      ("trtri_side", "trtri", trtri(0, FV), "side")]
+            if not elbo_mode:
+                steps.append(("xs_side", "gemm", gemm("xs_side"), "side"))
+        steps += [
+            ("build_rbf", "pairwise", pw("build_rbf"), "main"),
+            ("syrk", "gemm", gemm("syrk"), "main"),
+            ("potrf", "potrf", potrf(FV, 4), "main"),
+            ("trtri", "trtri", trtri(FV, 4), "main"),
+            ("inv3", "gemm", gemm("inv3"), "main"),
+            ("proj3", "gemm", gemm("proj3"), "main"),
+            ("v", "row", row(lib.nmgp_dsvi_hyper_f64), "main"),
+            ("trow", "row", row(lib.nmgp_dsvi_trow_f64), "main"),
+            ("build_gibbs", "pairwise", pw("build_gibbs"), "main"),
+            ("potrf_G", "potrf", potrf(NF + 3, 1), "main"),
+            ("trtri_G", "trtri", trtri(NF + 3, 1), "main"),
+            ("invG", "gemm", gemm("invG"), "main"),
+            ("projG", "gemm", gemm("projG"), "main"),
+            ("quad", "gemm", gemm("quad"), "main"),
         ]
+        if need_side:
+            steps.append(("join",))
         if elbo_mode:
             if with_kl:
-                steps.append(("kl", "row", row(lib.nmgp_dsvi_kl_f64)))
-            steps += [("recon", "row", row(lib.nmgp_dsvi_recon_f64)),
-                      ("finalize", "row", row(lib.nmgp_dsvi_finalize_f64))]
+                steps.append(("kl", "row", row(lib.nmgp_dsvi_kl_f64), "main"))
+            steps += [("recon", "row", row(lib.nmgp_dsvi_recon_f64), "main"),
+                      ("finalize", "row", row(lib.nmgp_dsvi_finalize_f64), "main")]
             return steps
         steps += [
-            ("kl", "row", row(lib.nmgp_dsvi_kl_f64)),
-            ("recon", "row", row(lib.nmgp_dsvi_recon_f64)),
-            ("bwd_w", "gemm", gemm("bwd_w")),
-            ("bwd_solve", "gemm", gemm("bwd_solve")),
-            ("bwd_kly", "gemm", gemm("bwd_kly")),
-            ("bwd_pr", "gemm", gemm("bwd_pr")),
-            ("bwd_build", "pairwise_bwd", pw("bwd_build")),
-            ("tbwd", "row", row(lib.nmgp_dsvi_tbwd_f64)),
-            ("bwd_t1", "gemm", gemm("bwd_t1")),
-            ("bwd_t2", "gemm", gemm("bwd_t2")),
-            ("bwd_tbuild", "pairwise_bwd", pw("bwd_tbuild")),
-            ("vbwd", "row", row(lib.nmgp_dsvi_vbwd_f64)),
-            ("bwd_v1", "gemm", gemm("bwd_v1")),
-            ("bwd_v2", "gemm", gemm("bwd_v2")),
-            ("finalize", "row", row(lib.nmgp_dsvi_finalize_f64)),
+            ("kl", "row", row(lib.nmgp_dsvi_kl_f64), "main"),
+            ("delta", "row", row(lib.nmgp_dsvi_delta_f64), "main"),
+            ("recon", "row", row(lib.nmgp_dsvi_recon_f64), "main"),
+            ("bwd_w", "gemm", gemm("bwd_w"), "main"),
+            ("bwd_solve", "gemm", gemm("bwd_solve"), "main"),
+            ("bwd_kly", "gemm", gemm("bwd_kly"), "main"),
+            ("bwd_pr", "gemm", gemm("bwd_pr"), "main"),
+            ("bwd_build", "pairwise_bwd", pw("bwd_build"), "main"),
+            ("tbwd", "row", row(lib.nmgp_dsvi_tbwd_f64), "main"),
+            ("bwd_t1", "gemm", gemm("bwd_t1"), "main"),
+            ("bwd_t2", "gemm", gemm("bwd_t2"), "main"),
+            ("bwd_tbuild", "pairwise_bwd", pw("bwd_tbuild"), "main"),
+            ("vbwd", "row", row(lib.nmgp_dsvi_vbwd_f64), "main"),
+            ("bwd_v1", "gemm", gemm("bwd_v1"), "main"),
+            ("bwd_v2", "gemm", gemm("bwd_v2"), "main"),
+            ("finalize", "row", row(lib.nmgp_dsvi_finalize_f64), "main"),
         ]
         return steps
 
     def _run(self, steps, stream, timer):
-        s = stream if stream is not None else L.stream_handle()
-        for name, kind, fn in steps:
+        main = stream if stream is not None else torch.cuda.current_stream(self.dev)
+        s_main = ctypes.c_void_p(main.cuda_stream)
+        if timer is None:
+            if getattr(self, "_side", None) is None:
+                self._side = torch.cuda.Stream(device=self.dev)
+            s_side = ctypes.c_void_p(self._side.cuda_stream)
+        for item in steps:
+            if len(item) == 1:
+                if timer is not None:
+                    continue                       # timed runs are serial on one stream
+                ev = torch.cuda.Event()
+                if item[0] == "fork":
+                    ev.record(main)
+                    self._side.wait_event(ev)
+                else:
+                    ev.record(self._side)
+                    main.wait_event(ev)
+                continue
+            name, kind, fn, where = item
             if timer is not None:
                 timer.start(name, kind)
-            fn(s)
-            if timer is not None:
+                fn(s_main)
                 timer.stop(name, kind)
+            else:
+                fn(s_side if where == "side" else s_main)
 
     def forward_backward(self, stream=None, timer=None):
         """Enqueue -SELBO (self.out[0]) and all gradients (into the bound grad vector)."""
@@ -413,13 +459,18 @@ class DsviEngine:
     def elbo_sample(self, stream=None, with_kl=False):
         """Enqueue one Monte-Carlo sample of compute_ELBO's reconstruction term (self.out[1]);
         with_kl also evaluates the KL terms from THIS sample's K_G22 (out[2..4])."""
-        self._run(self._schedule(1, with_kl), stream, None)
+        key = ("elbo", with_kl, self._theta.data_ptr(), self.frozen_mask, self.N)
+        cache = getattr(self, "_elbo_sched", {})
+        if key not in cache:
+            cache[key] = self._schedule(1, with_kl)
+            self._elbo_sched = cache
+        self._run(cache[key], stream, None)
         return self.out
 
     def gemm_groups(self):
         """(name, GemmGroup) of the training step, for FLOP accounting."""
         p = self._plan(0)
-        return [(n, p[n]) for n, k, _ in self._schedule(0) if k == "gemm"]
+        return [(it[0], p[it[0]]) for it in self._schedule(0) if len(it) > 1 and it[1] == "gemm"]
 
     def check_info(self):
         info = self.info.cpu()

@@ -61,14 +61,29 @@ def gemm_desc(C, A, B, m, n, k, sA, sB, sC, *, flags=0, alpha=1.0, beta=0.0, kb=
 class GemmGroup:
     """A fixed list of GEMM problems launched as ONE grouped kernel (descriptors uploaded once)."""
 
-    def __init__(self, descs, device, dtype, seg=None):
+    def __init__(self, descs, device, dtype, seg=None, target_wgs=512):
+        """Split-K is chosen per problem so that the launch has ~target_wgs workgroups when the
+        outputs alone are too few tiles (the M x B x M products P^T R with K = B)."""
         self.dtype = dtype
         self.seg = seg
         arr = (L.GemmDesc * len(descs))()
+        group_tiles = sum(d.tiles_m * d.tiles_n for d in descs)
+        esz = 8 if dtype == _F64 else 4
+        self._ws = []
         t = 0
         for i, d in enumerate(descs):
+            if d.ksplit <= 1 and d.k >= 256:
+                d.ksplit = max(1, min(16, d.k // 128, -(-target_wgs // max(group_tiles, 1))))
+            if d.ksplit > 1:
+                ntile = d.tiles_m * d.tiles_n
+                ws = torch.empty(ntile * d.ksplit * 4096, dtype=dtype, device=device)
+                ctr = torch.zeros(ntile, dtype=torch.int32, device=device)
+                self._ws += [ws, ctr]
+                d.ws, d.counters = ws.data_ptr(), ctr.data_ptr()
+            else:
+                d.ksplit = 1
             d.tile_start = t
-            t += d.tiles_m * d.tiles_n
+            t += d.tiles_m * d.tiles_n * d.ksplit
             arr[i] = d
         self.total = t
         self.n = len(descs)

@@ -67,6 +67,13 @@ typedef struct nmgp_gemm_desc {
   double alpha, beta, gamma, diag_add;
   int32_t tiles_m, tiles_n, tile_start;
   int32_t seg_span;      /* row_seg / k_seg cover seg[s] .. seg[s + max(seg_span,1)] */
+  /* split-K: ksplit > 1 cuts the k range into ksplit chunks; each chunk's 64x64 partial goes to
+   * ws (tiles_m*tiles_n*ksplit*4096 elements) and the last-arriving chunk of a tile (counter in
+   * `counters`, tiles_m*tiles_n zero-initialised int32, reset by the kernel) sums them in chunk
+   * order -- deterministic -- and applies the epilogue.  tiles = tiles_m*tiles_n*ksplit.        */
+  int32_t ksplit, pad2_;
+  void* ws;
+  int32_t* counters;
 } nmgp_gemm_desc;
 
 /* d_desc: device array of nprob descriptors (tiles_m/tiles_n/tile_start filled by the host,
@@ -185,7 +192,7 @@ typedef struct nmgp_dsvi_args {
   void* Xs;                   /* (NF, M, M) scratch: Cinv_f * L_f                              */
   void* v; void* vbar; void* ellZ; void* ellX; void* var_t;   /* (M),(M),(M),(B),(B)          */
   void* rowbuf;               /* (2D+5, B) per-row adjoints                                     */
-  void* facbuf;               /* KL (NF) | delta (4,M) | wvec (4,M) | sel (4, D*D)             */
+  void* facbuf;               /* KL (NF) | delta (4,M) | wvec (4,M) | sel (4,D*D) | e (NF,M)   */
   void* red;                  /* per-block partial sums                                        */
   void* out;                  /* [0] loss [1] SELBO_R [2] KL_W [3] KL_v [4] KL_U               */
   void* gib_row; void* gib_col; void* scal_part; void* phi;
@@ -198,6 +205,7 @@ int nmgp_dsvi_hyper_f64(const nmgp_dsvi_args* a, hipStream_t s);      /* hyper v
 int nmgp_dsvi_trow_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* t-row forward             */
 int nmgp_dsvi_recon_f64(const nmgp_dsvi_args* a, hipStream_t s);      /* recon + per-row adjoints  */
 int nmgp_dsvi_kl_f64(const nmgp_dsvi_args* a, hipStream_t s);         /* KL per factor + e-vectors */
+int nmgp_dsvi_delta_f64(const nmgp_dsvi_args* a, hipStream_t s);      /* prior diag adjoints delta, w */
 int nmgp_dsvi_tbwd_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* t-row backward            */
 int nmgp_dsvi_vbwd_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* v backward -> Phi         */
 int nmgp_dsvi_finalize_f64(const nmgp_dsvi_args* a, hipStream_t s);   /* loss + scalar gradients   */

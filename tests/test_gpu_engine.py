@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 CASES = {  # name: (D, M, loss rtol, grad rel-norm tol)
     "toy_forward": (2, 20, 1e-11, 1e-8),
-    "modelpt_forward": (2, 20, 1e-9, 1e-7),     # trained state: cond(K22) larger
+    "modelpt_forward": (2, 20, 1e-9, 1e-6),     # trained state: larger cond(K22), cancelling d/dsigma2_L1
     "mid_forward": (3, 64, 1e-11, 1e-8),
     "pm25_forward": (5, 256, 1e-9, 1e-6),
 }
@@ -85,7 +85,7 @@ def test_engine_intermediates_vs_mirror():
         "P_t": (eng.P[0], it["P"]["t"]), "P_0": (eng.P[1], it["P"]["0"]), "P_1": (eng.P[2], it["P"]["1"]),
         "Ainv_t": (eng.Ainv[0], it["Ainv"]["t"]), "v": (eng.v, it["v"]), "ellX": (eng.ellX, it["ellX"]),
         "K_G12": (eng.K12[3], it["KG12"]), "Ainv_G": (eng.Ainv[3], it["Ainv"]["G"]), "P_G": (eng.P[3], it["P"]["G"]),
-        "KL": (eng.facbuf[:eng.NF], it["KL"]), "R_G": (eng.R[3], it["Rm"]["G"]), "R_0": (eng.R[1], it["Rm"]["0"]),
+        "KL": (eng.facbuf[:eng.NF], torch.cat([it["KL"][:D], it["KL"][D + 1:], it["KL"][D:D + 1]])), "R_G": (eng.R[3], it["Rm"]["G"]), "R_0": (eng.R[1], it["Rm"]["0"]),
         "R_t": (eng.R[0], it["Rm"]["t"]), "Abar_G": (eng.Abar[3], it["Abar"]["G"]), "Abar_0": (eng.Abar[1], it["Abar"]["0"]),
         "Abar_t": (eng.Abar[0], it["Abar"]["t"]), "Pbar_G": (eng.Pbar[3], it["Pbar"]["G"]),
         "Pbar_0": (eng.Pbar[1], it["Pbar"]["0"]), "Pbar_t": (eng.Pbar[0], it["Pbar"]["t"]),

@@ -102,6 +102,30 @@ def test_gemm_kblocks_and_segments_grouped(ops):
     assert rel(out3, ref3) < 1e-14
 
 
+@pytest.mark.parametrize("K", [300, 2000, 4099])
+def test_gemm_split_k_deterministic(ops, K):
+    """Long-k products P^T R (few output tiles) take the split-K path; results are bit-identical
+    across launches (fixed-order reduction of the chunk partials)."""
+    g = torch.Generator().manual_seed(K)
+    M = 100
+    P = torch.randn(K, M, generator=g, dtype=F64)
+    R = torch.randn(K, M, generator=g, dtype=F64)
+    C0 = torch.randn(M, M, generator=g, dtype=F64)
+    Pd, Rd = P.to(DEV), R.to(DEV)
+    outs = []
+    for rep in range(3):
+        C = C0.clone().to(DEV)
+        d = ops.gemm_desc(C, Pd, Rd, M, M, K, (1, M, 0), (M, 1, 0), (M, 1), alpha=-1.0, beta=1.0)
+        grp = ops.GemmGroup([d], DEV, F64)
+        assert grp.descs[0].ksplit > 1
+        grp()
+        grp()          # counters were reset by the last arrivers: a second launch is valid too
+        outs.append(C.cpu())
+    ref = C0 - 2 * P.t() @ R
+    assert rel(outs[0], ref) < 1e-13
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+
+
 def _spd(n, batch, seed, cond_shift=0.1):
     g = torch.Generator().manual_seed(seed)
     G = torch.randn(batch, n, n + 3, generator=g, dtype=F64)
