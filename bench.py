@@ -231,6 +231,21 @@ def main():
         breakdown = {k: round(v, 4) for k, v in sorted(per_kind.items(), key=lambda kv: -kv[1])}
         breakdown_names = {k: round(v, 4) for k, v in sorted(per_name.items(), key=lambda kv: -kv[1])}
 
+    if roofline is not None:
+        # HBM traffic of the dominant kernel from the committed rocprofv3 PMC passes (FETCH_SIZE x2 per the
+        # gfx950 calibration note + WRITE_SIZE), averaged per launch; tools/pmc_summary.py writes them.
+        import glob
+        summaries = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pm25_bench_summary.json")))
+        if summaries:
+            with open(summaries[-1]) as fh:
+                ks = json.load(fh)["kernels"]
+            gk = [k for k in ks if k["name"].startswith("void nmgp::gemm_kernel<double>")]
+            if gk and "hbm_write_bytes_per_launch" in gk[0]:
+                roofline["traffic"] = int(gk[0]["hbm_read_bytes_per_launch_x2corrected"] +
+                                          gk[0]["hbm_write_bytes_per_launch"])
+                roofline["traffic_unit"] = "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
+                roofline["traffic_source"] = os.path.relpath(summaries[-1], ROOT)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds, xs, ys, z)
