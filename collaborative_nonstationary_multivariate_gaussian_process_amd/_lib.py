@@ -85,6 +85,8 @@ _SIGS = {
     "nmgp_potrf_batched_f32": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "nmgp_trtri_batched_f64": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp]),
     "nmgp_trtri_batched_f32": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp]),
+    "nmgp_chol_inv_batched_f64": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "nmgp_chol_inv_batched_f32": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "nmgp_pairwise_f64": (c_int, [c_vp, c_int, c_int, c_vp]),
     "nmgp_pairwise_f32": (c_int, [c_vp, c_int, c_int, c_vp]),
     "nmgp_pairwise_single_f64": (c_int, [ctypes.POINTER(PairwiseDesc), c_vp]),

@@ -4,19 +4,31 @@
 // (code/utils.py:46,119,276,347-348): the 4 priors K22 + 1e-4 I and the D+1+Q variational
 // covariances tril(S) tril(S)^T + 1e-4 I (code/nmgp_dsvi.py:172-177, KL at :266-295).
 //
-// Right-looking, 16-wide blocks:
-//   phase 1  (wave 0)   the 16x16 diagonal block is factored (and inverted) in registers with
-//                       wave shuffles: lane l holds row l&15, columns (l>>4)+4r  -- no LDS,
-//                       no barriers inside the block;
-//   phase 2  (4 waves)  panel  L[ib,kb] = A[ib,kb] * Lkk^-T  on the matrix cores, staged in LDS;
-//   phase 3  (4 waves)  trailing SYRK A[ib,jb] -= L[ib,kb] L[jb,kb]^T, one 16x16 MFMA tile per
-//                       wave step, operands from the LDS panel.
-// trtri runs the same three phases on L X = I (X = L^-1), block row by block row.
+// Right-looking, 16-wide blocks, 16 waves (1024 threads) per matrix:
+//   phase 1  (wave 0)   the 16x16 diagonal block is factored in registers with wave shuffles:
+//                       lane l holds row l&15, columns (l>>4)+4r -- no LDS, no barriers inside;
+//   phase 2  (1 thread  panel  L[i,kb] = A[i,kb] L_kk^-T  by forward substitution, one thread per
+//             per row)  row with L_kk broadcast from LDS, result staged in LDS;
+//   phase 3  (16 waves) trailing SYRK A[ib,jb] -= L[ib,kb] L[jb,kb]^T on the matrix cores, four
+//                       16x16 tiles in flight per wave so their global round trips overlap.
+// trtri inverts all diagonal blocks first (one wave each, in parallel), then sweeps block rows:
+// X[kb,:] = L_kk^-1 R[kb,:] and R[ib,:] -= L[ib,kb] X[kb,:] for ib > kb, again 4 tiles per wave.
 #include "common.hpp"
 
 namespace nmgp {
 
-constexpr int CP = 17;  // LDS pitch (elements) of the 16-wide panel: conflict-free ds_read_b64
+constexpr int CP = 17;
+
+#ifdef NMGP_CHOL_TRACE  // phase timestamps for tools/chol_probe.hip (never set in the library build)
+__device__ unsigned long long* g_chol_trace;
+#define CHOL_STAMP(kb, p) \
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_chol_trace[(kb) * 4 + (p)] = wall_clock64()
+#define CHOL_STAMPW(kb, p) \
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_chol_trace[512 + (kb) * 4 + (p)] = wall_clock64()
+#else
+#define CHOL_STAMP(kb, p)
+#define CHOL_STAMPW(kb, p)
+#endif  // LDS pitch (elements) of the 16-wide panel: conflict-free ds_read_b64
 
 // Factor the 16x16 diagonal block held in a[4] (lane l: row l&15, col (l>>4)+4r) in place and
 // return its inverse in x[4] (same layout). fail gets the 1-based first bad pivot, or 0.
@@ -78,18 +90,26 @@ __device__ inline void tri_decode(int tt, int& a, int& b) {
   b = tt - r * (r + 1) / 2;
 }
 
+// 1024 threads (16 waves) per matrix.  Phase 3 work is issued in batches of 4 tiles per wave so
+// four global round trips overlap; the panel is a row-wise forward substitution (one thread per
+// row, L_kk broadcast from LDS) instead of a diagonal-block inverse + MFMA.
+constexpr int CW = 16;         // waves per workgroup
+constexpr int CT = CW * 64;     // threads
+
 template <typename T>
-__global__ __launch_bounds__(256) void potrf_kernel(T* A, int n, int64_t lda, int64_t strideA, int32_t* info) {
+__global__ __launch_bounds__(CT) void potrf_kernel(T* A, int n, int64_t lda, int64_t strideA, int32_t* info) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int nt = (n + 15) >> 4;
-  T* Linv = (T*)smem_raw;          // 16 x CP
-  T* Ps = Linv + 16 * CP;          // (nt*16) x CP  panel
+  T* Lkk = (T*)smem_raw;           // 16 x CP  factored diagonal block
+  T* idg = Lkk + 16 * CP;          // 16       1 / L_jj
+  T* Ps = idg + 16;                // (nt*16) x CP  panel (rows of the current block column)
   int* s_fail = (int*)(Ps + nt * 16 * CP);
   T* Am = A + (int64_t)blockIdx.x * strideA;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   if (t == 0) *s_fail = 0;
   __syncthreads();
   for (int kb = 0; kb < nt; ++kb) {
+    CHOL_STAMP(kb, 0);
     if (w == 0) {
       const int i = lane & 15;
       const int gi = kb * 16 + i;
@@ -101,65 +121,91 @@ __global__ __launch_bounds__(256) void potrf_kernel(T* A, int n, int64_t lda, in
       }
       int fail = 0;
       chol16(a, x, lane, kb * 16, n, fail);
-      trinv16(a, x, lane);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int c = (lane >> 4) + 4 * r;
         const int gc = kb * 16 + c;
         if (gi < n && gc < n) Am[(int64_t)gi * lda + gc] = a[r];
-        Linv[i * CP + c] = x[r];
+        Lkk[i * CP + c] = a[r];
+        if (c == i) idg[i] = (T)1 / a[r];
       }
       if (lane == 0 && fail && *s_fail == 0) *s_fail = fail;
     }
     __syncthreads();
-    // phase 2: panel below the diagonal block
-    for (int ib = kb + 1 + w; ib < nt; ib += 4) {
-      typename Mfma<T>::acc_t acc = {0, 0, 0, 0};
-      const int gi = ib * 16 + (lane & 15);
+    CHOL_STAMP(kb, 1);
+    // phase 2: panel rows below the diagonal block solve x L_kk^T = a, one thread per row.  Loads
+    // are clamped in-bounds and masked (per-element branches here cost ~100 VGPRs of spills);
+    // the panel goes to global memory from LDS, coalesced, at the start of phase 3.
+    {
+      const int gi = (kb + 1) * 16 + t;
+      if (gi < nt * 16) {
+        T x[16];
+        const int64_t ro = (int64_t)min(gi, n - 1) * lda;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int kr = 4 * s + (lane >> 4);
-        const int gk = kb * 16 + kr;
-        const T av = (gi < n && gk < n) ? Am[(int64_t)gi * lda + gk] : (T)0;
-        const T bv = Linv[(lane & 15) * CP + kr];
-        acc = Mfma<T>::mma(av, bv, acc);
-      }
+        for (int c = 0; c < 16; ++c) {
+          const int gc = kb * 16 + c;
+          const T v = Am[ro + min(gc, n - 1)];
+          x[c] = (gi < n && gc < n) ? v : (T)0;
+        }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = Mfma<T>::row(lane, r), col = lane & 15;
-        const int gr = ib * 16 + row, gc = kb * 16 + col;
-        if (gr < n && gc < n) Am[(int64_t)gr * lda + gc] = acc[r];
-        Ps[(ib * 16 + row) * CP + col] = acc[r];
+        for (int j = 0; j < 16; ++j) {
+          T acc = x[j];
+#pragma unroll
+          for (int c = 0; c < 15; ++c)
+            if (c < j) acc -= x[c] * Lkk[j * CP + c];
+          x[j] = acc * idg[j];
+        }
+#pragma unroll
+        for (int c = 0; c < 16; ++c) Ps[gi * CP + c] = x[c];
       }
     }
     __syncthreads();
-    // phase 3: trailing lower-triangular update
+    CHOL_STAMP(kb, 2);
+    // phase 3: trailing lower-triangular SYRK, 4 tiles in flight per wave
     const int S = nt - kb - 1;
     const int ntile = S * (S + 1) / 2;
-    for (int tt = w; tt < ntile; tt += 4) {
-      int ibo, jbo;
-      tri_decode(tt, ibo, jbo);
-      const int ib = kb + 1 + ibo, jb = kb + 1 + jbo;
-      typename Mfma<T>::acc_t acc;
+    for (int idx = t; idx < S * 256; idx += CT) {
+      const int gi = (kb + 1) * 16 + (idx >> 4), gc = kb * 16 + (idx & 15);
+      if (gi < n && gc < n) Am[(int64_t)gi * lda + gc] = Ps[gi * CP + (idx & 15)];
+    }
+    for (int base = w; base < ntile; base += CW * 4) {
+      typename Mfma<T>::acc_t acc[4];
+      int ibs[4], jbs[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gr = ib * 16 + Mfma<T>::row(lane, r), gc = jb * 16 + (lane & 15);
-        acc[r] = (gr < n && gc < n) ? Am[(int64_t)gr * lda + gc] : (T)0;
+      for (int u = 0; u < 4; ++u) {
+        const int tt = base + u * CW;
+        ibs[u] = -1;
+        if (tt < ntile) {
+          int ibo, jbo;
+          tri_decode(tt, ibo, jbo);
+          ibs[u] = kb + 1 + ibo;
+          jbs[u] = kb + 1 + jbo;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int gr = ibs[u] * 16 + Mfma<T>::row(lane, r), gc = jbs[u] * 16 + (lane & 15);
+            acc[u][r] = (gr < n && gc < n) ? Am[(int64_t)gr * lda + gc] : (T)0;
+          }
+        }
       }
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int kr = 4 * s + (lane >> 4);
-        const T av = Ps[(ib * 16 + (lane & 15)) * CP + kr];
-        const T bv = Ps[(jb * 16 + (lane & 15)) * CP + kr];
-        acc = Mfma<T>::mma(-av, bv, acc);
-      }
+      for (int u = 0; u < 4; ++u) {
+        if (ibs[u] < 0) continue;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gr = ib * 16 + Mfma<T>::row(lane, r), gc = jb * 16 + (lane & 15);
-        if (gr < n && gc < n) Am[(int64_t)gr * lda + gc] = acc[r];
+        for (int s = 0; s < 4; ++s) {
+          const int kr = 4 * s + (lane >> 4);
+          const T av = Ps[(ibs[u] * 16 + (lane & 15)) * CP + kr];
+          const T bv = Ps[(jbs[u] * 16 + (lane & 15)) * CP + kr];
+          acc[u] = Mfma<T>::mma(-av, bv, acc[u]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gr = ibs[u] * 16 + Mfma<T>::row(lane, r), gc = jbs[u] * 16 + (lane & 15);
+          if (gr < n && gc < n) Am[(int64_t)gr * lda + gc] = acc[u][r];
+        }
       }
     }
     __syncthreads();
+    CHOL_STAMP(kb, 3);
   }
   for (int64_t idx = t; idx < (int64_t)n * n; idx += blockDim.x) {
     const int i = (int)(idx / n), j = (int)(idx - (int64_t)i * n);
@@ -168,13 +214,15 @@ __global__ __launch_bounds__(256) void potrf_kernel(T* A, int n, int64_t lda, in
   if (t == 0 && info) info[blockIdx.x] = *s_fail;
 }
 
+// X = L^{-1}: all diagonal-block inverses first (one wave each, in parallel), then block rows
+// kb = 0..nt-1:  X[kb, jb] = Li_kk R[kb, jb]  (R accumulated in X),  R[ib, jb] -= L[ib, kb] X[kb, jb].
 template <typename T>
-__global__ __launch_bounds__(256) void trtri_kernel(const T* L, int n, int64_t ldl, int64_t strideL, T* X, int64_t ldx,
-                                                    int64_t strideX) {
+__global__ __launch_bounds__(CT) void trtri_kernel(const T* L, int n, int64_t ldl, int64_t strideL, T* X, int64_t ldx,
+                                                   int64_t strideX) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int nt = (n + 15) >> 4;
-  T* Li = (T*)smem_raw;       // 16 x CP
-  T* Xrow = Li + 16 * CP;     // nt tiles of 16x16 (row-major, pitch 16)
+  T* Li = (T*)smem_raw;            // nt x (16 x CP) diagonal-block inverses
+  T* Xrow = Li + nt * 16 * CP;     // nt tiles of 16x16 (row-major, pitch 16): block row kb of X
   const T* Lm = L + (int64_t)blockIdx.x * strideL;
   T* Xm = X + (int64_t)blockIdx.x * strideX;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -182,32 +230,32 @@ __global__ __launch_bounds__(256) void trtri_kernel(const T* L, int n, int64_t l
     const int i = (int)(idx / n), j = (int)(idx - (int64_t)i * n);
     Xm[(int64_t)i * ldx + j] = 0;
   }
+  for (int kb = w; kb < nt; kb += CW) {
+    const int i = lane & 15, gi = kb * 16 + i;
+    T a[4], x[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gc = kb * 16 + (lane >> 4) + 4 * r;
+      a[r] = (gi < n && gc < n && gc <= gi) ? Lm[(int64_t)gi * ldl + gc] : (gi == gc ? (T)1 : (T)0);
+    }
+    trinv16(a, x, lane);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Li[(kb * 16 + i) * CP + (lane >> 4) + 4 * r] = x[r];
+  }
   __syncthreads();
   for (int kb = 0; kb < nt; ++kb) {
-    if (w == 0) {
-      const int i = lane & 15, gi = kb * 16 + i;
-      T a[4], x[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gc = kb * 16 + (lane >> 4) + 4 * r;
-        a[r] = (gi < n && gc < n && gc <= gi) ? Lm[(int64_t)gi * ldl + gc] : (gi == gc ? (T)1 : (T)0);
-      }
-      trinv16(a, x, lane);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Li[i * CP + (lane >> 4) + 4 * r] = x[r];
-    }
-    __syncthreads();
-    for (int jb = w; jb <= kb; jb += 4) {
+    const T* Lik = Li + kb * 16 * CP;
+    for (int jb = w; jb <= kb; jb += CW) {
       typename Mfma<T>::acc_t acc = {0, 0, 0, 0};
       if (jb == kb) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r] = Li[Mfma<T>::row(lane, r) * CP + (lane & 15)];
+        for (int r = 0; r < 4; ++r) acc[r] = Lik[Mfma<T>::row(lane, r) * CP + (lane & 15)];
       } else {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           const int kr = 4 * s + (lane >> 4);
           const int gk = kb * 16 + kr, gj = jb * 16 + (lane & 15);
-          const T av = Li[(lane & 15) * CP + kr];
+          const T av = Lik[(lane & 15) * CP + kr];
           const T bv = (gk < n && gj < n) ? Xm[(int64_t)gk * ldx + gj] : (T)0;
           acc = Mfma<T>::mma(av, bv, acc);
         }
@@ -221,41 +269,287 @@ __global__ __launch_bounds__(256) void trtri_kernel(const T* L, int n, int64_t l
       }
     }
     __syncthreads();
-    const int nr = nt - kb - 1, nc = kb + 1;
-    for (int tt = w; tt < nr * nc; tt += 4) {
-      const int ib = kb + 1 + tt / nc, jb = tt % nc;
-      typename Mfma<T>::acc_t acc;
+    const int nr = nt - kb - 1, nc = kb + 1, ntile = nr * nc;
+    for (int base = w; base < ntile; base += CW * 4) {
+      typename Mfma<T>::acc_t acc[4];
+      int ibs[4], jbs[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gr = ib * 16 + Mfma<T>::row(lane, r), gc = jb * 16 + (lane & 15);
-        acc[r] = (gr < n && gc < n) ? Xm[(int64_t)gr * ldx + gc] : (T)0;
+      for (int u = 0; u < 4; ++u) {
+        const int tt = base + u * CW;
+        ibs[u] = -1;
+        if (tt < ntile) {
+          ibs[u] = kb + 1 + tt / nc;
+          jbs[u] = tt % nc;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int gr = ibs[u] * 16 + Mfma<T>::row(lane, r), gc = jbs[u] * 16 + (lane & 15);
+            acc[u][r] = (gr < n && gc < n) ? Xm[(int64_t)gr * ldx + gc] : (T)0;
+          }
+        }
       }
-      const int gi = ib * 16 + (lane & 15);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int kr = 4 * s + (lane >> 4);
-        const int gk = kb * 16 + kr;
-        const T av = (gi < n && gk < n) ? Lm[(int64_t)gi * ldl + gk] : (T)0;
-        const T bv = Xrow[(jb * 16 + kr) * 16 + (lane & 15)];
-        acc = Mfma<T>::mma(-av, bv, acc);
-      }
+      for (int u = 0; u < 4; ++u) {
+        if (ibs[u] < 0) continue;
+        const int gi = ibs[u] * 16 + (lane & 15);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gr = ib * 16 + Mfma<T>::row(lane, r), gc = jb * 16 + (lane & 15);
-        if (gr < n && gc < n) Xm[(int64_t)gr * ldx + gc] = acc[r];
+        for (int s = 0; s < 4; ++s) {
+          const int kr = 4 * s + (lane >> 4);
+          const int gk = kb * 16 + kr;
+          const T av = (gi < n && gk < n) ? Lm[(int64_t)gi * ldl + gk] : (T)0;
+          const T bv = Xrow[(jbs[u] * 16 + kr) * 16 + (lane & 15)];
+          acc[u] = Mfma<T>::mma(-av, bv, acc[u]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gr = ibs[u] * 16 + Mfma<T>::row(lane, r), gc = jbs[u] * 16 + (lane & 15);
+          if (gr < n && gc < n) Xm[(int64_t)gr * ldx + gc] = acc[u][r];
+        }
       }
     }
     __syncthreads();
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused register-resident factor + inverse for n <= 256:  A -> L (in place),  X = L^{-1}.
+//
+// Every 16x16 lower tile (ib >= jb) lives in the accumulator registers of one wave for the whole
+// kernel (tile tt = w + 8u of the row-major lower-triangle order), so the trailing updates never
+// touch global memory.  A tile serves potrf until its block column jb is factored, then the same
+// registers hold the trtri remainder R[ib,jb] (initialised to I or 0), which is exactly the set of
+// tiles the right-looking trtri sweep touches at step kb >= jb.  Step kb:
+//   1. owners of block column kb spill it to LDS (colbuf) and reset the registers to R = 0;
+//   2. every wave factors the 16x16 diagonal block redundantly, one row per lane (lanes 0..15),
+//      broadcasting L_cj with v_readlane (no LDS, no barriers) while lanes 16..63 forward-solve
+//      their panel rows against it; 16 identity rows on the last wave give L_kk^-T;
+//   3. X[kb,:] = L_kk^-1 R[kb,:]  (the accumulator IS the MFMA B operand), then the potrf SYRK
+//      A[ib,jb] -= L[ib,kb] L[jb,kb]^T and the trtri update R[ib,jb] -= L[ib,kb] X[kb,jb], operands
+//      from LDS.  L and X leave through coalesced row copies of the LDS staging buffers.
+// The MFMA k-index of lane l in slice s is row(l, s), which makes the accumulator layout equal to
+// the B-operand layout for both f64 and f32.
+constexpr int RW = 8;  // waves per workgroup of the register-resident kernel
+
+template <typename T> __device__ inline T readlane(T v, int l);
+template <> __device__ inline double readlane<double>(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <> __device__ inline float readlane<float>(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// 1/sqrt(d): hardware estimate + Newton steps (2 for f64, 1 for f32) -> correctly rounded to ~1 ulp.
+template <typename T> __device__ inline T rsq_nr(T d);
+template <> __device__ inline double rsq_nr<double>(double d) {
+  double y = __builtin_amdgcn_rsq(d);
+#ifndef NMGP_RSQ_ONE_STEP
+  double h = d * y, r = fma(-h, y, 1.0);
+  y = fma(0.5 * y, r, y);
+  h = d * y;
+  r = fma(-h, y, 1.0);
+#else
+  const double h = d * y, r = fma(-h, y, 1.0);
+#endif
+  return fma(0.5 * y, r, y);
+}
+template <> __device__ inline float rsq_nr<float>(float d) {
+  const float y = __builtin_amdgcn_rsqf(d);
+  const float h = d * y, r = fmaf(-h, y, 1.0f);
+  return fmaf(0.5f * y, r, y);
+}
+
+template <typename T, int NTPW>
+__global__ __launch_bounds__(RW * 64) void chol_inv_kernel(T* A, int n, int64_t lda, int64_t strideA, T* X,
+                                                           int64_t ldx, int64_t strideX, int32_t* info) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  using acc_t = typename Mfma<T>::acc_t;
+  const int nt = (n + 15) >> 4, NR = nt * 16;
+  T* colbuf = (T*)smem_raw;   // NR x CP : block column kb before the panel step (local rows)
+  T* Ps = colbuf + NR * CP;   // NR x CP : L[:, kb] (local rows, diagonal block first)
+  T* Xrow = Ps + NR * CP;     // nt tiles x 16 rows x CP : X[kb, jb]
+  T* LiT = Xrow + NR * CP;    // 16 x CP : (L_kk^-1)^T
+  T* Am = A + (int64_t)blockIdx.x * strideA;
+  T* Xm = X + (int64_t)blockIdx.x * strideX;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int ntiles = nt * (nt + 1) / 2;
+  int ib[NTPW], jb[NTPW];
+  acc_t acc[NTPW];
+  int first_fail = 0;
+#pragma unroll
+  for (int u = 0; u < NTPW; ++u) {
+    const int tt = w + RW * u;
+    ib[u] = -1;
+    jb[u] = -1;
+    if (tt < ntiles) {
+      tri_decode(tt, ib[u], jb[u]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gr = ib[u] * 16 + Mfma<T>::row(lane, r), gc = jb[u] * 16 + (lane & 15);
+        const T v = Am[(int64_t)min(gr, n - 1) * lda + min(gc, n - 1)];
+        acc[u][r] = (gr < n && gc < n) ? v : (gr == gc ? (T)1 : (T)0);
+      }
+    }
+  }
+  // strictly-upper block tiles of both outputs are zero (issued first; the stores drain while the
+  // factorization runs -- the barriers below do not wait for global stores)
+  for (int i = w; i < n; i += RW) {
+    for (int j = ((i >> 4) + 1) * 16 + lane; j < n; j += 64) {
+      Am[(int64_t)i * lda + j] = 0;
+      Xm[(int64_t)i * ldx + j] = 0;
+    }
+  }
+  for (int kb = 0; kb < nt; ++kb) {
+    CHOL_STAMP(kb, 0);
+    const int nrow = NR - kb * 16;  // local rows of block column kb
+    // 1. block column kb -> colbuf, registers -> trtri remainder R
+#pragma unroll
+    for (int u = 0; u < NTPW; ++u) {
+      if (jb[u] == kb) {
+        const int dib = __builtin_amdgcn_readfirstlane(ib[u] - kb);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = Mfma<T>::row(lane, r);
+          colbuf[(dib * 16 + row) * CP + (lane & 15)] = acc[u][r];
+          acc[u][r] = 0;  // R[ib, kb] starts at 0; R[kb, kb] = I is applied in 3a
+        }
+      }
+    }
+    lds_barrier();
+    CHOL_STAMP(kb, 1);
+    // 2. diagonal factor (lanes 0..15 of every participating wave) + the nrow-16 panel rows and 16
+    //    identity rows on lanes 16..63.  Only ceil(nrow/48) waves take part: the diagonal work is
+    //    redundant per wave, so idle waves stay off the SIMDs.
+    if (w < (nrow + 47) / 48) {
+      int lr;
+      bool ident = false;
+      if (lane < 16) {
+        lr = lane;
+      } else {
+        const int slot = w * 48 + lane - 16;
+        ident = slot >= nrow - 16 && slot < nrow;
+        lr = ident ? slot - (nrow - 16) : 16 + slot;
+      }
+      const bool active = ident || lr < nrow;
+      T a[16];
+      {
+        // branch-free: a select on a loaded value lets the compiler sink each load into its own
+        // exec-masked branch with a full LDS wait (16 serialized round trips)
+        const T keep = (active && !ident) ? (T)1 : (T)0;
+        const T* src = colbuf + min(lr, NR - 1) * CP;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) a[c] = fma(src[c], keep, (ident && c == lr) ? (T)1 : (T)0);
+      }
+      // Critical path per column: readlane(d) -> sqrt -> reciprocal -> scale -> readlane -> fma.
+      // IEEE sqrt and a rounded reciprocal as LAPACK dpotf2 (sqrt, then DSCAL by ONE/AJJ): pivots
+      // with cancellation amplify a 1-ulp difference here (a refined rsqrt cost 1e-14 on the
+      // trained model.pt state against the reference).
+      CHOL_STAMPW(kb, 0);
+      unsigned int bad = 0;  // non-positive (or NaN) pivots of this block; NaN propagates onwards
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const T d = readlane(a[j], j);
+        bad |= (d > (T)0) ? 0u : (1u << j);
+        const T sj = dsqrt(d);
+        const T inv = (T)1 / sj;
+        a[j] = (lane == j) ? sj : a[j] * inv;
+#pragma unroll
+        for (int c = j + 1; c < 16; ++c) a[c] = fma(-a[j], readlane(a[j], c), a[c]);
+      }
+      CHOL_STAMPW(kb, 1);
+      if (bad && first_fail == 0) {
+        const int j0 = __builtin_ctz(bad);
+        if (kb * 16 + j0 < n) first_fail = kb * 16 + j0 + 1;
+      }
+#pragma unroll
+      for (int c = 0; c < 16; ++c) a[c] = (lane < 16 && c > lane) ? (T)0 : a[c];
+      // identity lanes hold rows of L_kk^-T: stored as LiT = (L_kk^-1)^T
+      if (ident || (active && (lane >= 16 || w == 0))) {
+        T* dst = (ident ? LiT : Ps) + lr * CP;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) dst[c] = a[c];
+      }
+      CHOL_STAMPW(kb, 2);
+    }
+    lds_barrier();
+    CHOL_STAMP(kb, 2);
+    // 3a. X[kb, jb] = L_kk^-1 R[kb, jb]
+#pragma unroll
+    for (int u = 0; u < NTPW; ++u) {
+      if (ib[u] == kb) {
+        const int xj = __builtin_amdgcn_readfirstlane(jb[u] - kb) + kb;
+        acc_t x = {0, 0, 0, 0};
+        if (xj == kb) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) x[r] = LiT[(lane & 15) * CP + Mfma<T>::row(lane, r)];
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) x = Mfma<T>::mma(LiT[Mfma<T>::row(lane, s) * CP + (lane & 15)], acc[u][s], x);
+        }
+        acc[u] = x;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Xrow[(xj * 16 + Mfma<T>::row(lane, r)) * CP + (lane & 15)] = x[r];
+      }
+    }
+    // 3b. potrf trailing update
+#pragma unroll
+    for (int u = 0; u < NTPW; ++u) {
+      if (jb[u] > kb) {
+        // readfirstlane of a loop-variant value: keeps per-tile LDS addresses from being hoisted
+        // out of the kb loop into (spilled) per-tile VGPRs
+        const int ra = __builtin_amdgcn_readfirstlane(ib[u] - kb) * 16 + (lane & 15);
+        const int rb = __builtin_amdgcn_readfirstlane(jb[u] - kb) * 16 + (lane & 15);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int kr = Mfma<T>::row(lane, s);
+          acc[u] = Mfma<T>::mma(-Ps[ra * CP + kr], Ps[rb * CP + kr], acc[u]);
+        }
+      }
+    }
+    for (int idx = t; idx < nrow * 16; idx += RW * 64) {
+      const int lr = idx >> 4, c = idx & 15;
+      const int gr = kb * 16 + lr, gc = kb * 16 + c;
+      if (gr < n && gc < n) Am[(int64_t)gr * lda + gc] = Ps[lr * CP + c];
+    }
+    lds_barrier();
+    CHOL_STAMP(kb, 3);
+    // 3c. trtri update of the rows below kb
+#pragma unroll
+    for (int u = 0; u < NTPW; ++u) {
+      if (ib[u] > kb && jb[u] >= 0 && jb[u] <= kb) {
+        const int ra = __builtin_amdgcn_readfirstlane(ib[u] - kb) * 16 + (lane & 15);
+        const int xj = __builtin_amdgcn_readfirstlane(jb[u] - kb) + kb;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int kr = Mfma<T>::row(lane, s);
+          acc[u] = Mfma<T>::mma(-Ps[ra * CP + kr], Xrow[(xj * 16 + kr) * CP + (lane & 15)], acc[u]);
+        }
+      }
+    }
+    for (int idx = t; idx < (kb + 1) * 256; idx += RW * 64) {
+      const int j = idx >> 8, k = (idx >> 4) & 15, c = idx & 15;
+      const int gr = kb * 16 + k, gc = j * 16 + c;
+      if (gr < n && gc < n) Xm[(int64_t)gr * ldx + gc] = Xrow[(j * 16 + k) * CP + c];
+    }
+  }
+  CHOL_STAMP(nt, 0);
+  if (t == 0 && info) info[blockIdx.x] = first_fail;  // wave 0 tracked the pivots
+}
+
+template <typename T> static size_t chol_inv_smem(int n) {
+  const int nt = (n + 15) >> 4;
+  return (size_t)(3 * nt * 16 * CP + 16 * CP) * sizeof(T);
+}
+
 template <typename T> static size_t potrf_smem(int n) {
   const int nt = (n + 15) >> 4;
-  return (size_t)(16 * CP + nt * 16 * CP) * sizeof(T) + 16;
+  return (size_t)(16 * CP + 16 + nt * 16 * CP) * sizeof(T) + 16;
 }
 template <typename T> static size_t trtri_smem(int n) {
   const int nt = (n + 15) >> 4;
-  return (size_t)(16 * CP + nt * 256) * sizeof(T);
+  return (size_t)(nt * 16 * CP + nt * 256) * sizeof(T);
 }
 
 template <typename T>
@@ -272,7 +566,7 @@ static int potrf_launch(T* A, int64_t n, int64_t lda, int64_t strideA, int64_t b
     (void)hipFuncSetAttribute((const void*)potrf_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_done = true;
   }
-  hipLaunchKernelGGL(potrf_kernel<T>, dim3((unsigned)batch), dim3(256), sm, s, A, (int)n, lda, strideA, info);
+  hipLaunchKernelGGL(potrf_kernel<T>, dim3((unsigned)batch), dim3(CT), sm, s, A, (int)n, lda, strideA, info);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
@@ -294,8 +588,54 @@ static int trtri_launch(const T* L, int64_t n, int64_t ldl, int64_t strideL, T* 
     (void)hipFuncSetAttribute((const void*)trtri_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_done = true;
   }
-  hipLaunchKernelGGL(trtri_kernel<T>, dim3((unsigned)batch), dim3(256), sm, s, L, (int)n, ldl, strideL, X, ldx,
+  hipLaunchKernelGGL(trtri_kernel<T>, dim3((unsigned)batch), dim3(CT), sm, s, L, (int)n, ldl, strideL, X, ldx,
                      strideX);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
+
+template <typename T, int NTPW>
+static void chol_inv_go(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx, int64_t sX, int64_t batch,
+                        int32_t* info, size_t sm, hipStream_t s) {
+  static bool attr_done = false;
+  if (!attr_done) {
+    (void)hipFuncSetAttribute((const void*)chol_inv_kernel<T, NTPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr_done = true;
+  }
+  hipLaunchKernelGGL((chol_inv_kernel<T, NTPW>), dim3((unsigned)batch), dim3(RW * 64), sm, s, A, n, lda, sA, X, ldx,
+                     sX, info);
+}
+
+// L = chol(A) in place and X = L^{-1}: fused register-resident kernel for n <= 256, otherwise the
+// separate potrf and trtri kernels back to back on the same stream.
+template <typename T>
+static int chol_inv_launch(T* A, int64_t n, int64_t lda, int64_t sA, T* X, int64_t ldx, int64_t sX, int64_t batch,
+                           int32_t* info, hipStream_t s) {
+  if (A == nullptr) return -1;
+  if (n < 0) return -2;
+  if (lda < n) return -3;
+  if (X == nullptr) return -5;
+  if (ldx < n) return -6;
+  if (batch < 0) return -8;
+  if (n == 0 || batch == 0) return NMGP_OK;
+  if (n > 256) {
+    const int rc = potrf_launch<T>(A, n, lda, sA, batch, info, s);
+    if (rc != NMGP_OK) return rc;
+    return trtri_launch<T>(A, n, lda, sA, X, ldx, sX, batch, s);
+  }
+  const int nt = (int)((n + 15) >> 4), ntiles = nt * (nt + 1) / 2;
+  const size_t sm = chol_inv_smem<T>((int)n);
+  if (ntiles <= RW * 1)
+    chol_inv_go<T, 1>(A, (int)n, lda, sA, X, ldx, sX, batch, info, sm, s);
+  else if (ntiles <= RW * 3)
+    chol_inv_go<T, 3>(A, (int)n, lda, sA, X, ldx, sX, batch, info, sm, s);
+  else if (ntiles <= RW * 5)
+    chol_inv_go<T, 5>(A, (int)n, lda, sA, X, ldx, sX, batch, info, sm, s);
+  else if (ntiles <= RW * 9)
+    chol_inv_go<T, 9>(A, (int)n, lda, sA, X, ldx, sX, batch, info, sm, s);
+  else
+    chol_inv_go<T, 17>(A, (int)n, lda, sA, X, ldx, sX, batch, info, sm, s);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
@@ -316,5 +656,13 @@ int nmgp_trtri_batched_f64(const double* L, int64_t n, int64_t ldl, int64_t sL, 
 int nmgp_trtri_batched_f32(const float* L, int64_t n, int64_t ldl, int64_t sL, float* X, int64_t ldx, int64_t sX,
                            int64_t b, hipStream_t s) {
   return nmgp::trtri_launch<float>(L, n, ldl, sL, X, ldx, sX, b, s);
+}
+int nmgp_chol_inv_batched_f64(double* A, int64_t n, int64_t lda, int64_t sA, double* X, int64_t ldx, int64_t sX,
+                              int64_t b, int32_t* info, hipStream_t s) {
+  return nmgp::chol_inv_launch<double>(A, n, lda, sA, X, ldx, sX, b, info, s);
+}
+int nmgp_chol_inv_batched_f32(float* A, int64_t n, int64_t lda, int64_t sA, float* X, int64_t ldx, int64_t sX,
+                              int64_t b, int32_t* info, hipStream_t s) {
+  return nmgp::chol_inv_launch<float>(A, n, lda, sA, X, ldx, sX, b, info, s);
 }
 }

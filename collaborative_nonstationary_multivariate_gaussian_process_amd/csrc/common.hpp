@@ -36,6 +36,11 @@ template <> struct Mfma<float> {
   __device__ static inline int row(int lane, int r) { return ((lane >> 4) << 2) + r; }
 };
 
+// Workgroup barrier that orders LDS only: waits for this wave's LDS traffic (lgkmcnt) but not for
+// its outstanding global stores, which __syncthreads() would drain (vmcnt(0)) at every barrier.
+// Only valid where waves exchange data exclusively through LDS.
+__device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 template <typename T> __device__ inline T shfl(T v, int src) { return __shfl(v, src, 64); }
 
 template <typename T> __device__ inline T wave_sum(T v) {

@@ -358,35 +358,30 @@ class DsviEngine:
         def pw(name):
             return lambda s: p[name](F64, s)
 
-        def potrf(first, count):
-            return lambda s: L.check(lib.nmgp_potrf_batched_f64(vp(Af + first * MM * 8), M, M, MM, count,
-                                                                vp(info + first * 4), s), "potrf")
-
-        def trtri(first, count):
-            return lambda s: L.check(lib.nmgp_trtri_batched_f64(vp(Af + first * MM * 8), M, M, MM,
-                                                                vp(Ci + first * MM * 8), M, MM, count, s), "trtri")
+        def chol(first, count):
+            # fused factor + inverse: Afac <- L (in place), Cinv <- L^{-1}
+            return lambda s: L.check(lib.nmgp_chol_inv_batched_f64(vp(Af + first * MM * 8), M, M, MM,
+                                                                   vp(Ci + first * MM * 8), M, MM, count,
+                                                                   vp(info + first * 4), s), "chol_inv")
 
         need_side = (not elbo_mode) or with_kl
         steps = []
         if need_side:
             steps += [("fork",),
                       ("syrk_side", "gemm", gemm("syrk_side"), "side"),
-                      ("potrf_side", "potrf", potrf(0, FV), "side"),
-                      ("trtri_side", "trtri", trtri(0, FV), "side")]
+                      ("chol_side", "chol", chol(0, FV), "side")]
             if not elbo_mode:
                 steps.append(("xs_side", "gemm", gemm("xs_side"), "side"))
         steps += [
             ("build_rbf", "pairwise", pw("build_rbf"), "main"),
             ("syrk", "gemm", gemm("syrk"), "main"),
-            ("potrf", "potrf", potrf(FV, 4), "main"),
-            ("trtri", "trtri", trtri(FV, 4), "main"),
+            ("chol", "chol", chol(FV, 4), "main"),
             ("inv3", "gemm", gemm("inv3"), "main"),
             ("proj3", "gemm", gemm("proj3"), "main"),
             ("v", "row", row(lib.nmgp_dsvi_hyper_f64), "main"),
             ("trow", "row", row(lib.nmgp_dsvi_trow_f64), "main"),
             ("build_gibbs", "pairwise", pw("build_gibbs"), "main"),
-            ("potrf_G", "potrf", potrf(NF + 3, 1), "main"),
-            ("trtri_G", "trtri", trtri(NF + 3, 1), "main"),
+            ("chol_G", "chol", chol(NF + 3, 1), "main"),
             ("invG", "gemm", gemm("invG"), "main"),
             ("projG", "gemm", gemm("projG"), "main"),
             ("quad", "gemm", gemm("quad"), "main"),

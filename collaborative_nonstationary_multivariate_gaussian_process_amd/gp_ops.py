@@ -114,10 +114,9 @@ class _SolveSPD(torch.autograd.Function):
     @staticmethod
     def forward(ctx, A, B):
         C = A.detach().contiguous().clone()
-        info = H.potrf_(C)
+        Ci, info = H.chol_inv_(C)
         if int(info.cpu()[0]) != 0:
             raise torch.linalg.LinAlgError("solve: A is not positive-definite")
-        Ci = H.trtri(C)
         Ainv = H.matmul(Ci, Ci, transA=True, maskA=L.A_UPPER, maskB=L.B_LOWER)
         X = _mm(Ainv, B)
         ctx.save_for_backward(Ainv, X)

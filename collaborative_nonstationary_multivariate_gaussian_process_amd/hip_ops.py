@@ -186,6 +186,22 @@ def trtri(Lm, out=None):
     return out
 
 
+def chol_inv_(A, out=None, info=None):
+    """Fused in-place lower Cholesky of A (batch, n, n) and X = L^{-1}; returns (X, info)."""
+    L.require_device(A, "A")
+    assert A.is_contiguous()
+    n = A.shape[-1]
+    batch = A.numel() // (n * n) if n else 0
+    if out is None:
+        out = torch.empty_like(A)
+    if info is None:
+        info = torch.zeros(max(batch, 1), dtype=torch.int32, device=A.device)
+    fn = getattr(L.lib(), "nmgp_chol_inv_batched_" + _sfx(A.dtype))
+    L.check(fn(ctypes.c_void_p(A.data_ptr()), n, n, n * n, ctypes.c_void_p(out.data_ptr()), n, n * n, batch,
+               ctypes.c_void_p(info.data_ptr()), L.stream_handle()), "chol_inv")
+    return out, info
+
+
 # ------------------------------------------------------------------------------------ pairwise
 def pairwise_desc(K, X, Z, *, mode, dist=L.DIST_DIFF, scale2=1.0, length_scale=1.0, ellX=None, ellZ=None,
                   sigX=None, sigZ=None, hyp=None, hyp_off=0, hyp_log=False, diag_add=0.0):

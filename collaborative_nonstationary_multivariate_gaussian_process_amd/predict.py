@@ -19,10 +19,9 @@ def _solve_rows(K12, K22, rhs):
     """K12 (K22 + 1e-4 I)^{-1} rhs  for rhs (M, k): Cholesky -> inverse -> two GEMMs."""
     A = K22.clone()
     A.diagonal().add_(JIT)
-    info = H.potrf_(A)
+    Ci, info = H.chol_inv_(A)
     if int(info.cpu()[0]) != 0:
         raise torch.linalg.LinAlgError("cholesky: K22 + 1e-4 I is not positive-definite")
-    Ci = H.trtri(A)
     Ainv = H.matmul(Ci, Ci, transA=True, maskA=L.A_UPPER, maskB=L.B_LOWER)
     return H.matmul(K12, H.matmul(Ainv, rhs))
 

@@ -101,6 +101,14 @@ int nmgp_trtri_batched_f64(const double* L, int64_t n, int64_t ldl, int64_t stri
                            double* X, int64_t ldx, int64_t strideX, int64_t batch, hipStream_t stream);
 int nmgp_trtri_batched_f32(const float* L, int64_t n, int64_t ldl, int64_t strideL,
                            float* X, int64_t ldx, int64_t strideX, int64_t batch, hipStream_t stream);
+/* Fused factor + inverse: A <- L = chol(A) in place (upper zeroed), X <- L^{-1}, info as potrf.
+ * n <= 256 runs one register-resident kernel per matrix (the DSVI shapes: code/nmgp_dsvi.py:172-177
+ * priors and variational covariances, whose inverses feed K12 K22^{-1} and the KL); larger n runs
+ * potrf then trtri on the same stream.                                                       */
+int nmgp_chol_inv_batched_f64(double* A, int64_t n, int64_t lda, int64_t strideA, double* X, int64_t ldx,
+                              int64_t strideX, int64_t batch, int32_t* info, hipStream_t stream);
+int nmgp_chol_inv_batched_f32(float* A, int64_t n, int64_t lda, int64_t strideA, float* X, int64_t ldx,
+                              int64_t strideX, int64_t batch, int32_t* info, hipStream_t stream);
 
 /* ------------------------------------------------------------------ pairwise kernel builder
  * mode RBF:   K = scale2 * exp(-0.5 * ||x/ls - z/ls||^2)          (code/utils.py:91-94)

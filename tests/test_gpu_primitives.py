@@ -145,6 +145,33 @@ def test_potrf_trtri(ops, n, batch):
     assert float(torch.triu(X.cpu(), 1).abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("n,batch", [(16, 2), (20, 3), (48, 1), (64, 2), (100, 5), (176, 2), (256, 4), (257, 1)])
+def test_chol_inv_fused(ops, n, batch):
+    # n <= 256 runs the register-resident fused kernel (every tile-count bucket), 257 the fallback
+    A = _spd(n, batch, 7 * n)
+    Ad = A.clone().to(DEV)
+    X, info = ops.chol_inv_(Ad)
+    assert int(info.abs().sum()) == 0
+    ref = torch.linalg.cholesky(A)
+    assert rel(Ad, ref) < 1e-13
+    assert rel(X, torch.linalg.inv(ref)) < 1e-11
+    assert float(torch.triu(Ad.cpu(), 1).abs().max()) == 0.0
+    assert float(torch.triu(X.cpu(), 1).abs().max()) == 0.0
+
+
+def test_chol_inv_f32_and_not_pd(ops):
+    A = _spd(200, 3, 3)
+    Ad = A.float().to(DEV)
+    X, info = ops.chol_inv_(Ad)
+    ref = torch.linalg.cholesky(A)
+    assert rel(Ad, ref) < 1e-5 and rel(X, torch.linalg.inv(ref)) < 1e-4
+    bad = A.clone()
+    bad[2, 130, 130] = -5.0
+    _, info = ops.chol_inv_(bad.to(DEV))
+    info = info.cpu()
+    assert int(info[0]) == 0 and int(info[1]) == 0 and int(info[2]) > 0
+
+
 def test_potrf_f32_and_not_pd(ops):
     A = _spd(96, 2, 1)
     Ld = A.float().to(DEV)
