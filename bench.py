@@ -141,6 +141,7 @@ def main():
 
     from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP, DsviTrainer
     from collaborative_nonstationary_multivariate_gaussian_process_amd.engine import param_layout
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import distributed as DD
 
     xs, ys = synth_data(rank)
     z = np.linspace(0, 1, M)
@@ -180,7 +181,7 @@ def main():
         else:
             trainer.grad_step(eng)
         if world > 1:
-            dist.all_reduce(model._grad, op=dist.ReduceOp.AVG)
+            DD.allreduce_mean_(model._grad)                  # one RCCL all-reduce of the flat gradient
             trainer.update()
         elif graph is None:
             trainer.update()

@@ -1,0 +1,84 @@
+"""Multi-GPU decomposition of the DSVI path (one process per GPU, RCCL over xGMI).
+
+Two independent axes:
+
+* **observations** (training, `inference` / bench): the global minibatch of W*b rows is cut into
+  W contiguous slices, rank r trains on slice r, every rank replicates the O(M^3) prior and
+  variational factorizations, and the flat gradient is averaged with ONE all-reduce before the
+  replicated Adam step.  Because the objective is -(N/b) R_r + KL on every rank, the average is
+  -(N/(W b)) sum_r R_r + KL: the gradient of the global-batch objective (bit-for-bit up to the
+  reduction order when the ranks share z_v and the row noise of the global batch).
+* **Monte-Carlo samples** (`compute_ELBO`, code/nmgp_dsvi.py:330-380): rank r evaluates samples
+  r, r+W, ...; one all-reduce of [sum_s R_s, KL] where only the rank owning the LAST sample
+  contributes the KL terms (the reference evaluates KL with the last sample's K_G22, :385).
+
+Backend-neutral (`nccl` = RCCL on the GPU box, `gloo` in the CPU tests); uses SUM + divide
+rather than ReduceOp.AVG, which gloo does not implement.
+"""
+import torch
+
+try:
+    import torch.distributed as dist
+except ImportError:  # pragma: no cover
+    dist = None
+
+
+def world_info(group=None):
+    """(rank, world_size) of `group`, or (0, 1) when torch.distributed is not initialised."""
+    if dist is None or not dist.is_available() or not dist.is_initialized():
+        return 0, 1
+    return dist.get_rank(group), dist.get_world_size(group)
+
+
+def shard_bounds(n, rank, world):
+    """[start, stop) of rank's contiguous share of n items; sizes differ by at most one."""
+    base, extra = divmod(int(n), int(world))
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def rank_slice(n, rank, world):
+    s, e = shard_bounds(n, rank, world)
+    return slice(s, e)
+
+
+def allreduce_mean_(t, group=None):
+    """In-place mean over ranks (no-op on one rank)."""
+    rank, world = world_info(group)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        t.div_(world)
+    return t
+
+
+def allreduce_sum_(t, group=None):
+    rank, world = world_info(group)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t
+
+
+def sample_ids(n_sample, rank, world):
+    """Monte-Carlo samples owned by `rank` (round-robin)."""
+    return list(range(rank, int(n_sample), int(world)))
+
+
+def last_sample_owner(n_sample, world):
+    return (int(n_sample) - 1) % int(world)
+
+
+def combine_elbo(r_sum, kl, n_sample, group=None, device=None, dtype=torch.float64):
+    """ELBO = (1/n) sum_s R_s - KL from per-rank partials.
+
+    r_sum: this rank's sum of reconstruction terms over its samples (0-d tensor or float);
+    kl:    KL_W + KL_v + KL_U evaluated with the last sample's K_G22 on its owner rank, None on
+           the other ranks.  Returns a 0-d tensor on `device` (identical on every rank).
+    """
+    rank, world = world_info(group)
+    dev = device if device is not None else (r_sum.device if torch.is_tensor(r_sum) else "cpu")
+    buf = torch.zeros(2, dtype=dtype, device=dev)
+    buf[0] = r_sum if torch.is_tensor(r_sum) else float(r_sum)
+    if kl is not None:
+        buf[1] = kl if torch.is_tensor(kl) else float(kl)
+    allreduce_sum_(buf, group)
+    return buf[0] / int(n_sample) - buf[1]

@@ -20,6 +20,7 @@ import torch
 from torch.nn import Parameter
 from torch.utils.data import DataLoader, Dataset
 
+from . import distributed as DD
 from . import hip_ops as H
 from .engine import DsviEngine, HYPER_NAMES, PARAM_NAMES, param_layout
 from .utils import TensorType, tridiagonal_jitter  # noqa: F401  (re-exported like the reference)
@@ -193,27 +194,42 @@ class NMGP(Model):
             print("forward+backward (fused) costs {}s".format(time.time() - t1))
         return loss
 
-    def compute_ELBO(self, inputs_list, outputs_list, index=None, n_sample=1000, verbose=False):
+    def compute_ELBO(self, inputs_list, outputs_list, index=None, n_sample=1000, verbose=False,
+                     distributed=False, group=None):
         """code/nmgp_dsvi.py:303-404: MC mean of the column-gathered reconstruction term minus the
-        KL terms of the LAST sample's K_G22 (reference quirks kept)."""
+        KL terms of the LAST sample's K_G22 (reference quirks kept).
+
+        distributed=True shards the samples over the ranks of `group` (every rank must call;
+        every rank returns the same value): rank r evaluates samples r, r+W, ..., the noise
+        stream is still consumed in sample order on every rank so results match one process.
+        """
         self._assert_views()
         x, y, sizes = self._prepare(inputs_list, outputs_list, index)
         B = sum(sizes)
         eng = self.engine(B, N=self.N)
         acc = torch.zeros((), dtype=F64, device=self.device_)
         Q = self.D * (self.D + 1) // 2
-        out = None
+        rank, world = DD.world_info(group) if distributed else (0, 1)
+        out, kl = None, None
         for s in range(n_sample):
             if verbose:
                 print("Monte Carlo index:", s)
             noise = self._torch_noise(B, Q) if self.noise == "torch" else None
+            if s % world != rank:                       # another rank's sample: keep the stream in step
+                if noise is None:
+                    H.counter_add_(self._noise_counter, 1)
+                continue
             eng.load_batch(x, y, sizes, noise=noise, index=index)
             if noise is None:
                 eng.device_noise(self._noise_seed, self._noise_counter)
                 H.counter_add_(self._noise_counter, 1)
             out = eng.elbo_sample(with_kl=(s == n_sample - 1))
             acc += out[1]
-        return (acc / n_sample - out[2] - out[3] - out[4]).detach().clone()
+            if s == n_sample - 1:
+                kl = out[2] + out[3] + out[4]
+        if world == 1:
+            return (acc / n_sample - out[2] - out[3] - out[4]).detach().clone()
+        return DD.combine_elbo(acc, kl, n_sample, group=group, device=self.device_).detach().clone()
 
     def predict_Y(self, inputs_list, index=None):
         """code/nmgp_dsvi.py:666-722: posterior-mean prediction (returns a tensor)."""
@@ -345,14 +361,19 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
               mu_v=None, mu_W=None, mu_U=None, sqrt_v=None, sqrt_W=None, sqrt_U=None, lr=0.01, itnum=1000,
               do_stop_criterion=False, seed=22, verbose=False, PATH="model.pt", continuous_training=False,
               show_ELBO=True, save_model=False, X_test_list=None, Y_test_list=None, device=None, noise="torch",
-              use_graph=False, n_elbo_sample=1000):
+              use_graph=False, n_elbo_sample=1000, distributed=False, group=None):
     """code/nmgp_dsvi.py:758-909 on the MI355X.
 
     Returns (model, loss_list, time_list), or (model, loss_list, rmse_test_list, time_list) when
     X_test_list is given -- as the reference.  Extra keyword-only knobs (defaults keep reference
     behaviour): device, noise ("torch" = reference RNG stream | "device"), use_graph (replay the
-    step as a HIP graph; needs noise="device"), n_elbo_sample (compute_ELBO samples).
+    step as a HIP graph; needs noise="device"), n_elbo_sample (compute_ELBO samples),
+    distributed (data-parallel over the ranks of `group`: every rank draws the same global
+    minibatch of batch_size * world rows -- the seeded DataLoader permutation -- trains on its
+    contiguous slice, and the gradients are averaged with one all-reduce before the replicated
+    Adam step; the reported loss is the rank mean; compute_ELBO shards its samples).
     """
+    rank, world = DD.world_info(group) if distributed else (0, 1)
     X_train_vec = np.concatenate(X_train_list)
     Y_train_vec = np.concatenate(Y_train_list)
     train_index = np.concatenate([np.ones_like(Y_train_list[i]) * i for i in range(dim_outputs)]).astype(int)
@@ -367,7 +388,7 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
     _apply_hyperpars(model, hyperpars, fix_hyperpars, continuous_training, PATH, opt_state)
     trainer = DsviTrainer(model, lr)
     trainer.load_optimizer_state(opt_state)
-    train_loader = DataLoader(trainData(X, Y, I), batch_size=batch_size, shuffle=True)
+    train_loader = DataLoader(trainData(X, Y, I), batch_size=batch_size * world, shuffle=True)
     loss_list, time_list = [], []
     if X_test_list is not None:
         rmse_test_list = []
@@ -382,6 +403,9 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
         batch = 0
         for X_batch, Y_batch, I_batch in train_loader:
             batch += 1
+            if world > 1:                               # this rank's slice of the global minibatch
+                sl = DD.rank_slice(X_batch.shape[0], rank, world)
+                X_batch, Y_batch, I_batch = X_batch[sl], Y_batch[sl], I_batch[sl]
             X_bl, Y_bl = vec2list(X_batch, Y_batch, I_batch, dim=dim_outputs)
             model._assert_views()
             x, y, sizes = model._prepare(X_bl, Y_bl)
@@ -390,11 +414,17 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
             nz = model._torch_noise(B, Q) if noise == "torch" else None
             eng.load_batch(x, y, sizes, noise=nz)
             if use_graph:
-                g = trainer.graphs.get(id(eng)) or trainer.capture(eng)
+                g = trainer.graphs.get(id(eng)) or trainer.capture(eng, include_update=(world == 1))
                 g.replay()
                 loss = eng.out[0]
-            else:
+            elif world == 1:
                 loss = trainer.step(eng, noise=nz)
+            else:
+                loss = trainer.grad_step(eng, noise=nz)
+            if world > 1:
+                DD.allreduce_mean_(model._grad, group)
+                trainer.update()
+                loss = DD.allreduce_mean_(loss.clone().reshape(1), group)[0]
             losses_dev.append(loss.clone())
             torch.cuda.synchronize(model.device_)
             time_list.append(time.time() - ts)
@@ -410,7 +440,7 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
                 print("Stop criteria is satisfied.")
                 break
         if epoch % 100 == 99 and show_ELBO:
-            elbo = model.compute_ELBO(X_list, Y_list, n_sample=n_elbo_sample)
+            elbo = model.compute_ELBO(X_list, Y_list, n_sample=n_elbo_sample, distributed=distributed, group=group)
             print("epoch: {}, ELBO: {}".format(epoch + 1, float(elbo)))
             print(print_mem(epoch + 1))
     print("training takes {}s".format(time.time() - ts))
@@ -420,7 +450,7 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
                     "optimizer_state_dict": _adam_state_dict(model, trainer, lr),
                     "loss": torch.tensor(float(losses_dev[-1]) if losses_dev else float("nan"))}, PATH)
     if show_ELBO:
-        elbo = model.compute_ELBO(X_list, Y_list, n_sample=n_elbo_sample)
+        elbo = model.compute_ELBO(X_list, Y_list, n_sample=n_elbo_sample, distributed=distributed, group=group)
         print("epoch: {}, ELBO: {}".format(epoch + 1, float(elbo)))
         print(print_mem(epoch + 1))
     if X_test_list is not None:

@@ -1,0 +1,94 @@
+"""Two ranks on one GPU (gloo transport; RCCL is exercised by bench.py under torchrun): the HIP
+path's sample-sharded compute_ELBO equals the single-process value, and data-parallel
+`inference` keeps the replicated parameters identical on every rank."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+WORLD = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, port, fn, q):
+    import traceback
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+        out = fn(rank)
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, out))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+
+
+def _run(fn):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    procs = [ctx.Process(target=_worker, args=(r, port, fn, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get() for _ in range(WORLD)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=300)
+    for r, out in res:
+        if isinstance(out, str):
+            raise AssertionError(f"rank {r} failed:\n{out}")
+    return [out for _, out in res]
+
+
+def _toy_model():
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP
+    from tests import _golden as G
+    g = G.load("toy_elbo")
+    xs, ys = G.split_lists(g)
+    model = NMGP(number_observations=int(g["N"]), dim_outputs=2, Z=g["z"], seed=22, device="cuda:0")
+    return model, xs, ys
+
+
+def _elbo(rank, distributed=True):
+    model, xs, ys = _toy_model()
+    torch.manual_seed(5)
+    xl = [torch.from_numpy(x) for x in xs]
+    yl = [torch.from_numpy(y) for y in ys]
+    return float(model.compute_ELBO(xl, yl, n_sample=5, distributed=distributed))
+
+
+def test_sample_sharded_compute_elbo_matches_one_process():
+    outs = _run(_elbo)
+    ref = _elbo(0, distributed=False)
+    assert outs[0] == outs[1]
+    assert outs[0] == pytest.approx(ref, rel=1e-12)
+
+
+def _dp_train(rank):
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import inference
+    from tests import _golden as G
+    g = G.load("toy_elbo")
+    xs, ys = G.split_lists(g)
+    torch.manual_seed(0)
+    model, losses, _ = inference(xs, ys, g["z"], 50, 2, hyperpars={}, fix_hyperpars=True, lr=0.005, itnum=1,
+                                 show_ELBO=False, device="cuda:0", noise="device", distributed=True)
+    return model._theta.detach().cpu().numpy(), [float(v) for v in losses]
+
+
+def test_data_parallel_inference_keeps_ranks_in_sync():
+    outs = _run(_dp_train)
+    (t0, l0), (t1, l1) = outs
+    assert np.array_equal(t0, t1)
+    assert l0 == l1 and len(l0) == 2            # 200 rows / (50 x 2 ranks) = 2 global steps
+    assert all(np.isfinite(l0))
