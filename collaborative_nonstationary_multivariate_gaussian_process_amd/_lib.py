@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnmgp_hip.so")
+LIB_PATH = os.environ.get("NMGP_LIB_OVERRIDE") or os.path.join(_HERE, "libnmgp_hip.so")  # override: A/B experiments
 
 c_int, c_i64, c_dbl, c_vp, c_u64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p, ctypes.c_uint64
 

@@ -14,6 +14,11 @@ namespace nmgp {
 
 constexpr int kWave = 64;
 
+// Global-address-space pointer.  Pointers that arrive inside descriptor structs are generic, and
+// generic (flat) loads count against lgkmcnt as well as vmcnt: an LDS wait would then also wait
+// for every outstanding prefetch.  Casting to addrspace(1) gives global_load/store instead.
+template <typename T> using GPtr = __attribute__((address_space(1))) T*;
+
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 

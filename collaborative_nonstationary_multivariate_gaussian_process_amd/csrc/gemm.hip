@@ -4,15 +4,20 @@
 // the reference's per-pair torch.solve / matmul calls (code/utils.py:117-146,
 // code/nmgp_dsvi.py:172-177, 227-237).
 //
-// Tile 64x64x16 per 256-thread workgroup: 4 waves in a 2x2 grid, each wave 32x32 = 2x2 MFMA
-// blocks of 16x16.  Operands are staged k-major in LDS (row pitch 80 elements so that the two
-// 16-lane k rows of one ds_read_b64 land on disjoint bank halves).  Triangular operand masks
-// trim the k range, so tril(S) tril(S)^T and L^-T L^-1 products skip the zero half.
+// Tile 64x64x32 per 256-thread workgroup: 4 waves in a 2x2 grid, each wave 32x32 = 2x2 MFMA
+// blocks of 16x16.  Operands are staged k-major in ONE LDS array (pitch 65: the k-major stores of a
+// k-contiguous operand are conflict-free).  Main loop = register prefetch pipeline: the global
+// loads of k-tile t+1 are in flight while the MFMAs of tile t run; masks (bounds, triangular
+// operands, k-scale) are applied when the registers are written to LDS, so nothing consumes a
+// prefetched value early.  Fast path: buffer loads whose per-element byte offsets are fixed for the
+// whole loop -- the k advance is a uniform change of the resource base, out-of-range reads give 0.
+// Triangular operand masks trim the k range, so tril(S) tril(S)^T and L^-T L^-1 skip the zero half.
 #include "common.hpp"
 
 namespace nmgp {
 
-constexpr int GBM = 64, GBN = 64, GBK = 16, GPAD = 16;
+constexpr int GBM = 64, GBN = 64, GBK = 32, LP = 65;
+constexpr int LDS_T = 2 * GBK * LP;  // A image + B image (elements)
 
 struct GemmArgs {
   const nmgp_gemm_desc* descs;
@@ -21,56 +26,223 @@ struct GemmArgs {
   nmgp_gemm_desc inl;
 };
 
+__device__ inline __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t nbytes) {
+  const int32_t nr = (int32_t)(nbytes <= 0 ? 0 : (nbytes > 0x7fffffffLL ? 0x7fffffffLL : nbytes));
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nr, 0x00020000);
+}
+template <typename T> __device__ inline T bload(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes);
+template <> __device__ inline double bload<double>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+template <> __device__ inline float bload<float>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+// Problem geometry resolved for one workgroup (all wave-uniform).
+struct Tile {
+  int64_t r0, k0;
+  int m, n, K, i0, j0, kbeg, kend, kbA, kbB, flags;
+};
+
+// Per-thread element map of a GBM x GBK (A) / GBK x GBN (B) tile, 8 elements each, chosen so that
+// each load instruction reads consecutive addresses across the wave for either layout.
+struct EltMap {
+  int a_il[8], a_kl[8], b_kl[8], b_jl[8];
+};
+
 template <typename T>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
-  __shared__ T As[GBK][GBM + GPAD];
-  __shared__ T Bs[GBK][GBN + GPAD];
+__device__ inline void stage_lds(T* As, T* Bs, const EltMap& em, const T (&ra)[8], const T (&rb)[8],
+                                 const T (&rs)[8], unsigned okm, bool kscale) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    As[em.a_kl[e] * LP + em.a_il[e]] = (okm >> e) & 1u ? ra[e] : (T)0;
+    T bv = (okm >> (8 + e)) & 1u ? rb[e] : (T)0;
+    if (kscale) bv *= rs[e];
+    Bs[em.b_kl[e] * LP + em.b_jl[e]] = bv;
+  }
+}
+
+template <typename T, typename Acc>
+__device__ inline void mma_tile(const T* As, const T* Bs, int lane, int wr, int wc, Acc& c00, Acc& c01, Acc& c10,
+                                Acc& c11) {
+#pragma unroll
+  for (int s = 0; s < GBK / 4; ++s) {
+    const int kr = s * 4 + (lane >> 4);
+    const T a0 = As[kr * LP + wr * 32 + (lane & 15)];
+    const T a1 = As[kr * LP + wr * 32 + 16 + (lane & 15)];
+    const T b0 = Bs[kr * LP + wc * 32 + (lane & 15)];
+    const T b1 = Bs[kr * LP + wc * 32 + 16 + (lane & 15)];
+    c00 = Mfma<T>::mma(a0, b0, c00);
+    c01 = Mfma<T>::mma(a0, b1, c01);
+    c10 = Mfma<T>::mma(a1, b0, c10);
+    c11 = Mfma<T>::mma(a1, b1, c11);
+  }
+}
+
+// Triangular-operand and bounds validity of element (gi, kk) of A / (kk, gj) of B.
+__device__ inline bool a_ok(int flags, int gi, int kk, int m, bool kin) {
+  return gi < m && kin && !(((flags & NMGP_A_LOWER) && kk > gi) || ((flags & NMGP_A_UPPER) && kk < gi));
+}
+__device__ inline bool b_ok(int flags, int gj, int kk, int n, bool kin) {
+  return gj < n && kin && !(((flags & NMGP_B_LOWER) && gj > kk) || ((flags & NMGP_B_UPPER) && gj < kk));
+}
+
+// Fast main loop: every k-tile lies inside one k-block of each operand (block length a multiple
+// of GBK, or no blocking), so an element's byte offset from the tile's k origin never changes.
+template <typename T, typename Acc>
+__device__ inline void mainloop_fast(const nmgp_gemm_desc& d, const Tile& tl, const EltMap& em, T* As, T* Bs, int lane,
+                                     int wr, int wc, Acc& c00, Acc& c01, Acc& c10, Acc& c11) {
+  const char* Ab = (const char*)d.A;
+  const char* Bb = (const char*)d.B;
+  const GPtr<const T> ksc = (GPtr<const T>)(d.kscale ? d.kscale : d.B);  // always a valid address
+  const bool ksf = (tl.flags & NMGP_KSCALE) != 0;
+  const bool kbA_on = tl.kbA < tl.K, kbB_on = tl.kbB < tl.K;
+  const int nkbA = kbA_on ? (tl.K + tl.kbA - 1) / tl.kbA : 1;
+  const int nkbB = kbB_on ? (tl.K + tl.kbB - 1) / tl.kbB : 1;
+  const int kinA = kbA_on ? tl.kbA : tl.K;  // k extent inside one block
+  const int kinB = kbB_on ? tl.kbB : tl.K;
+  // end of each operand's addressed extent (elements past the base pointer): the OOB bound
+  const int64_t endA = tl.r0 * d.sA_i + (int64_t)(tl.m - 1) * d.sA_i + (tl.k0 + kinA - 1) * d.sA_k +
+                       (int64_t)(nkbA - 1) * d.sA_kb + 1;
+  const int64_t endB = (tl.k0 + kinB - 1) * d.sB_k + (int64_t)(tl.n - 1) * d.sB_j + (int64_t)(nkbB - 1) * d.sB_kb + 1;
+  uint32_t offA[8], offB[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    offA[e] = (uint32_t)(((int64_t)(tl.i0 + em.a_il[e]) * d.sA_i + (int64_t)em.a_kl[e] * d.sA_k) * (int64_t)sizeof(T));
+    offB[e] = (uint32_t)(((int64_t)em.b_kl[e] * d.sB_k + (int64_t)(tl.j0 + em.b_jl[e]) * d.sB_j) * (int64_t)sizeof(T));
+  }
+  auto load = [&](int kt, T (&ra)[8], T (&rb)[8], T (&rs)[8], unsigned& okm) {
+    const int kbA_u = kbA_on ? kt / tl.kbA : 0, kbB_u = kbB_on ? kt / tl.kbB : 0;
+    const int kkA = kt - kbA_u * (kbA_on ? tl.kbA : 0);
+    const int kkB = kt - kbB_u * (kbB_on ? tl.kbB : 0);
+    const int64_t baseA = tl.r0 * d.sA_i + (tl.k0 + kkA) * d.sA_k + (int64_t)kbA_u * d.sA_kb;
+    const int64_t baseB = (tl.k0 + kkB) * d.sB_k + (int64_t)kbB_u * d.sB_kb;
+    const __amdgpu_buffer_rsrc_t rA = make_rsrc(Ab + baseA * (int64_t)sizeof(T), (endA - baseA) * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rB = make_rsrc(Bb + baseB * (int64_t)sizeof(T), (endB - baseB) * (int64_t)sizeof(T));
+    okm = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      ra[e] = bload<T>(rA, offA[e]);
+      const int gk = kt + em.a_kl[e];
+      okm |= a_ok(tl.flags, tl.i0 + em.a_il[e], kkA + em.a_kl[e], tl.m, gk < tl.kend) ? (1u << e) : 0u;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      rb[e] = bload<T>(rB, offB[e]);
+      const int gk = kt + em.b_kl[e];
+      rs[e] = ksc[tl.k0 + min(gk, tl.K - 1)];
+      okm |= b_ok(tl.flags, tl.j0 + em.b_jl[e], kkB + em.b_kl[e], tl.n, gk < tl.kend) ? (1u << (8 + e)) : 0u;
+    }
+  };
+  T ra[8], rb[8], rs[8];
+  unsigned okm = 0;
+  load(tl.kbeg, ra, rb, rs, okm);
+  for (int kt = tl.kbeg; kt < tl.kend; kt += GBK) {
+    stage_lds(As, Bs, em, ra, rb, rs, okm, ksf);
+    lds_barrier();
+    if (kt + GBK < tl.kend) load(kt + GBK, ra, rb, rs, okm);
+    mma_tile(As, Bs, lane, wr, wc, c00, c01, c10, c11);
+    lds_barrier();
+  }
+}
+
+// General main loop (k-blocks not aligned to GBK, small shapes): per-element block index.
+template <typename T, typename Acc>
+__device__ inline void mainloop_general(const nmgp_gemm_desc& d, const Tile& tl, const EltMap& em, T* As, T* Bs,
+                                        int lane, int wr, int wc, Acc& c00, Acc& c01, Acc& c10, Acc& c11) {
+  const GPtr<const T> A = (GPtr<const T>)d.A;
+  const GPtr<const T> Bm = (GPtr<const T>)d.B;
+  const GPtr<const T> ksc = (GPtr<const T>)(d.kscale ? d.kscale : d.B);
+  const bool ksf = (tl.flags & NMGP_KSCALE) != 0;
+  const bool kbA_on = tl.kbA < tl.K, kbB_on = tl.kbB < tl.K;
+  auto load = [&](int kt, T (&ra)[8], T (&rb)[8], T (&rs)[8], unsigned& okm) {
+    okm = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int gi = tl.i0 + em.a_il[e], gk = kt + em.a_kl[e];
+      const int gkc = min(gk, tl.K - 1);
+      const int kb = kbA_on ? gkc / tl.kbA : 0, kk = gkc - kb * (kbA_on ? tl.kbA : 0);
+      ra[e] = A[(tl.r0 + min(gi, tl.m - 1)) * d.sA_i + (tl.k0 + kk) * d.sA_k + (int64_t)kb * d.sA_kb];
+      okm |= a_ok(tl.flags, gi, kk, tl.m, gk < tl.kend) ? (1u << e) : 0u;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int gk = kt + em.b_kl[e], gj = tl.j0 + em.b_jl[e];
+      const int gkc = min(gk, tl.K - 1);
+      const int kb = kbB_on ? gkc / tl.kbB : 0, kk = gkc - kb * (kbB_on ? tl.kbB : 0);
+      rb[e] = Bm[(tl.k0 + kk) * d.sB_k + (int64_t)min(gj, tl.n - 1) * d.sB_j + (int64_t)kb * d.sB_kb];
+      rs[e] = ksc[tl.k0 + gkc];
+      okm |= b_ok(tl.flags, gj, kk, tl.n, gk < tl.kend) ? (1u << (8 + e)) : 0u;
+    }
+  };
+  T ra[8], rb[8], rs[8];
+  unsigned okm = 0;
+  load(tl.kbeg, ra, rb, rs, okm);
+  for (int kt = tl.kbeg; kt < tl.kend; kt += GBK) {
+    stage_lds(As, Bs, em, ra, rb, rs, okm, ksf);
+    lds_barrier();
+    if (kt + GBK < tl.kend) load(kt + GBK, ra, rb, rs, okm);
+    mma_tile(As, Bs, lane, wr, wc, c00, c01, c10, c11);
+    lds_barrier();
+  }
+}
+
+template <typename T, bool GROUPED>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args, const nmgp_gemm_desc* __restrict__ descs) {
+  // ONE shared array (a second __shared__ object can make hipcc wait vmcnt(0) in the k-loop)
+  __shared__ T smem[LDS_T + 2];
+  T* As = smem;
+  T* Bs = smem + GBK * LP;
+  int* s_last = (int*)(smem + LDS_T);
   int tile = blockIdx.x;
-  const nmgp_gemm_desc* dp = &args.inl;
-  if (args.descs != nullptr) {
+  int idx = 0;
+  if (GROUPED) {
     int lo = 0, hi = args.nprob - 1;
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (args.descs[mid].tile_start <= tile) lo = mid; else hi = mid - 1;
+      if (descs[mid].tile_start <= tile) lo = mid; else hi = mid - 1;
     }
-    dp = &args.descs[lo];
+    idx = lo;
   }
-  const nmgp_gemm_desc& d = *dp;
-  __shared__ int s_last;
+  // by value from a read-only uniform address: scalar loads once (a reference would be re-read after
+  // every barrier, whose asm clobbers memory)
+  const nmgp_gemm_desc d = GROUPED ? descs[idx] : args.inl;
   tile -= d.tile_start;
   const int ksplit = d.ksplit > 1 ? d.ksplit : 1;
   const int ks = tile % ksplit;
   tile /= ksplit;
   const int tn = tile % d.tiles_n, tm = tile / d.tiles_n;
-  int64_t r0 = 0;
-  int m = d.m;
+  Tile tl;
+  tl.r0 = 0;
+  tl.m = d.m;
   const int span = d.seg_span > 0 ? d.seg_span : 1;
   if (d.row_seg >= 0) {
-    r0 = args.seg[d.row_seg];
-    m = args.seg[d.row_seg + span] - (int)r0;
+    tl.r0 = args.seg[d.row_seg];
+    tl.m = args.seg[d.row_seg + span] - (int)tl.r0;
   }
-  int64_t k0 = 0;
-  int K = d.k;
+  tl.k0 = 0;
+  tl.K = d.k;
   if (d.k_seg >= 0) {
-    k0 = args.seg[d.k_seg];
-    K = args.seg[d.k_seg + span] - (int)k0;
+    tl.k0 = args.seg[d.k_seg];
+    tl.K = args.seg[d.k_seg + span] - (int)tl.k0;
   }
-  const int n = d.n;
-  const int i0 = tm * GBM, j0 = tn * GBN;
-  if (i0 >= m) return;
-  const int flags = d.flags;
-  const bool above = j0 > i0 + GBM - 1;
+  tl.n = d.n;
+  tl.i0 = tm * GBM;
+  tl.j0 = tn * GBN;
+  if (tl.i0 >= tl.m) return;
+  tl.flags = d.flags;
+  const int flags = tl.flags;
+  const bool above = tl.j0 > tl.i0 + GBM - 1;
   if (above && (flags & NMGP_OUT_LOWER)) return;
   const bool zero_tile = above && (flags & NMGP_OUT_TRIL);
-  const int kbA = d.kbA > 0 ? d.kbA : 0x7fffffff;
-  const int kbB = d.kbB > 0 ? d.kbB : 0x7fffffff;
-
-  int kbeg = 0, kend = K;
+  tl.kbA = d.kbA > 0 ? d.kbA : 0x7fffffff;
+  tl.kbB = d.kbB > 0 ? d.kbB : 0x7fffffff;
+  int kbeg = 0, kend = tl.K;
   if (d.k_seg < 0) {
-    if ((flags & NMGP_A_LOWER) && kbA >= K) kend = min(kend, i0 + GBM);
-    if ((flags & NMGP_A_UPPER) && kbA >= K) kbeg = max(kbeg, i0);
-    if ((flags & NMGP_B_LOWER) && kbB >= K) kbeg = max(kbeg, j0);
-    if ((flags & NMGP_B_UPPER) && kbB >= K) kend = min(kend, j0 + GBN);
+    if ((flags & NMGP_A_LOWER) && tl.kbA >= tl.K) kend = min(kend, tl.i0 + GBM);
+    if ((flags & NMGP_A_UPPER) && tl.kbA >= tl.K) kbeg = max(kbeg, tl.i0);
+    if ((flags & NMGP_B_LOWER) && tl.kbB >= tl.K) kbeg = max(kbeg, tl.j0);
+    if ((flags & NMGP_B_UPPER) && tl.kbB >= tl.K) kend = min(kend, tl.j0 + GBN);
   }
   kbeg = (kbeg / GBK) * GBK;
   if (zero_tile) {
@@ -83,72 +255,38 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
     kend = max(cb, min(kend, cb + chunk));
     kbeg = cb;
   }
+  tl.kbeg = kbeg;
+  tl.kend = kend;
 
-  const T* __restrict__ A = (const T*)d.A;
-  const T* __restrict__ Bm = (const T*)d.B;
-  const T* __restrict__ ksc = (const T*)d.kscale;
   const int t = threadIdx.x;
   const int lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
-  const bool a_kc = (d.sA_k == 1);
-  const bool b_jc = (d.sB_j == 1);
+  EltMap em;
+  const bool a_kc = (d.sA_k == 1), b_jc = (d.sB_j == 1);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    if (a_kc) { em.a_kl[e] = t & 31; em.a_il[e] = (t >> 5) + 8 * e; }
+    else { em.a_il[e] = t & 63; em.a_kl[e] = (t >> 6) + 4 * e; }
+    if (b_jc) { em.b_jl[e] = t & 63; em.b_kl[e] = (t >> 6) + 4 * e; }
+    else { em.b_kl[e] = t & 31; em.b_jl[e] = (t >> 5) + 8 * e; }
+  }
 
   using acc_t = typename Mfma<T>::acc_t;
   acc_t acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc10 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
-
-  for (int kt = kbeg; kt < kend; kt += GBK) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      int il, kl;
-      if (a_kc) { il = t >> 2; kl = ((t & 3) << 2) + e; }
-      else { kl = t >> 4; il = ((t & 15) << 2) + e; }
-      const int gi = i0 + il, gk = kt + kl;
-      T val = 0;
-      if (gi < m && gk < K) {
-        int kk = gk, kb = 0;
-        if (d.k_seg < 0 && kbA < K) { kb = gk / kbA; kk = gk - kb * kbA; }
-        const bool z = ((flags & NMGP_A_LOWER) && kk > gi) || ((flags & NMGP_A_UPPER) && kk < gi);
-        if (!z) val = A[(r0 + gi) * d.sA_i + (k0 + kk) * d.sA_k + (int64_t)kb * d.sA_kb];
-      }
-      As[kl][il] = val;
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      int kl, jl;
-      if (b_jc) { kl = t >> 4; jl = ((t & 15) << 2) + e; }
-      else { jl = t >> 2; kl = ((t & 3) << 2) + e; }
-      const int gk = kt + kl, gj = j0 + jl;
-      T val = 0;
-      if (gk < K && gj < n) {
-        int kk = gk, kb = 0;
-        if (d.k_seg < 0 && kbB < K) { kb = gk / kbB; kk = gk - kb * kbB; }
-        const bool z = ((flags & NMGP_B_LOWER) && gj > kk) || ((flags & NMGP_B_UPPER) && gj < kk);
-        if (!z) {
-          val = Bm[(k0 + kk) * d.sB_k + (int64_t)gj * d.sB_j + (int64_t)kb * d.sB_kb];
-          if (flags & NMGP_KSCALE) val *= ksc[k0 + gk];
-        }
-      }
-      Bs[kl][jl] = val;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int kr = s * 4 + (lane >> 4);
-      const T a0 = As[kr][wr * 32 + (lane & 15)];
-      const T a1 = As[kr][wr * 32 + 16 + (lane & 15)];
-      const T b0 = Bs[kr][wc * 32 + (lane & 15)];
-      const T b1 = Bs[kr][wc * 32 + 16 + (lane & 15)];
-      acc00 = Mfma<T>::mma(a0, b0, acc00);
-      acc01 = Mfma<T>::mma(a0, b1, acc01);
-      acc10 = Mfma<T>::mma(a1, b0, acc10);
-      acc11 = Mfma<T>::mma(a1, b1, acc11);
-    }
-    __syncthreads();
+  if (kbeg < kend) {
+    const bool kb_fast = (tl.kbA >= tl.K || tl.kbA % GBK == 0) && (tl.kbB >= tl.K || tl.kbB % GBK == 0);
+    if (kb_fast)
+      mainloop_fast<T>(d, tl, em, As, Bs, lane, wr, wc, acc00, acc01, acc10, acc11);
+    else
+      mainloop_general<T>(d, tl, em, As, Bs, lane, wr, wc, acc00, acc01, acc10, acc11);
   }
 
+  const int64_t r0 = tl.r0;
+  const int m = tl.m, n = tl.n, i0 = tl.i0, j0 = tl.j0;
   if (ksplit > 1 && !zero_tile) {
-    // deterministic split-K: publish this chunk's partial, the last arriver sums all chunks in order
-    T* ws = (T*)d.ws + (int64_t)(tm * d.tiles_n + tn) * ksplit * 4096;
-    T* mine = ws + (int64_t)ks * 4096 + t * 16;
+    // deterministic split-K (agent-scope release/acquire hand-off): publish this chunk's partial,
+    // the last arriver sums all chunks in chunk order
+    GPtr<T> ws = (GPtr<T>)d.ws + (int64_t)(tm * d.tiles_n + tn) * ksplit * 4096;
+    GPtr<T> mine = ws + (int64_t)ks * 4096 + t * 16;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       mine[r] = acc00[r];
@@ -169,13 +307,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      s_last = last;
+      *s_last = last;
     }
     __syncthreads();
-    if (!s_last) return;
+    if (!*s_last) return;
     acc00 = acc01 = acc10 = acc11 = acc_t{0, 0, 0, 0};
     for (int c = 0; c < ksplit; ++c) {
-      const T* src = ws + (int64_t)c * 4096 + t * 16;
+      GPtr<const T> src = ws + (int64_t)c * 4096 + t * 16;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         acc00[r] += src[r];
@@ -186,9 +324,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
     }
   }
 
-  T* __restrict__ C = (T*)d.C;
-  const T* __restrict__ E = (const T*)d.epi_E;
-  const T* __restrict__ rsp = (const T*)d.epi_rs;
+  const GPtr<T> C = (GPtr<T>)d.C;
+  const GPtr<const T> E = (GPtr<const T>)d.epi_E;
+  const GPtr<const T> rsp = (GPtr<const T>)d.epi_rs;
   const T alpha = (T)d.alpha, beta = (T)d.beta, gamma = (T)d.gamma, dadd = (T)d.diag_add;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -234,7 +372,7 @@ static int launch_grouped(const nmgp_gemm_desc* d_desc, int nprob, int total_til
   a.nprob = nprob;
   a.seg = d_seg;
   a.inl = nmgp_gemm_desc{};
-  hipLaunchKernelGGL(gemm_kernel<T>, dim3(total_tiles), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((gemm_kernel<T, true>), dim3(total_tiles), dim3(256), 0, s, a, d_desc);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
@@ -254,7 +392,8 @@ static int launch_single(const nmgp_gemm_desc* h, const int32_t* d_seg, hipStrea
   a.nprob = 1;
   a.seg = d_seg;
   a.inl = d;
-  hipLaunchKernelGGL(gemm_kernel<T>, dim3(d.tiles_m * d.tiles_n), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((gemm_kernel<T, false>), dim3(d.tiles_m * d.tiles_n), dim3(256), 0, s, a,
+                     (const nmgp_gemm_desc*)nullptr);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }

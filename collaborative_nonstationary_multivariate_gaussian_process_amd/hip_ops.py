@@ -3,6 +3,7 @@
 Everything here enqueues HIP kernels on torch's current stream; nothing falls back to CPU math.
 """
 import ctypes
+import os
 import math
 
 import torch
@@ -58,6 +59,10 @@ def gemm_desc(C, A, B, m, n, k, sA, sB, sC, *, flags=0, alpha=1.0, beta=0.0, kb=
     return d
 
 
+_KSPLIT_MIN_K = int(os.environ.get("NMGP_KSPLIT_MIN_K", "512"))
+_KSPLIT_CHUNK = int(os.environ.get("NMGP_KSPLIT_CHUNK", "256"))
+
+
 class GemmGroup:
     """A fixed list of GEMM problems launched as ONE grouped kernel (descriptors uploaded once)."""
 
@@ -72,8 +77,9 @@ class GemmGroup:
         self._ws = []
         t = 0
         for i, d in enumerate(descs):
-            if d.ksplit <= 1 and d.k >= 256:
-                d.ksplit = max(1, min(16, d.k // 128, -(-target_wgs // max(group_tiles, 1))))
+            if d.ksplit <= 1 and d.k >= _KSPLIT_MIN_K:
+                # split only while every chunk keeps >= _KSPLIT_CHUNK of k (a split adds a round trip)
+                d.ksplit = max(1, min(16, d.k // _KSPLIT_CHUNK, -(-target_wgs // max(group_tiles, 1))))
             if d.ksplit > 1:
                 ntile = d.tiles_m * d.tiles_n
                 ws = torch.empty(ntile * d.ksplit * 4096, dtype=dtype, device=device)
@@ -98,9 +104,9 @@ class GemmGroup:
         if self.n == 0 or self.total == 0:
             return
         s = stream if stream is not None else L.stream_handle()
+        segp = ctypes.c_void_p(self.seg.data_ptr()) if self.seg is not None else None
         fn = getattr(L.lib(), "nmgp_gemm_grouped_" + _sfx(self.dtype))
-        L.check(fn(ctypes.c_void_p(self.dev.data_ptr()), self.n, self.total,
-                   ctypes.c_void_p(self.seg.data_ptr()) if self.seg is not None else None, s), "gemm_grouped")
+        L.check(fn(ctypes.c_void_p(self.dev.data_ptr()), self.n, self.total, segp, s), "gemm_grouped")
 
 
 def desc_macs(d, seg=None):

@@ -102,7 +102,7 @@ def test_gemm_kblocks_and_segments_grouped(ops):
     assert rel(out3, ref3) < 1e-14
 
 
-@pytest.mark.parametrize("K", [300, 2000, 4099])
+@pytest.mark.parametrize("K", [600, 2000, 4099])
 def test_gemm_split_k_deterministic(ops, K):
     """Long-k products P^T R (few output tiles) take the split-K path; results are bit-identical
     across launches (fixed-order reduction of the chunk partials)."""
