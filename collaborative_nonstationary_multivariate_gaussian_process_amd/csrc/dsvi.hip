@@ -337,49 +337,62 @@ template <typename T> __device__ inline const T* fac_y(const Args& a, int f) {
   return Y + base + ((int64_t)i * D + j) * M;
 }
 
-// row-i sum of squares of tril(S): A1_ii - lam
-template <typename T> __device__ inline T row_sq(const T* S, int M, int i, int lane) {
-  T s = 0;
-  for (int c = lane; c <= i; c += 64) {
-    const T x = S[(int64_t)i * M + c];
-    s += x * x;
-  }
-  return wave_sum(s);
+// KL per factor, parallel over (factor, 16-row slab): 16 lanes per row sum tril(S)_i. squared
+// (A1_ii - lam) with independent loads, then the per-row logdet / trace-quirk / Mahalanobis terms;
+// each block leaves 4 partial sums in klpart[f][slab], summed in slab order by the finalize kernel.
+constexpr int KL_ROWS = 16;
+template <typename T> __device__ inline T* kl_part(const Args& a) {
+  return (T*)a.facbuf + a.NF + 8 * (int64_t)a.M + 4 * (int64_t)a.D * a.D + (int64_t)a.NF * a.M;
 }
 
 template <typename T>
 __global__ __launch_bounds__(256) void dsvi_kl_kernel(Args a) {
-  __shared__ T red[16];
+  __shared__ T red[4][16];
   const int M = a.M, D = a.D, NF = a.NF;
   const int64_t MM = (int64_t)M * M;
   const T lam = (T)a.jitter;
   const T* Af = (const T*)a.Afac;
   T* fb = (T*)a.facbuf;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int f = blockIdx.x, k = prior_of(f, D);
+  const int f = blockIdx.x, k = prior_of(f, D), slab = blockIdx.y;
+  const int q = threadIdx.x & 15, i = slab * KL_ROWS + (threadIdx.x >> 4);
   const T* S = fac_S<T>(a, f);
-  const T* C1 = Af + (int64_t)f * MM;
-  const T* C2 = Af + (int64_t)(NF + k) * MM;
-  const T* mu = fac_mu<T>(a, f);
-  const T* y = fac_y<T>(a, f);
-  T* ev = fb + NF + 8 * (int64_t)M + 4 * (int64_t)D * D + (int64_t)f * M;
   T ld1 = 0, ld2 = 0, t2 = 0, t3 = 0;
-  for (int i = w; i < M; i += 4) {
-    const T a1 = row_sq(S, M, i, lane) + lam;
-    if (lane == 0) {
-      const T c2 = C2[(int64_t)i * M + i];
-      ld1 += dlog(C1[(int64_t)i * M + i]);
-      ld2 += dlog(c2);
-      t2 += a1 / (c2 * c2);
-      t3 += mu[i] * y[i];
-      ev[i] = (T)0.5 - (T)0.5 * a1 / (c2 * c2);   // d KL / d C2_ii * C2_ii / 2 + 1/2
+  T sq = 0;
+  if (i < M) {
+    for (int c = q; c <= i; c += 16) {
+      const T x = S[(int64_t)i * M + c];
+      sq += x * x;
     }
   }
-  ld1 = block_sum(ld1, red);
-  ld2 = block_sum(ld2, red);
-  t2 = block_sum(t2, red);
-  t3 = block_sum(t3, red);
-  if (threadIdx.x == 0) fb[f] = ld2 - ld1 + (T)0.5 * (t2 + t3 - (T)M);
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+  if (i < M && q == 0) {
+    const T* C1 = Af + (int64_t)f * MM;
+    const T* C2 = Af + (int64_t)(NF + k) * MM;
+    const T a1 = sq + lam;
+    const T c2 = C2[(int64_t)i * M + i];
+    ld1 = dlog(C1[(int64_t)i * M + i]);
+    ld2 = dlog(c2);
+    t2 = a1 / (c2 * c2);
+    t3 = fac_mu<T>(a, f)[i] * fac_y<T>(a, f)[i];
+    T* ev = fb + NF + 8 * (int64_t)M + 4 * (int64_t)D * D + (int64_t)f * M;
+    ev[i] = (T)0.5 - (T)0.5 * a1 / (c2 * c2);   // d KL / d C2_ii * C2_ii / 2 + 1/2
+  }
+  // rows of this block in order: lane 0 of each 16-lane group holds one row's terms
+  T v[4] = {ld1, ld2, t2, t3};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    T x = v[j];
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) x += __shfl_xor(x, o, 64);   // the 4 rows of this wave
+    if ((threadIdx.x & 63) == 0) red[j][threadIdx.x >> 6] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int j = threadIdx.x;
+    const T tot = red[j][0] + red[j][1] + red[j][2] + red[j][3];
+    kl_part<T>(a)[((int64_t)f * gridDim.y + slab) * 4 + j] = tot;
+  }
 }
 
 // delta_k[i] = sum over the factors of prior k of e_f[i];  wvec_k[i] = 1 / C2_ii^2
@@ -432,13 +445,16 @@ __global__ __launch_bounds__(256) void dsvi_tbwd_kernel(Args a) {
 }
 
 // ------------------------------------------------------------------------------------ v backward
-// vbar = P_t^T tbar (already in a.vbar) + ell_Z * dL/dell_Z ;  w = C_v^T vbar ;
-// Psi = Phi + Phi^T with Phi = tril(w z_v^T), diagonal halved (Cholesky backward)
+// vbar = P_t^T tbar (a.vbar[0:M]) + ell_Z * dL/dell_Z  -> a.vbar[M:2M];  w = C_v^T vbar ;
+// Psi = Phi + Phi^T with Phi = tril(w z_v^T), diagonal halved (Cholesky backward).
+// Grid over row blocks of Psi: every block rebuilds vbar (cheap, coalesced partial sums), computes w
+// for its VBW_ROWS rows (one wave-reduction each) and writes those rows and the mirrored columns.
+constexpr int VBW_ROWS = 8;
 template <typename T>
-__global__ __launch_bounds__(1024) void dsvi_vbwd_kernel(Args a) {
+__global__ __launch_bounds__(256) void dsvi_vbwd_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   T* vbs = (T*)smem_raw;
-  T* ws = vbs + a.M;
+  T* wrow = vbs + a.M;
   const int M = a.M, B = a.B;
   const T* gcol = (const T*)a.gib_col;
   const T* grow = (const T*)a.gib_row;
@@ -450,22 +466,33 @@ __global__ __launch_bounds__(1024) void dsvi_vbwd_kernel(Args a) {
     for (int ct = 0; ct < a.n_ct; ++ct) ez += grow[(int64_t)a.n_ct * B + (int64_t)ct * M + c];   // G22 rows
     for (int rt = 0; rt < a.n_rt22; ++rt) ez += gcol[(int64_t)a.n_rt * M + (int64_t)rt * M + c];  // G22 cols
     const T vb = vbar[c] + ez * ellZ[c];
-    vbar[c] = vb;
     vbs[c] = vb;
+    if (blockIdx.x == 0) vbar[M + c] = vb;
   }
   __syncthreads();
   const T* Cv = (const T*)a.Afac + (int64_t)(a.NF - 1) * M * M;
-  for (int i = threadIdx.x; i < M; i += blockDim.x) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int i0 = blockIdx.x * VBW_ROWS;
+  for (int r = wv; r < VBW_ROWS; r += 4) {
+    const int i = i0 + r;
     T s = 0;
-    for (int k = i; k < M; ++k) s += Cv[(int64_t)k * M + i] * vbs[k];
-    ws[i] = s;
+    if (i < M)
+      for (int k = i + lane; k < M; k += 64) s += Cv[(int64_t)k * M + i] * vbs[k];
+    s = wave_sum(s);
+    if (lane == 0) wrow[r] = s;
   }
   __syncthreads();
   const T* zv = (const T*)a.noise;
   T* phi = (T*)a.phi;
-  for (int64_t idx = threadIdx.x; idx < (int64_t)M * M; idx += blockDim.x) {
-    const int i = (int)(idx / M), j = (int)(idx - (int64_t)i * M);
-    phi[idx] = i > j ? ws[i] * zv[j] : (i < j ? ws[j] * zv[i] : ws[i] * zv[i]);
+  for (int r = 0; r < VBW_ROWS; ++r) {
+    const int i = i0 + r;
+    if (i >= M) break;
+    const T wi = wrow[r];
+    for (int j = threadIdx.x; j <= i; j += blockDim.x) {
+      const T v = wi * zv[j];
+      phi[(int64_t)i * M + j] = v;     // row i, j <= i (diagonal: w_i z_i, the halved sum)
+      if (j < i) phi[(int64_t)j * M + i] = v;
+    }
   }
 }
 
@@ -491,8 +518,14 @@ __global__ __launch_bounds__(256) void dsvi_finalize_kernel(Args a) {
   c1 = block_sum(c1, red);
   vs = block_sum(vs, red);
   T klw = 0, klv = 0, klu = 0;
+  const int nslab = (M + KL_ROWS - 1) / KL_ROWS;
+  const T* kp = kl_part<T>(a);
   for (int f = threadIdx.x; f < NF; f += blockDim.x) {
-    const T v = fb[f];
+    T p[4] = {0, 0, 0, 0};
+    for (int sl = 0; sl < nslab; ++sl)
+      for (int j = 0; j < 4; ++j) p[j] += kp[((int64_t)f * nslab + sl) * 4 + j];
+    const T v = p[1] - p[0] + (T)0.5 * (p[2] + p[3] - (T)M);
+    ((T*)a.facbuf)[f] = v;                       // per-factor KL (kept for inspection)
     if (f < D) klw += v; else if (f == NF - 1) klv += v; else klu += v;
   }
   klw = block_sum(klw, red);
@@ -549,7 +582,7 @@ __global__ __launch_bounds__(256) void dsvi_finalize_kernel(Args a) {
   // KL mean gradients A2^{-1} mu (Y) and mu_v += vbar
   const T* Y = (const T*)a.Y;
   for (int64_t idx = threadIdx.x; idx < (int64_t)D * M; idx += blockDim.x) g[a.off_muW + idx] += Y[idx];
-  const T* vbar = (const T*)a.vbar;
+  const T* vbar = (const T*)a.vbar + M;   // completed by the v-backward kernel
   for (int c = threadIdx.x; c < M; c += blockDim.x) g[a.off_muv + c] += vbar[c] + Y[(int64_t)D * M + c];
   const int64_t yu0 = (int64_t)(D + 1) * M, yu1 = yu0 + (int64_t)D * D * M;
   for (int64_t idx = threadIdx.x; idx < (int64_t)D * D * M; idx += blockDim.x) {
@@ -653,7 +686,8 @@ int nmgp_dsvi_recon_f64(const Args* a, hipStream_t s) {
 }
 int nmgp_dsvi_kl_f64(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
-  hipLaunchKernelGGL(nmgp::dsvi_kl_kernel<double>, dim3(a->NF), dim3(256), 0, s, *a);
+  hipLaunchKernelGGL(nmgp::dsvi_kl_kernel<double>, dim3(a->NF, (a->M + nmgp::KL_ROWS - 1) / nmgp::KL_ROWS), dim3(256), 0,
+                     s, *a);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
@@ -672,7 +706,8 @@ int nmgp_dsvi_tbwd_f64(const Args* a, hipStream_t s) {
 int nmgp_dsvi_vbwd_f64(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
   const size_t sm = (size_t)2 * a->M * sizeof(double);
-  hipLaunchKernelGGL(nmgp::dsvi_vbwd_kernel<double>, dim3(1), dim3(1024), sm, s, *a);
+  hipLaunchKernelGGL(nmgp::dsvi_vbwd_kernel<double>, dim3((a->M + nmgp::VBW_ROWS - 1) / nmgp::VBW_ROWS), dim3(256), sm,
+                     s, *a);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }

@@ -78,10 +78,12 @@ class DsviEngine:
         self.Y = e(D + 1 + 2 * D * D, M)
         self.Xs = e(NF, M, M)
         self.T2 = e(M, M)
-        self.v, self.vbar, self.ellZ = e(M), e(M), e(M)
+        self.v, self.ellZ = e(M), e(M)
+        self.vbar = e(2 * M)            # [0:M] P_t^T tbar (GEMM), [M:2M] completed by the v-backward kernel
         self.ellX, self.var_t = e(B), e(B)
         self.rowbuf = e(2 * D + 5, B)
-        self.facbuf = e(NF + 8 * M + 4 * D * D + NF * M)
+        # KL per factor | delta/w vectors (8M) | selection weights (4D^2) | e_f rows (NF M) | KL slab partials
+        self.facbuf = e(NF + 8 * M + 4 * D * D + NF * M + NF * ((M + 15) // 16) * 4)
         self.nblk = (B + 3) // 4
         self.red = e(5 * self.nblk)
         self.out = e(8)
