@@ -340,24 +340,28 @@ template <> __device__ inline float readlane<float>(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
-// 1/sqrt(d): hardware estimate + Newton steps (2 for f64, 1 for f32) -> correctly rounded to ~1 ulp.
-template <typename T> __device__ inline T rsq_nr(T d);
-template <> __device__ inline double rsq_nr<double>(double d) {
-  double y = __builtin_amdgcn_rsq(d);
-#ifndef NMGP_RSQ_ONE_STEP
-  double h = d * y, r = fma(-h, y, 1.0);
-  y = fma(0.5 * y, r, y);
-  h = d * y;
-  r = fma(-h, y, 1.0);
-#else
-  const double h = d * y, r = fma(-h, y, 1.0);
-#endif
-  return fma(0.5 * y, r, y);
+// s = sqrt(d) and inv = 1/s, both rounded to nearest as IEEE sqrt and division give them (the
+// LAPACK dpotf2 pivot: sqrt, then scale by ONE/AJJ), in 9 dependent FMA-pipe operations instead of
+// the ~25 of the library expansions: rsqrt estimate + one Newton step (rel. err ~2^-46), a Markstein
+// residual correction for the square root and one for the reciprocal from the same estimate.  d is a
+// positive normal pivot; non-positive / NaN pivots propagate NaN (flagged by the caller).  A plain
+// refined rsqrt (s = d*y, inv = y) is 1-2 ulp off and measurably moved the trained model.pt loss
+// through a cancelling pivot (4.9e-9 relative), so both results are corrected.
+template <typename T> __device__ inline void sqrt_recip(T d, T& s, T& inv);
+template <> __device__ inline void sqrt_recip<double>(double d, double& s, double& inv) {
+  const double y0 = __builtin_amdgcn_rsq(d);
+  const double h = d * y0;
+  const double r = fma(-h, y0, 1.0);
+  const double y1 = fma(0.5 * y0, r, y0);
+  const double s0 = d * y1;
+  const double rr = fma(-s0, s0, d);
+  s = fma(rr, 0.5 * y1, s0);
+  const double e = fma(-s, y1, 1.0);
+  inv = fma(y1, e, y1);
 }
-template <> __device__ inline float rsq_nr<float>(float d) {
-  const float y = __builtin_amdgcn_rsqf(d);
-  const float h = d * y, r = fmaf(-h, y, 1.0f);
-  return fmaf(0.5f * y, r, y);
+template <> __device__ inline void sqrt_recip<float>(float d, float& s, float& inv) {
+  s = sqrtf(d);
+  inv = 1.0f / s;
 }
 
 template <typename T, int NTPW>
@@ -442,18 +446,15 @@ __global__ __launch_bounds__(RW * 64) void chol_inv_kernel(T* A, int n, int64_t 
 #pragma unroll
         for (int c = 0; c < 16; ++c) a[c] = fma(src[c], keep, (ident && c == lr) ? (T)1 : (T)0);
       }
-      // Critical path per column: readlane(d) -> sqrt -> reciprocal -> scale -> readlane -> fma.
-      // IEEE sqrt and a rounded reciprocal as LAPACK dpotf2 (sqrt, then DSCAL by ONE/AJJ): pivots
-      // with cancellation amplify a 1-ulp difference here (a refined rsqrt cost 1e-14 on the
-      // trained model.pt state against the reference).
+      // Critical path per column: readlane(d) -> sqrt_recip -> scale -> readlane -> fma.
       CHOL_STAMPW(kb, 0);
       unsigned int bad = 0;  // non-positive (or NaN) pivots of this block; NaN propagates onwards
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const T d = readlane(a[j], j);
         bad |= (d > (T)0) ? 0u : (1u << j);
-        const T sj = dsqrt(d);
-        const T inv = (T)1 / sj;
+        T sj, inv;
+        sqrt_recip(d, sj, inv);
         a[j] = (lane == j) ? sj : a[j] * inv;
 #pragma unroll
         for (int c = j + 1; c < 16; ++c) a[c] = fma(-a[j], readlane(a[j], c), a[c]);

@@ -59,8 +59,23 @@ def gemm_desc(C, A, B, m, n, k, sA, sB, sC, *, flags=0, alpha=1.0, beta=0.0, kb=
     return d
 
 
-_KSPLIT_MIN_K = int(os.environ.get("NMGP_KSPLIT_MIN_K", "512"))
-_KSPLIT_CHUNK = int(os.environ.get("NMGP_KSPLIT_CHUNK", "256"))
+
+
+GEMM_BK = 32   # k-tile of gemm_kernel (csrc/gemm.hip GBK)
+
+
+def _auto_ksplit(k_eff, group_tiles, work_per_wg):
+    """Split-K factor of one problem.  A split costs a workspace round trip and an ordered
+    reduction by the last arriver, so it is used only where it shortens the launch's critical
+    path (measured with tools/gemm_probe.py): tiny groups (<= 64 tiles: latency-bound k loops, chunks
+    down to 2 k-tiles), and problems whose k loop is more than twice the balanced per-workgroup
+    share (chunks >= 4 k-tiles)."""
+    kt = -(-max(k_eff, 1) // GEMM_BK)
+    if group_tiles <= 64 and kt >= 4:
+        return max(1, min(16, kt // 2, -(-256 // max(group_tiles, 1))))
+    if kt > 2 * work_per_wg and kt >= 8:
+        return max(1, min(16, kt // 4, -(-kt // work_per_wg)))
+    return 1
 
 
 class GemmGroup:
@@ -73,13 +88,19 @@ class GemmGroup:
         self.seg = seg
         arr = (L.GemmDesc * len(descs))()
         group_tiles = sum(d.tiles_m * d.tiles_n for d in descs)
+        nseg = (seg.numel() - 1) if seg is not None else 1
+        # expected k / rows of segment-addressed problems: their share of the (balanced) segments
+        frac = lambda d, s_: (max(d.seg_span, 1) / nseg) if s_ >= 0 else 1.0
+        eff = [(max(1, round(d.tiles_m * frac(d, d.row_seg))) * d.tiles_n,
+                max(1, round(max(d.k, 1) * frac(d, d.k_seg)))) for d in descs]
+        total_ktiles = sum(t_ * -(-k_ // GEMM_BK) for t_, k_ in eff)
+        work_per_wg = max(2, total_ktiles // target_wgs)   # k-tiles per workgroup if the launch were balanced
         esz = 8 if dtype == _F64 else 4
         self._ws = []
         t = 0
         for i, d in enumerate(descs):
-            if d.ksplit <= 1 and d.k >= _KSPLIT_MIN_K:
-                # split only while every chunk keeps >= _KSPLIT_CHUNK of k (a split adds a round trip)
-                d.ksplit = max(1, min(16, d.k // _KSPLIT_CHUNK, -(-target_wgs // max(group_tiles, 1))))
+            if d.ksplit <= 1:
+                d.ksplit = _auto_ksplit(eff[i][1], group_tiles, work_per_wg)
             if d.ksplit > 1:
                 ntile = d.tiles_m * d.tiles_n
                 ws = torch.empty(ntile * d.ksplit * 4096, dtype=dtype, device=device)
