@@ -254,7 +254,12 @@ class DsviEngine:
                          flags=L.A_UPPER | L.B_LOWER | L.OUT_TRIL | L.EPI_E_LOWER, alpha=-1.0, beta=1.0,
                          epi=(th, fac_off[f], (M, 1), (fb, NF + 4 * M + k * M), 1.0),
                          offs=(f * MM, f * MM, fac_off[f])))
-        p["bwd_solve"] = G(d18)
+        # R products on the main chain; the KL-only parts (prior adjoint init, L-bar of the variational
+        # factors) depend on forward quantities only and run on the side stream, overlapped with
+        # quad / recon (see _schedule)
+        p["bwd_R"] = G(d18[:3])
+        p["kl_abar"] = G(d18[3:7])
+        p["kl_lbar"] = G(d18[7:])
         # B4: Abar_k -= 1/2 Y_k diag(sel_k) Y_k^T
         ybase = [D * M, (D + 1) * M, (D + 1 + D * D) * M, 0]
         ncol = [1, D * D, D * D, D]
@@ -369,7 +374,7 @@ class DsviEngine:
         need_side = (not elbo_mode) or with_kl
         steps = []
         if need_side:
-            steps += [("fork",),
+            steps += [("sig", "main", "fork"), ("wait", "side", "fork"),
                       ("syrk_side", "gemm", gemm("syrk_side"), "side"),
                       ("chol_side", "chol", chol(0, FV), "side")]
             if not elbo_mode:
@@ -386,23 +391,35 @@ class DsviEngine:
             ("chol_G", "chol", chol(NF + 3, 1), "main"),
             ("invG", "gemm", gemm("invG"), "main"),
             ("projG", "gemm", gemm("projG"), "main"),
-            ("quad", "gemm", gemm("quad"), "main"),
         ]
-        if need_side:
-            steps.append(("join",))
         if elbo_mode:
+            steps.append(("quad", "gemm", gemm("quad"), "main"))
+            if need_side:
+                steps += [("sig", "side", "join"), ("wait", "main", "join")]
             if with_kl:
                 steps.append(("kl", "row", row(lib.nmgp_dsvi_kl_f64), "main"))
             steps += [("recon", "row", row(lib.nmgp_dsvi_recon_f64), "main"),
                       ("finalize", "row", row(lib.nmgp_dsvi_finalize_f64), "main")]
             return steps
+        # KL branch on the side stream once all prior factors and Y = A^-1 mu exist (after projG):
+        # KL terms, prior-diagonal adjoints, the variational factors' KL L-bar (first writer of those
+        # gradient rows -- bwd_w waits for it, so the accumulation order is fixed) and the KL part of
+        # the prior adjoints Abar (bwd_pr waits for it)
         steps += [
-            ("kl", "row", row(lib.nmgp_dsvi_kl_f64), "main"),
-            ("delta", "row", row(lib.nmgp_dsvi_delta_f64), "main"),
+            ("sig", "main", "kl_in"), ("wait", "side", "kl_in"),
+            ("kl", "row", row(lib.nmgp_dsvi_kl_f64), "side"),
+            ("delta", "row", row(lib.nmgp_dsvi_delta_f64), "side"),
+            ("kl_lbar", "gemm", gemm("kl_lbar"), "side"),
+            ("sig", "side", "kl_lbar"),
+            ("kl_abar", "gemm", gemm("kl_abar"), "side"),
+            ("bwd_kly", "gemm", gemm("bwd_kly"), "side"),
+            ("sig", "side", "kl_done"),
+            ("quad", "gemm", gemm("quad"), "main"),
             ("recon", "row", row(lib.nmgp_dsvi_recon_f64), "main"),
+            ("wait", "main", "kl_lbar"),
             ("bwd_w", "gemm", gemm("bwd_w"), "main"),
-            ("bwd_solve", "gemm", gemm("bwd_solve"), "main"),
-            ("bwd_kly", "gemm", gemm("bwd_kly"), "main"),
+            ("bwd_R", "gemm", gemm("bwd_R"), "main"),
+            ("wait", "main", "kl_done"),
             ("bwd_pr", "gemm", gemm("bwd_pr"), "main"),
             ("bwd_build", "pairwise_bwd", pw("bwd_build"), "main"),
             ("tbwd", "row", row(lib.nmgp_dsvi_tbwd_f64), "main"),
@@ -423,17 +440,19 @@ class DsviEngine:
             if getattr(self, "_side", None) is None:
                 self._side = torch.cuda.Stream(device=self.dev)
             s_side = ctypes.c_void_p(self._side.cuda_stream)
+        events = {}
         for item in steps:
-            if len(item) == 1:
+            if item[0] in ("sig", "wait"):
                 if timer is not None:
                     continue                       # timed runs are serial on one stream
-                ev = torch.cuda.Event()
-                if item[0] == "fork":
-                    ev.record(main)
-                    self._side.wait_event(ev)
+                _, who, tag = item
+                st = main if who == "main" else self._side
+                if item[0] == "sig":
+                    ev = torch.cuda.Event()
+                    ev.record(st)
+                    events[tag] = ev
                 else:
-                    ev.record(self._side)
-                    main.wait_event(ev)
+                    st.wait_event(events[tag])
                 continue
             name, kind, fn, where = item
             if timer is not None:
