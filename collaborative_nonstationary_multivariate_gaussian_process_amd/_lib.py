@@ -29,7 +29,8 @@ class GemmDesc(ctypes.Structure):
                 ("row_seg", c_int), ("k_seg", c_int),
                 ("alpha", c_dbl), ("beta", c_dbl), ("gamma", c_dbl), ("diag_add", c_dbl),
                 ("tiles_m", c_int), ("tiles_n", c_int), ("tile_start", c_int), ("seg_span", c_int),
-                ("ksplit", c_int), ("pad2_", c_int), ("ws", c_vp), ("counters", c_vp)]
+                ("ksplit", c_int), ("pad2_", c_int), ("ws", c_vp), ("counters", c_vp),
+                ("sA_b", c_i64), ("sB_b", c_i64), ("sC_b", c_i64), ("batch", c_int), ("pad3_", c_int)]
 
 
 class PairwiseDesc(ctypes.Structure):

@@ -366,7 +366,8 @@ template <> __device__ inline void sqrt_recip<float>(float d, float& s, float& i
 
 template <typename T, int NTPW>
 __global__ __launch_bounds__(RW * 64) void chol_inv_kernel(T* A, int n, int64_t lda, int64_t strideA, T* X,
-                                                           int64_t ldx, int64_t strideX, int32_t* info) {
+                                                           int64_t ldx, int64_t strideX, int32_t* info,
+                                                           int col_off, int info_first) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   using acc_t = typename Mfma<T>::acc_t;
   const int nt = (n + 15) >> 4, NR = nt * 16;
@@ -536,7 +537,12 @@ __global__ __launch_bounds__(RW * 64) void chol_inv_kernel(T* A, int n, int64_t 
     }
   }
   CHOL_STAMP(nt, 0);
-  if (t == 0 && info) info[blockIdx.x] = first_fail;  // wave 0 tracked the pivots
+  // wave 0 tracked the pivots; in a blocked factorization (col_off > 0) an earlier block's failure
+  // stays the reported one
+  if (t == 0 && info) {
+    if (info_first) info[blockIdx.x] = first_fail ? first_fail + col_off : 0;
+    else if (first_fail && info[blockIdx.x] == 0) info[blockIdx.x] = first_fail + col_off;
+  }
 }
 
 template <typename T> static size_t chol_inv_smem(int n) {
@@ -597,7 +603,7 @@ static int trtri_launch(const T* L, int64_t n, int64_t ldl, int64_t strideL, T* 
 
 template <typename T, int NTPW>
 static void chol_inv_go(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx, int64_t sX, int64_t batch,
-                        int32_t* info, size_t sm, hipStream_t s) {
+                        int32_t* info, size_t sm, hipStream_t s, int col_off, int info_first) {
   static bool attr_done = false;
   if (!attr_done) {
     (void)hipFuncSetAttribute((const void*)chol_inv_kernel<T, NTPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -605,11 +611,107 @@ static void chol_inv_go(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx,
     attr_done = true;
   }
   hipLaunchKernelGGL((chol_inv_kernel<T, NTPW>), dim3((unsigned)batch), dim3(RW * 64), sm, s, A, n, lda, sA, X, ldx,
-                     sX, info);
+                     sX, info, col_off, info_first);
 }
 
-// L = chol(A) in place and X = L^{-1}: fused register-resident kernel for n <= 256, otherwise the
-// separate potrf and trtri kernels back to back on the same stream.
+// one diagonal block (n <= 256) with the fused register-resident kernel
+template <typename T>
+static int chol_inv_small(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx, int64_t sX, int64_t batch,
+                          int32_t* info, hipStream_t s, int col_off, int info_first) {
+  const int nt = (n + 15) >> 4, ntiles = nt * (nt + 1) / 2;
+  const size_t sm = chol_inv_smem<T>(n);
+  if (ntiles <= RW * 1)
+    chol_inv_go<T, 1>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+  else if (ntiles <= RW * 3)
+    chol_inv_go<T, 3>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+  else if (ntiles <= RW * 5)
+    chol_inv_go<T, 5>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+  else if (ntiles <= RW * 9)
+    chol_inv_go<T, 9>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+  else
+    chol_inv_go<T, 17>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
+
+// rows x cols block copy / zero, batched over blockIdx.y (the blocked path's scratch moves)
+template <typename T>
+__global__ __launch_bounds__(256) void block_copy_kernel(const T* src, int64_t lds, int64_t sS, T* dst, int64_t ldd,
+                                                         int64_t sD, int rows, int cols) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)rows * cols) return;
+  const int r = (int)(idx / cols), c = (int)(idx - (int64_t)r * cols);
+  const int64_t b = blockIdx.y;
+  dst[b * sD + (int64_t)r * ldd + c] = src ? src[b * sS + (int64_t)r * lds + c] : (T)0;
+}
+template <typename T>
+static int block_copy(const T* src, int64_t lds, int64_t sS, T* dst, int64_t ldd, int64_t sD, int rows, int cols,
+                      int64_t batch, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return NMGP_OK;
+  const int64_t nb = ((int64_t)rows * cols + 255) / 256;
+  hipLaunchKernelGGL(block_copy_kernel<T>, dim3((unsigned)nb, (unsigned)batch), dim3(256), 0, s, src, lds, sS, dst, ldd,
+                     sD, rows, cols);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
+
+static nmgp_gemm_desc gdesc(const void* A, int64_t sAi, int64_t sAk, const void* B, int64_t sBk, int64_t sBj, void* C,
+                            int64_t sCi, int64_t sCj, int m, int n, int k, int flags, double alpha, double beta,
+                            int64_t sAb, int64_t sBb, int64_t sCb, int64_t batch) {
+  nmgp_gemm_desc d{};
+  d.A = A; d.B = B; d.C = C;
+  d.sA_i = sAi; d.sA_k = sAk; d.sB_k = sBk; d.sB_j = sBj; d.sC_i = sCi; d.sC_j = sCj;
+  d.m = m; d.n = n; d.k = k; d.flags = flags; d.row_seg = -1; d.k_seg = -1;
+  d.alpha = alpha; d.beta = beta;
+  d.sA_b = sAb; d.sB_b = sBb; d.sC_b = sCb; d.batch = (int)batch;
+  return d;
+}
+
+// Recursive factor + inverse for n > 256 (the HCP / ECoG / stress shapes).  With A split at n1
+// (a multiple of 128 near n/2):
+//   [L11, X11] = chol_inv(A11)                         (recursion; leaves <= 128: fused kernel)
+//   L21 = A21 X11^T                                    (GEMM, A21 staged in X21's place)
+//   A22 -= L21 L21^T                                   (GEMM, lower output only -- the SYRK)
+//   [L22, X22] = chol_inv(A22)                         (recursion)
+//   X21 = -X22 (L21 X11)                               (two GEMMs, product staged transposed in X12)
+// so the 2 n^3 / 3 flops run in GEMMs of size ~n/2, n/4, ... on the matrix cores, and only the
+// 128-wide leaves are serial.  X's strictly upper part is scratch and is left zero; the factor's
+// strictly upper part is zeroed block by block.
+template <typename T>
+static int chol_inv_rec(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx, int64_t sX, int64_t batch,
+                        int32_t* info, hipStream_t s, int col_off) {
+  if (n <= 128) return chol_inv_small<T>(A, n, lda, sA, X, ldx, sX, batch, info, s, col_off, col_off == 0);
+  int n1 = ((n / 2 + 127) / 128) * 128;
+  if (n1 >= n) n1 = n - 128;
+  const int n2 = n - n1;
+  int rc;
+  T* A21 = A + (int64_t)n1 * lda;
+  T* A22 = A21 + n1;
+  T* X21 = X + (int64_t)n1 * ldx;
+  T* X22 = X21 + n1;
+  T* X12 = X + n1;
+  if ((rc = chol_inv_rec<T>(A, n1, lda, sA, X, ldx, sX, batch, info, s, col_off)) != NMGP_OK) return rc;
+  if ((rc = block_copy<T>(A21, lda, sA, X21, ldx, sX, n2, n1, batch, s)) != NMGP_OK) return rc;
+  // L21 = A21 X11^T   (B(k,j) = X11[j][k]: upper triangular)
+  nmgp_gemm_desc d1 = gdesc(X21, ldx, 1, X, 1, ldx, A21, lda, 1, n2, n1, n1, NMGP_B_UPPER, 1.0, 0.0, sX, sX, sA, batch);
+  if ((rc = gemm_single<T>(d1, s)) != NMGP_OK) return rc;
+  // A22 -= L21 L21^T (lower)
+  nmgp_gemm_desc d2 = gdesc(A21, lda, 1, A21, 1, lda, A22, lda, 1, n2, n2, n1, NMGP_OUT_LOWER, -1.0, 1.0, sA, sA, sA,
+                            batch);
+  if ((rc = gemm_single<T>(d2, s)) != NMGP_OK) return rc;
+  if ((rc = block_copy<T>(nullptr, 0, 0, A + n1, lda, sA, n1, n2, batch, s)) != NMGP_OK) return rc;   // L12 = 0
+  if ((rc = chol_inv_rec<T>(A22, n2, lda, sA, X22, ldx, sX, batch, info, s, col_off + n1)) != NMGP_OK) return rc;
+  // T = L21 X11 (X11 lower) stored transposed in X12;  X21 = -X22 T
+  nmgp_gemm_desc d3 = gdesc(A21, lda, 1, X, ldx, 1, X12, 1, ldx, n2, n1, n1, NMGP_B_LOWER, 1.0, 0.0, sA, sX, sX, batch);
+  if ((rc = gemm_single<T>(d3, s)) != NMGP_OK) return rc;
+  nmgp_gemm_desc d4 = gdesc(X22, ldx, 1, X12, 1, ldx, X21, ldx, 1, n2, n1, n2, NMGP_A_LOWER, -1.0, 0.0, sX, sX, sX,
+                            batch);
+  if ((rc = gemm_single<T>(d4, s)) != NMGP_OK) return rc;
+  return block_copy<T>(nullptr, 0, 0, X12, ldx, sX, n1, n2, batch, s);   // X12 = 0
+}
+
+// L = chol(A) in place and X = L^{-1}: fused register-resident kernel for n <= 256, the recursive
+// GEMM-based path above otherwise.
 template <typename T>
 static int chol_inv_launch(T* A, int64_t n, int64_t lda, int64_t sA, T* X, int64_t ldx, int64_t sX, int64_t batch,
                            int32_t* info, hipStream_t s) {
@@ -620,25 +722,9 @@ static int chol_inv_launch(T* A, int64_t n, int64_t lda, int64_t sA, T* X, int64
   if (ldx < n) return -6;
   if (batch < 0) return -8;
   if (n == 0 || batch == 0) return NMGP_OK;
-  if (n > 256) {
-    const int rc = potrf_launch<T>(A, n, lda, sA, batch, info, s);
-    if (rc != NMGP_OK) return rc;
-    return trtri_launch<T>(A, n, lda, sA, X, ldx, sX, batch, s);
-  }
-  const int nt = (int)((n + 15) >> 4), ntiles = nt * (nt + 1) / 2;
-  const size_t sm = chol_inv_smem<T>((int)n);
-  if (ntiles <= RW * 1)
-    chol_inv_go<T, 1>(A, (int)n, lda, sA, X, ldx, sX, batch, info, sm, s);
-  else if (ntiles <= RW * 3)
-    chol_inv_go<T, 3>(A, (int)n, lda, sA, X, ldx, sX, batch, info, sm, s);
-  else if (ntiles <= RW * 5)
-    chol_inv_go<T, 5>(A, (int)n, lda, sA, X, ldx, sX, batch, info, sm, s);
-  else if (ntiles <= RW * 9)
-    chol_inv_go<T, 9>(A, (int)n, lda, sA, X, ldx, sX, batch, info, sm, s);
-  else
-    chol_inv_go<T, 17>(A, (int)n, lda, sA, X, ldx, sX, batch, info, sm, s);
-  NMGP_CHECK_LAUNCH();
-  return NMGP_OK;
+  if (batch > 65535) return -8;
+  if (n > 256) return chol_inv_rec<T>(A, (int)n, lda, sA, X, ldx, sX, batch, info, s, 0);
+  return chol_inv_small<T>(A, (int)n, lda, sA, X, ldx, sX, batch, info, s, 0, 1);
 }
 
 }  // namespace nmgp

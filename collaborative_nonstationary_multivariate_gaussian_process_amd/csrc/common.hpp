@@ -46,6 +46,9 @@ template <> struct Mfma<float> {
 // Only valid where waves exchange data exclusively through LDS.
 __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// single-problem (optionally batched) GEMM launch, defined in gemm.hip
+template <typename T> int gemm_single(const nmgp_gemm_desc& d, hipStream_t s);
+
 template <typename T> __device__ inline T shfl(T v, int src) { return __shfl(v, src, 64); }
 
 template <typename T> __device__ inline T wave_sum(T v) {

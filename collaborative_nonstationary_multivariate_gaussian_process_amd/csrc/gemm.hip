@@ -206,7 +206,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args, const nmgp_gem
   }
   // by value from a read-only uniform address: scalar loads once (a reference would be re-read after
   // every barrier, whose asm clobbers memory)
-  const nmgp_gemm_desc d = GROUPED ? descs[idx] : args.inl;
+  nmgp_gemm_desc d = GROUPED ? descs[idx] : args.inl;
+  if (!GROUPED && d.batch > 1) {            // batched single problem: blockIdx.y = problem
+    const int64_t b = blockIdx.y;
+    d.A = (const char*)d.A + b * d.sA_b * (int64_t)sizeof(T);
+    d.B = (const char*)d.B + b * d.sB_b * (int64_t)sizeof(T);
+    d.C = (char*)d.C + b * d.sC_b * (int64_t)sizeof(T);
+  }
   tile -= d.tile_start;
   const int ksplit = d.ksplit > 1 ? d.ksplit : 1;
   const int ks = tile % ksplit;
@@ -392,11 +398,16 @@ static int launch_single(const nmgp_gemm_desc* h, const int32_t* d_seg, hipStrea
   a.nprob = 1;
   a.seg = d_seg;
   a.inl = d;
-  hipLaunchKernelGGL((gemm_kernel<T, false>), dim3(d.tiles_m * d.tiles_n), dim3(256), 0, s, a,
-                     (const nmgp_gemm_desc*)nullptr);
+  hipLaunchKernelGGL((gemm_kernel<T, false>), dim3(d.tiles_m * d.tiles_n, d.batch > 1 ? d.batch : 1), dim3(256), 0, s,
+                     a, (const nmgp_gemm_desc*)nullptr);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
+
+// internal entry for other translation units (blocked Cholesky)
+template <typename T> int gemm_single(const nmgp_gemm_desc& d, hipStream_t s) { return launch_single<T>(&d, nullptr, s); }
+template int gemm_single<double>(const nmgp_gemm_desc&, hipStream_t);
+template int gemm_single<float>(const nmgp_gemm_desc&, hipStream_t);
 
 }  // namespace nmgp
 

@@ -74,6 +74,10 @@ typedef struct nmgp_gemm_desc {
   int32_t ksplit, pad2_;
   void* ws;
   int32_t* counters;
+  /* batch (single-problem launches only): problem b uses A + b*sA_b, B + b*sB_b, C + b*sC_b;
+   * batch <= 1 means one problem.  Split-K and batch are exclusive.                           */
+  int64_t sA_b, sB_b, sC_b;
+  int32_t batch, pad3_;
 } nmgp_gemm_desc;
 
 /* d_desc: device array of nprob descriptors (tiles_m/tiles_n/tile_start filled by the host,
@@ -103,8 +107,10 @@ int nmgp_trtri_batched_f32(const float* L, int64_t n, int64_t ldl, int64_t strid
                            float* X, int64_t ldx, int64_t strideX, int64_t batch, hipStream_t stream);
 /* Fused factor + inverse: A <- L = chol(A) in place (upper zeroed), X <- L^{-1}, info as potrf.
  * n <= 256 runs one register-resident kernel per matrix (the DSVI shapes: code/nmgp_dsvi.py:172-177
- * priors and variational covariances, whose inverses feed K12 K22^{-1} and the KL); larger n runs
- * potrf then trtri on the same stream.                                                       */
+ * priors and variational covariances, whose inverses feed K12 K22^{-1} and the KL); larger n (HCP
+ * M=512, ECoG M=1024, the M=4096 stress case) recurses on halves: 128-wide leaves use that kernel,
+ * the panel / SYRK / inverse products are batched MFMA GEMMs of size ~n/2, n/4, ...  X's strictly
+ * upper part is used as scratch and left zero.  batch <= 65535.                                */
 int nmgp_chol_inv_batched_f64(double* A, int64_t n, int64_t lda, int64_t strideA, double* X, int64_t ldx,
                               int64_t strideX, int64_t batch, int32_t* info, hipStream_t stream);
 int nmgp_chol_inv_batched_f32(float* A, int64_t n, int64_t lda, int64_t strideA, float* X, int64_t ldx,

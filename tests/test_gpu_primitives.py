@@ -159,6 +159,30 @@ def test_chol_inv_fused(ops, n, batch):
     assert float(torch.triu(X.cpu(), 1).abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("n,batch,dt", [(300, 2, F64), (512, 2, F64), (700, 1, F64), (520, 2, torch.float32)])
+def test_chol_inv_blocked(ops, n, batch, dt):
+    # n > 256: blocked path (128-wide diagonal blocks + batched GEMM panel / SYRK / inverse products)
+    A = _spd(n, batch, n + 1)
+    Ad = A.to(dt).to(DEV)
+    X, info = ops.chol_inv_(Ad)
+    assert int(info.abs().sum()) == 0
+    ref = torch.linalg.cholesky(A)
+    tl, tx = (1e-13, 1e-11) if dt == F64 else (1e-5, 1e-4)
+    assert rel(Ad, ref) < tl
+    assert rel(X, torch.linalg.inv(ref)) < tx
+    assert float(torch.triu(Ad.cpu(), 1).abs().max()) == 0.0
+    assert float(torch.triu(X.cpu(), 1).abs().max()) == 0.0
+
+
+def test_chol_inv_blocked_not_pd_reports_global_column(ops):
+    A = _spd(400, 2, 9)
+    bad = A.clone()
+    bad[1, 300, 300] = -50.0                       # third diagonal block: global column 301
+    _, info = ops.chol_inv_(bad.to(DEV))
+    info = info.cpu()
+    assert int(info[0]) == 0 and int(info[1]) == 301
+
+
 def test_chol_inv_f32_and_not_pd(ops):
     A = _spd(200, 3, 3)
     Ad = A.float().to(DEV)
