@@ -161,13 +161,12 @@ def main():
     Ib = torch.tensor(np.stack([b[2] for b in host_batches]), dtype=torch.int32, device=dev)
     Sb = torch.tensor(np.stack([b[3] for b in host_batches]), dtype=torch.int32, device=dev)
 
-    def load(bi):
-        eng.x.copy_(Xb[bi], non_blocking=True)
-        eng.y.copy_(Yb[bi], non_blocking=True)
-        eng.row_out.copy_(Ib[bi], non_blocking=True)
-        eng.seg.copy_(Sb[bi], non_blocking=True)
+    # the epoch stays in HBM; every step starts with one on-device gather of the next minibatch
+    batch_ctr = eng.bind_dataset(Xb, Yb, Ib, Sb)
 
-    load(0)
+    def load(bi):
+        batch_ctr.fill_(bi)
+
     if world > 1:
         dist.broadcast(model._theta, 0)
     graph = None
@@ -175,7 +174,6 @@ def main():
         graph = trainer.capture(eng, include_update=(world == 1))
 
     def step(i):
-        load(i % nb)
         if graph is not None:
             graph.replay()
         else:

@@ -614,6 +614,27 @@ __global__ void adam_kernel(T* th, const T* g, T* m, T* v, int64_t n, const int6
 
 __global__ void counter_add_kernel(int64_t* c, int64_t inc) { c[0] += inc; }
 
+// ------------------------------------------------------------------------------------ batch gather
+// One block: every thread reads the batch index first, the copy is grid-strided over the block,
+// then (after a barrier) thread 0 advances the counter for the next step.
+__global__ __launch_bounds__(1024) void batch_gather_kernel(const double* Xb, const double* Yb, const int32_t* Ib,
+                                                            const int32_t* Sb, int64_t B, int64_t nseg, int64_t nbatch,
+                                                            int64_t* ctr, double* x, double* y, int32_t* ro,
+                                                            int32_t* seg) {
+  const int64_t b = ctr[0] % nbatch;
+  const double* xs = Xb + b * B;
+  const double* ys = Yb + b * B;
+  const int32_t* is = Ib + b * B;
+  for (int64_t i = threadIdx.x; i < B; i += blockDim.x) {
+    x[i] = xs[i];
+    y[i] = ys[i];
+    ro[i] = is[i];
+  }
+  for (int64_t i = threadIdx.x; i < nseg; i += blockDim.x) seg[i] = Sb[b * nseg + i];
+  __syncthreads();
+  if (threadIdx.x == 0) ctr[0] += 1;
+}
+
 // ------------------------------------------------------------------------------------ Philox
 __device__ inline void philox_round(uint32_t (&c)[4], uint32_t (&k)[2]) {
   const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
@@ -753,6 +774,18 @@ int nmgp_normal_f64(double* out, int64_t n, uint64_t seed, const int64_t* counte
   const int64_t nt = (n + 3) / 4;
   hipLaunchKernelGGL(nmgp::normal_kernel<double>, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, out, n, seed,
                      counter, offset);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
+int nmgp_batch_gather_f64(const double* Xb, const double* Yb, const int32_t* Ib, const int32_t* Sb, int64_t B,
+                          int64_t nseg, int64_t nbatch, int64_t* ctr, double* x, double* y, int32_t* ro, int32_t* seg,
+                          hipStream_t s) {
+  if (!Xb || !Yb || !Ib || !Sb) return -1;
+  if (B <= 0 || nseg <= 0 || nbatch <= 0) return -5;
+  if (!ctr) return -8;
+  if (!x || !y || !ro || !seg) return -9;
+  hipLaunchKernelGGL(nmgp::batch_gather_kernel, dim3(1), dim3(1024), 0, s, Xb, Yb, Ib, Sb, B, nseg, nbatch, ctr, x, y,
+                     ro, seg);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }

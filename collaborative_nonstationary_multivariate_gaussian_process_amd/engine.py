@@ -334,6 +334,30 @@ class DsviEngine:
         if noise is not None:
             self.noise.copy_(torch.as_tensor(noise, dtype=F64).reshape(-1))
 
+    def bind_dataset(self, Xb, Yb, Ib, Sb, counter=None):
+        """Keep an epoch of pre-split minibatches resident in HBM (Xb, Yb (nb, B) f64; Ib (nb, B) int32
+        output ids; Sb (nb, D+1) int32 segment tables, rows grouped by output as vec2list makes them).
+        Each step then starts with ONE gather launch (batch (*counter) % nb, counter advanced on the
+        device), so a captured step graph walks the epoch by itself."""
+        nb, B = Xb.shape
+        assert B == self.B and Sb.shape == (nb, self.D + 1)
+        for t, dt in ((Xb, F64), (Yb, F64), (Ib, torch.int32), (Sb, torch.int32)):
+            assert t.is_cuda and t.dtype == dt and t.is_contiguous()
+        if counter is None:
+            counter = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self._dataset = (Xb, Yb, Ib, Sb, counter)
+        self._sched_key = None
+        return counter
+
+    def gather_batch(self, stream=None):
+        Xb, Yb, Ib, Sb, ctr = self._dataset
+        s = L.stream_handle() if stream is None else stream
+        L.check(L.lib().nmgp_batch_gather_f64(*(ctypes.c_void_p(t.data_ptr()) for t in (Xb, Yb, Ib, Sb)), self.B,
+                                              self.D + 1, Xb.shape[0], ctypes.c_void_p(ctr.data_ptr()),
+                                              *(ctypes.c_void_p(t.data_ptr()) for t in (self.x, self.y, self.row_out,
+                                                                                        self.seg)), s),
+                "batch_gather")
+
     def device_noise(self, seed, counter):
         H.normal_(self.noise, seed, counter=counter)
 

@@ -321,8 +321,11 @@ class DsviTrainer:
             self.step_count.fill_(max(steps))
 
     def grad_step(self, eng, noise=None, timer=None):
-        """Noise (device Philox unless host noise was loaded) + fused forward/backward."""
+        """[Minibatch gather if a dataset is bound] + noise (device Philox unless host noise was
+        loaded) + fused forward/backward."""
         mdl = self.model
+        if getattr(eng, "_dataset", None) is not None:
+            eng.gather_batch()
         if noise is None:
             eng.device_noise(mdl._noise_seed, mdl._noise_counter)
             H.counter_add_(mdl._noise_counter, 1)

@@ -235,6 +235,14 @@ int nmgp_adam_f32(float* theta, const float* grad, float* m, float* v, int64_t n
 int nmgp_normal_f64(double* out, int64_t n, uint64_t seed, const int64_t* counter, int64_t offset,
                     hipStream_t stream);
 int nmgp_counter_add(int64_t* counter, int64_t inc, hipStream_t stream);
+/* On-device minibatch pipeline (replaces the host DataLoader + vec2list split of
+ * code/nmgp_dsvi.py:816-837 for a dataset resident in HBM): copies minibatch
+ * b = (*batch_counter) % nbatch of pre-split, output-grouped batches (Xb/Yb (nbatch,B) f64, Ib
+ * (nbatch,B) int32 row->output, Sb (nbatch,nseg) int32 segment table) into the engine's inputs
+ * and then advances *batch_counter -- one launch, graph-capturable, no host work per step.      */
+int nmgp_batch_gather_f64(const double* Xb, const double* Yb, const int32_t* Ib, const int32_t* Sb, int64_t B,
+                          int64_t nseg, int64_t nbatch, int64_t* batch_counter, double* x, double* y,
+                          int32_t* row_out, int32_t* seg, hipStream_t stream);
 
 #ifdef __cplusplus
 }
