@@ -16,6 +16,14 @@
 
 namespace nmgp {
 
+#ifdef NMGP_GEMM_TRACE  // per-phase timestamps of workgroup 0 (tools/gemm_trace.hip only)
+__device__ unsigned long long* g_gemm_trace;
+#define GEMM_STAMP(i) \
+  if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) g_gemm_trace[i] = __builtin_readcyclecounter()
+#else
+#define GEMM_STAMP(i)
+#endif
+
 constexpr int GBM = 64, GBN = 64, GBK = 32, LP = 65;
 constexpr int LDS_T = 2 * GBK * LP;  // A image + B image (elements)
 
@@ -89,18 +97,22 @@ __device__ inline bool b_ok(int flags, int gj, int kk, int n, bool kin) {
 
 // Fast main loop: every k-tile lies inside one k-block of each operand (block length a multiple
 // of GBK, or no blocking), so an element's byte offset from the tile's k origin never changes.
-template <typename T, typename Acc>
+// Masks are computed only for k-tiles that need them (the k tail, tiles straddling a triangular
+// operand's diagonal): rows past m / columns past n only feed outputs that are never stored, and
+// reads past the operand's extent return 0 (buffer range check).  KS: k-scaled B (compile time).
+template <typename T, bool KS, typename Acc>
 __device__ inline void mainloop_fast(const nmgp_gemm_desc& d, const Tile& tl, const EltMap& em, T* As, T* Bs, int lane,
                                      int wr, int wc, Acc& c00, Acc& c01, Acc& c10, Acc& c11) {
   const char* Ab = (const char*)d.A;
   const char* Bb = (const char*)d.B;
-  const GPtr<const T> ksc = (GPtr<const T>)(d.kscale ? d.kscale : d.B);  // always a valid address
-  const bool ksf = (tl.flags & NMGP_KSCALE) != 0;
+  const GPtr<const T> ksc = (GPtr<const T>)(d.kscale ? d.kscale : d.B);
   const bool kbA_on = tl.kbA < tl.K, kbB_on = tl.kbB < tl.K;
   const int nkbA = kbA_on ? (tl.K + tl.kbA - 1) / tl.kbA : 1;
   const int nkbB = kbB_on ? (tl.K + tl.kbB - 1) / tl.kbB : 1;
   const int kinA = kbA_on ? tl.kbA : tl.K;  // k extent inside one block
   const int kinB = kbB_on ? tl.kbB : tl.K;
+  const bool aLo = (tl.flags & NMGP_A_LOWER) != 0, aUp = (tl.flags & NMGP_A_UPPER) != 0;
+  const bool bLo = (tl.flags & NMGP_B_LOWER) != 0, bUp = (tl.flags & NMGP_B_UPPER) != 0;
   // end of each operand's addressed extent (elements past the base pointer): the OOB bound
   const int64_t endA = tl.r0 * d.sA_i + (int64_t)(tl.m - 1) * d.sA_i + (tl.k0 + kinA - 1) * d.sA_k +
                        (int64_t)(nkbA - 1) * d.sA_kb + 1;
@@ -119,30 +131,45 @@ __device__ inline void mainloop_fast(const nmgp_gemm_desc& d, const Tile& tl, co
     const int64_t baseB = (tl.k0 + kkB) * d.sB_k + (int64_t)kbB_u * d.sB_kb;
     const __amdgpu_buffer_rsrc_t rA = make_rsrc(Ab + baseA * (int64_t)sizeof(T), (endA - baseA) * (int64_t)sizeof(T));
     const __amdgpu_buffer_rsrc_t rB = make_rsrc(Bb + baseB * (int64_t)sizeof(T), (endB - baseB) * (int64_t)sizeof(T));
-    okm = 0;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      ra[e] = bload<T>(rA, offA[e]);
-      const int gk = kt + em.a_kl[e];
-      okm |= a_ok(tl.flags, tl.i0 + em.a_il[e], kkA + em.a_kl[e], tl.m, gk < tl.kend) ? (1u << e) : 0u;
+    for (int e = 0; e < 8; ++e) ra[e] = bload<T>(rA, offA[e]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) rb[e] = bload<T>(rB, offB[e]);
+    if (KS) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) rs[e] = ksc[tl.k0 + min(kt + em.b_kl[e], tl.K - 1)];
     }
+    // wave-uniform: does this k-tile need element masks at all?
+    // (a triangle applies inside each k-block, so wholly-masked tiles are possible when blocked)
+    const bool need = (kt + GBK > tl.kend) || (aLo && kkA + GBK - 1 > tl.i0) || (aUp && kkA < tl.i0 + GBM - 1) ||
+                      (bLo && tl.j0 + GBN - 1 > kkB) || (bUp && tl.j0 < kkB + GBK - 1);
+    okm = 0xffffu;
+    if (need) {
+      okm = 0;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      rb[e] = bload<T>(rB, offB[e]);
-      const int gk = kt + em.b_kl[e];
-      rs[e] = ksc[tl.k0 + min(gk, tl.K - 1)];
-      okm |= b_ok(tl.flags, tl.j0 + em.b_jl[e], kkB + em.b_kl[e], tl.n, gk < tl.kend) ? (1u << (8 + e)) : 0u;
+      for (int e = 0; e < 8; ++e) {
+        okm |= a_ok(tl.flags, tl.i0 + em.a_il[e], kkA + em.a_kl[e], 0x7fffffff, kt + em.a_kl[e] < tl.kend) ? (1u << e)
+                                                                                                          : 0u;
+        okm |= b_ok(tl.flags, tl.j0 + em.b_jl[e], kkB + em.b_kl[e], 0x7fffffff, kt + em.b_kl[e] < tl.kend)
+                   ? (1u << (8 + e))
+                   : 0u;
+      }
     }
   };
   T ra[8], rb[8], rs[8];
   unsigned okm = 0;
   load(tl.kbeg, ra, rb, rs, okm);
+  GEMM_STAMP(2);
+  [[maybe_unused]] int it = 0;
   for (int kt = tl.kbeg; kt < tl.kend; kt += GBK) {
-    stage_lds(As, Bs, em, ra, rb, rs, okm, ksf);
+    stage_lds(As, Bs, em, ra, rb, rs, okm, KS);
     lds_barrier();
+    GEMM_STAMP(3 + 2 * min(it, 30));
     if (kt + GBK < tl.kend) load(kt + GBK, ra, rb, rs, okm);
     mma_tile(As, Bs, lane, wr, wc, c00, c01, c10, c11);
     lds_barrier();
+    GEMM_STAMP(4 + 2 * min(it, 30));
+    ++it;
   }
 }
 
@@ -194,6 +221,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args, const nmgp_gem
   T* As = smem;
   T* Bs = smem + GBK * LP;
   int* s_last = (int*)(smem + LDS_T);
+  GEMM_STAMP(0);
   int tile = blockIdx.x;
   int idx = 0;
   if (GROUPED) {
@@ -263,6 +291,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args, const nmgp_gem
   }
   tl.kbeg = kbeg;
   tl.kend = kend;
+  GEMM_STAMP(1);
 
   const int t = threadIdx.x;
   const int lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
@@ -280,12 +309,15 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args, const nmgp_gem
   acc_t acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc10 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
   if (kbeg < kend) {
     const bool kb_fast = (tl.kbA >= tl.K || tl.kbA % GBK == 0) && (tl.kbB >= tl.K || tl.kbB % GBK == 0);
-    if (kb_fast)
-      mainloop_fast<T>(d, tl, em, As, Bs, lane, wr, wc, acc00, acc01, acc10, acc11);
+    if (kb_fast && (flags & NMGP_KSCALE))
+      mainloop_fast<T, true>(d, tl, em, As, Bs, lane, wr, wc, acc00, acc01, acc10, acc11);
+    else if (kb_fast)
+      mainloop_fast<T, false>(d, tl, em, As, Bs, lane, wr, wc, acc00, acc01, acc10, acc11);
     else
       mainloop_general<T>(d, tl, em, As, Bs, lane, wr, wc, acc00, acc01, acc10, acc11);
   }
 
+  GEMM_STAMP(70);
   const int64_t r0 = tl.r0;
   const int m = tl.m, n = tl.n, i0 = tl.i0, j0 = tl.j0;
   if (ksplit > 1 && !zero_tile) {
@@ -364,6 +396,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args, const nmgp_gem
       C[ci] = val;
     }
   }
+  GEMM_STAMP(71);
 }
 
 template <typename T>
