@@ -20,16 +20,21 @@ namespace nmgp {
 __device__ unsigned long long* g_gemm_trace;
 #define GEMM_STAMP(i) \
   if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) g_gemm_trace[i] = __builtin_readcyclecounter()
+#define GEMM_STAMPB(i) \
+  if (threadIdx.x == 0 && blockIdx.y == 0) g_gemm_trace[1024 + blockIdx.x * 4 + (i)] = wall_clock64()
 #else
 #define GEMM_STAMP(i)
+#define GEMM_STAMPB(i)
 #endif
 
 constexpr int GBM = 64, GBN = 64, GBK = 32, LP = 65;
-constexpr int LDS_T = 2 * GBK * LP;  // A image + B image (elements)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int LDS_T = 2 * GBK * LP;  // one stage: A image + B image (elements); two stages in flight
 
 struct GemmArgs {
   const nmgp_gemm_desc* descs;
   int nprob;
+  int coop;  // whole grid co-resident: split-K chunks combine cooperatively
   const int32_t* seg;
   nmgp_gemm_desc inl;
 };
@@ -46,6 +51,14 @@ template <> __device__ inline float bload<float>(__amdgpu_buffer_rsrc_t r, uint3
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
 
+template <typename T> __device__ inline T bload_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes);
+template <> __device__ inline double bload_sc1<double>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 16));
+}
+template <> __device__ inline float bload_sc1<float>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 16));
+}
+
 // Problem geometry resolved for one workgroup (all wave-uniform).
 struct Tile {
   int64_t r0, k0;
@@ -53,38 +66,90 @@ struct Tile {
 };
 
 // Per-thread element map of a GBM x GBK (A) / GBK x GBN (B) tile, 8 elements each, chosen so that
-// each load instruction reads consecutive addresses across the wave for either layout.
+// each load instruction reads consecutive addresses across the wave for either layout.  Element e
+// sits at a wave-uniform stride from element 0, so the map costs 4 registers, not 32.
 struct EltMap {
-  int a_il[8], a_kl[8], b_kl[8], b_jl[8];
+  int a_il0, a_kl0, a_ie, a_ke;  // A element e: row a_il0 + e*a_ie, k a_kl0 + e*a_ke
+  int b_kl0, b_jl0, b_ke, b_je;  // B element e: k b_kl0 + e*b_ke, column b_jl0 + e*b_je
+  __device__ int a_il(int e) const { return a_il0 + e * a_ie; }
+  __device__ int a_kl(int e) const { return a_kl0 + e * a_ke; }
+  __device__ int b_kl(int e) const { return b_kl0 + e * b_ke; }
+  __device__ int b_jl(int e) const { return b_jl0 + e * b_je; }
 };
 
-template <typename T>
-__device__ inline void stage_lds(T* As, T* Bs, const EltMap& em, const T (&ra)[8], const T (&rb)[8],
-                                 const T (&rs)[8], unsigned okm, bool kscale) {
+template <typename T, typename Acc>
+__device__ inline void mma_step(T a0, T a1, T b0, T b1, Acc& c00, Acc& c01, Acc& c10, Acc& c11) {
+  c00 = Mfma<T>::mma(a0, b0, c00);
+  c01 = Mfma<T>::mma(a0, b1, c01);
+  c10 = Mfma<T>::mma(a1, b0, c10);
+  c11 = Mfma<T>::mma(a1, b1, c11);
+}
+
+// MFMAs of one LDS stage (As/Bs).  stage(s) runs between the MFMAs of k-step s: the fast main loop
+// writes one element per operand of the next k-tile to the other LDS stage there and refetches a
+// register unit from global memory, so LDS writes, address arithmetic, vector-memory issue and the
+// fragment reads of step s+2 all issue while the matrix pipe is busy.
+struct NoStage {
+  __device__ void operator()(int) const {}
+};
+
+template <typename T, typename Acc, typename Stage = NoStage>
+__device__ inline void mma_tile(const T* As, const T* Bs, int lane, int wr, int wc, Acc& c00, Acc& c01, Acc& c10,
+                                Acc& c11, const Stage& stage = Stage()) {
+  const T* pa = As + (lane >> 4) * LP + wr * 32 + (lane & 15);
+  const T* pb = Bs + (lane >> 4) * LP + wc * 32 + (lane & 15);
+  // fragments of k-steps s and s+1 in registers; step s+2 is read while step s multiplies
+  T f[2][4];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    As[em.a_kl[e] * LP + em.a_il[e]] = (okm >> e) & 1u ? ra[e] : (T)0;
-    T bv = (okm >> (8 + e)) & 1u ? rb[e] : (T)0;
-    if (kscale) bv *= rs[e];
-    Bs[em.b_kl[e] * LP + em.b_jl[e]] = bv;
+  for (int u = 0; u < 2; ++u) {
+    const int o = u * 4 * LP;
+    f[u][0] = pa[o];
+    f[u][1] = pa[o + 16];
+    f[u][2] = pb[o];
+    f[u][3] = pb[o + 16];
+  }
+#pragma unroll
+  for (int s = 0; s < GBK / 4; ++s) {
+    const int u = s & 1;
+    const T a0 = f[u][0], a1 = f[u][1], b0 = f[u][2], b1 = f[u][3];
+    if (s + 2 < GBK / 4) {
+      const int o = (s + 2) * 4 * LP;
+      f[u][0] = pa[o];
+      f[u][1] = pa[o + 16];
+      f[u][2] = pb[o];
+      f[u][3] = pb[o + 16];
+    }
+    mma_step(a0, a1, b0, b1, c00, c01, c10, c11);
+    stage(s);
   }
 }
 
-template <typename T, typename Acc>
-__device__ inline void mma_tile(const T* As, const T* Bs, int lane, int wr, int wc, Acc& c00, Acc& c01, Acc& c10,
-                                Acc& c11) {
-#pragma unroll
-  for (int s = 0; s < GBK / 4; ++s) {
-    const int kr = s * 4 + (lane >> 4);
-    const T a0 = As[kr * LP + wr * 32 + (lane & 15)];
-    const T a1 = As[kr * LP + wr * 32 + 16 + (lane & 15)];
-    const T b0 = Bs[kr * LP + wc * 32 + (lane & 15)];
-    const T b1 = Bs[kr * LP + wc * 32 + 16 + (lane & 15)];
-    c00 = Mfma<T>::mma(a0, b0, c00);
-    c01 = Mfma<T>::mma(a0, b1, c01);
-    c10 = Mfma<T>::mma(a1, b0, c10);
-    c11 = Mfma<T>::mma(a1, b1, c11);
-  }
+// Zero element e of a register tile unless bit e of okm is set (bitwise, so no load is sunk into a
+// branch and a NaN in a masked-off triangle cannot leak through a multiply).
+template <typename T> __device__ inline T keep_if(T v, bool ok);
+template <> __device__ inline double keep_if<double>(double v, bool ok) {
+  return __builtin_bit_cast(double, __builtin_bit_cast(unsigned long long, v) & (ok ? ~0ull : 0ull));
+}
+template <> __device__ inline float keep_if<float>(float v, bool ok) {
+  return __builtin_bit_cast(float, __builtin_bit_cast(unsigned int, v) & (ok ? ~0u : 0u));
+}
+
+// Fast-path register tile: 16-byte units (V = 16/sizeof(T) consecutive elements along the operand's
+// contiguous dimension), 8/V units per thread and operand, so one buffer_load_dwordx4 fetches V
+// elements (vector-memory issue, not bandwidth, bounds the staging beside the MFMAs).  Unit e of A
+// starts at (row a_mn0 + e*a_mne, k a_k0 + e*a_ke); its elements run along k if a_pk else along rows.
+struct UnitMap {
+  int a_mn0, a_k0, a_mne, a_ke, a_pk;
+  int b_mn0, b_k0, b_mne, b_ke, b_pk;
+};
+
+template <typename T> __device__ inline T unit_elem(u32x4 u, int v);
+template <> __device__ inline double unit_elem<double>(u32x4 u, int v) {
+  const unsigned lo = v ? u[2] : u[0], hi = v ? u[3] : u[1];
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+template <> __device__ inline float unit_elem<float>(u32x4 u, int v) {
+  return __builtin_bit_cast(float, v == 0 ? u[0] : v == 1 ? u[1] : v == 2 ? u[2] : u[3]);
 }
 
 // Triangular-operand and bounds validity of element (gi, kk) of A / (kk, gj) of B.
@@ -95,16 +160,35 @@ __device__ inline bool b_ok(int flags, int gj, int kk, int n, bool kin) {
   return gj < n && kin && !(((flags & NMGP_B_LOWER) && gj > kk) || ((flags & NMGP_B_UPPER) && gj < kk));
 }
 
-// Fast main loop: every k-tile lies inside one k-block of each operand (block length a multiple
-// of GBK, or no blocking), so an element's byte offset from the tile's k origin never changes.
-// Masks are computed only for k-tiles that need them (the k tail, tiles straddling a triangular
-// operand's diagonal): rows past m / columns past n only feed outputs that are never stored, and
-// reads past the operand's extent return 0 (buffer range check).  KS: k-scaled B (compile time).
+// Whether the fast main loop can address this tile: k-blocks aligned to GBK, and each operand's
+// extent from the tile's first k-tile within the 2 GiB a buffer resource range check covers.
+template <typename T>
+__device__ inline bool fast_ok(const nmgp_gemm_desc& d, const Tile& tl) {
+  const bool kbA_on = tl.kbA < tl.K, kbB_on = tl.kbB < tl.K;
+  if ((kbA_on && tl.kbA % GBK) || (kbB_on && tl.kbB % GBK)) return false;
+  const int nkbA = kbA_on ? (tl.K + tl.kbA - 1) / tl.kbA : 1, nkbB = kbB_on ? (tl.K + tl.kbB - 1) / tl.kbB : 1;
+  const int kinA = kbA_on ? tl.kbA : tl.K, kinB = kbB_on ? tl.kbB : tl.K;
+  const int64_t spanA = ((int64_t)(tl.m - 1) * d.sA_i + (int64_t)(kinA - 1) * d.sA_k + (int64_t)(nkbA - 1) * d.sA_kb);
+  const int64_t spanB = ((int64_t)(kinB - 1) * d.sB_k + (int64_t)(tl.n - 1) * d.sB_j + (int64_t)(nkbB - 1) * d.sB_kb);
+  const int64_t lim = 0x7fffffffLL / (int64_t)sizeof(T) - 64;
+  return d.sA_i >= 0 && d.sA_k >= 0 && d.sA_kb >= 0 && d.sB_k >= 0 && d.sB_j >= 0 && d.sB_kb >= 0 && spanA < lim &&
+         spanB < lim;
+}
+
+// Fast main loop: k-blocks aligned to GBK, so each operand is addressed by one buffer resource over
+// its whole extent and per-unit byte offsets that advance by a uniform step per k-tile (a jump at a
+// k-block boundary).  Reads past the extent return 0 (the range check is per dword).  Element masks
+// are applied, when staging, only to k-tiles that need them (the k tail, tiles straddling a
+// triangular operand's diagonal); rows past m / columns past n need none: they only feed outputs
+// that are never stored.  Two LDS stages: the MFMAs of k-tile t run while tile t+1 is written from
+// registers to the other stage and tile t+2 is fetched into them; one barrier per k-tile.  KS:
+// k-scaled B.
 template <typename T, bool KS, typename Acc>
-__device__ inline void mainloop_fast(const nmgp_gemm_desc& d, const Tile& tl, const EltMap& em, T* As, T* Bs, int lane,
+__device__ inline void mainloop_fast(const nmgp_gemm_desc& d, const Tile& tl, const UnitMap& um, T* S, int lane,
                                      int wr, int wc, Acc& c00, Acc& c01, Acc& c10, Acc& c11) {
-  const char* Ab = (const char*)d.A;
-  const char* Bb = (const char*)d.B;
+  constexpr int V = 16 / (int)sizeof(T);  // elements per unit
+  constexpr int NU = 8 / V;               // units per thread and operand
+  constexpr int64_t sz = sizeof(T);
   const GPtr<const T> ksc = (GPtr<const T>)(d.kscale ? d.kscale : d.B);
   const bool kbA_on = tl.kbA < tl.K, kbB_on = tl.kbB < tl.K;
   const int nkbA = kbA_on ? (tl.K + tl.kbA - 1) / tl.kbA : 1;
@@ -113,70 +197,142 @@ __device__ inline void mainloop_fast(const nmgp_gemm_desc& d, const Tile& tl, co
   const int kinB = kbB_on ? tl.kbB : tl.K;
   const bool aLo = (tl.flags & NMGP_A_LOWER) != 0, aUp = (tl.flags & NMGP_A_UPPER) != 0;
   const bool bLo = (tl.flags & NMGP_B_LOWER) != 0, bUp = (tl.flags & NMGP_B_UPPER) != 0;
-  // end of each operand's addressed extent (elements past the base pointer): the OOB bound
+  // position of the first k-tile inside its k-block
+  int kbuA = kbA_on ? tl.kbeg / tl.kbA : 0, kbuB = kbB_on ? tl.kbeg / tl.kbB : 0;
+  int kkA = tl.kbeg - kbuA * (kbA_on ? tl.kbA : 0), kkB = tl.kbeg - kbuB * (kbB_on ? tl.kbB : 0);
+  const int64_t baseA = tl.r0 * d.sA_i + (tl.k0 + kkA) * d.sA_k + (int64_t)kbuA * d.sA_kb;
+  const int64_t baseB = (tl.k0 + kkB) * d.sB_k + (int64_t)kbuB * d.sB_kb;
   const int64_t endA = tl.r0 * d.sA_i + (int64_t)(tl.m - 1) * d.sA_i + (tl.k0 + kinA - 1) * d.sA_k +
                        (int64_t)(nkbA - 1) * d.sA_kb + 1;
   const int64_t endB = (tl.k0 + kinB - 1) * d.sB_k + (int64_t)(tl.n - 1) * d.sB_j + (int64_t)(nkbB - 1) * d.sB_kb + 1;
-  uint32_t offA[8], offB[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    offA[e] = (uint32_t)(((int64_t)(tl.i0 + em.a_il[e]) * d.sA_i + (int64_t)em.a_kl[e] * d.sA_k) * (int64_t)sizeof(T));
-    offB[e] = (uint32_t)(((int64_t)em.b_kl[e] * d.sB_k + (int64_t)(tl.j0 + em.b_jl[e]) * d.sB_j) * (int64_t)sizeof(T));
-  }
-  auto load = [&](int kt, T (&ra)[8], T (&rb)[8], T (&rs)[8], unsigned& okm) {
-    const int kbA_u = kbA_on ? kt / tl.kbA : 0, kbB_u = kbB_on ? kt / tl.kbB : 0;
-    const int kkA = kt - kbA_u * (kbA_on ? tl.kbA : 0);
-    const int kkB = kt - kbB_u * (kbB_on ? tl.kbB : 0);
-    const int64_t baseA = tl.r0 * d.sA_i + (tl.k0 + kkA) * d.sA_k + (int64_t)kbA_u * d.sA_kb;
-    const int64_t baseB = (tl.k0 + kkB) * d.sB_k + (int64_t)kbB_u * d.sB_kb;
-    const __amdgpu_buffer_rsrc_t rA = make_rsrc(Ab + baseA * (int64_t)sizeof(T), (endA - baseA) * (int64_t)sizeof(T));
-    const __amdgpu_buffer_rsrc_t rB = make_rsrc(Bb + baseB * (int64_t)sizeof(T), (endB - baseB) * (int64_t)sizeof(T));
-#pragma unroll
-    for (int e = 0; e < 8; ++e) ra[e] = bload<T>(rA, offA[e]);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) rb[e] = bload<T>(rB, offB[e]);
-    if (KS) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) rs[e] = ksc[tl.k0 + min(kt + em.b_kl[e], tl.K - 1)];
-    }
-    // wave-uniform: does this k-tile need element masks at all?
-    // (a triangle applies inside each k-block, so wholly-masked tiles are possible when blocked)
-    const bool need = (kt + GBK > tl.kend) || (aLo && kkA + GBK - 1 > tl.i0) || (aUp && kkA < tl.i0 + GBM - 1) ||
-                      (bLo && tl.j0 + GBN - 1 > kkB) || (bUp && tl.j0 < kkB + GBK - 1);
+  const __amdgpu_buffer_rsrc_t rA = make_rsrc((const char*)d.A + baseA * sz, (endA - baseA) * sz);
+  const __amdgpu_buffer_rsrc_t rB = make_rsrc((const char*)d.B + baseB * sz, (endB - baseB) * sz);
+  // unit e's byte offset = o + e * os; per k-tile the offsets advance by step (jump at a block end)
+  uint32_t oA = (uint32_t)(((int64_t)(tl.i0 + um.a_mn0) * d.sA_i + (int64_t)um.a_k0 * d.sA_k) * sz);
+  uint32_t oB = (uint32_t)(((int64_t)um.b_k0 * d.sB_k + (int64_t)(tl.j0 + um.b_mn0) * d.sB_j) * sz);
+  const uint32_t osA = (uint32_t)(((int64_t)um.a_mne * d.sA_i + (int64_t)um.a_ke * d.sA_k) * sz);
+  const uint32_t osB = (uint32_t)(((int64_t)um.b_ke * d.sB_k + (int64_t)um.b_mne * d.sB_j) * sz);
+  const uint32_t stepA = (uint32_t)(GBK * d.sA_k * sz), stepB = (uint32_t)(GBK * d.sB_k * sz);
+  const uint32_t jumpA = (uint32_t)((d.sA_kb - (int64_t)(kinA - GBK) * d.sA_k) * sz);
+  const uint32_t jumpB = (uint32_t)((d.sB_kb - (int64_t)(kinB - GBK) * d.sB_k) * sz);
+  // element s = e*V + v of this thread: LDS offsets of its A and B slots
+  const int wa = um.a_k0 * LP + um.a_mn0, wsa = um.a_ke * LP + um.a_mne, wva = um.a_pk ? LP : 1;
+  const int wb = um.b_k0 * LP + um.b_mn0, wsb = um.b_ke * LP + um.b_mne, wvb = um.b_pk ? LP : 1;
+  auto a_mn = [&](int s) { return um.a_mn0 + (s / V) * um.a_mne + (um.a_pk ? 0 : s % V); };
+  auto a_k = [&](int s) { return um.a_k0 + (s / V) * um.a_ke + (um.a_pk ? s % V : 0); };
+  auto b_mn = [&](int s) { return um.b_mn0 + (s / V) * um.b_mne + (um.b_pk ? 0 : s % V); };
+  auto b_k = [&](int s) { return um.b_k0 + (s / V) * um.b_ke + (um.b_pk ? s % V : 0); };
+
+  unsigned okm = 0xffffu;  // element masks of the k-tile being fetched (bit s: A, bit 8+s: B)
+  bool need = false;
+  // wave-uniform: does k-tile kt need element masks at all?  (a triangle applies inside each
+  // k-block, so wholly-masked tiles are possible when blocked)
+  auto prep = [&](int kt) {
+    need = (kt + GBK > tl.kend) || (aLo && kkA + GBK - 1 > tl.i0) || (aUp && kkA < tl.i0 + GBM - 1) ||
+           (bLo && tl.j0 + GBN - 1 > kkB) || (bUp && tl.j0 < kkB + GBK - 1);
     okm = 0xffffu;
     if (need) {
       okm = 0;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        okm |= a_ok(tl.flags, tl.i0 + em.a_il[e], kkA + em.a_kl[e], 0x7fffffff, kt + em.a_kl[e] < tl.kend) ? (1u << e)
-                                                                                                          : 0u;
-        okm |= b_ok(tl.flags, tl.j0 + em.b_jl[e], kkB + em.b_kl[e], 0x7fffffff, kt + em.b_kl[e] < tl.kend)
-                   ? (1u << (8 + e))
-                   : 0u;
+      for (int q = 0; q < 8; ++q) {
+        okm |= a_ok(tl.flags, tl.i0 + a_mn(q), kkA + a_k(q), 0x7fffffff, kt + a_k(q) < tl.kend) ? (1u << q) : 0u;
+        okm |= b_ok(tl.flags, tl.j0 + b_mn(q), kkB + b_k(q), 0x7fffffff, kt + b_k(q) < tl.kend) ? (1u << (8 + q))
+                                                                                                 : 0u;
       }
     }
   };
-  T ra[8], rb[8], rs[8];
-  unsigned okm = 0;
-  load(tl.kbeg, ra, rb, rs, okm);
+  u32x4 ra[NU], rb[NU];
+  T rs[8];
+  int kload = tl.kbeg;  // k-tile the issue() calls fetch
+  auto issue = [&](int e) {
+    ra[e] = __builtin_amdgcn_raw_buffer_load_b128(rA, oA + e * osA, 0, 0);
+    rb[e] = __builtin_amdgcn_raw_buffer_load_b128(rB, oB + e * osB, 0, 0);
+    if (KS) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) rs[e * V + v] = ksc[tl.k0 + min(kload + b_k(e * V + v), tl.K - 1)];
+    }
+  };
+  auto advance = [&]() {
+    kload += GBK;
+    kkA += GBK;
+    if (kbA_on && kkA >= kinA) { kkA = 0; oA += jumpA; } else { oA += stepA; }
+    kkB += GBK;
+    if (kbB_on && kkB >= kinB) { kkB = 0; oB += jumpB; } else { oB += stepB; }
+  };
+  unsigned okm_st = 0xffffu;  // masks of the k-tile held in registers
+  // element s of the register tile into LDS stage N (masked if the tile needs it); the last
+  // element of a unit frees its registers for the refetch
+  auto put = [&](T* N, int s, bool masked) {
+    const int e = s / V, v = s % V;
+    T a = unit_elem<T>(ra[e], v), b = unit_elem<T>(rb[e], v);
+    if (masked) {
+      a = keep_if(a, (okm_st >> s) & 1u);
+      b = keep_if(b, (okm_st >> (8 + s)) & 1u);
+    }
+    if (KS) b *= rs[s];
+    N[wa + e * wsa + v * wva] = a;
+    N[GBK * LP + wb + e * wsb + v * wvb] = b;
+  };
+  prep(kload);
+#pragma unroll
+  for (int e = 0; e < NU; ++e) issue(e);
+  advance();
+  okm_st = okm;
   GEMM_STAMP(2);
+  if (need) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) put(S, q, true);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) put(S, q, false);
+  }
+  // tiles past kend read garbage or zeros and are masked when staged, so the fetch needs no guard
+  prep(kload);
+#pragma unroll
+  for (int e = 0; e < NU; ++e) issue(e);
+  advance();
+  okm_st = okm;
+  bool need_st = need;
+  prep(kload);
+  lds_barrier();
+  int cur = 0;
   [[maybe_unused]] int it = 0;
-  for (int kt = tl.kbeg; kt < tl.kend; kt += GBK) {
-    stage_lds(As, Bs, em, ra, rb, rs, okm, KS);
-    lds_barrier();
+  for (int kt = tl.kbeg; kt + GBK < tl.kend; kt += GBK) {
+    T* As = S + cur * LDS_T;
+    T* Ns = S + (cur ^ 1) * LDS_T;
     GEMM_STAMP(3 + 2 * min(it, 30));
-    if (kt + GBK < tl.kend) load(kt + GBK, ra, rb, rs, okm);
-    mma_tile(As, Bs, lane, wr, wc, c00, c01, c10, c11);
+    if (need_st) {
+      mma_tile(As, As + GBK * LP, lane, wr, wc, c00, c01, c10, c11, [&](int q) {
+        put(Ns, q, true);
+        if (q % V == V - 1) issue(q / V);
+      });
+    } else {
+      mma_tile(As, As + GBK * LP, lane, wr, wc, c00, c01, c10, c11, [&](int q) {
+        put(Ns, q, false);
+        if (q % V == V - 1) issue(q / V);
+      });
+    }
+    okm_st = okm;
+    need_st = need;
+    GEMM_STAMP(100 + 4 * min(it, 30));
+    advance();
+    prep(kload);
+    GEMM_STAMP(101 + 4 * min(it, 30));
     lds_barrier();
     GEMM_STAMP(4 + 2 * min(it, 30));
+    cur ^= 1;
     ++it;
   }
+  T* As = S + cur * LDS_T;
+  mma_tile(As, As + GBK * LP, lane, wr, wc, c00, c01, c10, c11);
 }
 
-// General main loop (k-blocks not aligned to GBK, small shapes): per-element block index.
+// General main loop (k-blocks not aligned to GBK, small shapes): per-element block index and
+// clamped unconditional loads (masked when staged), one LDS stage, next k-tile fetched during the
+// MFMAs.
 template <typename T, typename Acc>
-__device__ inline void mainloop_general(const nmgp_gemm_desc& d, const Tile& tl, const EltMap& em, T* As, T* Bs,
-                                        int lane, int wr, int wc, Acc& c00, Acc& c01, Acc& c10, Acc& c11) {
+__device__ inline void mainloop_general(const nmgp_gemm_desc& d, const Tile& tl, const EltMap& em, T* S, int lane,
+                                        int wr, int wc, Acc& c00, Acc& c01, Acc& c10, Acc& c11) {
   const GPtr<const T> A = (GPtr<const T>)d.A;
   const GPtr<const T> Bm = (GPtr<const T>)d.B;
   const GPtr<const T> ksc = (GPtr<const T>)(d.kscale ? d.kscale : d.B);
@@ -186,7 +342,7 @@ __device__ inline void mainloop_general(const nmgp_gemm_desc& d, const Tile& tl,
     okm = 0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int gi = tl.i0 + em.a_il[e], gk = kt + em.a_kl[e];
+      const int gi = tl.i0 + em.a_il(e), gk = kt + em.a_kl(e);
       const int gkc = min(gk, tl.K - 1);
       const int kb = kbA_on ? gkc / tl.kbA : 0, kk = gkc - kb * (kbA_on ? tl.kbA : 0);
       ra[e] = A[(tl.r0 + min(gi, tl.m - 1)) * d.sA_i + (tl.k0 + kk) * d.sA_k + (int64_t)kb * d.sA_kb];
@@ -194,7 +350,7 @@ __device__ inline void mainloop_general(const nmgp_gemm_desc& d, const Tile& tl,
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int gk = kt + em.b_kl[e], gj = tl.j0 + em.b_jl[e];
+      const int gk = kt + em.b_kl(e), gj = tl.j0 + em.b_jl(e);
       const int gkc = min(gk, tl.K - 1);
       const int kb = kbB_on ? gkc / tl.kbB : 0, kk = gkc - kb * (kbB_on ? tl.kbB : 0);
       rb[e] = Bm[(tl.k0 + kk) * d.sB_k + (int64_t)min(gj, tl.n - 1) * d.sB_j + (int64_t)kb * d.sB_kb];
@@ -202,11 +358,18 @@ __device__ inline void mainloop_general(const nmgp_gemm_desc& d, const Tile& tl,
       okm |= b_ok(tl.flags, gj, kk, tl.n, gk < tl.kend) ? (1u << (8 + e)) : 0u;
     }
   };
+  T* As = S;
+  T* Bs = S + GBK * LP;
   T ra[8], rb[8], rs[8];
   unsigned okm = 0;
   load(tl.kbeg, ra, rb, rs, okm);
   for (int kt = tl.kbeg; kt < tl.kend; kt += GBK) {
-    stage_lds(As, Bs, em, ra, rb, rs, okm, ksf);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      As[em.a_kl(e) * LP + em.a_il(e)] = keep_if(ra[e], (okm >> e) & 1u);
+      const T bv = keep_if(rb[e], (okm >> (8 + e)) & 1u);
+      Bs[em.b_kl(e) * LP + em.b_jl(e)] = ksf ? bv * rs[e] : bv;
+    }
     lds_barrier();
     if (kt + GBK < tl.kend) load(kt + GBK, ra, rb, rs, okm);
     mma_tile(As, Bs, lane, wr, wc, c00, c01, c10, c11);
@@ -217,11 +380,10 @@ __device__ inline void mainloop_general(const nmgp_gemm_desc& d, const Tile& tl,
 template <typename T, bool GROUPED>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args, const nmgp_gemm_desc* __restrict__ descs) {
   // ONE shared array (a second __shared__ object can make hipcc wait vmcnt(0) in the k-loop)
-  __shared__ T smem[LDS_T + 2];
-  T* As = smem;
-  T* Bs = smem + GBK * LP;
-  int* s_last = (int*)(smem + LDS_T);
+  __shared__ T smem[2 * LDS_T + 2];
+  int* s_last = (int*)(smem + 2 * LDS_T);
   GEMM_STAMP(0);
+  GEMM_STAMPB(0);
   int tile = blockIdx.x;
   int idx = 0;
   if (GROUPED) {
@@ -296,107 +458,222 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args, const nmgp_gem
   const int t = threadIdx.x;
   const int lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
   EltMap em;
-  const bool a_kc = (d.sA_k == 1), b_jc = (d.sB_j == 1);
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    if (a_kc) { em.a_kl[e] = t & 31; em.a_il[e] = (t >> 5) + 8 * e; }
-    else { em.a_il[e] = t & 63; em.a_kl[e] = (t >> 6) + 4 * e; }
-    if (b_jc) { em.b_jl[e] = t & 63; em.b_kl[e] = (t >> 6) + 4 * e; }
-    else { em.b_kl[e] = t & 31; em.b_jl[e] = (t >> 5) + 8 * e; }
+  if (d.sA_k == 1) { em.a_kl0 = t & 31; em.a_il0 = t >> 5; em.a_ie = 8; em.a_ke = 0; }
+  else { em.a_il0 = t & 63; em.a_kl0 = t >> 6; em.a_ie = 0; em.a_ke = 4; }
+  if (d.sB_j == 1) { em.b_jl0 = t & 63; em.b_kl0 = t >> 6; em.b_je = 0; em.b_ke = 4; }
+  else { em.b_kl0 = t & 31; em.b_jl0 = t >> 5; em.b_je = 8; em.b_ke = 0; }
+  UnitMap um;
+  {
+    constexpr int V = 16 / (int)sizeof(T);
+    constexpr int KU = GBK / V, MU = GBM / V, NUU = GBN / V;
+    if (d.sA_k == 1) { um.a_k0 = (t % KU) * V; um.a_mn0 = t / KU; um.a_mne = 256 / KU; um.a_ke = 0; um.a_pk = 1; }
+    else { um.a_mn0 = (t % MU) * V; um.a_k0 = t / MU; um.a_ke = 256 / MU; um.a_mne = 0; um.a_pk = 0; }
+    if (d.sB_j == 1) { um.b_mn0 = (t % NUU) * V; um.b_k0 = t / NUU; um.b_ke = 256 / NUU; um.b_mne = 0; um.b_pk = 0; }
+    else { um.b_k0 = (t % KU) * V; um.b_mn0 = t / KU; um.b_mne = 256 / KU; um.b_ke = 0; um.b_pk = 1; }
   }
 
   using acc_t = typename Mfma<T>::acc_t;
   acc_t acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc10 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
   if (kbeg < kend) {
-    const bool kb_fast = (tl.kbA >= tl.K || tl.kbA % GBK == 0) && (tl.kbB >= tl.K || tl.kbB % GBK == 0);
+    const bool kb_fast = fast_ok<T>(d, tl);
     if (kb_fast && (flags & NMGP_KSCALE))
-      mainloop_fast<T, true>(d, tl, em, As, Bs, lane, wr, wc, acc00, acc01, acc10, acc11);
+      mainloop_fast<T, true>(d, tl, um, smem, lane, wr, wc, acc00, acc01, acc10, acc11);
     else if (kb_fast)
-      mainloop_fast<T, false>(d, tl, em, As, Bs, lane, wr, wc, acc00, acc01, acc10, acc11);
+      mainloop_fast<T, false>(d, tl, um, smem, lane, wr, wc, acc00, acc01, acc10, acc11);
     else
-      mainloop_general<T>(d, tl, em, As, Bs, lane, wr, wc, acc00, acc01, acc10, acc11);
+      mainloop_general<T>(d, tl, em, smem, lane, wr, wc, acc00, acc01, acc10, acc11);
   }
 
   GEMM_STAMP(70);
+  GEMM_STAMPB(1);
   const int64_t r0 = tl.r0;
   const int m = tl.m, n = tl.n, i0 = tl.i0, j0 = tl.j0;
-  if (ksplit > 1 && !zero_tile) {
-    // deterministic split-K (agent-scope release/acquire hand-off): publish this chunk's partial,
-    // the last arriver sums all chunks in chunk order
-    GPtr<T> ws = (GPtr<T>)d.ws + (int64_t)(tm * d.tiles_n + tn) * ksplit * 4096;
-    GPtr<T> mine = ws + (int64_t)ks * 4096 + t * 16;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      mine[r] = acc00[r];
-      mine[4 + r] = acc01[r];
-      mine[8 + r] = acc10[r];
-      mine[12 + r] = acc11[r];
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      int32_t* ctr = d.counters + tm * d.tiles_n + tn;
-      const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = (old == ksplit - 1);
-      if (last) {
-        __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      *s_last = last;
-    }
-    __syncthreads();
-    if (!*s_last) return;
-    acc00 = acc01 = acc10 = acc11 = acc_t{0, 0, 0, 0};
-    for (int c = 0; c < ksplit; ++c) {
-      GPtr<const T> src = ws + (int64_t)c * 4096 + t * 16;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        acc00[r] += src[r];
-        acc01[r] += src[4 + r];
-        acc10[r] += src[8 + r];
-        acc11[r] += src[12 + r];
-      }
-    }
-  }
-
   const GPtr<T> C = (GPtr<T>)d.C;
   const GPtr<const T> E = (GPtr<const T>)d.epi_E;
   const GPtr<const T> rsp = (GPtr<const T>)d.epi_rs;
   const T alpha = (T)d.alpha, beta = (T)d.beta, gamma = (T)d.gamma, dadd = (T)d.diag_add;
+  // C(gi, gj) <- alpha * acc [+ beta C] [+ gamma rs(i) E] [+ diag], honouring the output masks
+  auto emit = [&](int gi, int gj, T a) {
+    if (gi >= m || gj >= n) return;
+    const bool upper = gj > gi;
+    if (upper && (flags & NMGP_OUT_LOWER)) return;
+    const int64_t ci = (r0 + gi) * d.sC_i + (int64_t)gj * d.sC_j;
+    T val;
+    if (upper && (flags & NMGP_OUT_TRIL)) {
+      val = 0;
+    } else {
+      val = alpha * a;
+      if (beta != (T)0) val += beta * C[ci];
+      if (flags & NMGP_EPI) {
+        T e = 0;
+        if (!((flags & NMGP_EPI_E_LOWER) && upper)) e = E[(r0 + gi) * d.sE_i + (int64_t)gj * d.sE_j];
+        T rs = rsp ? rsp[r0 + gi] : (T)1;
+        if (flags & NMGP_EPI_RS_NEG) rs = -rs;
+        val += gamma * rs * e;
+      }
+      if ((flags & NMGP_DIAG_ADD) && gi == gj) val += dadd;
+    }
+    C[ci] = val;
+  };
+
+  if (ksplit > 1 && !zero_tile) {
+    // Deterministic split-K.  Every chunk publishes its partial tile write-through (sc1 stores: no
+    // L2 write-back fence) and, after the workgroup's stores drained, one lane adds to the tile's
+    // counter.  Partials are read back only with sc1 loads, which bypass the possibly stale L1, so
+    // no acquire fence either.  Thread t owns values [16t, 16t+16) of a chunk (128 B, whole lines).
+    constexpr int V = 16 / (int)sizeof(T);  // elements per 16-B access
+    const char* wsb = (const char*)d.ws + (int64_t)(tm * d.tiles_n + tn) * ksplit * 4096 * (int64_t)sizeof(T);
+    const __amdgpu_buffer_rsrc_t rws = make_rsrc(wsb, (int64_t)ksplit * 4096 * (int64_t)sizeof(T));
+    {
+      T vals[16];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        vals[r] = acc00[r];
+        vals[4 + r] = acc01[r];
+        vals[8 + r] = acc10[r];
+        vals[12 + r] = acc11[r];
+      }
+      const uint32_t off = (uint32_t)(((int64_t)ks * 4096 + t * 16) * (int64_t)sizeof(T));
+#pragma unroll
+      for (int q = 0; q < 16 / V; ++q) {
+        T w[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) w[v] = vals[q * V + v];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), rws, off + q * 16, 0, 16 /* sc1 */);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    GEMM_STAMPB(2);
+    int32_t* ctr = d.counters + tm * d.tiles_n + tn;
+    if (args.coop) {
+      // Cooperative combine (the host enables it only when the whole grid is co-resident): all
+      // chunks of the tile wait for each other, then chunk ks sums 256-value blocks b = ks, ks+S, ...
+      // of the tile over all S chunks in chunk order and stores them -- S workgroups share the
+      // combine instead of one summing S x 32 KB alone.
+      if (t == 0) {
+        __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // bounded spin: a lost peer must not hang the GPU (the result is then wrong, not stuck)
+        for (int spin = 0; spin < (1 << 24); ++spin) {
+          if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ksplit) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the poll
+      constexpr int CB = 8;  // chunks in flight per thread
+      for (int blk = ks; blk < 16; blk += ksplit) {
+        const int idx = blk * 256 + t;
+        T sum = 0;
+        for (int c0 = 0; c0 < ksplit; c0 += CB) {
+          T v[CB];
+#pragma unroll
+          for (int cc = 0; cc < CB; ++cc) {
+            const int c = min(c0 + cc, ksplit - 1);
+            v[cc] = bload_sc1<T>(rws, (uint32_t)(((int64_t)c * 4096 + idx) * (int64_t)sizeof(T)));
+          }
+#pragma unroll
+          for (int cc = 0; cc < CB; ++cc) sum += keep_if(v[cc], c0 + cc < ksplit);
+        }
+        // value idx of the tile = element (idx & 15) of owner thread idx >> 4's accumulators
+        const int tau = idx >> 4, q = (idx >> 2) & 3, r = idx & 3;
+        const int ol = tau & 63, ow = tau >> 6;
+        emit(i0 + (ow >> 1) * 32 + (q >> 1) * 16 + Mfma<T>::row(ol, r), j0 + (ow & 1) * 32 + (q & 1) * 16 + (ol & 15),
+             sum);
+      }
+      if (t == 0) {
+        // the last workgroup to leave resets the counter for the next launch
+        const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == 2 * ksplit - 1) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      GEMM_STAMPB(3);
+      return;
+    }
+    // Last arriver combines the whole tile.
+    if (t == 0) {
+      const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (old == ksplit - 1);
+      if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *s_last = last;
+    }
+    __syncthreads();
+    if (!*s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the poll
+    acc00 = acc01 = acc10 = acc11 = acc_t{0, 0, 0, 0};
+    constexpr int CU = 4;  // chunks in flight
+    for (int c0 = 0; c0 < ksplit; c0 += CU) {
+      u32x4 raw[CU][16 / V];
+#pragma unroll
+      for (int cc = 0; cc < CU; ++cc) {
+        const int c = min(c0 + cc, ksplit - 1);
+        const uint32_t off = (uint32_t)(((int64_t)c * 4096 + t * 16) * (int64_t)sizeof(T));
+#pragma unroll
+        for (int q = 0; q < 16 / V; ++q) raw[cc][q] = __builtin_amdgcn_raw_buffer_load_b128(rws, off + q * 16, 0, 16);
+      }
+#pragma unroll
+      for (int cc = 0; cc < CU; ++cc) {
+        // chunks past the last were loaded clamped: add them as zeros (branch-free, so the loads of
+        // all CU chunks stay in flight together)
+        const bool live = c0 + cc < ksplit;
+        T vals[16];
+#pragma unroll
+        for (int q = 0; q < 16 / V; ++q) {
+          struct W { T v[V]; } w = __builtin_bit_cast(W, raw[cc][q]);
+#pragma unroll
+          for (int v = 0; v < V; ++v) vals[q * V + v] = keep_if(w.v[v], live);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          acc00[r] += vals[r];
+          acc01[r] += vals[4 + r];
+          acc10[r] += vals[8 + r];
+          acc11[r] += vals[12 + r];
+        }
+      }
+    }
+  }
+
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const acc_t& acc = q == 0 ? acc00 : q == 1 ? acc01 : q == 2 ? acc10 : acc11;
     const int mi = q >> 1, ni = q & 1;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int gi = i0 + wr * 32 + mi * 16 + Mfma<T>::row(lane, r);
-      const int gj = j0 + wc * 32 + ni * 16 + (lane & 15);
-      if (gi >= m || gj >= n) continue;
-      const bool upper = gj > gi;
-      if (upper && (flags & NMGP_OUT_LOWER)) continue;
-      const int64_t ci = (r0 + gi) * d.sC_i + (int64_t)gj * d.sC_j;
-      T val;
-      if (upper && (flags & NMGP_OUT_TRIL)) {
-        val = 0;
-      } else {
-        val = alpha * acc[r];
-        if (beta != (T)0) val += beta * C[ci];
-        if (flags & NMGP_EPI) {
-          T e = 0;
-          if (!((flags & NMGP_EPI_E_LOWER) && upper)) e = E[(r0 + gi) * d.sE_i + (int64_t)gj * d.sE_j];
-          T rs = rsp ? rsp[r0 + gi] : (T)1;
-          if (flags & NMGP_EPI_RS_NEG) rs = -rs;
-          val += gamma * rs * e;
-        }
-        if ((flags & NMGP_DIAG_ADD) && gi == gj) val += dadd;
-      }
-      C[ci] = val;
-    }
+    for (int r = 0; r < 4; ++r)
+      emit(i0 + wr * 32 + mi * 16 + Mfma<T>::row(lane, r), j0 + wc * 32 + ni * 16 + (lane & 15), acc[r]);
   }
   GEMM_STAMP(71);
+  GEMM_STAMPB(3);
+}
+
+// Extra dynamic LDS per workgroup (experiment knob NMGP_GEMM_LDS_RESERVE=bytes, applied to grids of at
+// most NMGP_GEMM_LDS_RESERVE_MAXWG workgroups): reserving LDS forces one workgroup per CU.
+static size_t lds_reserve(int wgs) {
+  static int bytes = -1, maxwg = 0;
+  if (bytes < 0) {
+    const char* e = getenv("NMGP_GEMM_LDS_RESERVE");
+    const char* m = getenv("NMGP_GEMM_LDS_RESERVE_MAXWG");
+    bytes = e ? atoi(e) : 0;
+    maxwg = m ? atoi(m) : 256;
+  }
+  return (bytes > 0 && wgs <= maxwg) ? (size_t)bytes : 0;
+}
+
+// Workgroups of the grouped kernel that are certainly resident at once: CUs x min(occupancy API, 2)
+// (LDS and VGPRs allow two 256-thread workgroups per CU; the API can report one block too many).
+template <typename T>
+static int coresident_wgs() {
+  static int cap = -1;
+  if (cap < 0) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, gemm_kernel<T, true>, 256, 0) != hipSuccess) {
+      cap = 0;
+    } else {
+      cap = cus * (per < 2 ? per : 2);
+    }
+  }
+  return cap;
 }
 
 template <typename T>
@@ -409,9 +686,10 @@ static int launch_grouped(const nmgp_gemm_desc* d_desc, int nprob, int total_til
   GemmArgs a;
   a.descs = d_desc;
   a.nprob = nprob;
+  a.coop = total_tiles <= coresident_wgs<T>() ? 1 : 0;
   a.seg = d_seg;
   a.inl = nmgp_gemm_desc{};
-  hipLaunchKernelGGL((gemm_kernel<T, true>), dim3(total_tiles), dim3(256), 0, s, a, d_desc);
+  hipLaunchKernelGGL((gemm_kernel<T, true>), dim3(total_tiles), dim3(256), lds_reserve(total_tiles), s, a, d_desc);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
@@ -429,6 +707,7 @@ static int launch_single(const nmgp_gemm_desc* h, const int32_t* d_seg, hipStrea
   GemmArgs a;
   a.descs = nullptr;
   a.nprob = 1;
+  a.coop = 0;
   a.seg = d_seg;
   a.inl = d;
   hipLaunchKernelGGL((gemm_kernel<T, false>), dim3(d.tiles_m * d.tiles_n, d.batch > 1 ? d.batch : 1), dim3(256), 0, s,

@@ -1,5 +1,5 @@
 // Phase-level timing of the batched potrf/trtri kernels (standalone; not part of the library).
-//   hipcc -O3 --offload-arch=gfx950 -DNMGP_CHOL_TRACE -I<pkg>/csrc tools/chol_probe.hip -o /tmp/chol_probe
+//   hipcc -O3 --offload-arch=gfx950 -DNMGP_CHOL_TRACE -I<pkg>/csrc -Iinclude tools/chol_probe.hip <pkg>/csrc/gemm.hip -o /tmp/chol_probe
 //   ./chol_probe [n] [batch]
 // Prints kernel times (hipEvents, averaged) and, for potrf, the per-block-step split of wall-clock
 // time between phase 1 (diagonal factor), phase 2 (panel) and phase 3 (trailing update).
@@ -88,6 +88,35 @@ int main(int argc, char** argv) {
     if (r >= 3) tf += ms;
   }
   printf("fused chol_inv %.2f us\n", 1000 * tf / reps);
+  {
+    // recursive (two-level) path at the same n, graph-captured so launch gaps are as in the engine
+    hipStream_t cs;
+    HC(hipStreamCreate(&cs));
+    for (int lvl = 0; lvl < 2; ++lvl) {
+      hipGraph_t g;
+      hipGraphExec_t ge;
+      HC(hipStreamBeginCapture(cs, hipStreamCaptureModeGlobal));
+      int rc = lvl == 0 ? nmgp::chol_inv_small<double>(dA, n, n, (int64_t)n * n, dX, n, (int64_t)n * n, batch, dinfo,
+                                                       cs, 0, 1)
+                        : nmgp::chol_inv_rec<double>(dA, n, n, (int64_t)n * n, dX, n, (int64_t)n * n, batch, dinfo,
+                                                     cs, 0);
+      HC(hipStreamEndCapture(cs, &g));
+      if (rc != 0) return 5;
+      HC(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+      float tg = 0;
+      for (int r = 0; r < reps + 3; ++r) {
+        HC(hipMemcpy(dA, dA0, bytes, hipMemcpyDeviceToDevice));
+        HC(hipEventRecord(e0, cs));
+        HC(hipGraphLaunch(ge, cs));
+        HC(hipEventRecord(e1, cs));
+        HC(hipEventSynchronize(e1));
+        float ms;
+        HC(hipEventElapsedTime(&ms, e0, e1));
+        if (r >= 3) tg += ms;
+      }
+      printf("%s (graph) %.2f us\n", lvl == 0 ? "fused" : "recursive 128-leaf", 1000 * tg / reps);
+    }
+  }
   {
     std::vector<unsigned long long> tr((nt + 1) * 4);
     HC(hipMemcpy(tr.data(), dtr, tr.size() * 8, hipMemcpyDeviceToHost));

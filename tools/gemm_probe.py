@@ -16,6 +16,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    verbose = "-v" in sys.argv
     import bench
     from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP, DsviTrainer
     D, M, B = bench.D, bench.M, bench.B
@@ -60,6 +61,17 @@ def main():
         total_ms += ms
         total_gf += gf
         print(f"{name:12s} {len(grp.descs):5d} {grp.total:6d} {ms:8.4f} {gf:8.4f} {gf / ms:7.3f}")
+        if verbose:
+            shapes = {}
+            for dd in grp.descs:
+                segs = seg if dd.row_seg >= 0 or dd.k_seg >= 0 else None
+                m = int(segs[dd.row_seg + max(dd.seg_span, 1)] - segs[dd.row_seg]) if dd.row_seg >= 0 else dd.m
+                k = int(segs[dd.k_seg + max(dd.seg_span, 1)] - segs[dd.k_seg]) if dd.k_seg >= 0 else dd.k
+                key = (m, dd.n, k, dd.kbA, dd.kbB, dd.flags, dd.ksplit, int(dd.sA_k == 1), int(dd.sB_j == 1))
+                shapes[key] = shapes.get(key, 0) + 1
+            for key, c in sorted(shapes.items(), key=lambda t: -t[0][0] * t[0][1] * t[0][2] * t[1]):
+                print(f"    {c:3d} x m={key[0]} n={key[1]} k={key[2]} kbA={key[3]} kbB={key[4]} flags={key[5]} "
+                      f"ksplit={key[6]} a_kc={key[7]} b_jc={key[8]}")
     print(f"{'TOTAL':12s} {'':5s} {'':6s} {total_ms:8.4f} {total_gf:8.4f} {total_gf / total_ms:7.3f}")
 
 
