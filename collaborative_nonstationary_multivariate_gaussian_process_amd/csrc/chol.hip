@@ -15,6 +15,9 @@
 // X[kb,:] = L_kk^-1 R[kb,:] and R[ib,:] -= L[ib,kb] X[kb,:] for ib > kb, again 4 tiles per wave.
 #include "common.hpp"
 
+#include <cstdlib>
+#include <type_traits>
+
 namespace nmgp {
 
 constexpr int CP = 17;
@@ -25,7 +28,10 @@ __device__ unsigned long long* g_chol_trace;
   if (threadIdx.x == 0 && blockIdx.x == 0) g_chol_trace[(kb) * 4 + (p)] = wall_clock64()
 #define CHOL_STAMPW(kb, p) \
   if (threadIdx.x == 0 && blockIdx.x == 0) g_chol_trace[512 + (kb) * 4 + (p)] = wall_clock64()
+#define CHOL_STAMP1(kb, p) \
+  if (threadIdx.x == 0 && blockIdx.x == 1) g_chol_trace[256 + (kb) * 4 + (p)] = wall_clock64()
 #else
+#define CHOL_STAMP1(kb, p)
 #define CHOL_STAMP(kb, p)
 #define CHOL_STAMPW(kb, p)
 #endif  // LDS pitch (elements) of the 16-wide panel: conflict-free ds_read_b64
@@ -545,6 +551,288 @@ __global__ __launch_bounds__(RW * 64) void chol_inv_kernel(T* A, int n, int64_t 
   }
 }
 
+// Two workgroups per matrix (f64, 32 <= n <= 256): the fused kernel's MFMA work is split by role and
+// the roles run concurrently, pipelined one block step apart.
+//   role 0 (potrf): spill block column kb, panel factor (L_kk, L_kk^-1, L[:, kb]), trailing SYRK on
+//     its register tiles; publishes L[:, kb] (final output A) and L_kk^-1 (the final diagonal block
+//     of X) write-through, then a progress flag.
+//   role 1 (trtri): register tiles of R (starts as I); per step waits for the flag, reads L[:, kb] and
+//     L_kk^-1 (sc1 loads), forms X[kb, :] = L_kk^-1 R[kb, :] and updates the rows below.
+// Visibility: payload stored sc1 and drained (vmcnt(0)) in every storing wave before a barrier and the
+// flag store; the consumer polls the flag with an agent-scope load and reads the payload with sc1
+// loads only (MI355X guide, inter-workgroup hand-off, row 1).  The flag lives in X(0, n-1), inside a
+// strictly upper block tile (n >= 32) that role 1 zeroes at the end; its values carry a 48-bit tag
+// so stale bits in an uninitialised X cannot pass for progress.  Role 1 waits only on its own
+// role 0 (block 2b before 2b+1) and every spin is bounded: a lost peer gives wrong output, not a hang.
+constexpr unsigned long long kFlagTag = 0x7ff8d5a1c0de0000ull;
+
+template <int NTPW>
+__device__ __attribute__((always_inline)) inline void chol2_potrf_role(double* Am, double* Xm, int n, int64_t lda, int64_t ldx, int32_t* info, int col_off,
+                                  int info_first, int mat, unsigned char* smem_raw) {
+  using T = double;
+  using acc_t = typename Mfma<T>::acc_t;
+  const int nt = (n + 15) >> 4, NR = nt * 16;
+  T* colbuf = (T*)smem_raw;   // role 0: NR x CP block column kb before the panel step
+  T* Ps = colbuf + NR * CP;   // NR x CP : L[:, kb] (local rows, diagonal block first)
+  T* Xrow = Ps + NR * CP;     // role 1: nt tiles x 16 rows x CP : X[kb, jb]
+  T* LiT = Xrow + NR * CP;    // 16 x CP : (L_kk^-1)^T
+  unsigned long long* flag = (unsigned long long*)(Xm + (n - 1));
+  const __amdgpu_buffer_rsrc_t rAm = make_rsrc(Am, ((int64_t)(n - 1) * lda + n) * (int64_t)sizeof(T));
+  const __amdgpu_buffer_rsrc_t rXm = make_rsrc(Xm, ((int64_t)(n - 1) * ldx + n) * (int64_t)sizeof(T));
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int ntiles = nt * (nt + 1) / 2;
+  int ib[NTPW], jb[NTPW];
+  acc_t acc[NTPW];
+#pragma unroll
+  for (int u = 0; u < NTPW; ++u) {
+    const int tt = w + RW * u;
+    ib[u] = -1;
+    jb[u] = -1;
+    if (tt < ntiles) {
+      tri_decode(tt, ib[u], jb[u]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gr = ib[u] * 16 + Mfma<T>::row(lane, r), gc = jb[u] * 16 + (lane & 15);
+        const T v = Am[(int64_t)min(gr, n - 1) * lda + min(gc, n - 1)];
+        acc[u][r] = (gr < n && gc < n) ? v : (gr == gc ? (T)1 : (T)0);
+      }
+    }
+  }
+  int first_fail = 0;
+  // strictly-upper block tiles of L are zero (the stores drain while the factorization runs)
+  for (int i = w; i < n; i += RW)
+    for (int j = ((i >> 4) + 1) * 16 + lane; j < n; j += 64) Am[(int64_t)i * lda + j] = 0;
+  for (int kb = 0; kb < nt; ++kb) {
+    CHOL_STAMP(kb, 0);
+    const int nrow = NR - kb * 16;
+#pragma unroll
+    for (int u = 0; u < NTPW; ++u) {
+      if (jb[u] == kb) {
+        const int dib = __builtin_amdgcn_readfirstlane(ib[u] - kb);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) colbuf[(dib * 16 + Mfma<T>::row(lane, r)) * CP + (lane & 15)] = acc[u][r];
+      }
+    }
+    lds_barrier();
+    CHOL_STAMP(kb, 1);
+    if (w < (nrow + 47) / 48) {
+      int lr;
+      bool ident = false;
+      if (lane < 16) {
+        lr = lane;
+      } else {
+        const int slot = w * 48 + lane - 16;
+        ident = slot >= nrow - 16 && slot < nrow;
+        lr = ident ? slot - (nrow - 16) : 16 + slot;
+      }
+      const bool active = ident || lr < nrow;
+      T a[16];
+      {
+        const T keep = (active && !ident) ? (T)1 : (T)0;
+        const T* src = colbuf + min(lr, NR - 1) * CP;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) a[c] = fma(src[c], keep, (ident && c == lr) ? (T)1 : (T)0);
+      }
+      unsigned int bad = 0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const T d = readlane(a[j], j);
+        bad |= (d > (T)0) ? 0u : (1u << j);
+        T sj, inv;
+        sqrt_recip(d, sj, inv);
+        a[j] = (lane == j) ? sj : a[j] * inv;
+#pragma unroll
+        for (int c = j + 1; c < 16; ++c) a[c] = fma(-a[j], readlane(a[j], c), a[c]);
+      }
+      if (bad && first_fail == 0) {
+        const int j0 = __builtin_ctz(bad);
+        if (kb * 16 + j0 < n) first_fail = kb * 16 + j0 + 1;
+      }
+#pragma unroll
+      for (int c = 0; c < 16; ++c) a[c] = (lane < 16 && c > lane) ? (T)0 : a[c];
+      if (ident || (active && (lane >= 16 || w == 0))) {
+        T* dst = (ident ? LiT : Ps) + lr * CP;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) dst[c] = a[c];
+      }
+    }
+    lds_barrier();
+    CHOL_STAMP(kb, 2);
+    // publish L[:, kb] (final output) and L_kk^-1 (= the final X[kb, kb]) write-through
+    for (int idx = t; idx < nrow * 16; idx += RW * 64) {
+      const int lr = idx >> 4, c = idx & 15;
+      const int gr = kb * 16 + lr, gc = kb * 16 + c;
+      if (gr < n && gc < n) bstore_sc1<T>(rAm, (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)), Ps[lr * CP + c]);
+    }
+    if (t < 256) {
+      const int r = t >> 4, c = t & 15;
+      const int gr = kb * 16 + r, gc = kb * 16 + c;
+      if (gr < n && gc < n) bstore_sc1<T>(rXm, (uint32_t)(((int64_t)gr * ldx + gc) * sizeof(T)), LiT[c * CP + r]);
+    }
+    // trailing SYRK while the stores drain
+#pragma unroll
+    for (int u = 0; u < NTPW; ++u) {
+      if (jb[u] > kb) {
+        const int ra = __builtin_amdgcn_readfirstlane(ib[u] - kb) * 16 + (lane & 15);
+        const int rb = __builtin_amdgcn_readfirstlane(jb[u] - kb) * 16 + (lane & 15);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int kr = Mfma<T>::row(lane, s);
+          acc[u] = Mfma<T>::mma(-Ps[ra * CP + kr], Ps[rb * CP + kr], acc[u]);
+        }
+      }
+    }
+    CHOL_STAMP(kb, 3);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    if (t == 0) __hip_atomic_store(flag, kFlagTag + (unsigned long long)(kb + 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+  }
+  CHOL_STAMP(nt, 0);
+  if (t == 0 && info) {
+    if (info_first) info[mat] = first_fail ? first_fail + col_off : 0;
+    else if (first_fail && info[mat] == 0) info[mat] = first_fail + col_off;
+  }
+}
+
+template <int NTPW>
+__device__ __attribute__((always_inline)) inline void chol2_trtri_role(double* Am, double* Xm, int n, int64_t lda, int64_t ldx, int32_t* info, int col_off,
+                                  int info_first, int mat, unsigned char* smem_raw) {
+  using T = double;
+  using acc_t = typename Mfma<T>::acc_t;
+  const int nt = (n + 15) >> 4, NR = nt * 16;
+  T* colbuf = (T*)smem_raw;   // role 0: NR x CP block column kb before the panel step
+  T* Ps = colbuf + NR * CP;   // NR x CP : L[:, kb] (local rows, diagonal block first)
+  T* Xrow = Ps + NR * CP;     // role 1: nt tiles x 16 rows x CP : X[kb, jb]
+  T* LiT = Xrow + NR * CP;    // 16 x CP : (L_kk^-1)^T
+  unsigned long long* flag = (unsigned long long*)(Xm + (n - 1));
+  const __amdgpu_buffer_rsrc_t rAm = make_rsrc(Am, ((int64_t)(n - 1) * lda + n) * (int64_t)sizeof(T));
+  const __amdgpu_buffer_rsrc_t rXm = make_rsrc(Xm, ((int64_t)(n - 1) * ldx + n) * (int64_t)sizeof(T));
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int ntiles = nt * (nt + 1) / 2;
+  int ib[NTPW], jb[NTPW];
+  acc_t acc[NTPW];
+#pragma unroll
+  for (int u = 0; u < NTPW; ++u) {
+    const int tt = w + RW * u;
+    ib[u] = -1;
+    jb[u] = -1;
+    if (tt < ntiles) {
+      tri_decode(tt, ib[u], jb[u]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gr = ib[u] * 16 + Mfma<T>::row(lane, r), gc = jb[u] * 16 + (lane & 15);
+        acc[u][r] = gr == gc ? (T)1 : (T)0;  // R starts as the identity
+      }
+    }
+  }
+  for (int i = w; i < n; i += RW)
+    for (int j = ((i >> 4) + 1) * 16 + lane; j < n; j += 64)
+      if (i != 0 || j != n - 1) Xm[(int64_t)i * ldx + j] = 0;
+  for (int kb = 0; kb < nt; ++kb) {
+    const int nrow = NR - kb * 16;
+    if (t == 0) {
+      for (int spin = 0; spin < (1 << 26); ++spin) {
+        const unsigned long long f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (f >= kFlagTag + (unsigned long long)(kb + 1) && f <= kFlagTag + (unsigned long long)nt) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    CHOL_STAMP1(kb, 0);
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the poll
+    {
+      // all loads in flight before any LDS store: one memory round trip per step, not one per element
+      constexpr int PER = 256 * 16 / (RW * 64);  // elements per thread at n = 256
+      T v[PER];
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int idx = t + q * RW * 64, lr = idx >> 4, c = idx & 15;
+        const int gr = kb * 16 + lr, gc = kb * 16 + c;
+        // rows past n (and past this column's rows) load as 0: offset past the resource's range
+        const uint32_t off =
+            (idx < nrow * 16 && gr < n && gc < n) ? (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)) : 0x80000000u;
+        v[q] = bload_sc1<T>(rAm, off);
+      }
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int idx = t + q * RW * 64;
+        if (idx < nrow * 16) Ps[(idx >> 4) * CP + (idx & 15)] = v[q];
+      }
+    }
+    if (t < 256) {
+      const int r = t >> 4, c = t & 15;
+      const int gr = kb * 16 + r, gc = kb * 16 + c;
+      const uint32_t off = (gr < n && gc < n) ? (uint32_t)(((int64_t)gr * ldx + gc) * sizeof(T)) : 0x80000000u;
+      T v = bload_sc1<T>(rXm, off);
+      if (gr >= n || gc >= n) v = (gr == gc) ? (T)1 : (T)0;  // padded identity past n
+      LiT[c * CP + r] = v;
+    }
+    lds_barrier();
+    CHOL_STAMP1(kb, 1);
+    // X[kb, jb] = L_kk^-1 R[kb, jb]
+#pragma unroll
+    for (int u = 0; u < NTPW; ++u) {
+      if (ib[u] == kb) {
+        const int xj = __builtin_amdgcn_readfirstlane(jb[u] - kb) + kb;
+        acc_t x = {0, 0, 0, 0};
+        if (xj == kb) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) x[r] = LiT[(lane & 15) * CP + Mfma<T>::row(lane, r)];
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) x = Mfma<T>::mma(LiT[Mfma<T>::row(lane, s) * CP + (lane & 15)], acc[u][s], x);
+        }
+        acc[u] = x;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Xrow[(xj * 16 + Mfma<T>::row(lane, r)) * CP + (lane & 15)] = x[r];
+      }
+    }
+    lds_barrier();
+    CHOL_STAMP1(kb, 2);
+    // rows below kb: R[ib, jb] -= L[ib, kb] X[kb, jb]
+#pragma unroll
+    for (int u = 0; u < NTPW; ++u) {
+      if (ib[u] > kb && jb[u] >= 0 && jb[u] <= kb) {
+        const int ra = __builtin_amdgcn_readfirstlane(ib[u] - kb) * 16 + (lane & 15);
+        const int xj = __builtin_amdgcn_readfirstlane(jb[u] - kb) + kb;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int kr = Mfma<T>::row(lane, s);
+          acc[u] = Mfma<T>::mma(-Ps[ra * CP + kr], Xrow[(xj * 16 + kr) * CP + (lane & 15)], acc[u]);
+        }
+      }
+    }
+    for (int idx = t; idx < (kb + 1) * 256; idx += RW * 64) {
+      const int j = idx >> 8, k = (idx >> 4) & 15, c = idx & 15;
+      const int gr = kb * 16 + k, gc = j * 16 + c;
+      if (gr < n && gc < n) Xm[(int64_t)gr * ldx + gc] = Xrow[(j * 16 + k) * CP + c];
+    }
+    // the next step's loads overwrite Ps / LiT / Xrow: everyone must be done reading them
+    lds_barrier();
+    CHOL_STAMP1(kb, 3);
+  }
+  if (t == 0) __hip_atomic_store(flag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int NTPW>
+__global__ __launch_bounds__(RW * 64) void chol_inv2_kernel(double* A, int n, int64_t lda, int64_t strideA, double* X,
+                                                            int64_t ldx, int64_t strideX, int32_t* info, int col_off,
+                                                            int info_first) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int mat = blockIdx.x >> 1;
+  double* Am = A + (int64_t)mat * strideA;
+  double* Xm = X + (int64_t)mat * strideX;
+  // separate functions: with one shared tile set the two roles' live ranges merged past the
+  // register file
+  if ((blockIdx.x & 1) == 0)
+    chol2_potrf_role<NTPW>(Am, Xm, n, lda, ldx, info, col_off, info_first, mat, smem_raw);
+  else
+    chol2_trtri_role<NTPW>(Am, Xm, n, lda, ldx, info, col_off, info_first, mat, smem_raw);
+}
+
 template <typename T> static size_t chol_inv_smem(int n) {
   const int nt = (n + 15) >> 4;
   return (size_t)(3 * nt * 16 * CP + 16 * CP) * sizeof(T);
@@ -615,11 +903,42 @@ static void chol_inv_go(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx,
 }
 
 // one diagonal block (n <= 256) with the fused register-resident kernel
+template <int NTPW>
+static void chol_inv2_go(double* A, int n, int64_t lda, int64_t sA, double* X, int64_t ldx, int64_t sX, int64_t batch,
+                         int32_t* info, size_t sm, hipStream_t s, int col_off, int info_first) {
+  static bool attr_done = false;
+  if (!attr_done) {
+    (void)hipFuncSetAttribute((const void*)chol_inv2_kernel<NTPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr_done = true;
+  }
+  hipLaunchKernelGGL((chol_inv2_kernel<NTPW>), dim3((unsigned)(2 * batch)), dim3(RW * 64), sm, s, A, n, lda, sA, X,
+                     ldx, sX, info, col_off, info_first);
+}
+
+// Two-role split pays from n = 32 up; its workgroup pairs must be co-resident, so a launch holds at
+// most 128 matrices (256 workgroups, one per CU).
+static bool use_two_role(int n, int64_t batch) { return n >= 32 && n <= 256 && batch <= 128; }
+
 template <typename T>
 static int chol_inv_small(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx, int64_t sX, int64_t batch,
                           int32_t* info, hipStream_t s, int col_off, int info_first) {
   const int nt = (n + 15) >> 4, ntiles = nt * (nt + 1) / 2;
   const size_t sm = chol_inv_smem<T>(n);
+  if constexpr (std::is_same<T, double>::value) {
+    if (use_two_role(n, batch) && !getenv("NMGP_CHOL_FUSED1")) {
+      if (ntiles <= RW * 3)
+        chol_inv2_go<3>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+      else if (ntiles <= RW * 5)
+        chol_inv2_go<5>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+      else if (ntiles <= RW * 9)
+        chol_inv2_go<9>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+      else
+        chol_inv2_go<17>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+      NMGP_CHECK_LAUNCH();
+      return NMGP_OK;
+    }
+  }
   if (ntiles <= RW * 1)
     chol_inv_go<T, 1>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
   else if (ntiles <= RW * 3)

@@ -41,6 +41,38 @@ template <> struct Mfma<float> {
   __device__ static inline int row(int lane, int r) { return ((lane >> 4) << 2) + r; }
 };
 
+// Raw buffer resources: loads past num_records return 0 (checked per dword), so a buffer load is a
+// bounds-checked load without a branch.  aux 16 = sc1 (bypass this CU's L1 on loads; write through
+// on stores) for data handed between workgroups inside a launch.
+__device__ inline __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t nbytes) {
+  const int32_t nr = (int32_t)(nbytes <= 0 ? 0 : (nbytes > 0x7fffffffLL ? 0x7fffffffLL : nbytes));
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nr, 0x00020000);
+}
+template <typename T> __device__ inline T bload(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes);
+template <> __device__ inline double bload<double>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+template <> __device__ inline float bload<float>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+template <typename T> __device__ inline T bload_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes);
+template <> __device__ inline double bload_sc1<double>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 16));
+}
+template <> __device__ inline float bload_sc1<float>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 16));
+}
+
+template <typename T> __device__ inline void bstore_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes, T v);
+template <> __device__ inline void bstore_sc1<double>(__amdgpu_buffer_rsrc_t r, uint32_t off, double v) {
+  typedef unsigned int u32x2_ __attribute__((ext_vector_type(2)));
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_, v), r, off, 0, 16);
+}
+template <> __device__ inline void bstore_sc1<float>(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, off, 0, 16);
+}
+
 // Workgroup barrier that orders LDS only: waits for this wave's LDS traffic (lgkmcnt) but not for
 // its outstanding global stores, which __syncthreads() would drain (vmcnt(0)) at every barrier.
 // Only valid where waves exchange data exclusively through LDS.

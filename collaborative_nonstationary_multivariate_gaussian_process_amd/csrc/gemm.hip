@@ -39,26 +39,6 @@ struct GemmArgs {
   nmgp_gemm_desc inl;
 };
 
-__device__ inline __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t nbytes) {
-  const int32_t nr = (int32_t)(nbytes <= 0 ? 0 : (nbytes > 0x7fffffffLL ? 0x7fffffffLL : nbytes));
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nr, 0x00020000);
-}
-template <typename T> __device__ inline T bload(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes);
-template <> __device__ inline double bload<double>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
-}
-template <> __device__ inline float bload<float>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
-}
-
-template <typename T> __device__ inline T bload_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes);
-template <> __device__ inline double bload_sc1<double>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 16));
-}
-template <> __device__ inline float bload_sc1<float>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 16));
-}
-
 // Problem geometry resolved for one workgroup (all wave-uniform).
 struct Tile {
   int64_t r0, k0;

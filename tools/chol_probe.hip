@@ -114,7 +114,35 @@ int main(int argc, char** argv) {
         HC(hipEventElapsedTime(&ms, e0, e1));
         if (r >= 3) tg += ms;
       }
-      printf("%s (graph) %.2f us\n", lvl == 0 ? "fused" : "recursive 128-leaf", 1000 * tg / reps);
+      printf("%s (graph) %.2f us\n", lvl == 0 ? "chol_inv_small" : "recursive 128-leaf", 1000 * tg / reps);
+      if (lvl == 0) {
+        std::vector<unsigned long long> tr((nt + 1) * 4);
+        HC(hipMemcpy(tr.data(), dtr, tr.size() * 8, hipMemcpyDeviceToHost));
+        double q[4] = {0, 0, 0, 0};
+        for (int kb = 0; kb < nt; ++kb) {
+          q[0] += (tr[kb * 4 + 1] - tr[kb * 4]) * 10.0;
+          q[1] += (tr[kb * 4 + 2] - tr[kb * 4 + 1]) * 10.0;
+          q[2] += (tr[kb * 4 + 3] - tr[kb * 4 + 2]) * 10.0;
+          q[3] += (tr[(kb + 1) * 4] - tr[kb * 4 + 3]) * 10.0;
+        }
+        printf("  block 0 phases (ns, summed over steps): spill %.0f  panel %.0f  publish+syrk %.0f  drain+flag %.0f"
+               "  (total %.0f)\n", q[0], q[1], q[2], q[3], (tr[nt * 4] - tr[0]) * 10.0);
+        std::vector<unsigned long long> t1(256 + nt * 4);
+        HC(hipMemcpy(t1.data(), dtr, t1.size() * 8, hipMemcpyDeviceToHost));
+        double w1 = 0, l1 = 0, a1 = 0, c1 = 0;
+        for (int kb = 0; kb < nt; ++kb) {
+          const unsigned long long* r1 = &t1[256 + kb * 4];
+          w1 += (r1[0] - (kb ? t1[256 + (kb - 1) * 4 + 3] : tr[0])) * 10.0;
+          l1 += (r1[1] - r1[0]) * 10.0;
+          a1 += (r1[2] - r1[1]) * 10.0;
+          c1 += (r1[3] - r1[2]) * 10.0;
+        }
+        printf("  block 1 phases (ns, summed): wait-flag %.0f  load %.0f  X-row %.0f  update+store %.0f  (ends %.0f after "
+               "block 0)\n", w1, l1, a1, c1, ((double)t1[256 + (nt - 1) * 4 + 3] - (double)tr[nt * 4]) * 10.0);
+        printf("  per step lag (flag seen - role0 step end, ns):");
+        for (int kb = 0; kb < nt; ++kb) printf(" %.0f", ((double)t1[256 + kb * 4] - (double)tr[(kb + 1) * 4]) * 10.0);
+        printf("\n");
+      }
     }
   }
   {
