@@ -97,10 +97,18 @@ class GemmGroup:
         work_per_wg = max(2, total_ktiles // target_wgs)   # k-tiles per workgroup if the launch were balanced
         esz = 8 if dtype == _F64 else 4
         self._ws = []
-        t = 0
         for i, d in enumerate(descs):
             if d.ksplit <= 1:
                 d.ksplit = _auto_ksplit(eff[i][1], group_tiles, work_per_wg)
+        # longest k-loop per workgroup first: those workgroups are dispatched first instead of
+        # forming the launch's tail (problems of one group write disjoint outputs, so their order in
+        # the launch is free)
+        order = sorted(range(len(descs)), key=lambda i: -(-(-eff[i][1] // GEMM_BK) // max(descs[i].ksplit, 1)))
+        descs = [descs[i] for i in order]
+        t = 0
+        for i, d in enumerate(descs):
+            if d.ksplit <= 1:
+                d.ksplit = 1
             if d.ksplit > 1:
                 ntile = d.tiles_m * d.tiles_n
                 ws = torch.empty(ntile * d.ksplit * 4096, dtype=dtype, device=device)
