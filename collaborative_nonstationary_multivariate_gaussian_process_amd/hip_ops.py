@@ -193,6 +193,30 @@ def matmul(A, B, transA=False, transB=False, maskA=0, maskB=0, out=None, alpha=1
     return out
 
 
+def bmm(A, B, transA=False, transB=False, maskA=0, maskB=0, out=None, alpha=1.0):
+    """Batched C[b] = alpha op(A[b]) op(B[b]) in ONE launch (grid.y = batch).  A or B may be 2-D and is
+    then shared by every batch entry (batch stride 0)."""
+    L.require_device(A, "A")
+    A = A.contiguous()
+    B = B.contiguous()
+    nb = A.shape[0] if A.dim() == 3 else B.shape[0]
+    a2, b2 = A.shape[-2:], B.shape[-2:]
+    m, k = (a2[1], a2[0]) if transA else a2
+    k2, n = (b2[1], b2[0]) if transB else b2
+    assert k == k2 and (A.dim() == 2 or A.shape[0] == nb) and (B.dim() == 2 or B.shape[0] == nb), (A.shape, B.shape)
+    if out is None:
+        out = torch.empty(nb, m, n, dtype=A.dtype, device=A.device)
+    sA = (1, a2[1], 0) if transA else (a2[1], 1, 0)
+    sB = (1, b2[1], 0) if transB else (b2[1], 1, 0)
+    d = gemm_desc(out, A, B, m, n, k, sA, sB, (n, 1), flags=maskA | maskB, alpha=alpha)
+    d.batch = int(nb)
+    d.sA_b = a2[0] * a2[1] if A.dim() == 3 else 0
+    d.sB_b = b2[0] * b2[1] if B.dim() == 3 else 0
+    d.sC_b = m * n
+    gemm_single(d, A.dtype)
+    return out
+
+
 # ------------------------------------------------------------------------------------ Cholesky
 def potrf_(A, info=None):
     """In-place lower Cholesky of a (batch, n, n) or (n, n) contiguous device tensor."""

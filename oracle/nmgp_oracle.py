@@ -337,6 +337,57 @@ def predict_Y(p, x_list, z, index=None):
         return Y[rows, cols]
 
 
+def sample_Y(p, x_list, z, noise, n_sample=1000, index=None):
+    """NMGP.sample_Y (code/nmgp_dsvi.py:406-490): posterior-predictive samples of the observed
+    outputs -> (Ys (S, N), Ls (S, N, D): row I_n of L, Gs (S, D, N), tilde_ells (S, N))."""
+    with torch.no_grad():
+        D, M = p["mu_W"].shape
+        sizes = [int(np.asarray(x).reshape(-1).shape[0]) for x in x_list]
+        I = output_ids(sizes, index)
+        rows, cols = torch.from_numpy(np.arange(I.shape[0])), torch.from_numpy(I)
+        inputs = torch.cat([torch.as_tensor(np.asarray(x, np.float64)).reshape(-1) for x in x_list]).view(-1, 1)
+        Z = torch.as_tensor(np.asarray(z, np.float64)).reshape(-1, 1)
+        Sigma_W, Sigma_v, Sigma_U = _covs(p)
+        h = _hyper(p)
+        N = inputs.shape[0]
+        Ys, Ls, Gs, Ts = [], [], [], []
+        for _ in range(n_sample):
+            c = _sample_core(p, Sigma_v, Sigma_U, h, Z, inputs, D, noise, N)
+            l = c["L"].permute(2, 0, 1)[rows, cols]                  # row I_n (nmgp_dsvi.py:466)
+            K_G12 = create_Gibbs(inputs, Z, c["ell_X"], c["ell_Z"])
+            K_G22 = create_Gibbs(Z, Z, c["ell_Z"], c["ell_Z"])
+            G = MGP_d(K_G12, K_G22, torch.ones(N, dtype=DT), p["mu_W"], Sigma_W, noise)
+            F = torch.sum(l * G.t(), 1)
+            Y = reparameterize(F, torch.ones_like(F) * h["s2_err"], noise(N))
+            Ys.append(Y), Ls.append(l), Gs.append(G), Ts.append(c["t_ell"])
+        return torch.stack(Ys), torch.stack(Ls), torch.stack(Gs), torch.stack(Ts)
+
+
+def sample_FY(p, x, z, noise, n_sample=1000):
+    """NMGP.sample_FY (code/nmgp_dsvi.py:492-580): samples of all D outputs at x plus the implied
+    correlation matrices -> (tilde_ells (S, N), Ys (S, N, D), corrs (S, N, D, D))."""
+    with torch.no_grad():
+        D, M = p["mu_W"].shape
+        inputs = torch.as_tensor(np.asarray(x, np.float64)).reshape(-1, 1)
+        Z = torch.as_tensor(np.asarray(z, np.float64)).reshape(-1, 1)
+        Sigma_W, Sigma_v, Sigma_U = _covs(p)
+        h = _hyper(p)
+        N = inputs.shape[0]
+        Ts, Ys, Cs = [], [], []
+        for _ in range(n_sample):
+            c = _sample_core(p, Sigma_v, Sigma_U, h, Z, inputs, D, noise, N)
+            K_G12 = create_Gibbs(inputs, Z, c["ell_X"], c["ell_Z"])
+            K_G22 = create_Gibbs(Z, Z, c["ell_Z"], c["ell_Z"])
+            G = MGP_d(K_G12, K_G22, torch.ones(N, dtype=DT), p["mu_W"], Sigma_W, noise)
+            Ln = c["L"].permute(2, 0, 1)                               # (N, D, D)
+            F = torch.matmul(Ln, G.permute(1, 0).unsqueeze(2))[:, :, 0]
+            Y = reparameterize(F, torch.ones_like(F) * h["s2_err"], noise(F.numel()).reshape(F.shape))
+            cov = torch.matmul(Ln, c["L"].permute(2, 1, 0))
+            invstd = torch.sqrt(torch.diag_embed(1. / torch.diagonal(cov, dim1=-2, dim2=-1)))
+            Ts.append(c["t_ell"]), Ys.append(Y), Cs.append(torch.matmul(torch.matmul(invstd, cov), invstd))
+        return torch.stack(Ts), torch.stack(Ys), torch.stack(Cs)
+
+
 def adam_step(params, grads, state, lr, betas=(0.9, 0.999), eps=1e-8):
     """torch.optim.Adam default update (code/nmgp_dsvi.py:777, :854), restated."""
     b1, b2 = betas

@@ -482,6 +482,47 @@ def case_inference():
     save("toy_inference", d)
 
 
+def case_sample():
+    """sample_Y / sample_FY (code/nmgp_dsvi.py:406-580) on the trained model.pt state with injected
+    noise (reference call order per sample: z_v (M), z_t (N), Q x (N), G (D, N), z_F)."""
+    X_list, _, _, _ = toy_data("low")
+    ck = torch.load(os.path.join(REF, "code", "notebook", "model.pt"), weights_only=True)
+    M, D, S = 20, 2, 3
+    Q = D * (D + 1) // 2
+    z = np.linspace(0, 1, M)
+    m = build_model(200, D, z, seed=22)
+    m.load_state_dict(ck["model_state_dict"])
+    params = model_params(m)
+    Xs = [X_list[0][:17], X_list[1][:13]]
+    N = sum(x.shape[0] for x in Xs)
+    rng = np.random.default_rng(5)
+    noise_y = []
+    for _ in range(S):
+        noise_y += [rng.standard_normal(M).astype(np.float32), rng.standard_normal(N).astype(np.float32)]
+        noise_y += [rng.standard_normal(N).astype(np.float32) for _ in range(Q)]
+        noise_y += [rng.standard_normal((D, N)).astype(np.float32), rng.standard_normal(N).astype(np.float32)]
+    TAPE.inject(noise_y)
+    Ys, Ls, Gs, Ts = m.sample_Y([torch.from_numpy(x).type(DT) for x in Xs], n_sample=S)
+    TAPE.off()
+    xf = np.linspace(0.03, 0.97, 11)
+    Nf = xf.shape[0]
+    noise_f = []
+    for _ in range(S):
+        noise_f += [rng.standard_normal(M).astype(np.float32), rng.standard_normal(Nf).astype(np.float32)]
+        noise_f += [rng.standard_normal(Nf).astype(np.float32) for _ in range(Q)]
+        noise_f += [rng.standard_normal((D, Nf)).astype(np.float32), rng.standard_normal((Nf, D)).astype(np.float32)]
+    TAPE.inject(noise_f)
+    Tf, Yf, Cf = m.sample_FY(torch.from_numpy(xf).type(DT), n_sample=S)
+    TAPE.off()
+    flat = lambda arrs: np.concatenate([np.asarray(a, np.float64).reshape(-1) for a in arrs])
+    d = {"z": z, "n_sample": S, "x0": Xs[0], "x1": Xs[1], "noise_y": flat(noise_y), "xf": xf,
+         "noise_f": flat(noise_f), "Ys": np64(Ys), "Ls": np64(Ls), "Gs": np64(Gs), "tilde_ells": np64(Ts),
+         "fy_tilde_ells": np64(Tf), "fy_Ys": np64(Yf), "fy_corrs": np64(Cf)}
+    for k, v in params.items():
+        d["p_" + k] = v
+    save("sample_cases", d)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     if len(sys.argv) > 1:
@@ -496,3 +537,4 @@ if __name__ == "__main__":
     case_utils()
     case_legacy()
     case_inference()
+    case_sample()

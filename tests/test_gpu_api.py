@@ -191,3 +191,42 @@ def test_device_noise_graph_step_is_finite_and_matches_eager():
     assert np.isfinite(res[0][0])
     assert res[0][0] == pytest.approx(res[1][0], rel=1e-12)
     assert _rel(res[1][1], res[0][1]) < 1e-12
+
+
+def test_sample_Y_and_sample_FY_replay_reference_noise():
+    """§8f f1: NMGP sampling on the device with the reference's recorded noise (model.pt state).
+    Tolerance 1e-7 relative: Cholesky solves replace the reference's LU and (P Sigma) o P becomes
+    (P tril S)^2 on a trained state whose K22 + 1e-4 I has cond ~1e6 (measured 2.4e-9)."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import predict
+    g = G.load("sample_cases")
+    S = int(g["n_sample"])
+    m = _model_from(g, 2, 20, 200)
+    ys, ls, gs, ts = predict.sample_Y(m, [torch.from_numpy(g["x0"]), torch.from_numpy(g["x1"])], n_sample=S,
+                                      noise_tape=g["noise_y"])
+    for got, key in [(ys, "Ys"), (ls, "Ls"), (gs, "Gs"), (ts, "tilde_ells")]:
+        assert tuple(got.shape) == g[key].shape, key
+        assert _rel(got, g[key]) < 1e-7, (key, _rel(got, g[key]))
+    tf, yf, cf = predict.sample_FY(m, torch.from_numpy(g["xf"]), n_sample=S, noise_tape=g["noise_f"])
+    for got, key in [(tf, "fy_tilde_ells"), (yf, "fy_Ys"), (cf, "fy_corrs")]:
+        assert tuple(got.shape) == g[key].shape, key
+        assert _rel(got, g[key]) < 1e-7, (key, _rel(got, g[key]))
+
+
+def test_sample_Y_module_api_shapes_and_moments():
+    """Module-level sample_Y / sample_FY (numpy out, device Philox noise): shapes as the reference's,
+    sample means near predict_Y's posterior mean, correlation matrices with unit diagonal."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import nmgp_dsvi as NM
+    g = G.load("sample_cases")
+    m = _model_from(g, 2, 20, 200)
+    torch.manual_seed(0)
+    X = [g["x0"], g["x1"]]
+    ys, ls, gs, ts = NM.sample_Y(m, X, n_sample=400)
+    N = sum(x.shape[0] for x in X)
+    assert ys.shape == (400, N) and ls.shape == (400, N, 2) and gs.shape == (400, 2, N) and ts.shape == (400, N)
+    assert np.all(np.isfinite(ys))
+    mean = NM.predict_Y(m, X)
+    # the predictive mean of l*G is not l_mean*G_mean, but on this trained state they are close
+    assert np.max(np.abs(ys.mean(0) - mean)) < 0.5
+    tf, yf, cf = NM.sample_FY(m, g["xf"], n_sample=50)
+    assert tf.shape == (50, 11) and yf.shape == (50, 11, 2) and cf.shape == (50, 11, 2, 2)
+    np.testing.assert_allclose(np.diagonal(cf, axis1=2, axis2=3), 1.0, rtol=0, atol=1e-12)

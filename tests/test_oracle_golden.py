@@ -156,3 +156,20 @@ def test_inference_two_adam_steps():
     np.testing.assert_allclose(losses, g["loss_list"], rtol=1e-12)
     for k in O.PARAM_NAMES:
         np.testing.assert_allclose(p[k].detach().numpy(), g["final_" + k], rtol=1e-10, atol=1e-13, err_msg=k)
+
+
+# ------------------------------------------------------------------- sample_Y / sample_FY (§8f f1)
+def test_oracle_sample_Y_and_sample_FY_match_reference():
+    g = G.load("sample_cases")
+    p = G.params(g)
+    S = int(g["n_sample"])
+    ys, ls, gs, ts = O.sample_Y(p, [g["x0"], g["x1"]], g["z"], O.TapeNoise(g["noise_y"]), n_sample=S)
+    for got, key in [(ys, "Ys"), (ls, "Ls"), (gs, "Gs"), (ts, "tilde_ells")]:
+        ref = g[key]
+        assert got.shape == ref.shape
+        assert np.max(np.abs(got.numpy() - ref)) <= 1e-10 * max(1.0, np.max(np.abs(ref))), key
+    tf, yf, cf = O.sample_FY(p, g["xf"], g["z"], O.TapeNoise(g["noise_f"]), n_sample=S)
+    for got, key in [(tf, "fy_tilde_ells"), (yf, "fy_Ys"), (cf, "fy_corrs")]:
+        ref = g[key]
+        assert got.shape == ref.shape
+        assert np.max(np.abs(got.numpy() - ref)) <= 1e-10 * max(1.0, np.max(np.abs(ref))), key
