@@ -96,24 +96,36 @@ _SIGS = {
     "nmgp_pairwise_bwd_f32": (c_int, [c_vp, c_int, c_int, c_vp]),
     "nmgp_pairwise_bwd_single_f64": (c_int, [ctypes.POINTER(PairwiseBwdDesc), c_vp]),
     "nmgp_colsum_f64": (c_int, [c_vp, c_i64, c_i64, c_dbl, c_vp, c_vp]),
+    "nmgp_colsum_f32": (c_int, [c_vp, c_i64, c_i64, c_dbl, c_vp, c_vp]),
     "nmgp_kron_product_f64": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "nmgp_kron_product_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "nmgp_kron_product_diag_f64": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "nmgp_kron_mv_f64": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "nmgp_kron_mv_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "nmgp_dsvi_hyper_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_hyper_f32": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_trow_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_trow_f32": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_recon_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_recon_f32": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_kl_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_kl_f32": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_delta_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_delta_f32": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_tbwd_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_tbwd_f32": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_vbwd_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_vbwd_f32": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_finalize_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_finalize_f32": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_adam_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_dbl, c_dbl, c_dbl, c_dbl, c_vp]),
     "nmgp_adam_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_dbl, c_dbl, c_dbl, c_dbl, c_vp]),
     "nmgp_normal_f64": (c_int, [c_vp, c_i64, c_u64, c_vp, c_i64, c_vp]),
+    "nmgp_normal_f32": (c_int, [c_vp, c_i64, c_u64, c_vp, c_i64, c_vp]),
     "nmgp_counter_add": (c_int, [c_vp, c_i64, c_vp]),
     "nmgp_batch_gather_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                      c_vp]),
+    "nmgp_batch_gather_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_vp]),
 }
 

@@ -72,6 +72,12 @@ template <typename T, int NR> __device__ inline void setlane(T (&r)[NR], int d, 
     if ((d >> 6) == u && lane == (d & 63)) r[u] = v;
 }
 
+// Marginal variances of the sampled GPs (k11 - rowsum(P o K12) [+ ||P L||^2]).  fp64 keeps the
+// reference's arithmetic exactly; in fp32 the cancellation can leave them a few ulps of k11 below 0
+// and sqrt(var + 1e-4) would turn NaN on ill-conditioned K22, so they are floored at 0.
+template <typename T> __device__ inline T var_floor(T v) { return v; }
+template <> __device__ inline float var_floor<float>(float v) { return v > 0.f ? v : 0.f; }
+
 // ------------------------------------------------------------------------------------ v
 template <typename T>
 __global__ __launch_bounds__(256) void dsvi_v_kernel(Args a) {
@@ -108,7 +114,7 @@ __global__ __launch_bounds__(256) void dsvi_trow_kernel(Args a) {
   mean = wave_sum(mean);
   q = wave_sum(q);
   if (lane == 0) {
-    const T var = hyp<T>(a, 0) - q;
+    const T var = var_floor(hyp<T>(a, 0) - q);
     const T zt = ((const T*)a.noise)[M + r];
     const T tl = mean + zt * dsqrt(var + (T)a.jitter);
     ((T*)a.ellX)[r] = dexp(tl);
@@ -191,7 +197,7 @@ __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
       }
       pm = wave_sum(pm);
       pq = wave_sum(pq);
-      const T s2p = (diag ? s21 : s20) - (diag ? q1 : q0) + pq;
+      const T s2p = var_floor((diag ? s21 : s20) - (diag ? q1 : q0) + pq);
       const T sd = dsqrt(s2p + lam);
       const T zz = noise[M + B + (int64_t)(pi * (pi + 1) / 2 + pj) * B + r];
       const T smp = pm + zz * sd;
@@ -617,13 +623,13 @@ __global__ void counter_add_kernel(int64_t* c, int64_t inc) { c[0] += inc; }
 // ------------------------------------------------------------------------------------ batch gather
 // One block: every thread reads the batch index first, the copy is grid-strided over the block,
 // then (after a barrier) thread 0 advances the counter for the next step.
-__global__ __launch_bounds__(1024) void batch_gather_kernel(const double* Xb, const double* Yb, const int32_t* Ib,
+template <typename T>
+__global__ __launch_bounds__(1024) void batch_gather_kernel(const T* Xb, const T* Yb, const int32_t* Ib,
                                                             const int32_t* Sb, int64_t B, int64_t nseg, int64_t nbatch,
-                                                            int64_t* ctr, double* x, double* y, int32_t* ro,
-                                                            int32_t* seg) {
+                                                            int64_t* ctr, T* x, T* y, int32_t* ro, int32_t* seg) {
   const int64_t b = ctr[0] % nbatch;
-  const double* xs = Xb + b * B;
-  const double* ys = Yb + b * B;
+  const T* xs = Xb + b * B;
+  const T* ys = Yb + b * B;
   const int32_t* is = Ib + b * B;
   for (int64_t i = threadIdx.x; i < B; i += blockDim.x) {
     x[i] = xs[i];
@@ -681,63 +687,99 @@ using nmgp::Args;
     if ((a) == nullptr) return -1; \
   } while (0)
 
-extern "C" {
-int nmgp_dsvi_hyper_f64(const Args* a, hipStream_t s) {
+namespace nmgp {
+// One definition per entry point, instantiated below for f64 and f32 (extern "C" wrappers).
+template <typename T> static int dsvi_hyper(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
-  hipLaunchKernelGGL(nmgp::dsvi_v_kernel<double>, dim3(nmgp::blocks_rows(a->M)), dim3(256), 0, s, *a);
+  hipLaunchKernelGGL(dsvi_v_kernel<T>, dim3(blocks_rows(a->M)), dim3(256), 0, s, *a);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
-int nmgp_dsvi_trow_f64(const Args* a, hipStream_t s) {
+template <typename T> static int dsvi_trow(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
-  hipLaunchKernelGGL(nmgp::dsvi_trow_kernel<double>, dim3(nmgp::blocks_rows(a->B)), dim3(256), 0, s, *a);
+  hipLaunchKernelGGL(dsvi_trow_kernel<T>, dim3(blocks_rows(a->B)), dim3(256), 0, s, *a);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
-int nmgp_dsvi_recon_f64(const Args* a, hipStream_t s) {
+template <typename T> static int dsvi_recon(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
   if (a->D > 128) return -1;
-  const size_t sm = (size_t)4 * a->M * sizeof(double);
+  const size_t sm = (size_t)4 * a->M * sizeof(T);
   if (a->D <= 64)
-    hipLaunchKernelGGL((nmgp::dsvi_recon_kernel<double, 1>), dim3(nmgp::blocks_rows(a->B)), dim3(256), sm, s, *a);
+    hipLaunchKernelGGL((dsvi_recon_kernel<T, 1>), dim3(blocks_rows(a->B)), dim3(256), sm, s, *a);
   else
-    hipLaunchKernelGGL((nmgp::dsvi_recon_kernel<double, 2>), dim3(nmgp::blocks_rows(a->B)), dim3(256), sm, s, *a);
+    hipLaunchKernelGGL((dsvi_recon_kernel<T, 2>), dim3(blocks_rows(a->B)), dim3(256), sm, s, *a);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
-int nmgp_dsvi_kl_f64(const Args* a, hipStream_t s) {
+template <typename T> static int dsvi_kl(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
-  hipLaunchKernelGGL(nmgp::dsvi_kl_kernel<double>, dim3(a->NF, (a->M + nmgp::KL_ROWS - 1) / nmgp::KL_ROWS), dim3(256), 0,
-                     s, *a);
+  hipLaunchKernelGGL(dsvi_kl_kernel<T>, dim3(a->NF, (a->M + KL_ROWS - 1) / KL_ROWS), dim3(256), 0, s, *a);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
-int nmgp_dsvi_delta_f64(const Args* a, hipStream_t s) {
+template <typename T> static int dsvi_delta(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
-  hipLaunchKernelGGL(nmgp::dsvi_delta_kernel<double>, dim3((unsigned)((a->M + 255) / 256), 4), dim3(256), 0, s, *a);
+  hipLaunchKernelGGL(dsvi_delta_kernel<T>, dim3((unsigned)((a->M + 255) / 256), 4), dim3(256), 0, s, *a);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
-int nmgp_dsvi_tbwd_f64(const Args* a, hipStream_t s) {
+template <typename T> static int dsvi_tbwd(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
-  hipLaunchKernelGGL(nmgp::dsvi_tbwd_kernel<double>, dim3(nmgp::blocks_rows(a->B)), dim3(256), 0, s, *a);
+  hipLaunchKernelGGL(dsvi_tbwd_kernel<T>, dim3(blocks_rows(a->B)), dim3(256), 0, s, *a);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
-int nmgp_dsvi_vbwd_f64(const Args* a, hipStream_t s) {
+template <typename T> static int dsvi_vbwd(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
-  const size_t sm = (size_t)2 * a->M * sizeof(double);
-  hipLaunchKernelGGL(nmgp::dsvi_vbwd_kernel<double>, dim3((a->M + nmgp::VBW_ROWS - 1) / nmgp::VBW_ROWS), dim3(256), sm,
-                     s, *a);
+  const size_t sm = (size_t)2 * a->M * sizeof(T);
+  hipLaunchKernelGGL(dsvi_vbwd_kernel<T>, dim3((a->M + VBW_ROWS - 1) / VBW_ROWS), dim3(256), sm, s, *a);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
-int nmgp_dsvi_finalize_f64(const Args* a, hipStream_t s) {
+template <typename T> static int dsvi_finalize(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
-  hipLaunchKernelGGL(nmgp::dsvi_finalize_kernel<double>, dim3(1), dim3(256), 0, s, *a);
+  hipLaunchKernelGGL(dsvi_finalize_kernel<T>, dim3(1), dim3(256), 0, s, *a);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
+template <typename T>
+static int normal_launch(T* out, int64_t n, uint64_t seed, const int64_t* counter, int64_t offset, hipStream_t s) {
+  if (!out) return -1;
+  if (n <= 0) return NMGP_OK;
+  const int64_t nt = (n + 3) / 4;
+  hipLaunchKernelGGL(normal_kernel<T>, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, out, n, seed, counter,
+                     offset);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
+template <typename T>
+static int batch_gather(const T* Xb, const T* Yb, const int32_t* Ib, const int32_t* Sb, int64_t B, int64_t nseg,
+                        int64_t nbatch, int64_t* ctr, T* x, T* y, int32_t* ro, int32_t* seg, hipStream_t s) {
+  if (!Xb || !Yb || !Ib || !Sb) return -1;
+  if (B <= 0 || nseg <= 0 || nbatch <= 0) return -5;
+  if (!ctr) return -8;
+  if (!x || !y || !ro || !seg) return -9;
+  hipLaunchKernelGGL(batch_gather_kernel<T>, dim3(1), dim3(1024), 0, s, Xb, Yb, Ib, Sb, B, nseg, nbatch, ctr, x, y, ro,
+                     seg);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
+}  // namespace nmgp
+
+extern "C" {
+#define NMGP_DSVI_ENTRY(name)                                                                     \
+  int nmgp_dsvi_##name##_f64(const Args* a, hipStream_t s) { return nmgp::dsvi_##name<double>(a, s); } \
+  int nmgp_dsvi_##name##_f32(const Args* a, hipStream_t s) { return nmgp::dsvi_##name<float>(a, s); }
+NMGP_DSVI_ENTRY(hyper)
+NMGP_DSVI_ENTRY(trow)
+NMGP_DSVI_ENTRY(recon)
+NMGP_DSVI_ENTRY(kl)
+NMGP_DSVI_ENTRY(delta)
+NMGP_DSVI_ENTRY(tbwd)
+NMGP_DSVI_ENTRY(vbwd)
+NMGP_DSVI_ENTRY(finalize)
+#undef NMGP_DSVI_ENTRY
 int nmgp_adam_f64(double* th, const double* g, double* m, double* v, int64_t n, int64_t* step, double lr,
                   double b1, double b2, double eps, hipStream_t s) {
   if (!th) return -1;
@@ -769,25 +811,20 @@ int nmgp_adam_f32(float* th, const float* g, float* m, float* v, int64_t n, int6
   return NMGP_OK;
 }
 int nmgp_normal_f64(double* out, int64_t n, uint64_t seed, const int64_t* counter, int64_t offset, hipStream_t s) {
-  if (!out) return -1;
-  if (n <= 0) return NMGP_OK;
-  const int64_t nt = (n + 3) / 4;
-  hipLaunchKernelGGL(nmgp::normal_kernel<double>, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, out, n, seed,
-                     counter, offset);
-  NMGP_CHECK_LAUNCH();
-  return NMGP_OK;
+  return nmgp::normal_launch<double>(out, n, seed, counter, offset, s);
+}
+int nmgp_normal_f32(float* out, int64_t n, uint64_t seed, const int64_t* counter, int64_t offset, hipStream_t s) {
+  return nmgp::normal_launch<float>(out, n, seed, counter, offset, s);
 }
 int nmgp_batch_gather_f64(const double* Xb, const double* Yb, const int32_t* Ib, const int32_t* Sb, int64_t B,
                           int64_t nseg, int64_t nbatch, int64_t* ctr, double* x, double* y, int32_t* ro, int32_t* seg,
                           hipStream_t s) {
-  if (!Xb || !Yb || !Ib || !Sb) return -1;
-  if (B <= 0 || nseg <= 0 || nbatch <= 0) return -5;
-  if (!ctr) return -8;
-  if (!x || !y || !ro || !seg) return -9;
-  hipLaunchKernelGGL(nmgp::batch_gather_kernel, dim3(1), dim3(1024), 0, s, Xb, Yb, Ib, Sb, B, nseg, nbatch, ctr, x, y,
-                     ro, seg);
-  NMGP_CHECK_LAUNCH();
-  return NMGP_OK;
+  return nmgp::batch_gather<double>(Xb, Yb, Ib, Sb, B, nseg, nbatch, ctr, x, y, ro, seg, s);
+}
+int nmgp_batch_gather_f32(const float* Xb, const float* Yb, const int32_t* Ib, const int32_t* Sb, int64_t B,
+                          int64_t nseg, int64_t nbatch, int64_t* ctr, float* x, float* y, int32_t* ro, int32_t* seg,
+                          hipStream_t s) {
+  return nmgp::batch_gather<float>(Xb, Yb, Ib, Sb, B, nseg, nbatch, ctr, x, y, ro, seg, s);
 }
 int nmgp_counter_add(int64_t* c, int64_t inc, hipStream_t s) {
   if (!c) return -1;

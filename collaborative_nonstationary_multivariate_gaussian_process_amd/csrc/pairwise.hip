@@ -283,6 +283,15 @@ int nmgp_pairwise_bwd_single_f64(const nmgp_pairwise_bwd_desc* h, hipStream_t s)
   d.tiles = nmgp::pw_tiles(d.n, d.m);
   return nmgp::pwb_launch<double>(nullptr, 1, d.tiles, &d, s);
 }
+int nmgp_colsum_f32(const float* a, int64_t rows, int64_t cols, double beta, float* out, hipStream_t s) {
+  if (!a) return -1;
+  if (!out) return -5;
+  if (cols <= 0) return NMGP_OK;
+  hipLaunchKernelGGL(nmgp::colsum_kernel<float>, dim3((unsigned)((cols + 255) / 256)), dim3(256), 0, s, a, rows, cols,
+                     (float)beta, out);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
 int nmgp_colsum_f64(const double* a, int64_t rows, int64_t cols, double beta, double* out, hipStream_t s) {
   if (!a) return -1;
   if (!out) return -5;

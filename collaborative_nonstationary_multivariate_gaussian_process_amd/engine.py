@@ -1,4 +1,5 @@
-"""The DSVI step engine: closed-form -SELBO and all 13 gradients on the MI355X (fp64).
+"""The DSVI step engine: closed-form -SELBO and all 13 gradients on the MI355X (fp64, or fp32 for
+the HCP / ECoG-shaped configurations of SURVEY §8d).
 
 One engine instance owns the device workspace for a fixed (D outputs, M inducing points,
 B minibatch rows) and enqueues the ~30 HIP launches of one step on torch's
@@ -18,7 +19,12 @@ from . import _lib as L
 from . import hip_ops as H
 
 F64 = torch.float64
+F32 = torch.float32
 JITTER = 1e-4   # code/utils.py:7
+
+
+def _sfx(dt):
+    return "f64" if dt == F64 else "f32"
 
 PARAM_NAMES = ["mu_W", "sqrt_W", "mu_v", "sqrt_v", "mu_U", "sqrt_U",
                "sigma2_tildeell_log", "length_scales_tildeell_log", "sigma2_L0_log",
@@ -44,10 +50,14 @@ def pair_list(D):
 class DsviEngine:
     """Workspace + launch schedule of one DSVI step for fixed (D, M, B)."""
 
-    def __init__(self, D, M, B, z, device="cuda", jitter=JITTER):
+    def __init__(self, D, M, B, z, device="cuda", jitter=JITTER, dtype=F64):
         if not torch.cuda.is_available():
             raise RuntimeError("DsviEngine needs a HIP device; there is no CPU fallback")
+        if dtype not in (F64, F32):
+            raise ValueError("DsviEngine computes in float64 or float32")
         L.lib()
+        self.dt = dtype
+        self.sfx = _sfx(dtype)
         self.D, self.M, self.B = D, M, B
         self.Q = D * (D + 1) // 2
         self.NF = D + 1 + self.Q
@@ -55,8 +65,8 @@ class DsviEngine:
         self.jitter = jitter
         self.offs, self.nparam = param_layout(D, M)
         Q, NF = self.Q, self.NF
-        e = lambda *shape: torch.zeros(*shape, dtype=F64, device=self.dev)
-        self.Z = torch.as_tensor(np.asarray(z, np.float64).reshape(-1, 1), device=self.dev).contiguous()
+        e = lambda *shape: torch.zeros(*shape, dtype=self.dt, device=self.dev)
+        self.Z = torch.as_tensor(np.asarray(z, np.float64).reshape(-1, 1), device=self.dev).to(self.dt).contiguous()
         assert self.Z.shape[0] == M
         # minibatch (rows grouped by output) + noise
         self.x = e(B)
@@ -111,8 +121,9 @@ class DsviEngine:
 
     # ------------------------------------------------------------------------------------ binding
     def bind(self, theta, grad, frozen_mask=0, N=None):
-        """Attach the flat parameter / gradient vectors (device, fp64) and build the launch plans."""
-        assert theta.dtype == F64 and theta.is_cuda and theta.numel() == self.nparam
+        """Attach the flat parameter / gradient vectors (device, engine dtype) and build the launch plans."""
+        assert theta.dtype == self.dt and theta.is_cuda and theta.numel() == self.nparam
+        assert grad.dtype == self.dt
         if self._theta is not None and theta.data_ptr() == self._theta.data_ptr() and \
                 grad.data_ptr() == self._grad.data_ptr() and frozen_mask == self.frozen_mask:
             if N is not None:
@@ -159,7 +170,7 @@ class DsviEngine:
         prior_of = [3] * D + [2 if i == j else 1 for (i, j) in pairs] + [0]
         FV = NF - 1
         dev, seg = self.dev, self.seg
-        G = lambda descs: H.GemmGroup(descs, dev, F64, seg=seg)
+        G = lambda descs: H.GemmGroup(descs, dev, self.dt, seg=seg)
         g = H.gemm_desc
         rows_all = dict(row_seg=0, seg_span=D)          # all rows of the minibatch via the segment table
         p = {}
@@ -327,21 +338,21 @@ class DsviEngine:
             seg[k + 1] = n
         seg = np.cumsum(seg).astype(np.int32)
         row_out = np.repeat(np.arange(D, dtype=np.int32), np.diff(seg))
-        self.x.copy_(torch.as_tensor(np.asarray(x, np.float64).reshape(-1)))
-        self.y.copy_(torch.as_tensor(np.asarray(y, np.float64).reshape(-1)))
+        self.x.copy_(torch.as_tensor(np.asarray(x, np.float64).reshape(-1)).to(self.dt))
+        self.y.copy_(torch.as_tensor(np.asarray(y, np.float64).reshape(-1)).to(self.dt))
         self.seg.copy_(torch.from_numpy(seg))
         self.row_out.copy_(torch.from_numpy(row_out))
         if noise is not None:
-            self.noise.copy_(torch.as_tensor(noise, dtype=F64).reshape(-1))
+            self.noise.copy_(torch.as_tensor(noise, dtype=F64).reshape(-1).to(self.dt))
 
     def bind_dataset(self, Xb, Yb, Ib, Sb, counter=None):
-        """Keep an epoch of pre-split minibatches resident in HBM (Xb, Yb (nb, B) f64; Ib (nb, B) int32
+        """Keep an epoch of pre-split minibatches resident in HBM (Xb, Yb (nb, B) engine dtype; Ib (nb, B) int32
         output ids; Sb (nb, D+1) int32 segment tables, rows grouped by output as vec2list makes them).
         Each step then starts with ONE gather launch (batch (*counter) % nb, counter advanced on the
         device), so a captured step graph walks the epoch by itself."""
         nb, B = Xb.shape
         assert B == self.B and Sb.shape == (nb, self.D + 1)
-        for t, dt in ((Xb, F64), (Yb, F64), (Ib, torch.int32), (Sb, torch.int32)):
+        for t, dt in ((Xb, self.dt), (Yb, self.dt), (Ib, torch.int32), (Sb, torch.int32)):
             assert t.is_cuda and t.dtype == dt and t.is_contiguous()
         if counter is None:
             counter = torch.zeros(1, dtype=torch.int64, device=self.dev)
@@ -352,14 +363,14 @@ class DsviEngine:
     def gather_batch(self, stream=None):
         Xb, Yb, Ib, Sb, ctr = self._dataset
         s = L.stream_handle() if stream is None else stream
-        L.check(L.lib().nmgp_batch_gather_f64(*(ctypes.c_void_p(t.data_ptr()) for t in (Xb, Yb, Ib, Sb)), self.B,
+        L.check(getattr(L.lib(), "nmgp_batch_gather_" + self.sfx)(*(ctypes.c_void_p(t.data_ptr()) for t in (Xb, Yb, Ib, Sb)), self.B,
                                               self.D + 1, Xb.shape[0], ctypes.c_void_p(ctr.data_ptr()),
                                               *(ctypes.c_void_p(t.data_ptr()) for t in (self.x, self.y, self.row_out,
                                                                                         self.seg)), s),
                 "batch_gather")
 
     def device_noise(self, seed, counter):
-        H.normal_(self.noise, seed, counter=counter)
+        H.normal_(self.noise, seed, counter=counter)   # dtype-dispatched Philox normals
 
     # ------------------------------------------------------------------------------------ step
     def _call(self, fn, a, s):
@@ -387,12 +398,15 @@ class DsviEngine:
             return lambda s: p[name](s)
 
         def pw(name):
-            return lambda s: p[name](F64, s)
+            return lambda s: p[name](self.dt, s)
+
+        chol_fn = getattr(lib, "nmgp_chol_inv_batched_" + self.sfx)
 
         def chol(first, count):
             # fused factor + inverse: Afac <- L (in place), Cinv <- L^{-1}
-            return lambda s: L.check(lib.nmgp_chol_inv_batched_f64(vp(Af + first * MM * 8), M, M, MM,
-                                                                   vp(Ci + first * MM * 8), M, MM, count,
+            es = self.Afac.element_size()
+            return lambda s: L.check(chol_fn(vp(Af + first * MM * es), M, M, MM,
+                                                                   vp(Ci + first * MM * es), M, MM, count,
                                                                    vp(info + first * 4), s), "chol_inv")
 
         need_side = (not elbo_mode) or with_kl
@@ -409,8 +423,8 @@ class DsviEngine:
             ("chol", "chol", chol(FV, 4), "main"),
             ("inv3", "gemm", gemm("inv3"), "main"),
             ("proj3", "gemm", gemm("proj3"), "main"),
-            ("v", "row", row(lib.nmgp_dsvi_hyper_f64), "main"),
-            ("trow", "row", row(lib.nmgp_dsvi_trow_f64), "main"),
+            ("v", "row", row(getattr(lib, "nmgp_dsvi_hyper_" + self.sfx)), "main"),
+            ("trow", "row", row(getattr(lib, "nmgp_dsvi_trow_" + self.sfx)), "main"),
             ("build_gibbs", "pairwise", pw("build_gibbs"), "main"),
             ("chol_G", "chol", chol(NF + 3, 1), "main"),
             ("invG", "gemm", gemm("invG"), "main"),
@@ -421,9 +435,9 @@ class DsviEngine:
             if need_side:
                 steps += [("sig", "side", "join"), ("wait", "main", "join")]
             if with_kl:
-                steps.append(("kl", "row", row(lib.nmgp_dsvi_kl_f64), "main"))
-            steps += [("recon", "row", row(lib.nmgp_dsvi_recon_f64), "main"),
-                      ("finalize", "row", row(lib.nmgp_dsvi_finalize_f64), "main")]
+                steps.append(("kl", "row", row(getattr(lib, "nmgp_dsvi_kl_" + self.sfx)), "main"))
+            steps += [("recon", "row", row(getattr(lib, "nmgp_dsvi_recon_" + self.sfx)), "main"),
+                      ("finalize", "row", row(getattr(lib, "nmgp_dsvi_finalize_" + self.sfx)), "main")]
             return steps
         # KL branch on the side stream once all prior factors and Y = A^-1 mu exist (after projG):
         # KL terms, prior-diagonal adjoints, the variational factors' KL L-bar (first writer of those
@@ -431,29 +445,29 @@ class DsviEngine:
         # the prior adjoints Abar (bwd_pr waits for it)
         steps += [
             ("sig", "main", "kl_in"), ("wait", "side", "kl_in"),
-            ("kl", "row", row(lib.nmgp_dsvi_kl_f64), "side"),
-            ("delta", "row", row(lib.nmgp_dsvi_delta_f64), "side"),
+            ("kl", "row", row(getattr(lib, "nmgp_dsvi_kl_" + self.sfx)), "side"),
+            ("delta", "row", row(getattr(lib, "nmgp_dsvi_delta_" + self.sfx)), "side"),
             ("kl_lbar", "gemm", gemm("kl_lbar"), "side"),
             ("sig", "side", "kl_lbar"),
             ("kl_abar", "gemm", gemm("kl_abar"), "side"),
             ("bwd_kly", "gemm", gemm("bwd_kly"), "side"),
             ("sig", "side", "kl_done"),
             ("quad", "gemm", gemm("quad"), "main"),
-            ("recon", "row", row(lib.nmgp_dsvi_recon_f64), "main"),
+            ("recon", "row", row(getattr(lib, "nmgp_dsvi_recon_" + self.sfx)), "main"),
             ("wait", "main", "kl_lbar"),
             ("bwd_w", "gemm", gemm("bwd_w"), "main"),
             ("bwd_R", "gemm", gemm("bwd_R"), "main"),
             ("wait", "main", "kl_done"),
             ("bwd_pr", "gemm", gemm("bwd_pr"), "main"),
             ("bwd_build", "pairwise_bwd", pw("bwd_build"), "main"),
-            ("tbwd", "row", row(lib.nmgp_dsvi_tbwd_f64), "main"),
+            ("tbwd", "row", row(getattr(lib, "nmgp_dsvi_tbwd_" + self.sfx)), "main"),
             ("bwd_t1", "gemm", gemm("bwd_t1"), "main"),
             ("bwd_t2", "gemm", gemm("bwd_t2"), "main"),
             ("bwd_tbuild", "pairwise_bwd", pw("bwd_tbuild"), "main"),
-            ("vbwd", "row", row(lib.nmgp_dsvi_vbwd_f64), "main"),
+            ("vbwd", "row", row(getattr(lib, "nmgp_dsvi_vbwd_" + self.sfx)), "main"),
             ("bwd_v1", "gemm", gemm("bwd_v1"), "main"),
             ("bwd_v2", "gemm", gemm("bwd_v2"), "main"),
-            ("finalize", "row", row(lib.nmgp_dsvi_finalize_f64), "main"),
+            ("finalize", "row", row(getattr(lib, "nmgp_dsvi_finalize_" + self.sfx)), "main"),
         ]
         return steps
 

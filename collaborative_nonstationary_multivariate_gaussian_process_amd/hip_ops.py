@@ -358,7 +358,8 @@ def bwd_tiles(n, m):
 
 
 def colsum(a2d, out, beta=0.0):
-    L.check(L.lib().nmgp_colsum_f64(ctypes.c_void_p(a2d.data_ptr()), a2d.shape[0], a2d.shape[1], beta,
+    L.check(getattr(L.lib(), "nmgp_colsum_" + _sfx(a2d.dtype))(ctypes.c_void_p(a2d.data_ptr()), a2d.shape[0],
+                                                               a2d.shape[1], beta,
                                     ctypes.c_void_p(out.data_ptr()), L.stream_handle()), "colsum")
     return out
 
@@ -400,9 +401,10 @@ def adam_(theta, grad, m, v, step, lr, betas=(0.9, 0.999), eps=1e-8):
 
 
 def normal_(out, seed, counter=None, offset=0):
-    L.check(L.lib().nmgp_normal_f64(ctypes.c_void_p(out.data_ptr()), out.numel(), ctypes.c_uint64(seed),
-                                    ctypes.c_void_p(counter.data_ptr()) if counter is not None else None,
-                                    int(offset), L.stream_handle()), "normal")
+    fn = getattr(L.lib(), "nmgp_normal_" + _sfx(out.dtype))
+    L.check(fn(ctypes.c_void_p(out.data_ptr()), out.numel(), ctypes.c_uint64(seed),
+               ctypes.c_void_p(counter.data_ptr()) if counter is not None else None,
+               int(offset), L.stream_handle()), "normal")
     return out
 
 

@@ -94,8 +94,14 @@ class NMGP(Model):
     """code/nmgp_dsvi.py:99-155: variational parameters + 7 log hyper-parameters."""
 
     def __init__(self, number_observations, dim_outputs, Z, minibatch_size=None, mu_v=None, mu_W=None, mu_U=None,
-                 sqrt_v=None, sqrt_W=None, sqrt_U=None, seed=22, device=None, noise="torch"):
+                 sqrt_v=None, sqrt_W=None, sqrt_U=None, seed=22, device=None, noise="torch", dtype=F64):
+        """Reference signature plus: ``device``; ``noise`` ("torch": the reference's CPU randn stream,
+        "device": Philox on the GPU); ``dtype`` (float64 = the reference's arithmetic; float32 for
+        the HCP / ECoG-shaped configurations, SURVEY §8d, parity gates loss 1e-3 / grad 2e-2)."""
         super().__init__()
+        if dtype not in (torch.float64, torch.float32):
+            raise ValueError("dtype must be torch.float64 or torch.float32")
+        self.dtype_ = dtype
         self.device_ = torch.device(device) if device is not None else _default_device()
         Zt = torch.as_tensor(Z).detach().to(F64).reshape(-1, 1)
         self.Z = Zt.to(self.device_)
@@ -119,8 +125,8 @@ class NMGP(Model):
         for k, v in zip(HYPER_NAMES, hyper0):
             init[k] = torch.tensor(v, dtype=F64)
         self._offs, n = param_layout(D, M)
-        self._theta = torch.zeros(n, dtype=F64, device=self.device_)
-        self._grad = torch.zeros(n, dtype=F64, device=self.device_)
+        self._theta = torch.zeros(n, dtype=dtype, device=self.device_)
+        self._grad = torch.zeros(n, dtype=dtype, device=self.device_)
         self._grad_views = []
         for k in PARAM_NAMES:
             o, shp = self._offs[k]
@@ -146,14 +152,15 @@ class NMGP(Model):
         for k in PARAM_NAMES:
             p = getattr(self, k)
             o = self._offs[k][0]
-            if p.data_ptr() != self._theta.data_ptr() + o * 8:
+            if p.data_ptr() != self._theta.data_ptr() + o * self._theta.element_size():
                 raise RuntimeError(f"parameter {k} no longer aliases the flat device vector "
                                    "(re-assigning .data is not supported; use .data.copy_)")
 
     def engine(self, B, N=None):
         eng = self._engines.get(B)
         if eng is None:
-            eng = DsviEngine(self.D, self.M, B, self.Z.cpu().numpy().reshape(-1), device=self.device_)
+            eng = DsviEngine(self.D, self.M, B, self.Z.cpu().numpy().reshape(-1), device=self.device_,
+                             dtype=self.dtype_)
             self._engines[B] = eng
         eng.bind(self._theta, self._grad, frozen_mask=self._frozen_mask(), N=self.N if N is None else N)
         return eng
@@ -364,7 +371,7 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
               mu_v=None, mu_W=None, mu_U=None, sqrt_v=None, sqrt_W=None, sqrt_U=None, lr=0.01, itnum=1000,
               do_stop_criterion=False, seed=22, verbose=False, PATH="model.pt", continuous_training=False,
               show_ELBO=True, save_model=False, X_test_list=None, Y_test_list=None, device=None, noise="torch",
-              use_graph=False, n_elbo_sample=1000, distributed=False, group=None):
+              use_graph=False, n_elbo_sample=1000, distributed=False, group=None, dtype=F64):
     """code/nmgp_dsvi.py:758-909 on the MI355X.
 
     Returns (model, loss_list, time_list), or (model, loss_list, rmse_test_list, time_list) when
@@ -386,7 +393,7 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
     X_list, Y_list = vec2list(X, Y, I, dim=dim_outputs)
     model = NMGP(number_observations=Y_train_vec.shape[0], dim_outputs=dim_outputs, Z=np.asarray(z, np.float64),
                  minibatch_size=batch_size, mu_v=mu_v, mu_W=mu_W, mu_U=mu_U, sqrt_v=sqrt_v, sqrt_W=sqrt_W,
-                 sqrt_U=sqrt_U, seed=seed, device=device, noise=noise)
+                 sqrt_U=sqrt_U, seed=seed, device=device, noise=noise, dtype=dtype)
     opt_state = {}
     _apply_hyperpars(model, hyperpars, fix_hyperpars, continuous_training, PATH, opt_state)
     trainer = DsviTrainer(model, lr)

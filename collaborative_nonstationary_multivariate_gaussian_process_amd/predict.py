@@ -34,7 +34,7 @@ def predict_mean(model, inputs_list, index=None):
     I = torch.cat([torch.full((x.shape[0],), int(j), dtype=torch.long) for x, j in zip(xs, ids)]).to(dev)
     x = torch.cat(xs).to(dev).reshape(-1, 1).contiguous()
     Z = model.Z
-    th = {k: getattr(model, k).detach() for k in ["mu_W", "mu_v", "mu_U"]}
+    th = {k: getattr(model, k).detach().to(F64) for k in ["mu_W", "mu_v", "mu_U"]}   # predicts in fp64
     hyp = {k: float(torch.exp(getattr(model, k).detach())) for k in
            ["sigma2_tildeell_log", "length_scales_tildeell_log", "sigma2_L0_log", "length_scales_L0_log",
             "sigma2_L1_log", "length_scales_L1_log"]}
@@ -116,8 +116,8 @@ def _sampling_setup(model, x):
     dev = model.device_
     D, M = model.D, model.M
     Z = model.Z
-    p = {k: getattr(model, k).detach() for k in ["mu_W", "sqrt_W", "mu_v", "sqrt_v", "mu_U", "sqrt_U"]}
-    hyp = {k: float(torch.exp(getattr(model, k).detach())) for k in
+    p = {k: getattr(model, k).detach().to(F64) for k in ["mu_W", "sqrt_W", "mu_v", "sqrt_v", "mu_U", "sqrt_U"]}
+    hyp = {k: float(torch.exp(getattr(model, k).detach().to(F64))) for k in
            ["sigma2_tildeell_log", "length_scales_tildeell_log", "sigma2_L0_log", "length_scales_L0_log",
             "sigma2_L1_log", "length_scales_L1_log", "sigma2_err_log"]}
     N = x.shape[0]

@@ -164,6 +164,7 @@ int nmgp_pairwise_bwd_single_f64(const nmgp_pairwise_bwd_desc* h_desc, hipStream
 
 /* Deterministic column sums of a (rows x cols) row-major array: out[j] = beta*out[j] + sum_i a[i*cols+j] */
 int nmgp_colsum_f64(const double* a, int64_t rows, int64_t cols, double beta, double* out, hipStream_t stream);
+int nmgp_colsum_f32(const float* a, int64_t rows, int64_t cols, double beta, float* out, hipStream_t stream);
 
 /* ------------------------------------------------------------------ Kronecker kernels
  * kronecker_product (SIM_code/Utility/kronecker_operation.py:5-22): out[(i*r2+k)*(c1*c2)+j*c2+l] =
@@ -223,6 +224,15 @@ int nmgp_dsvi_delta_f64(const nmgp_dsvi_args* a, hipStream_t s);      /* prior d
 int nmgp_dsvi_tbwd_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* t-row backward            */
 int nmgp_dsvi_vbwd_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* v backward -> Phi         */
 int nmgp_dsvi_finalize_f64(const nmgp_dsvi_args* a, hipStream_t s);   /* loss + scalar gradients   */
+/* fp32 twins (HCP / ECoG-shaped configurations): same arguments, every buffer float */
+int nmgp_dsvi_hyper_f32(const nmgp_dsvi_args* a, hipStream_t s);
+int nmgp_dsvi_trow_f32(const nmgp_dsvi_args* a, hipStream_t s);
+int nmgp_dsvi_recon_f32(const nmgp_dsvi_args* a, hipStream_t s);
+int nmgp_dsvi_kl_f32(const nmgp_dsvi_args* a, hipStream_t s);
+int nmgp_dsvi_delta_f32(const nmgp_dsvi_args* a, hipStream_t s);
+int nmgp_dsvi_tbwd_f32(const nmgp_dsvi_args* a, hipStream_t s);
+int nmgp_dsvi_vbwd_f32(const nmgp_dsvi_args* a, hipStream_t s);
+int nmgp_dsvi_finalize_f32(const nmgp_dsvi_args* a, hipStream_t s);
 
 /* ------------------------------------------------------------------ optimiser / RNG
  * torch.optim.Adam update (code/nmgp_dsvi.py:777,854) on a flat parameter vector; step is a
@@ -234,6 +244,8 @@ int nmgp_adam_f32(float* theta, const float* grad, float* m, float* v, int64_t n
 /* Counter-based Philox4x32-10 standard normals: out[i] = N(0,1) for stream (seed, *counter + i) */
 int nmgp_normal_f64(double* out, int64_t n, uint64_t seed, const int64_t* counter, int64_t offset,
                     hipStream_t stream);
+int nmgp_normal_f32(float* out, int64_t n, uint64_t seed, const int64_t* counter, int64_t offset,
+                    hipStream_t stream);
 int nmgp_counter_add(int64_t* counter, int64_t inc, hipStream_t stream);
 /* On-device minibatch pipeline (replaces the host DataLoader + vec2list split of
  * code/nmgp_dsvi.py:816-837 for a dataset resident in HBM): copies minibatch
@@ -242,6 +254,9 @@ int nmgp_counter_add(int64_t* counter, int64_t inc, hipStream_t stream);
  * and then advances *batch_counter -- one launch, graph-capturable, no host work per step.      */
 int nmgp_batch_gather_f64(const double* Xb, const double* Yb, const int32_t* Ib, const int32_t* Sb, int64_t B,
                           int64_t nseg, int64_t nbatch, int64_t* batch_counter, double* x, double* y,
+                          int32_t* row_out, int32_t* seg, hipStream_t stream);
+int nmgp_batch_gather_f32(const float* Xb, const float* Yb, const int32_t* Ib, const int32_t* Sb, int64_t B,
+                          int64_t nseg, int64_t nbatch, int64_t* batch_counter, float* x, float* y,
                           int32_t* row_out, int32_t* seg, hipStream_t stream);
 
 #ifdef __cplusplus
