@@ -83,10 +83,39 @@ template <typename T> int gemm_single(const nmgp_gemm_desc& d, hipStream_t s);
 
 template <typename T> __device__ inline T shfl(T v, int src) { return __shfl(v, src, 64); }
 
+// Wave-wide sum on DPP (register-to-register lane moves; no LDS round trip as __shfl_xor's
+// ds_bpermute has): quad swaps, half-row and row mirrors, then row_bcast:15 / row_bcast:31 carry
+// the row sums into row 3; lane 63 holds the total, read back to every lane.  Fixed pattern:
+// deterministic.  Disabled rows of the broadcast steps add the `old` operand, 0.
+template <int CTRL, int ROWS> __device__ inline int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS> __device__ inline float dpp_t(float v) {
+  return __builtin_bit_cast(float, dpp_i<CTRL, ROWS>(__builtin_bit_cast(int, v)));
+}
+template <int CTRL, int ROWS> __device__ inline double dpp_t(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = dpp_i<CTRL, ROWS>((int)(b & 0xffffffffLL)), hi = dpp_i<CTRL, ROWS>((int)(b >> 32));
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+template <typename T> __device__ inline T wave_total(T v);
+template <> __device__ inline float wave_total<float>(float v) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+template <> __device__ inline double wave_total<double>(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), 63);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 template <typename T> __device__ inline T wave_sum(T v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_t<0xB1, 0xf>(v);    // quad_perm [1,0,3,2]
+  v += dpp_t<0x4E, 0xf>(v);    // quad_perm [2,3,0,1]
+  v += dpp_t<0x141, 0xf>(v);   // row_half_mirror
+  v += dpp_t<0x140, 0xf>(v);   // row_mirror: every lane holds its 16-lane row sum
+  v += dpp_t<0x142, 0xa>(v);   // row_bcast:15 into rows 1, 3
+  v += dpp_t<0x143, 0xc>(v);   // row_bcast:31 into rows 2, 3
+  return wave_total(v);
 }
 
 // Block-wide deterministic sum (blockDim.x multiple of 64, <= 1024). Result valid in all threads.
@@ -100,6 +129,26 @@ template <typename T> __device__ inline T block_sum(T v, T* scratch /* >= 16 */)
   for (int i = 0; i < nw; ++i) s += scratch[i];
   __syncthreads();
   return s;
+}
+
+// K block-wide deterministic sums in one pass (two barriers instead of 3K); scratch >= 16*K.
+template <typename T, int K> __device__ inline void block_sum_n(T (&v)[K], T* scratch) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = wave_sum(v[k]);
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) scratch[k * 16 + w] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    T s = 0;
+    for (int i = 0; i < nw; ++i) s += scratch[k * 16 + i];
+    v[k] = s;
+  }
+  __syncthreads();
 }
 
 template <typename T> __device__ inline T dexp(T x) { return exp(x); }

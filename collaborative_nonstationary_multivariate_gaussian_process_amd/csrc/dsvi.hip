@@ -125,91 +125,99 @@ __global__ __launch_bounds__(256) void dsvi_trow_kernel(Args a) {
 // ------------------------------------------------------------------------------------ recon
 // training (elbo_mode 0): row r of output o uses pairs (o, s) for s <= o  -> l_r[s] = L[o,s,r]
 // ELBO     (elbo_mode 1): row r uses pairs (s, o) for s >= o (column gather, nmgp_dsvi.py:361)
-template <typename T, int NR>
+//
+// One workgroup per row, columns across the 256 threads: the row's 3 + 4*ns dot products (ns =
+// latent functions / pairs the row uses) are formed column-parallel with every load independent,
+// reduced per wave then across the 4 waves in LDS; wave 0 forms the row's likelihood and per-s
+// adjoints; all threads then scale the W rows and build the P-bar rows column-parallel.  Enough
+// rows in flight (B workgroups, 4 waves each) to cover HBM latency.
+template <typename T>
 __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  __shared__ T red[16];
-  T* rowacc_all = (T*)smem_raw;
   const int M = a.M, B = a.B, D = a.D;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r = blockIdx.x * 4 + w;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int r = blockIdx.x;
   const bool elbo = a.elbo_mode != 0;
-  T Rrow = 0, epart = 0, c0p = 0, c1p = 0;
-  if (r < B) {
-    const int o = a.row_out[r];
-    const T lam = (T)a.jitter;
-    const T* th = (const T*)a.theta;
-    const T s20 = hyp<T>(a, 2), s21 = hyp<T>(a, 4), s2e = hyp<T>(a, 6);
-    const int64_t BM = (int64_t)B * M;
-    const T* K12 = (const T*)a.K12;
-    const T* P = (const T*)a.P;
-    const T* PG = P + 3 * BM + (int64_t)r * M;
-    const T* KG = K12 + 3 * BM + (int64_t)r * M;
-    const T* P0 = P + 1 * BM + (int64_t)r * M;
-    const T* K0 = K12 + 1 * BM + (int64_t)r * M;
-    const T* P1 = P + 2 * BM + (int64_t)r * M;
-    const T* K1 = K12 + 2 * BM + (int64_t)r * M;
-    T* WG = (T*)a.WG;
-    T* WP = (T*)a.WP;
-    const T* muW = th + a.off_muW;
-    const T* muU = th + a.off_muU;
-    const T* noise = (const T*)a.noise;
-    const int slo = elbo ? o : 0, shi = elbo ? D - 1 : o;
+  const int o = a.row_out[r];
+  const int slo = elbo ? o : 0, shi = elbo ? D - 1 : o, ns = shi - slo + 1;
+  const int K = 3 + 4 * ns;                 // dot products of this row
+  T* part = (T*)smem_raw;                   // [4 waves][K] wave partials
+  T* sv = part + 4 * (3 + 4 * D);           // per-s results: fg, fp, mbar, sbar  (4 x D)
+  T* scal = sv + 4 * D;                     // cg, c0, c1
+  const T lam = (T)a.jitter;
+  const T* th = (const T*)a.theta;
+  const T s20 = hyp<T>(a, 2), s21 = hyp<T>(a, 4), s2e = hyp<T>(a, 6);
+  const int64_t BM = (int64_t)B * M;
+  const T* K12 = (const T*)a.K12;
+  const T* P = (const T*)a.P;
+  const T* PG = P + 3 * BM + (int64_t)r * M;
+  const T* KG = K12 + 3 * BM + (int64_t)r * M;
+  const T* P0 = P + 1 * BM + (int64_t)r * M;
+  const T* K0 = K12 + 1 * BM + (int64_t)r * M;
+  const T* P1 = P + 2 * BM + (int64_t)r * M;
+  const T* K1 = K12 + 2 * BM + (int64_t)r * M;
+  T* WG = (T*)a.WG;
+  T* WP = (T*)a.WP;
+  const T* muW = th + a.off_muW;
+  const T* muU = th + a.off_muU;
+  const T* noise = (const T*)a.noise;
 
-    T qG = 0, q0 = 0, q1 = 0;
-    for (int c = lane; c < M; c += 64) {
-      qG += PG[c] * KG[c];
-      q0 += P0[c] * K0[c];
-      q1 += P1[c] * K1[c];
+  // ---- phase 1: column-parallel dot products
+  {
+    T q[3] = {0, 0, 0};
+    for (int c = t; c < M; c += 256) {
+      q[0] += PG[c] * KG[c];
+      q[1] += P0[c] * K0[c];
+      q[2] += P1[c] * K1[c];
     }
-    qG = wave_sum(qG);
-    q0 = wave_sum(q0);
-    q1 = wave_sum(q1);
-
-    T mreg[NR], greg[NR], lreg[NR], sdreg[NR], zreg[NR];
 #pragma unroll
-    for (int u = 0; u < NR; ++u) mreg[u] = greg[u] = lreg[u] = sdreg[u] = zreg[u] = 0;
-    for (int s = slo; s <= shi; ++s) {
-      // latent function s: m = P_G mu_W[s], g = 1 - rowsum(P_G o K_G12) + ||P_G L_W[s]||^2
-      const T* wg = WG + (int64_t)s * BM + (int64_t)r * M;
-      const T* mw = muW + (int64_t)s * M;
-      T sm = 0, sq = 0;
-      for (int c = lane; c < M; c += 64) {
-        sm += PG[c] * mw[c];
-        const T x = wg[c];
-        sq += x * x;
-      }
-      sm = wave_sum(sm);
-      sq = wave_sum(sq);
-      setlane(mreg, s, lane, sm);
-      setlane(greg, s, lane, (T)1 - qG + sq);
-      // coefficient pair: training (o, s), ELBO (s, o)
+    for (int k = 0; k < 3; ++k) {
+      const T v = wave_sum(q[k]);
+      if (lane == 0) part[w * K + k] = v;
+    }
+  }
+  for (int u = 0; u < ns; ++u) {
+    const int s = slo + u;
+    const int pi = elbo ? s : o, pj = elbo ? o : s;
+    const T* Pk = (s == o) ? P1 : P0;
+    const T* wg = WG + (int64_t)s * BM + (int64_t)r * M;
+    const T* wp = WP + (int64_t)s * BM + (int64_t)r * M;
+    const T* mw = muW + (int64_t)s * M;
+    const T* mu = muU + ((int64_t)pi * D + pj) * M;
+    T d4[4] = {0, 0, 0, 0};
+    for (int c = t; c < M; c += 256) {
+      const T x = wg[c], y = wp[c];
+      d4[0] += PG[c] * mw[c];
+      d4[1] += x * x;
+      d4[2] += Pk[c] * mu[c];
+      d4[3] += y * y;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const T v = wave_sum(d4[k]);
+      if (lane == 0) part[w * K + 3 + 4 * u + k] = v;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2 (wave 0): likelihood of the row and the per-s adjoints
+  T Rrow = 0, epart = 0, c0p = 0, c1p = 0;
+  if (w == 0) {
+    auto tot = [&](int k) { return part[k] + part[K + k] + part[2 * K + k] + part[3 * K + k]; };
+    const T qG = tot(0), q0 = tot(1), q1 = tot(2);
+    T lm = 0, lg = 0;
+    for (int u = lane; u < ns; u += 64) {
+      const int s = slo + u;
       const int pi = elbo ? s : o, pj = elbo ? o : s;
       const bool diag = (s == o);
-      const T* Pk = diag ? P1 : P0;
-      const T* mu = muU + ((int64_t)pi * D + pj) * M;
-      const T* wp = WP + (int64_t)s * BM + (int64_t)r * M;
-      T pm = 0, pq = 0;
-      for (int c = lane; c < M; c += 64) {
-        pm += Pk[c] * mu[c];
-        const T x = wp[c];
-        pq += x * x;
-      }
-      pm = wave_sum(pm);
-      pq = wave_sum(pq);
-      const T s2p = var_floor((diag ? s21 : s20) - (diag ? q1 : q0) + pq);
+      const T m = tot(3 + 4 * u), g = (T)1 - qG + tot(4 + 4 * u);
+      const T s2p = var_floor((diag ? s21 : s20) - (diag ? q1 : q0) + tot(6 + 4 * u));
       const T sd = dsqrt(s2p + lam);
       const T zz = noise[M + B + (int64_t)(pi * (pi + 1) / 2 + pj) * B + r];
-      const T smp = pm + zz * sd;
-      setlane(lreg, s, lane, diag ? dexp(smp) : smp);
-      setlane(sdreg, s, lane, sd);
-      setlane(zreg, s, lane, zz);
-    }
-    T lm = 0, lg = 0;
-#pragma unroll
-    for (int u = 0; u < NR; ++u) {
-      lm += lreg[u] * mreg[u];
-      lg += lreg[u] * lreg[u] * greg[u];
+      const T smp = tot(5 + 4 * u) + zz * sd;
+      const T l = diag ? dexp(smp) : smp;
+      lm += l * m;
+      lg += l * l * g;
     }
     const T F = wave_sum(lm);
     lg = wave_sum(lg);
@@ -217,100 +225,91 @@ __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
     const T var = sc * sc;
     const T res = ((const T*)a.y)[r] - F;
     Rrow = -(res * res) / ((T)2 * var) - dlog(sc) - (T)kLogSqrt2Pi - ((T)0.5 / s2e) * lg;
-
     if (!elbo) {
       const T cc = -(T)a.N_over_B;
       const T Fbar = cc * res / var;
-      T mbar[NR], gbar[NR], sbar[NR], s2pb[NR];
-      T cg = 0, c0 = 0;
-#pragma unroll
-      for (int u = 0; u < NR; ++u) {
-        const int s = lane + 64 * u;
-        const bool inr = s <= o;
-        mbar[u] = inr ? Fbar * lreg[u] : (T)0;
-        gbar[u] = inr ? cc * (-(lreg[u] * lreg[u]) / ((T)2 * s2e)) : (T)0;
-        const T lbar = Fbar * mreg[u] + cc * (-(lreg[u] * greg[u]) / s2e);
-        const T sb = inr ? (s == o ? lbar * lreg[u] : lbar) : (T)0;
-        sbar[u] = sb;
-        s2pb[u] = inr ? sb * zreg[u] / ((T)2 * sdreg[u]) : (T)0;
-        cg += gbar[u];
-        if (s < o) c0 += s2pb[u];
+      RowBuf<T> rb{(T*)a.rowbuf, B, D};
+      T cg = 0, c0 = 0, c1 = 0;
+      for (int s = lane; s < D; s += 64) {
+        T mbar = 0, gbar = 0, sbar = 0, s2pb = 0;
+        if (s <= o) {
+          const int u = s;                      // training: slo = 0
+          const bool diag = (s == o);
+          const T m = tot(3 + 4 * u), g = (T)1 - qG + tot(4 + 4 * u);
+          const T s2p = var_floor((diag ? s21 : s20) - (diag ? q1 : q0) + tot(6 + 4 * u));
+          const T sd = dsqrt(s2p + lam);
+          const T zz = noise[M + B + (int64_t)(o * (o + 1) / 2 + s) * B + r];
+          const T smp = tot(5 + 4 * u) + zz * sd;
+          const T l = diag ? dexp(smp) : smp;
+          mbar = Fbar * l;
+          gbar = cc * (-(l * l) / ((T)2 * s2e));
+          const T lbar = Fbar * m + cc * (-(l * g) / s2e);
+          sbar = diag ? lbar * l : lbar;
+          s2pb = sbar * zz / ((T)2 * sd);
+          cg += gbar;
+          if (s < o) c0 += s2pb; else c1 = s2pb;
+          sv[s] = (T)2 * gbar;
+          sv[D + s] = (T)2 * s2pb;
+          sv[2 * D + s] = mbar;
+          sv[3 * D + s] = sbar;
+        }
+        rb.mbar(s)[r] = mbar;
+        rb.sbar(s)[r] = sbar;
       }
       cg = wave_sum(cg);
       c0 = wave_sum(c0);
-      const T c1 = bcast(s2pb, o);
+      c1 = wave_sum(c1);                        // one lane holds it
       c0p = c0;
       c1p = c1;
-      // d loss / d log s2_err  (Normal_logprob with scale sqrt(s2e), then the -0.5/s2e sum)
       epart = cc * ((res * res / (sc * sc * sc) - (T)1 / sc) / ((T)2 * sc) + (T)0.5 * lg / (s2e * s2e)) * s2e;
-      // W-hat: scale the quadratic-form rows in place by 2*adjoint
-      for (int s = 0; s <= o; ++s) {
-        const T fg = (T)2 * bcast(gbar, s);
-        const T fp = (T)2 * bcast(s2pb, s);
-        T* wg = WG + (int64_t)s * BM + (int64_t)r * M;
-        T* wp = WP + (int64_t)s * BM + (int64_t)r * M;
-        for (int c = lane; c < M; c += 64) {
-          wg[c] *= fg;
-          wp[c] *= fp;
-        }
-      }
-      // rows of the latent functions s > o are not computed by the W GEMM (l_s = 0 there) but the
-      // k-concatenated P-bar GEMM reads them: store exact zeros
-      for (int s = o + 1; s < D; ++s) {
-        T* wg = WG + (int64_t)s * BM + (int64_t)r * M;
-        for (int c = lane; c < M; c += 64) wg[c] = (T)0;
-      }
-      // P-bar initial rows (the rank-<=D mean terms and the -c*K12 diagonal term)
-      T* acc = rowacc_all + (int64_t)w * M;
-      T* PbG = (T*)a.Pbar + 3 * BM + (int64_t)r * M;
-      T* Pb0 = (T*)a.Pbar + 1 * BM + (int64_t)r * M;
-      T* Pb1 = (T*)a.Pbar + 2 * BM + (int64_t)r * M;
-      for (int c = lane; c < M; c += 64) acc[c] = -cg * KG[c];
-      for (int d = 0; d <= o; ++d) {
-        const T mb = bcast(mbar, d);
-        const T* mw = muW + (int64_t)d * M;
-        for (int c = lane; c < M; c += 64) acc[c] += mb * mw[c];
-      }
-      for (int c = lane; c < M; c += 64) PbG[c] = acc[c];
-      for (int c = lane; c < M; c += 64) acc[c] = -c0 * K0[c];
-      for (int j = 0; j < o; ++j) {
-        const T sb = bcast(sbar, j);
-        const T* mu = muU + ((int64_t)o * D + j) * M;
-        for (int c = lane; c < M; c += 64) acc[c] += sb * mu[c];
-      }
-      for (int c = lane; c < M; c += 64) Pb0[c] = acc[c];
-      {
-        const T sb = bcast(sbar, o);
-        const T* mu = muU + ((int64_t)o * D + o) * M;
-        for (int c = lane; c < M; c += 64) Pb1[c] = sb * mu[c] - c1 * K1[c];
-      }
-      RowBuf<T> rb{(T*)a.rowbuf, B, D};
-#pragma unroll
-      for (int u = 0; u < NR; ++u) {
-        const int s = lane + 64 * u;
-        if (s < D) {
-          rb.mbar(s)[r] = mbar[u];
-          rb.sbar(s)[r] = sbar[u];
-        }
-      }
       if (lane == 0) {
+        scal[0] = cg;
+        scal[1] = c0;
+        scal[2] = c1;
         rb.cG()[r] = cg;
         rb.c0()[r] = c0;
         rb.c1()[r] = c1;
       }
     }
+    if (lane == 0) {
+      T* rp = (T*)a.red + (int64_t)r * 4;
+      rp[0] = Rrow;
+      rp[1] = epart;
+      rp[2] = c0p;
+      rp[3] = c1p;
+    }
   }
-  if ((threadIdx.x & 63) != 0) Rrow = epart = c0p = c1p = 0;   // every lane holds the row's value
-  Rrow = block_sum(Rrow, red);
-  epart = block_sum(epart, red);
-  c0p = block_sum(c0p, red);
-  c1p = block_sum(c1p, red);
-  if (threadIdx.x == 0) {
-    T* rp = (T*)a.red + (int64_t)blockIdx.x * 4;
-    rp[0] = Rrow;
-    rp[1] = epart;
-    rp[2] = c0p;
-    rp[3] = c1p;
+  if (elbo) return;
+  __syncthreads();
+
+  // ---- phase 3: W-hat rows (scaled in place by 2*adjoint), zero rows, P-bar initial rows
+  const T cg = scal[0], c0 = scal[1], c1 = scal[2];
+  for (int s = 0; s <= o; ++s) {
+    const T fg = sv[s], fp = sv[D + s];
+    T* wg = WG + (int64_t)s * BM + (int64_t)r * M;
+    T* wp = WP + (int64_t)s * BM + (int64_t)r * M;
+    for (int c = t; c < M; c += 256) {
+      wg[c] *= fg;
+      wp[c] *= fp;
+    }
+  }
+  // rows of the latent functions s > o are not computed by the W GEMM (l_s = 0 there) but the
+  // k-concatenated P-bar GEMM reads them: store exact zeros
+  for (int s = o + 1; s < D; ++s) {
+    T* wg = WG + (int64_t)s * BM + (int64_t)r * M;
+    for (int c = t; c < M; c += 256) wg[c] = (T)0;
+  }
+  T* PbG = (T*)a.Pbar + 3 * BM + (int64_t)r * M;
+  T* Pb0 = (T*)a.Pbar + 1 * BM + (int64_t)r * M;
+  T* Pb1 = (T*)a.Pbar + 2 * BM + (int64_t)r * M;
+  for (int c = t; c < M; c += 256) {
+    T acc = -cg * KG[c];
+    for (int d = 0; d <= o; ++d) acc += sv[2 * D + d] * muW[(int64_t)d * M + c];
+    PbG[c] = acc;
+    acc = -c0 * K0[c];
+    for (int j = 0; j < o; ++j) acc += sv[3 * D + j] * muU[((int64_t)o * D + j) * M + c];
+    Pb0[c] = acc;
+    Pb1[c] = sv[3 * D + o] * muU[((int64_t)o * D + o) * M + c] - c1 * K1[c];
   }
 }
 
@@ -504,39 +503,71 @@ __global__ __launch_bounds__(256) void dsvi_vbwd_kernel(Args a) {
 
 // ------------------------------------------------------------------------------------ finalize
 template <typename T>
-__global__ __launch_bounds__(256) void dsvi_finalize_kernel(Args a) {
-  __shared__ T red[16];
+__global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
+  // every partial sum of the step in ONE pass: 5 row-block sums, per-factor KL slabs, 12 scalar
+  // partials of the RBF backward problems; all loads of a thread are independent, one multi-value
+  // block reduction (fixed order, deterministic)
+  __shared__ T red[16 * 20];
   __shared__ T sc[8];
+  __shared__ T klstage[1024 * 4];
+#ifdef NMGP_FIN_TRACE
+  const unsigned long long t0 = wall_clock64();
+#endif
   const int D = a.D, M = a.M, NF = a.NF;
   const T* rp = (const T*)a.red;
-  const T* fb = (const T*)a.facbuf;
-  T R = 0, e = 0, c0 = 0, c1 = 0, vs = 0;
-  for (int b = threadIdx.x; b < a.nblk_rows; b += blockDim.x) {
-    R += rp[b * 4 + 0];
-    e += rp[b * 4 + 1];
-    c0 += rp[b * 4 + 2];
-    c1 += rp[b * 4 + 3];
-    if (!a.elbo_mode) vs += rp[(int64_t)a.nblk_rows * 4 + b];
+  T acc[20];
+#pragma unroll
+  for (int k = 0; k < 20; ++k) acc[k] = 0;
+  for (int b = threadIdx.x; b < a.nblk_rows; b += blockDim.x) {   // recon: one partial per row
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] += rp[b * 4 + k];
   }
-  R = block_sum(R, red);
-  e = block_sum(e, red);
-  c0 = block_sum(c0, red);
-  c1 = block_sum(c1, red);
-  vs = block_sum(vs, red);
-  T klw = 0, klv = 0, klu = 0;
+  if (!a.elbo_mode)                                                // t-row backward: per 4-row block
+    for (int b = threadIdx.x; b < (a.B + 3) / 4; b += blockDim.x) acc[4] += rp[(int64_t)a.nblk_rows * 4 + b];
   const int nslab = (M + KL_ROWS - 1) / KL_ROWS;
   const T* kp = kl_part<T>(a);
-  for (int f = threadIdx.x; f < NF; f += blockDim.x) {
-    T p[4] = {0, 0, 0, 0};
-    for (int sl = 0; sl < nslab; ++sl)
-      for (int j = 0; j < 4; ++j) p[j] += kp[((int64_t)f * nslab + sl) * 4 + j];
-    const T v = p[1] - p[0] + (T)0.5 * (p[2] + p[3] - (T)M);
-    ((T*)a.facbuf)[f] = v;                       // per-factor KL (kept for inspection)
-    if (f < D) klw += v; else if (f == NF - 1) klv += v; else klu += v;
+  // per-factor KL from its slab partials, summed in slab order; the partials are brought in by
+  // (factor, slab) in parallel chunks that fit LDS, so no thread walks a dependent chain of loads
+  {
+    constexpr int CH = 1024;                     // (factor, slab) pairs per chunk, 4 values each
+    T* stage = klstage;
+    const int fpc = CH / nslab;                  // whole factors per chunk (M <= 16384: fpc >= 1)
+    for (int fb = 0; fb < NF; fb += fpc) {
+      const int nf = min(fpc, NF - fb), base = fb * nslab, n = nf * nslab;
+      for (int i = threadIdx.x; i < n; i += blockDim.x) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) stage[i * 4 + j] = kp[(int64_t)(base + i) * 4 + j];
+      }
+      __syncthreads();
+      for (int f = fb + (int)threadIdx.x; f < fb + nf; f += blockDim.x) {
+        T p[4] = {0, 0, 0, 0};
+        for (int sl = 0; sl < nslab; ++sl)
+          for (int j = 0; j < 4; ++j) p[j] += stage[((f - fb) * nslab + sl) * 4 + j];
+        const T v = p[1] - p[0] + (T)0.5 * (p[2] + p[3] - (T)M);
+        ((T*)a.facbuf)[f] = v;                   // per-factor KL (kept for inspection)
+        acc[f < D ? 5 : (f == NF - 1 ? 6 : 7)] += v;
+      }
+      __syncthreads();
+    }
   }
-  klw = block_sum(klw, red);
-  klv = block_sum(klv, red);
-  klu = block_sum(klu, red);
+  if (!a.elbo_mode) {
+    const T* sp = (const T*)a.scal_part;
+#pragma unroll
+    for (int p = 0; p < 6; ++p)
+      for (int64_t t = a.scal_off[p] + threadIdx.x; t < a.scal_off[p + 1]; t += blockDim.x) {
+        acc[8 + 2 * p] += sp[t * 2 + 0];
+        acc[9 + 2 * p] += sp[t * 2 + 1];
+      }
+  }
+#ifdef NMGP_FIN_TRACE
+  const unsigned long long t1 = wall_clock64();
+#endif
+  block_sum_n(acc, red);
+#ifdef NMGP_FIN_TRACE
+  const unsigned long long t2 = wall_clock64();
+#endif
+  const T R = acc[0], e = acc[1], c0 = acc[2], c1 = acc[3], vs = acc[4];
+  const T klw = acc[5], klv = acc[6], klu = acc[7];
   T* out = (T*)a.out;
   if (a.elbo_mode) {
     if (threadIdx.x == 0) {
@@ -547,24 +578,14 @@ __global__ __launch_bounds__(256) void dsvi_finalize_kernel(Args a) {
     }
     return;
   }
-  // scalar partials of the RBF backward problems: L0_12, L0_22, L1_12, L1_22, t12, t22
-  const T* sp = (const T*)a.scal_part;
-  for (int p = 0; p < 6; ++p) {
-    T s0 = 0, s1 = 0;
-    for (int64_t t = a.scal_off[p] + threadIdx.x; t < a.scal_off[p + 1]; t += blockDim.x) {
-      s0 += sp[t * 2 + 0];
-      s1 += sp[t * 2 + 1];
-    }
-    s0 = block_sum(s0, red);
-    s1 = block_sum(s1, red);
-    if (threadIdx.x == 0) {
-      if (p == 0) { sc[0] = s0; sc[1] = s1; }
-      else if (p == 1) { sc[0] += s0; sc[1] += s1; }
-      else if (p == 2) { sc[2] = s0; sc[3] = s1; }
-      else if (p == 3) { sc[2] += s0; sc[3] += s1; }
-      else if (p == 4) { sc[4] = s0; sc[5] = s1; }
-      else { sc[4] += s0; sc[5] += s1; }
-    }
+  // L0_12 + L0_22, L1_12 + L1_22, t12 + t22 (sigma2 / length-scale partials)
+  if (threadIdx.x == 0) {
+    sc[0] = acc[8] + acc[10];
+    sc[1] = acc[9] + acc[11];
+    sc[2] = acc[12] + acc[14];
+    sc[3] = acc[13] + acc[15];
+    sc[4] = acc[16] + acc[18];
+    sc[5] = acc[17] + acc[19];
   }
   __syncthreads();
   T* g = (T*)a.grad;
@@ -597,6 +618,15 @@ __global__ __launch_bounds__(256) void dsvi_finalize_kernel(Args a) {
     if (j > i) continue;
     g[a.off_muU + idx] += (i == j ? Y[yu1 + idx] : Y[yu0 + idx]);
   }
+#ifdef NMGP_FIN_TRACE
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t3 = wall_clock64();
+    out[5] = (T)(t1 - t0);
+    out[6] = (T)(t2 - t1);
+    out[7] = (T)(t3 - t2);
+  }
+#endif
 }
 
 // ------------------------------------------------------------------------------------ Adam
@@ -704,11 +734,8 @@ template <typename T> static int dsvi_trow(const Args* a, hipStream_t s) {
 template <typename T> static int dsvi_recon(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
   if (a->D > 128) return -1;
-  const size_t sm = (size_t)4 * a->M * sizeof(T);
-  if (a->D <= 64)
-    hipLaunchKernelGGL((dsvi_recon_kernel<T, 1>), dim3(blocks_rows(a->B)), dim3(256), sm, s, *a);
-  else
-    hipLaunchKernelGGL((dsvi_recon_kernel<T, 2>), dim3(blocks_rows(a->B)), dim3(256), sm, s, *a);
+  const size_t sm = (size_t)(4 * (3 + 4 * a->D) + 4 * a->D + 4) * sizeof(T);
+  hipLaunchKernelGGL(dsvi_recon_kernel<T>, dim3((unsigned)a->B), dim3(256), sm, s, *a);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
@@ -739,7 +766,8 @@ template <typename T> static int dsvi_vbwd(const Args* a, hipStream_t s) {
 }
 template <typename T> static int dsvi_finalize(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
-  hipLaunchKernelGGL(dsvi_finalize_kernel<T>, dim3(1), dim3(256), 0, s, *a);
+  if (a->M > 16384) return -2;
+  hipLaunchKernelGGL(dsvi_finalize_kernel<T>, dim3(1), dim3(1024), 0, s, *a);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }

@@ -94,8 +94,8 @@ class DsviEngine:
         self.rowbuf = e(2 * D + 5, B)
         # KL per factor | delta/w vectors (8M) | selection weights (4D^2) | e_f rows (NF M) | KL slab partials
         self.facbuf = e(NF + 8 * M + 4 * D * D + NF * M + NF * ((M + 15) // 16) * 4)
-        self.nblk = (B + 3) // 4
-        self.red = e(5 * self.nblk)
+        self.nblk = B                       # recon partials: one per row; then (B+3)//4 t-row partials
+        self.red = e(4 * B + (B + 3) // 4)
         self.out = e(8)
         self.n_ct = (M + 63) // 64
         self.n_rt = (B + 31) // 32
