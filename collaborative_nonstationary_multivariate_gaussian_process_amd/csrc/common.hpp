@@ -151,6 +151,16 @@ template <typename T, int K> __device__ inline void block_sum_n(T (&v)[K], T* sc
   __syncthreads();
 }
 
+// v if ok else +0, bitwise: no load is sunk into a branch (loads of a batch stay in flight together)
+// and a NaN in a masked-off element cannot leak through a multiply.
+template <typename T> __device__ inline T keep_if(T v, bool ok);
+template <> __device__ inline double keep_if<double>(double v, bool ok) {
+  return __builtin_bit_cast(double, __builtin_bit_cast(unsigned long long, v) & (ok ? ~0ull : 0ull));
+}
+template <> __device__ inline float keep_if<float>(float v, bool ok) {
+  return __builtin_bit_cast(float, __builtin_bit_cast(unsigned int, v) & (ok ? ~0u : 0u));
+}
+
 template <typename T> __device__ inline T dexp(T x) { return exp(x); }
 template <> __device__ inline float dexp<float>(float x) { return expf(x); }
 template <typename T> __device__ inline T dlog(T x) { return log(x); }

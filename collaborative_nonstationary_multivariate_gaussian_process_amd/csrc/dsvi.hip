@@ -515,15 +515,59 @@ __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
 #endif
   const int D = a.D, M = a.M, NF = a.NF;
   const T* rp = (const T*)a.red;
+  const int t = threadIdx.x;
   T acc[20];
 #pragma unroll
   for (int k = 0; k < 20; ++k) acc[k] = 0;
-  for (int b = threadIdx.x; b < a.nblk_rows; b += blockDim.x) {   // recon: one partial per row
+  // Loads are clamped and masked (keep_if) instead of guarded, so the first RU strides of every
+  // partial array are in flight together: one memory round trip instead of one per loop trip.
+  constexpr int RU = 4;
+  const int nbr = a.nblk_rows;                                     // recon: one partial per row
+  T rv[RU][4];
+#pragma unroll
+  for (int u = 0; u < RU; ++u) {
+    const int b = min(t + u * 1024, nbr - 1);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) rv[u][k] = rp[b * 4 + k];
+  }
+  const int ntb = a.elbo_mode ? 0 : (a.B + 3) / 4;                 // t-row backward: per 4-row block
+  const T tv = rp[(int64_t)nbr * 4 + min(t, max(ntb - 1, 0))];
+  T sv[6][2][2];
+  const T* sp = (const T*)a.scal_part;
+  if (!a.elbo_mode) {
+#pragma unroll
+    for (int p = 0; p < 6; ++p)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int64_t i = max(min(a.scal_off[p] + t + u * 1024, a.scal_off[p + 1] - 1), (int64_t)0);
+        sv[p][u][0] = sp[i * 2 + 0];
+        sv[p][u][1] = sp[i * 2 + 1];
+      }
+  }
+#pragma unroll
+  for (int u = 0; u < RU; ++u)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] += keep_if(rv[u][k], t + u * 1024 < nbr);
+  for (int b = t + RU * 1024; b < nbr; b += 1024)
 #pragma unroll
     for (int k = 0; k < 4; ++k) acc[k] += rp[b * 4 + k];
+  acc[4] += keep_if(tv, t < ntb);
+  for (int b = t + 1024; b < ntb; b += 1024) acc[4] += rp[(int64_t)nbr * 4 + b];
+  if (!a.elbo_mode) {
+#pragma unroll
+    for (int p = 0; p < 6; ++p) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bool ok = a.scal_off[p] + t + u * 1024 < a.scal_off[p + 1];
+        acc[8 + 2 * p] += keep_if(sv[p][u][0], ok);
+        acc[9 + 2 * p] += keep_if(sv[p][u][1], ok);
+      }
+      for (int64_t i = a.scal_off[p] + t + 2048; i < a.scal_off[p + 1]; i += 1024) {
+        acc[8 + 2 * p] += sp[i * 2 + 0];
+        acc[9 + 2 * p] += sp[i * 2 + 1];
+      }
+    }
   }
-  if (!a.elbo_mode)                                                // t-row backward: per 4-row block
-    for (int b = threadIdx.x; b < (a.B + 3) / 4; b += blockDim.x) acc[4] += rp[(int64_t)a.nblk_rows * 4 + b];
   const int nslab = (M + KL_ROWS - 1) / KL_ROWS;
   const T* kp = kl_part<T>(a);
   // per-factor KL from its slab partials, summed in slab order; the partials are brought in by
@@ -534,12 +578,15 @@ __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
     const int fpc = CH / nslab;                  // whole factors per chunk (M <= 16384: fpc >= 1)
     for (int fb = 0; fb < NF; fb += fpc) {
       const int nf = min(fpc, NF - fb), base = fb * nslab, n = nf * nslab;
-      for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      if (t < n) {
+        T q[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) stage[i * 4 + j] = kp[(int64_t)(base + i) * 4 + j];
+        for (int j = 0; j < 4; ++j) q[j] = kp[(int64_t)(base + t) * 4 + j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) stage[t * 4 + j] = q[j];
       }
       __syncthreads();
-      for (int f = fb + (int)threadIdx.x; f < fb + nf; f += blockDim.x) {
+      for (int f = fb + t; f < fb + nf; f += blockDim.x) {
         T p[4] = {0, 0, 0, 0};
         for (int sl = 0; sl < nslab; ++sl)
           for (int j = 0; j < 4; ++j) p[j] += stage[((f - fb) * nslab + sl) * 4 + j];
@@ -549,15 +596,6 @@ __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
       }
       __syncthreads();
     }
-  }
-  if (!a.elbo_mode) {
-    const T* sp = (const T*)a.scal_part;
-#pragma unroll
-    for (int p = 0; p < 6; ++p)
-      for (int64_t t = a.scal_off[p] + threadIdx.x; t < a.scal_off[p + 1]; t += blockDim.x) {
-        acc[8 + 2 * p] += sp[t * 2 + 0];
-        acc[9 + 2 * p] += sp[t * 2 + 1];
-      }
   }
 #ifdef NMGP_FIN_TRACE
   const unsigned long long t1 = wall_clock64();
@@ -606,17 +644,42 @@ __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
     gs[6] = e;                            // sigma2_err_log
     for (int k = 0; k < 7; ++k) g[a.off_hyp + k] = (a.frozen_mask >> k & 1) ? (T)0 : gs[k];
   }
-  // KL mean gradients A2^{-1} mu (Y) and mu_v += vbar
-  const T* Y = (const T*)a.Y;
-  for (int64_t idx = threadIdx.x; idx < (int64_t)D * M; idx += blockDim.x) g[a.off_muW + idx] += Y[idx];
-  const T* vbar = (const T*)a.vbar + M;   // completed by the v-backward kernel
-  for (int c = threadIdx.x; c < M; c += blockDim.x) g[a.off_muv + c] += vbar[c] + Y[(int64_t)D * M + c];
+  // KL mean gradients A2^{-1} mu (Y) and mu_v += vbar: element-wise, batches of 4 strides with all
+  // loads issued before the stores (restrict: g does not alias Y / vbar)
+  T* __restrict__ gw = g;
+  const T* __restrict__ Y = (const T*)a.Y;
+  const T* __restrict__ vbar = (const T*)a.vbar + M;   // completed by the v-backward kernel
+  const int DM = D * M;
+  for (int i0 = t; i0 < DM; i0 += 4096) {
+    T gv[4], yv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = min(i0 + u * 1024, DM - 1);
+      gv[u] = gw[a.off_muW + i];
+      yv[u] = Y[i];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i0 + u * 1024 < DM) gw[a.off_muW + i0 + u * 1024] = gv[u] + yv[u];
+  }
+  for (int c = t; c < M; c += 1024) gw[a.off_muv + c] += vbar[c] + Y[(int64_t)DM + c];
   const int64_t yu0 = (int64_t)(D + 1) * M, yu1 = yu0 + (int64_t)D * D * M;
-  for (int64_t idx = threadIdx.x; idx < (int64_t)D * D * M; idx += blockDim.x) {
-    const int ij = (int)(idx / M);
-    const int i = ij / D, j = ij - i * D;
-    if (j > i) continue;
-    g[a.off_muU + idx] += (i == j ? Y[yu1 + idx] : Y[yu0 + idx]);
+  const int DDM = D * D * M;
+  for (int i0 = t; i0 < DDM; i0 += 4096) {
+    T gv[4], yv[4];
+    bool live[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int idx = min(i0 + u * 1024, DDM - 1);
+      const int ij = idx / M;
+      const int i = ij / D, j = ij - i * D;
+      live[u] = j <= i && i0 + u * 1024 < DDM;
+      gv[u] = gw[a.off_muU + idx];
+      yv[u] = Y[(i == j ? yu1 : yu0) + idx];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (live[u]) gw[a.off_muU + i0 + u * 1024] = gv[u] + yv[u];
   }
 #ifdef NMGP_FIN_TRACE
   __syncthreads();
@@ -630,6 +693,8 @@ __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
 }
 
 // ------------------------------------------------------------------------------------ Adam
+__device__ inline unsigned long long bits_of(double x) { return __builtin_bit_cast(unsigned long long, x); }
+__device__ inline unsigned int bits_of(float x) { return __builtin_bit_cast(unsigned int, x); }
 template <typename T>
 __global__ void adam_kernel(T* th, const T* g, T* m, T* v, int64_t n, const int64_t* step, T lr, T b1, T b2,
                             T eps) {
@@ -640,8 +705,13 @@ __global__ void adam_kernel(T* th, const T* g, T* m, T* v, int64_t n, const int6
   const T bc2s = (T)sqrt(1.0 - pow((double)b2, t));
   const T gi = g[i];
   T mi = m[i];
+  const T v0 = v[i];
+  // grad, exp_avg and exp_avg_sq all +0 (the never-used strictly-upper triangles and unused (i<j)
+  // blocks of the factor parameters): the update below leaves every value bit-identical, so the
+  // parameter is neither read nor written
+  if ((bits_of(gi) | bits_of(mi) | bits_of(v0)) == 0) return;
   mi = mi + ((T)1 - b1) * (gi - mi);          // exp_avg.lerp_(grad, 1 - beta1)
-  const T vi = v[i] * b2 + ((T)1 - b2) * gi * gi;
+  const T vi = v0 * b2 + ((T)1 - b2) * gi * gi;
   m[i] = mi;
   v[i] = vi;
   const T denom = dsqrt(vi) / bc2s + eps;

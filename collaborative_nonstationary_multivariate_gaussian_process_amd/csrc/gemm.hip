@@ -104,15 +104,6 @@ __device__ inline void mma_tile(const T* As, const T* Bs, int lane, int wr, int 
   }
 }
 
-// Zero element e of a register tile unless bit e of okm is set (bitwise, so no load is sunk into a
-// branch and a NaN in a masked-off triangle cannot leak through a multiply).
-template <typename T> __device__ inline T keep_if(T v, bool ok);
-template <> __device__ inline double keep_if<double>(double v, bool ok) {
-  return __builtin_bit_cast(double, __builtin_bit_cast(unsigned long long, v) & (ok ? ~0ull : 0ull));
-}
-template <> __device__ inline float keep_if<float>(float v, bool ok) {
-  return __builtin_bit_cast(float, __builtin_bit_cast(unsigned int, v) & (ok ? ~0u : 0u));
-}
 
 // Fast-path register tile: 16-byte units (V = 16/sizeof(T) consecutive elements along the operand's
 // contiguous dimension), 8/V units per thread and operand, so one buffer_load_dwordx4 fetches V
@@ -232,12 +223,22 @@ __device__ inline void mainloop_fast(const nmgp_gemm_desc& d, const Tile& tl, co
       for (int v = 0; v < V; ++v) rs[e * V + v] = ksc[tl.k0 + min(kload + b_k(e * V + v), tl.K - 1)];
     }
   };
-  auto advance = [&]() {
+  auto step1 = [&]() {
     kload += GBK;
     kkA += GBK;
     if (kbA_on && kkA >= kinA) { kkA = 0; oA += jumpA; } else { oA += stepA; }
     kkB += GBK;
     if (kbB_on && kkB >= kinB) { kkB = 0; oB += jumpB; } else { oB += stepB; }
+  };
+  // k-tiles wholly inside a triangular operand's zero triangle are never fetched (inside k-blocks
+  // the range trimming of the caller cannot remove them; uniform scalar test)
+  auto tile_empty = [&]() {
+    return (aLo && kkA > tl.i0 + GBM - 1) || (aUp && kkA + GBK - 1 < tl.i0) || (bLo && tl.j0 > kkB + GBK - 1) ||
+           (bUp && tl.j0 + GBN - 1 < kkB);
+  };
+  auto advance = [&]() {
+    step1();
+    while (kload < tl.kend && tile_empty()) step1();
   };
   unsigned okm_st = 0xffffu;  // masks of the k-tile held in registers
   // element s of the register tile into LDS stage N (masked if the tile needs it); the last
@@ -253,6 +254,8 @@ __device__ inline void mainloop_fast(const nmgp_gemm_desc& d, const Tile& tl, co
     N[wa + e * wsa + v * wva] = a;
     N[GBK * LP + wb + e * wsb + v * wvb] = b;
   };
+  while (kload < tl.kend && tile_empty()) step1();
+  if (kload >= tl.kend) return;  // every k-tile of the range is structurally zero
   prep(kload);
 #pragma unroll
   for (int e = 0; e < NU; ++e) issue(e);
@@ -267,6 +270,7 @@ __device__ inline void mainloop_fast(const nmgp_gemm_desc& d, const Tile& tl, co
     for (int q = 0; q < 8; ++q) put(S, q, false);
   }
   // tiles past kend read garbage or zeros and are masked when staged, so the fetch needs no guard
+  int kreg = kload;  // k-tile now being fetched into the registers
   prep(kload);
 #pragma unroll
   for (int e = 0; e < NU; ++e) issue(e);
@@ -277,7 +281,7 @@ __device__ inline void mainloop_fast(const nmgp_gemm_desc& d, const Tile& tl, co
   lds_barrier();
   int cur = 0;
   [[maybe_unused]] int it = 0;
-  for (int kt = tl.kbeg; kt + GBK < tl.kend; kt += GBK) {
+  while (kreg < tl.kend) {  // LDS stage cur holds a tile, the registers hold tile kreg
     T* As = S + cur * LDS_T;
     T* Ns = S + (cur ^ 1) * LDS_T;
     GEMM_STAMP(3 + 2 * min(it, 30));
@@ -294,6 +298,7 @@ __device__ inline void mainloop_fast(const nmgp_gemm_desc& d, const Tile& tl, co
     }
     okm_st = okm;
     need_st = need;
+    kreg = kload;
     GEMM_STAMP(100 + 4 * min(it, 30));
     advance();
     prep(kload);

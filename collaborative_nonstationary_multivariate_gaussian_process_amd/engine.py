@@ -239,6 +239,10 @@ class DsviEngine:
             if i > 0:
                 d17.append(g(self.Pbar, self.WP, th, B, M, i * M, (M, 1, BM), (1, M, MM), (M, 1), flags=L.B_UPPER,
                              kb=(M, M), beta=1.0, offs=(0, sU + (i * D) * MM, 1 * BM), row_seg=i))
+        # the P-bar products feed R (main chain); the L-bar / mu-bar products below only accumulate
+        # gradient rows, so they run on the side stream beside bwd_R .. bwd_v2
+        p["bwd_w"] = G(d17)
+        d17 = []
         for d in range(D):
             d17.append(g(gr, self.P, self.WG, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_TRIL, beta=1.0,
                          offs=(3 * BM, d * BM, sW + d * MM), k_seg=d, seg_span=D - d))
@@ -250,7 +254,7 @@ class DsviEngine:
                          offs=(typ * BM, j * BM, sU + (i * D + j) * MM), k_seg=i))
             d17.append(g(gr, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1), beta=1.0,
                          offs=(typ * BM, (D + j) * B, muU + (i * D + j) * M), k_seg=i))
-        p["bwd_w"] = G(d17)
+        p["bwd_lbar"] = G(d17)
         # B3: R_k = Pbar_k Ainv_k (G,0,1) ; Abar_k = Cinv^T diag(delta) Cinv ; KL L-bar
         d18 = [g(self.R, self.Pbar, self.Ainv, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), offs=(k * BM, k * MM, k * BM),
                  **rows_all) for k in (3, 1, 2)]
@@ -441,7 +445,7 @@ class DsviEngine:
             return steps
         # KL branch on the side stream once all prior factors and Y = A^-1 mu exist (after projG):
         # KL terms, prior-diagonal adjoints, the variational factors' KL L-bar (first writer of those
-        # gradient rows -- bwd_w waits for it, so the accumulation order is fixed) and the KL part of
+        # gradient rows -- bwd_lbar follows it on the same stream, so the accumulation order is fixed) and the KL part of
         # the prior adjoints Abar (bwd_pr waits for it)
         steps += [
             ("sig", "main", "kl_in"), ("wait", "side", "kl_in"),
@@ -454,8 +458,12 @@ class DsviEngine:
             ("sig", "side", "kl_done"),
             ("quad", "gemm", gemm("quad"), "main"),
             ("recon", "row", row(getattr(lib, "nmgp_dsvi_recon_" + self.sfx)), "main"),
-            ("wait", "main", "kl_lbar"),
+            ("sig", "main", "recon"),
             ("bwd_w", "gemm", gemm("bwd_w"), "main"),
+            # L-bar / mu-bar gradient rows: after the KL L-bar (their first writer, same stream) and recon
+            ("wait", "side", "recon"),
+            ("bwd_lbar", "gemm", gemm("bwd_lbar"), "side"),
+            ("sig", "side", "lbar_done"),
             ("bwd_R", "gemm", gemm("bwd_R"), "main"),
             ("wait", "main", "kl_done"),
             ("bwd_pr", "gemm", gemm("bwd_pr"), "main"),
@@ -467,6 +475,7 @@ class DsviEngine:
             ("vbwd", "row", row(getattr(lib, "nmgp_dsvi_vbwd_" + self.sfx)), "main"),
             ("bwd_v1", "gemm", gemm("bwd_v1"), "main"),
             ("bwd_v2", "gemm", gemm("bwd_v2"), "main"),
+            ("wait", "main", "lbar_done"),
             ("finalize", "row", row(getattr(lib, "nmgp_dsvi_finalize_" + self.sfx)), "main"),
         ]
         return steps

@@ -62,6 +62,7 @@ def gemm_desc(C, A, B, m, n, k, sA, sB, sC, *, flags=0, alpha=1.0, beta=0.0, kb=
 
 
 GEMM_BK = 32   # k-tile of gemm_kernel (csrc/gemm.hip GBK)
+_KSPLIT_FACTOR = float(os.environ.get("NMGP_KSPLIT_FACTOR", "2.0"))   # tuning knob (tools/gemm_probe.py)
 
 
 def _auto_ksplit(k_eff, group_tiles, work_per_wg):
@@ -73,7 +74,7 @@ def _auto_ksplit(k_eff, group_tiles, work_per_wg):
     kt = -(-max(k_eff, 1) // GEMM_BK)
     if group_tiles <= 64 and kt >= 4:
         return max(1, min(16, kt // 2, -(-256 // max(group_tiles, 1))))
-    if kt > 2 * work_per_wg and kt >= 8:
+    if kt > _KSPLIT_FACTOR * work_per_wg and kt >= 8:
         return max(1, min(16, kt // 4, -(-kt // work_per_wg)))
     return 1
 

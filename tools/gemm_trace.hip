@@ -15,15 +15,16 @@ int main(int argc, char** argv) {
   const int m = argc > 1 ? atoi(argv[1]) : 2000, n = argc > 2 ? atoi(argv[2]) : 256, k = argc > 3 ? atoi(argv[3]) : 256;
   const int ks = argc > 4 ? atoi(argv[4]) : 1;
   const int transA = argc > 5 ? atoi(argv[5]) : 0;
+  const int nprob = argc > 6 ? atoi(argv[6]) : 1;   // copies of the problem in one grouped launch
   double *A, *B, *C, *ws;
   int32_t* ctr;
-  const int tm = (m + 63) / 64, tn = (n + 63) / 64, nblk = tm * tn * ks;
+  const int tm = (m + 63) / 64, tn = (n + 63) / 64, nblk1 = tm * tn * ks, nblk = nblk1 * nprob;
   hipMalloc(&A, (size_t)m * k * 8);
   hipMalloc(&B, (size_t)k * n * 8);
   hipMalloc(&C, (size_t)m * n * 8);
-  hipMalloc(&ws, (size_t)tm * tn * ks * 4096 * 8);
-  hipMalloc(&ctr, (size_t)tm * tn * 4);
-  hipMemset(ctr, 0, (size_t)tm * tn * 4);
+  hipMalloc(&ws, (size_t)tm * tn * ks * 4096 * 8 * nprob);
+  hipMalloc(&ctr, (size_t)tm * tn * 4 * nprob);
+  hipMemset(ctr, 0, (size_t)tm * tn * 4 * nprob);
   hipMemset(A, 0, (size_t)m * k * 8);
   hipMemset(B, 0, (size_t)k * n * 8);
   const int NT = 1024 + 4 * nblk;
@@ -39,15 +40,21 @@ int main(int argc, char** argv) {
   d.sB_k = n; d.sB_j = 1; d.sC_i = n; d.sC_j = 1;
   d.m = m; d.n = n; d.k = k; d.row_seg = -1; d.k_seg = -1; d.alpha = 1.0;
   d.tiles_m = tm; d.tiles_n = tn; d.tile_start = 0; d.ksplit = ks; d.ws = ws; d.counters = ctr; d.batch = 1;
+  std::vector<nmgp_gemm_desc> hd(nprob, d);
+  for (int p = 0; p < nprob; ++p) {
+    hd[p].tile_start = p * nblk1;
+    hd[p].ws = ws + (size_t)p * tm * tn * ks * 4096;
+    hd[p].counters = ctr + (size_t)p * tm * tn;
+  }
   nmgp_gemm_desc* dd;
-  hipMalloc(&dd, sizeof(d));
-  hipMemcpy(dd, &d, sizeof(d), hipMemcpyHostToDevice);
+  hipMalloc(&dd, sizeof(d) * nprob);
+  hipMemcpy(dd, hd.data(), sizeof(d) * nprob, hipMemcpyHostToDevice);
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  for (int r = 0; r < 3; ++r) nmgp::launch_grouped<double>(dd, 1, nblk, nullptr, 0);
+  for (int r = 0; r < 3; ++r) nmgp::launch_grouped<double>(dd, nprob, nblk, nullptr, 0);
   hipEventRecord(e0);
-  nmgp::launch_grouped<double>(dd, 1, nblk, nullptr, 0);
+  nmgp::launch_grouped<double>(dd, nprob, nblk, nullptr, 0);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms;
@@ -56,12 +63,13 @@ int main(int argc, char** argv) {
   {
     // untraced: average of 20 back-to-back launches
     hipEventRecord(e0);
-    for (int r = 0; r < 20; ++r) nmgp::launch_grouped<double>(dd, 1, nblk, nullptr, 0);
+    for (int r = 0; r < 20; ++r) nmgp::launch_grouped<double>(dd, nprob, nblk, nullptr, 0);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms20;
     hipEventElapsedTime(&ms20, e0, e1);
-    const double fl = 2.0 * m * n * k;
+    const double fl = 2.0 * m * n * k * nprob;
+    printf("nprob %d: ", nprob);
     printf("%dx%dx%d ksplit %d transA %d: %.2f us per launch (20 back-to-back), %.2f TF/s\n", m, n, k, ks, transA,
            ms20 * 50, fl / (ms20 / 20 * 1e-3) / 1e12);
     return 0;
@@ -69,6 +77,7 @@ int main(int argc, char** argv) {
 #endif
   std::vector<unsigned long long> t(NT);
   hipMemcpy(t.data(), tr, NT * 8, hipMemcpyDeviceToHost);
+  printf("nprob %d: ", nprob);
   printf("%dx%dx%d ksplit %d transA %d: kernel %.2f us, %d workgroups; WG0 cycles: desc %llu, first-load-issue %llu\n",
          m, n, k, ks, transA, ms * 1000, nblk, t[1] - t[0], t[2] - t[1]);
   for (int it = 0; it < 31 && t[3 + 2 * it]; ++it)
