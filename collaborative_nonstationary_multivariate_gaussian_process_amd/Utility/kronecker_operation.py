@@ -2,9 +2,10 @@
 
 ``kronecker_product`` / ``kronecker_product_diag`` are bit-exact (one multiply per element, the
 reference's operand order); ``kron_mv`` is (B kron K) y without forming the product (two MFMA GEMMs,
-reference reshape order).  ``kron_inv`` / ``kron_logdet`` use the eigendecompositions the reference
-takes with the removed ``torch.symeig``; the symmetric eigensolver itself is the library
-one (``torch.linalg.eigh`` on the device) -- a HIP Jacobi eigensolver is SURVEY §8f row f2 (next).
+reference reshape order).  ``kron_inv`` / ``kron_logdet`` take the eigendecompositions the reference
+takes with the removed ``torch.symeig`` on the HIP Jacobi eigensolver (``eig.hip``:
+in-LDS parallel Jacobi for n <= 64, block Jacobi above).  Eigenvector signs are arbitrary, as
+LAPACK's are; every output here is invariant to them.
 """
 import torch
 
@@ -37,8 +38,8 @@ def kron_mv(B, K, y):
 
 def kron_inv(sigma2, B, K):
     """kronecker_operation.py:36-53."""
-    wB, vB = torch.linalg.eigh(_dev(B))
-    wK, vK = torch.linalg.eigh(_dev(K))
+    wB, vB = H.syevj(_dev(B))
+    wK, vK = H.syevj(_dev(K))
     U = kronecker_product(vB, vK)
     t = kronecker_product_diag(wB, wK)
     Us = U * (1.0 / (t + _dev(sigma2)))[None, :]
@@ -47,6 +48,6 @@ def kron_inv(sigma2, B, K):
 
 def kron_logdet(sigma2, B, K):
     """kronecker_operation.py:56-69."""
-    wB = torch.linalg.eigvalsh(_dev(B))
-    wK = torch.linalg.eigvalsh(_dev(K))
+    wB = H.syevj(_dev(B))[0]
+    wK = H.syevj(_dev(K))[0]
     return torch.log(kronecker_product_diag(wB, wK) + _dev(sigma2)).sum()

@@ -986,6 +986,47 @@ static nmgp_gemm_desc gdesc(const void* A, int64_t sAi, int64_t sAk, const void*
   return d;
 }
 
+int gemm_big_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C, int64_t sCi,
+                 int64_t sCj, int m, int n, int k, int flags, float alpha, float beta, int64_t sAb, int64_t sBb,
+                 int64_t sCb, int batch, void* ws, hipStream_t s);
+size_t gemm_big_ws_bytes();
+
+// f32 recursion (same algebra as chol_inv_rec below) with the products on the 128x128 MFMA kernel
+// of gemm_big.hip, split-K into `ws` where the tile grid would not fill the chip.
+static int chol_inv_rec_big(float* A, int n, int64_t lda, int64_t sA, float* X, int64_t ldx, int64_t sX,
+                            int64_t batch, int32_t* info, hipStream_t s, int col_off, void* ws) {
+  if (n <= 128) return chol_inv_small<float>(A, n, lda, sA, X, ldx, sX, batch, info, s, col_off, col_off == 0);
+  int n1 = ((n / 2 + 127) / 128) * 128;
+  if (n1 >= n) n1 = n - 128;
+  const int n2 = n - n1, nb = (int)batch;
+  int rc;
+  float* A21 = A + (int64_t)n1 * lda;
+  float* A22 = A21 + n1;
+  float* X21 = X + (int64_t)n1 * ldx;
+  float* X22 = X21 + n1;
+  float* X12 = X + n1;
+  if ((rc = chol_inv_rec_big(A, n1, lda, sA, X, ldx, sX, batch, info, s, col_off, ws)) != NMGP_OK) return rc;
+  if ((rc = block_copy<float>(A21, lda, sA, X21, ldx, sX, n2, n1, batch, s)) != NMGP_OK) return rc;
+  // L21 = A21 X11^T      (op(B)(k,j) = X11[j][k], upper)
+  if ((rc = gemm_big_f32(X21, ldx, X, ldx, 1, A21, lda, 1, n2, n1, n1, NMGP_B_UPPER, 1.f, 0.f, sX, sX, sA, nb, ws,
+                         s)) != NMGP_OK)
+    return rc;
+  // A22 -= L21 L21^T     (lower tiles only: the trailing SYRK)
+  if ((rc = gemm_big_f32(A21, lda, A21, lda, 1, A22, lda, 1, n2, n2, n1, NMGP_OUT_LOWER, -1.f, 1.f, sA, sA, sA, nb,
+                         ws, s)) != NMGP_OK)
+    return rc;
+  if ((rc = block_copy<float>(nullptr, 0, 0, A + n1, lda, sA, n1, n2, batch, s)) != NMGP_OK) return rc;   // L12 = 0
+  if ((rc = chol_inv_rec_big(A22, n2, lda, sA, X22, ldx, sX, batch, info, s, col_off + n1, ws)) != NMGP_OK) return rc;
+  // T = L21 X11 (op(B)(k,j) = X11[k][j], lower), stored transposed in X12;  X21 = -X22 T
+  if ((rc = gemm_big_f32(A21, lda, X, ldx, 0, X12, 1, ldx, n2, n1, n1, NMGP_B_LOWER, 1.f, 0.f, sA, sX, sX, nb, ws,
+                         s)) != NMGP_OK)
+    return rc;
+  if ((rc = gemm_big_f32(X22, ldx, X12, ldx, 1, X21, ldx, 1, n2, n1, n2, NMGP_A_LOWER, -1.f, 0.f, sX, sX, sX, nb, ws,
+                         s)) != NMGP_OK)
+    return rc;
+  return block_copy<float>(nullptr, 0, 0, X12, ldx, sX, n1, n2, batch, s);   // X12 = 0
+}
+
 // Recursive factor + inverse for n > 256 (the HCP / ECoG / stress shapes).  With A split at n1
 // (a multiple of 128 near n/2):
 //   [L11, X11] = chol_inv(A11)                         (recursion; leaves <= 128: fused kernel)
@@ -998,8 +1039,10 @@ static nmgp_gemm_desc gdesc(const void* A, int64_t sAi, int64_t sAk, const void*
 // strictly upper part is zeroed block by block.
 template <typename T>
 static int chol_inv_rec(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx, int64_t sX, int64_t batch,
-                        int32_t* info, hipStream_t s, int col_off) {
+                        int32_t* info, hipStream_t s, int col_off, void* ws) {
   if (n <= 128) return chol_inv_small<T>(A, n, lda, sA, X, ldx, sX, batch, info, s, col_off, col_off == 0);
+  if constexpr (std::is_same<T, float>::value) return chol_inv_rec_big(A, n, lda, sA, X, ldx, sX, batch, info, s,
+                                                                       col_off, ws);
   int n1 = ((n / 2 + 127) / 128) * 128;
   if (n1 >= n) n1 = n - 128;
   const int n2 = n - n1;
@@ -1009,7 +1052,7 @@ static int chol_inv_rec(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx,
   T* X21 = X + (int64_t)n1 * ldx;
   T* X22 = X21 + n1;
   T* X12 = X + n1;
-  if ((rc = chol_inv_rec<T>(A, n1, lda, sA, X, ldx, sX, batch, info, s, col_off)) != NMGP_OK) return rc;
+  if ((rc = chol_inv_rec<T>(A, n1, lda, sA, X, ldx, sX, batch, info, s, col_off, ws)) != NMGP_OK) return rc;
   if ((rc = block_copy<T>(A21, lda, sA, X21, ldx, sX, n2, n1, batch, s)) != NMGP_OK) return rc;
   // L21 = A21 X11^T   (B(k,j) = X11[j][k]: upper triangular)
   nmgp_gemm_desc d1 = gdesc(X21, ldx, 1, X, 1, ldx, A21, lda, 1, n2, n1, n1, NMGP_B_UPPER, 1.0, 0.0, sX, sX, sA, batch);
@@ -1019,7 +1062,8 @@ static int chol_inv_rec(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx,
                             batch);
   if ((rc = gemm_single<T>(d2, s)) != NMGP_OK) return rc;
   if ((rc = block_copy<T>(nullptr, 0, 0, A + n1, lda, sA, n1, n2, batch, s)) != NMGP_OK) return rc;   // L12 = 0
-  if ((rc = chol_inv_rec<T>(A22, n2, lda, sA, X22, ldx, sX, batch, info, s, col_off + n1)) != NMGP_OK) return rc;
+  if ((rc = chol_inv_rec<T>(A22, n2, lda, sA, X22, ldx, sX, batch, info, s, col_off + n1, ws)) != NMGP_OK)
+    return rc;
   // T = L21 X11 (X11 lower) stored transposed in X12;  X21 = -X22 T
   nmgp_gemm_desc d3 = gdesc(A21, lda, 1, X, ldx, 1, X12, 1, ldx, n2, n1, n1, NMGP_B_LOWER, 1.0, 0.0, sA, sX, sX, batch);
   if ((rc = gemm_single<T>(d3, s)) != NMGP_OK) return rc;
@@ -1033,7 +1077,7 @@ static int chol_inv_rec(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx,
 // GEMM-based path above otherwise.
 template <typename T>
 static int chol_inv_launch(T* A, int64_t n, int64_t lda, int64_t sA, T* X, int64_t ldx, int64_t sX, int64_t batch,
-                           int32_t* info, hipStream_t s) {
+                           int32_t* info, hipStream_t s, void* ws = nullptr) {
   if (A == nullptr) return -1;
   if (n < 0) return -2;
   if (lda < n) return -3;
@@ -1042,7 +1086,7 @@ static int chol_inv_launch(T* A, int64_t n, int64_t lda, int64_t sA, T* X, int64
   if (batch < 0) return -8;
   if (n == 0 || batch == 0) return NMGP_OK;
   if (batch > 65535) return -8;
-  if (n > 256) return chol_inv_rec<T>(A, (int)n, lda, sA, X, ldx, sX, batch, info, s, 0);
+  if (n > 256) return chol_inv_rec<T>(A, (int)n, lda, sA, X, ldx, sX, batch, info, s, 0, ws);
   return chol_inv_small<T>(A, (int)n, lda, sA, X, ldx, sX, batch, info, s, 0, 1);
 }
 
@@ -1070,5 +1114,13 @@ int nmgp_chol_inv_batched_f64(double* A, int64_t n, int64_t lda, int64_t sA, dou
 int nmgp_chol_inv_batched_f32(float* A, int64_t n, int64_t lda, int64_t sA, float* X, int64_t ldx, int64_t sX,
                               int64_t b, int32_t* info, hipStream_t s) {
   return nmgp::chol_inv_launch<float>(A, n, lda, sA, X, ldx, sX, b, info, s);
+}
+int64_t nmgp_chol_inv_workspace_size_f32(int64_t n, int64_t batch) {
+  return (n > 256 && batch > 0) ? (int64_t)nmgp::gemm_big_ws_bytes() : 0;
+}
+int nmgp_chol_inv_batched_ws_f32(float* A, int64_t n, int64_t lda, int64_t sA, float* X, int64_t ldx, int64_t sX,
+                                 int64_t b, int32_t* info, void* ws, int64_t ws_bytes, hipStream_t s) {
+  if (ws != nullptr && ws_bytes < nmgp_chol_inv_workspace_size_f32(n, b)) return -11;
+  return nmgp::chol_inv_launch<float>(A, n, lda, sA, X, ldx, sX, b, info, s, ws);
 }
 }

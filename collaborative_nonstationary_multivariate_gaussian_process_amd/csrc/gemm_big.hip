@@ -1,0 +1,368 @@
+// Large-tile f32 GEMM / SYRK for the recursive Cholesky of big matrices (HCP M=512, ECoG M=1024,
+// the M=4096 stress case): the trailing update A22 -= L21 L21^T and the three inverse / panel
+// products of chol_inv_rec (chol.hip).  The step GEMMs of the DSVI engine stay on the grouped
+// 64x64 kernel (gemm.hip); this one is for few, large, dense problems.
+//
+//   * 128x128x32 block tile, 256 threads = 4 waves in 2x2, each wave 64x64 as 2x2
+//     v_mfma_f32_32x32x2_f32 accumulators (exact f32 products, 64 FLOP/clk/SIMD: the fp32 peak).
+//   * k is permuted inside a k-tile: at k-step s lane l feeds k = 16*(l>>5) + s instead of the
+//     instruction's 2s + (l>>5), for both operands -- a sum over k does not care -- so each lane's
+//     16 operand values of a k-tile are contiguous in LDS and arrive with four ds_read_b128.
+//   * LDS images [row][k] with a 36-float pitch (conflict-free b128 reads), two stages; the next
+//     k-tile's 16-byte global (buffer) loads are in flight while the current one's 64 MFMAs issue.
+//   * Triangular operands restrict each tile's k range (A_LOWER / B_UPPER / B_LOWER) and only the
+//     k-tiles that straddle the diagonal, and a k tail, pay for element masks.  OUT_LOWER launches
+//     only the lower tiles (SYRK).
+//   * Deterministic split-K when the grid would not fill the chip: partials are published
+//     write-through (sc1) into caller workspace, the last-arriving chunk of a tile sums them in
+//     chunk order (its own from registers) and applies the epilogue.
+//   * blockIdx -> tile mapping is XCD-aware: the 8 XCDs each get a contiguous run of tiles (shared
+//     A rows stay in one L2).
+#include "common.hpp"
+
+namespace nmgp {
+
+constexpr int BBM = 128, BBN = 128, BBK = 32, BP = 36;   // tile and LDS pitch (floats, 144 B rows)
+constexpr int BSTAGE = (BBM + BBN) * BP;                  // floats per LDS stage
+constexpr int BSLOT = BBM * BBN;                          // floats per split-K partial tile
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4g __attribute__((ext_vector_type(4)));
+
+struct BigGemmArgs {
+  const float* A; const float* B; float* C;
+  int64_t lda, ldb, sCi, sCj;
+  int64_t sAb, sBb, sCb;
+  int m, n, k, flags;
+  int b_kcontig;            // 1: op(B)(k,j) = B[j*ldb + k]; 0: op(B)(k,j) = B[k*ldb + j]
+  float alpha, beta;
+  int tiles_m, tiles_n, tiles;   // tiles per batch item (lower tiles only with OUT_LOWER)
+  int ksplit;
+  float* ws; int32_t* counters;
+};
+
+__device__ inline float4 ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+__global__ __launch_bounds__(256) void gemm_big_kernel(BigGemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float big_smem[];
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int S = g.ksplit;
+
+  // XCD-aware block order: hardware places block b on XCD b % 8; give each XCD a contiguous run
+  int bid = blockIdx.x;
+  const int nb = gridDim.x;
+  if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);
+  const int tile = bid / S, split = bid - tile * S;
+  const int64_t bat = blockIdx.y;
+  int tm, tn;
+  if (g.flags & NMGP_OUT_LOWER) {   // row-major over the lower triangle of the tile grid
+    tm = (int)((sqrtf(8.0f * (float)tile + 1.0f) - 1.0f) * 0.5f);
+    while ((tm + 1) * (tm + 2) / 2 <= tile) ++tm;
+    while (tm * (tm + 1) / 2 > tile) --tm;
+    tn = tile - tm * (tm + 1) / 2;
+  } else {
+    tm = tile / g.tiles_n;
+    tn = tile - tm * g.tiles_n;
+  }
+  const int i0 = tm * BBM, j0 = tn * BBN;
+  const int fl = g.flags;
+  const bool aLo = fl & NMGP_A_LOWER, bUp = fl & NMGP_B_UPPER, bLo = fl & NMGP_B_LOWER;
+
+  // this tile's structurally nonzero k range, in whole k-tiles, then this split's share
+  int kbeg = 0, kend = g.k;
+  if (aLo) kend = min(kend, i0 + BBM);
+  if (bUp) kend = min(kend, j0 + BBN);
+  if (bLo) kbeg = max(kbeg, j0);
+  kbeg = (kbeg / BBK) * BBK;
+  const int nkt = kend > kbeg ? (kend - kbeg + BBK - 1) / BBK : 0;
+  const int chunk = (nkt + S - 1) / S;
+  const int kt0 = kbeg + min(split * chunk, nkt) * BBK;
+  const int kt1 = min(kend, kbeg + min((split + 1) * chunk, nkt) * BBK);
+
+  const float* Ab = g.A + bat * g.sAb;
+  const float* Bb = g.B + bat * g.sBb;
+  const __amdgpu_buffer_rsrc_t rA = make_rsrc(Ab, ((int64_t)(g.m - 1) * g.lda + g.k) * 4);
+  const __amdgpu_buffer_rsrc_t rB =
+      g.b_kcontig ? make_rsrc(Bb, ((int64_t)(g.n - 1) * g.ldb + g.k) * 4)
+                  : make_rsrc(Bb, ((int64_t)(g.k - 1) * g.ldb + g.n) * 4);
+
+  // loader maps: A and k-contiguous B: row t>>3 (+32q), k 4*(t&7);  j-contiguous B: k t>>5 (+8q), j 4*(t&31)
+  const int lr = t >> 3, lk = (t & 7) * 4;
+  const int jr = t >> 5, jc = (t & 31) * 4;
+  float4 ra[4], rb[4];
+
+  auto load = [&](int kt) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t row = i0 + lr + 32 * q;
+      ra[q] = ld4(rA, (uint32_t)((row * g.lda + kt + lk) * 4));
+    }
+    if (g.b_kcontig) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = j0 + lr + 32 * q;
+        rb[q] = ld4(rB, (uint32_t)((row * g.ldb + kt + lk) * 4));
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t kr = kt + jr + 8 * q;
+        rb[q] = ld4(rB, (uint32_t)((kr * g.ldb + j0 + jc) * 4));
+      }
+    }
+    // element masks only on k-tiles that straddle a triangle's diagonal or the k tail
+    const bool need = (kt + BBK > kend) || (aLo && kt + BBK - 1 > i0) || (bUp && kt + BBK - 1 > j0) ||
+                      (bLo && kt < j0 + BBN - 1);
+    if (need) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = i0 + lr + 32 * q;
+        float* a = (float*)&ra[q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int kk = kt + lk + e;
+          a[e] = keep_if(a[e], kk < kend && (!aLo || kk <= i));
+        }
+        float* b = (float*)&rb[q];
+        if (g.b_kcontig) {
+          const int j = j0 + lr + 32 * q;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int kk = kt + lk + e;
+            b[e] = keep_if(b[e], kk < kend && (!bUp || kk <= j) && (!bLo || kk >= j));
+          }
+        } else {
+          const int kk = kt + jr + 8 * q;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int j = j0 + jc + e;
+            b[e] = keep_if(b[e], kk < kend && (!bUp || kk <= j) && (!bLo || kk >= j));
+          }
+        }
+      }
+    }
+  };
+  auto store_lds = [&](float* st) {
+    float* As = st;
+    float* Bs = st + BBM * BP;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *(float4*)&As[(lr + 32 * q) * BP + lk] = ra[q];
+    if (g.b_kcontig) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) *(float4*)&Bs[(lr + 32 * q) * BP + lk] = rb[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float* b = (const float*)&rb[q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Bs[(jc + e) * BP + jr + 8 * q] = b[e];
+      }
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+
+  if (kt0 < kt1) {
+    load(kt0);
+    store_lds(big_smem);
+    __syncthreads();
+    int st = 0;
+    const int ko = 16 * (lane >> 5), rl = lane & 31;
+    for (int kt = kt0; kt < kt1; kt += BBK) {
+      const bool more = kt + BBK < kt1;
+      if (more) load(kt + BBK);
+      const float* As = big_smem + st * BSTAGE;
+      const float* Bs = As + BBM * BP;
+      float4 fa[2][4], fb[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          fa[h][c] = *(const float4*)&As[(64 * wr + 32 * h + rl) * BP + ko + 4 * c];
+          fb[h][c] = *(const float4*)&Bs[(64 * wc + 32 * h + rl) * BP + ko + 4 * c];
+        }
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const float a0 = ((const float*)&fa[0][s >> 2])[s & 3], a1 = ((const float*)&fa[1][s >> 2])[s & 3];
+        const float b0 = ((const float*)&fb[0][s >> 2])[s & 3], b1 = ((const float*)&fb[1][s >> 2])[s & 3];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+      }
+      if (more) store_lds(big_smem + (st ^ 1) * BSTAGE);
+      lds_barrier();
+      st ^= 1;
+    }
+  }
+
+  // split-K: publish, last arriver combines in chunk order
+  if (S > 1) {
+    __shared__ int s_last;
+    const int64_t slot0 = ((bat * g.tiles + tile) * (int64_t)S) * BSLOT;
+    const __amdgpu_buffer_rsrc_t rws = make_rsrc(g.ws + slot0, (int64_t)S * BSLOT * 4);
+    {
+      const uint32_t off = (uint32_t)(((int64_t)split * BSLOT + t * 64) * 4);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            u32x4g v;
+            v[0] = __float_as_uint(acc[a][b][4 * q + 0]);
+            v[1] = __float_as_uint(acc[a][b][4 * q + 1]);
+            v[2] = __float_as_uint(acc[a][b][4 * q + 2]);
+            v[3] = __float_as_uint(acc[a][b][4 * q + 3]);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rws, off + ((a * 2 + b) * 4 + q) * 16, 0, 16 /* sc1 */);
+          }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int32_t* ctr = g.counters + bat * g.tiles + tile;
+    if (t == 0) {
+      const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (old == S - 1);
+      if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    f32x16 sum[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sum[a][b][r] = 0.0f;
+    for (int c = 0; c < S; ++c) {
+      if (c == split) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) sum[a][b] += acc[a][b];
+        continue;
+      }
+      const uint32_t off = (uint32_t)(((int64_t)c * BSLOT + t * 64) * 4);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const u32x4g v = __builtin_amdgcn_raw_buffer_load_b128(rws, off + ((a * 2 + b) * 4 + q) * 16, 0, 16);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sum[a][b][4 * q + e] += __uint_as_float(v[e]);
+          }
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[a][b] = sum[a][b];
+  }
+
+  // epilogue: C = alpha * acc + beta * C on the stored part
+  float* Cb = g.C + bat * g.sCb;
+  const bool lower = fl & NMGP_OUT_LOWER;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = i0 + 64 * wr + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int j = j0 + 64 * wc + 32 * b + (lane & 31);
+        if (i < g.m && j < g.n && (!lower || j <= i)) {
+          float* c = Cb + (int64_t)i * g.sCi + (int64_t)j * g.sCj;
+          float v = g.alpha * acc[a][b][r];
+          if (g.beta != 0.0f) v += g.beta * *c;
+          *c = v;
+        }
+      }
+}
+
+// Partial slots the split-K path may use per call (workspace = slots * 64 KB + counters).
+constexpr int kBigSlots = 1024;
+size_t gemm_big_ws_bytes() { return (size_t)kBigSlots * BSLOT * sizeof(float) + (size_t)kBigSlots * sizeof(int32_t); }
+
+static int cu_count() {
+  static int cus = -1;
+  if (cus < 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess)
+      cus = 256;
+  }
+  return cus;
+}
+
+// C(i,j) = alpha * sum_k A[i*lda + k] * op(B)(k,j) + beta * C(i,j), batched over `batch` problems.
+// ws: gemm_big_ws_bytes() of device memory whose counter part is zero (the kernel leaves it zero),
+// or nullptr (no split-K).
+int gemm_big_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C, int64_t sCi,
+                 int64_t sCj, int m, int n, int k, int flags, float alpha, float beta, int64_t sAb, int64_t sBb,
+                 int64_t sCb, int batch, void* ws, hipStream_t s) {
+  if (m <= 0 || n <= 0 || batch <= 0) return NMGP_OK;
+  if ((flags & NMGP_OUT_LOWER) && m != n) return -1;
+  BigGemmArgs g;
+  g.A = A; g.B = B; g.C = C;
+  g.lda = lda; g.ldb = ldb; g.sCi = sCi; g.sCj = sCj;
+  g.sAb = sAb; g.sBb = sBb; g.sCb = sCb;
+  g.m = m; g.n = n; g.k = k; g.flags = flags; g.b_kcontig = b_kcontig;
+  g.alpha = alpha; g.beta = beta;
+  g.tiles_m = (m + BBM - 1) / BBM;
+  g.tiles_n = (n + BBN - 1) / BBN;
+  g.tiles = (flags & NMGP_OUT_LOWER) ? g.tiles_m * (g.tiles_m + 1) / 2 : g.tiles_m * g.tiles_n;
+  int S = 1;
+  const int64_t total = (int64_t)g.tiles * batch;
+  const int nkt = (k + BBK - 1) / BBK;
+  if (ws && total < 2 * cu_count() && nkt >= 8) {
+    S = (int)((2 * cu_count() + total - 1) / total);
+    S = min(S, nkt / 4);
+    S = min(S, 16);
+    while (S > 1 && total * S > kBigSlots) --S;
+    if (total > kBigSlots) S = 1;
+  }
+  g.ksplit = S;
+  g.ws = (float*)ws;
+  g.counters = ws ? (int32_t*)((char*)ws + (size_t)kBigSlots * BSLOT * sizeof(float)) : nullptr;
+  static bool attr = false;
+  const size_t lds = 2 * BSTAGE * sizeof(float);
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(gemm_big_kernel, dim3((unsigned)(g.tiles * S), (unsigned)batch), dim3(256), lds, s, g);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
+
+}  // namespace nmgp
+
+extern "C" {
+int64_t nmgp_gemm_big_workspace_size(void) { return (int64_t)nmgp::gemm_big_ws_bytes(); }
+int nmgp_gemm_big_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C, int64_t sCi,
+                      int64_t sCj, int m, int n, int k, int flags, double alpha, double beta, int64_t sAb, int64_t sBb,
+                      int64_t sCb, int batch, void* ws, hipStream_t s) {
+  if (A == nullptr) return -1;
+  if (lda < k) return -2;
+  if (B == nullptr) return -3;
+  if (C == nullptr) return -6;
+  if (m < 0) return -9;
+  if (n < 0) return -10;
+  if (k < 0) return -11;
+  if (batch < 0 || batch > 65535) return -18;
+  return nmgp::gemm_big_f32(A, lda, B, ldb, b_kcontig, C, sCi, sCj, m, n, k, flags, (float)alpha, (float)beta, sAb,
+                            sBb, sCb, batch, ws, s);
+}
+}

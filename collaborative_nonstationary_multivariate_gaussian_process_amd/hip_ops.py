@@ -246,8 +246,23 @@ def trtri(Lm, out=None):
     return out
 
 
-def chol_inv_(A, out=None, info=None):
-    """Fused in-place lower Cholesky of A (batch, n, n) and X = L^{-1}; returns (X, info)."""
+_WS = {}
+
+
+def big_workspace(device, nbytes):
+    """Zero-filled device workspace of the split-K GEMM paths, one per device, grown on demand (the
+    kernels leave its counters zero again, so it is reused by every call in stream order)."""
+    key = torch.device(device).index or 0
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.zeros(int(nbytes), dtype=torch.uint8, device=device)
+        _WS[key] = ws
+    return ws
+
+
+def chol_inv_(A, out=None, info=None, ws=None):
+    """Fused in-place lower Cholesky of A (batch, n, n) and X = L^{-1}; returns (X, info).
+    f32 with n > 256 runs the recursive path with split-K workspace (`ws`, or a cached one)."""
     L.require_device(A, "A")
     assert A.is_contiguous()
     n = A.shape[-1]
@@ -256,10 +271,66 @@ def chol_inv_(A, out=None, info=None):
         out = torch.empty_like(A)
     if info is None:
         info = torch.zeros(max(batch, 1), dtype=torch.int32, device=A.device)
-    fn = getattr(L.lib(), "nmgp_chol_inv_batched_" + _sfx(A.dtype))
+    lib = L.lib()
+    if A.dtype == torch.float32:
+        need = lib.nmgp_chol_inv_workspace_size_f32(n, batch)
+        if need > 0:
+            if ws is None:
+                ws = big_workspace(A.device, need)
+            L.check(lib.nmgp_chol_inv_batched_ws_f32(ctypes.c_void_p(A.data_ptr()), n, n, n * n,
+                                                     ctypes.c_void_p(out.data_ptr()), n, n * n, batch,
+                                                     ctypes.c_void_p(info.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+                                                     ws.numel(), L.stream_handle()), "chol_inv")
+            return out, info
+    fn = getattr(lib, "nmgp_chol_inv_batched_" + _sfx(A.dtype))
     L.check(fn(ctypes.c_void_p(A.data_ptr()), n, n, n * n, ctypes.c_void_p(out.data_ptr()), n, n * n, batch,
                ctypes.c_void_p(info.data_ptr()), L.stream_handle()), "chol_inv")
     return out, info
+
+
+def gemm_big(A, B, C, *, b_kcontig=True, flags=0, alpha=1.0, beta=0.0, ctrans=False, ws=None, split=True):
+    """C = alpha * A op(B) + beta * C on the 128x128 f32 MFMA kernel (gemm_big.hip).
+    A (m, k) row-major; B (n, k) if b_kcontig (op(B) = B^T) else (k, n); C (m, n), or (n, m)
+    holding C^T when ctrans.  Leading batch dimension optional (contiguous)."""
+    for t, nm in ((A, "A"), (B, "B"), (C, "C")):
+        L.require_device(t, nm)
+        assert t.dtype == torch.float32 and t.is_contiguous()
+    batched = A.dim() == 3
+    m, k = A.shape[-2:]
+    n = B.shape[-2] if b_kcontig else B.shape[-1]
+    assert (B.shape[-1] if b_kcontig else B.shape[-2]) == k
+    assert tuple(C.shape[-2:]) == ((n, m) if ctrans else (m, n))
+    batch = A.shape[0] if batched else 1
+    if split and ws is None:
+        ws = big_workspace(A.device, L.lib().nmgp_gemm_big_workspace_size())
+    sCi, sCj = (1, m) if ctrans else (n, 1)
+    L.check(L.lib().nmgp_gemm_big_f32(ctypes.c_void_p(A.data_ptr()), k, ctypes.c_void_p(B.data_ptr()),
+                                      B.shape[-1], 1 if b_kcontig else 0, ctypes.c_void_p(C.data_ptr()), sCi, sCj,
+                                      m, n, k, flags, alpha, beta, m * k if batched else 0,
+                                      B.shape[-2] * B.shape[-1] if batched else 0, m * n if batched else 0, batch,
+                                      ctypes.c_void_p(ws.data_ptr()) if ws is not None else None,
+                                      L.stream_handle()), "gemm_big")
+    return C
+
+
+def syevj(A):
+    """Symmetric eigendecomposition (parallel cyclic / block Jacobi, eig.hip) of (n, n) or (batch, n, n)
+    f64 device matrices: returns (w ascending, V with eigenvectors as columns), like torch.linalg.eigh."""
+    L.require_device(A, "A")
+    assert A.dtype == torch.float64
+    A = A.contiguous()
+    n = A.shape[-1]
+    batch = A.numel() // (n * n) if n else 0
+    w = torch.empty(A.shape[:-1], dtype=A.dtype, device=A.device)
+    V = torch.empty_like(A)
+    lib = L.lib()
+    need = lib.nmgp_syevj_workspace_size_f64(n)
+    ws = big_workspace(A.device, need) if need > 0 else None
+    L.check(lib.nmgp_syevj_batched_f64(ctypes.c_void_p(A.data_ptr()), n, n, n * n, batch,
+                                       ctypes.c_void_p(w.data_ptr()), n, ctypes.c_void_p(V.data_ptr()), n, n * n,
+                                       ctypes.c_void_p(ws.data_ptr()) if ws is not None else None,
+                                       ws.numel() if ws is not None else 0, L.stream_handle()), "syevj")
+    return w, V
 
 
 # ------------------------------------------------------------------------------------ pairwise

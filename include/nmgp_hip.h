@@ -115,6 +115,27 @@ int nmgp_chol_inv_batched_f64(double* A, int64_t n, int64_t lda, int64_t strideA
                               int64_t strideX, int64_t batch, int32_t* info, hipStream_t stream);
 int nmgp_chol_inv_batched_f32(float* A, int64_t n, int64_t lda, int64_t strideA, float* X, int64_t ldx,
                               int64_t strideX, int64_t batch, int32_t* info, hipStream_t stream);
+/* The same with caller workspace for n > 256 (f32): the recursion's products then run split-K where
+ * their 128x128 tile grid would not fill the chip (M=4096 stress case).  ws: at least
+ * nmgp_chol_inv_workspace_size_f32(n, batch) bytes, zero-filled once before first use (the kernels
+ * leave their counters zero again); ws == NULL runs without split-K.                           */
+int64_t nmgp_chol_inv_workspace_size_f32(int64_t n, int64_t batch);
+int nmgp_chol_inv_batched_ws_f32(float* A, int64_t n, int64_t lda, int64_t strideA, float* X, int64_t ldx,
+                                 int64_t strideX, int64_t batch, int32_t* info, void* ws, int64_t ws_bytes,
+                                 hipStream_t stream);
+
+/* ------------------------------------------------------------------ large-tile f32 GEMM / SYRK
+ * C(i,j) = alpha * sum_k A[i*lda + k] * op(B)(k,j) + beta * C[i*sCi + j*sCj], batched with strides
+ * sAb/sBb/sCb; op(B)(k,j) = B[j*ldb + k] (b_kcontig = 1) or B[k*ldb + j] (0).  flags: NMGP_A_LOWER,
+ * NMGP_B_UPPER, NMGP_B_LOWER (structural zeros: k ranges trimmed, diagonal k-tiles masked) and
+ * NMGP_OUT_LOWER (m == n: only the lower triangle is computed and stored -- SYRK).  128x128 tiles on
+ * v_mfma_f32_32x32x2_f32.  The trailing update / panel / inverse products of the recursive
+ * Cholesky (the torch.cholesky of code/utils.py:46,276,347 at M >= 512).  ws as above
+ * (nmgp_gemm_big_workspace_size bytes) or NULL.                                                */
+int64_t nmgp_gemm_big_workspace_size(void);
+int nmgp_gemm_big_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C,
+                      int64_t sCi, int64_t sCj, int m, int n, int k, int flags, double alpha, double beta,
+                      int64_t sAb, int64_t sBb, int64_t sCb, int batch, void* ws, hipStream_t stream);
 
 /* ------------------------------------------------------------------ pairwise kernel builder
  * mode RBF:   K = scale2 * exp(-0.5 * ||x/ls - z/ls||^2)          (code/utils.py:91-94)

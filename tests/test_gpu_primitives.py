@@ -159,7 +159,8 @@ def test_chol_inv_fused(ops, n, batch):
     assert float(torch.triu(X.cpu(), 1).abs().max()) == 0.0
 
 
-@pytest.mark.parametrize("n,batch,dt", [(300, 2, F64), (512, 2, F64), (700, 1, F64), (520, 2, torch.float32)])
+@pytest.mark.parametrize("n,batch,dt", [(300, 2, F64), (512, 2, F64), (700, 1, F64), (520, 2, torch.float32),
+                                        (1000, 1, torch.float32), (2048, 1, torch.float32)])
 def test_chol_inv_blocked(ops, n, batch, dt):
     # n > 256: blocked path (128-wide diagonal blocks + batched GEMM panel / SYRK / inverse products)
     A = _spd(n, batch, n + 1)
@@ -172,6 +173,77 @@ def test_chol_inv_blocked(ops, n, batch, dt):
     assert rel(X, torch.linalg.inv(ref)) < tx
     assert float(torch.triu(Ad.cpu(), 1).abs().max()) == 0.0
     assert float(torch.triu(X.cpu(), 1).abs().max()) == 0.0
+
+
+def _f32_ref(A, opB, flags, alpha=1.0, beta=0.0, C=None):
+    A = A.double()
+    opB = opB.double()
+    if flags & 1:                       # A_LOWER
+        A = torch.tril(A)
+    if flags & 8:                       # B_UPPER: op(B)(k, j) = 0 for j < k
+        opB = torch.triu(opB)
+    if flags & 4:                       # B_LOWER: op(B)(k, j) = 0 for j > k
+        opB = torch.tril(opB)
+    out = alpha * A @ opB
+    if C is not None:
+        out = out + beta * C.double()
+    return out
+
+
+@pytest.mark.parametrize("m,n,k", [(128, 128, 32), (300, 200, 77), (1, 7, 5), (640, 384, 1000), (256, 256, 2048)])
+@pytest.mark.parametrize("b_kcontig", [True, False])
+def test_gemm_big_f32(ops, m, n, k, b_kcontig):
+    # 128x128 f32 MFMA kernel (gemm_big.hip) vs fp64: tolerance of an exact-f32 fma chain over k
+    g = torch.Generator().manual_seed(m + 3 * n + 7 * k)
+    A = torch.randn(m, k, generator=g)
+    B = torch.randn((n, k) if b_kcontig else (k, n), generator=g)
+    C0 = torch.randn(m, n, generator=g)
+    opB = B.t() if b_kcontig else B
+    for alpha, beta in ((1.0, 0.0), (-1.0, 1.0)):
+        C = C0.clone().to(DEV)
+        ops.gemm_big(A.to(DEV), B.to(DEV), C, b_kcontig=b_kcontig, alpha=alpha, beta=beta)
+        assert rel(C, _f32_ref(A, opB, 0, alpha, beta, C0)) < 2e-6
+    # transposed store
+    Ct = torch.zeros(n, m, device=DEV)
+    ops.gemm_big(A.to(DEV), B.to(DEV), Ct, b_kcontig=b_kcontig, ctrans=True)
+    assert rel(Ct.t(), _f32_ref(A, opB, 0)) < 2e-6
+
+
+@pytest.mark.parametrize("flags,b_kcontig", [(1, True), (8, True), (4, False), (16, True)])
+def test_gemm_big_masks_and_syrk(ops, flags, b_kcontig):
+    # triangular operands: garbage outside the triangle must not leak (masked k-tiles); SYRK stores lower only
+    n = 520
+    g = torch.Generator().manual_seed(flags)
+    A = torch.randn(n, n, generator=g)
+    B = A.clone() if flags == 16 else torch.randn(n, n, generator=g)
+    C0 = torch.randn(n, n, generator=g)
+    C = C0.clone().to(DEV)
+    ops.gemm_big(A.to(DEV), B.to(DEV), C, b_kcontig=b_kcontig, flags=flags, alpha=-1.0, beta=1.0)
+    opB = B.t() if b_kcontig else B
+    ref = _f32_ref(A, opB, flags, -1.0, 1.0, C0)
+    if flags == 16:
+        lo = torch.tril(torch.ones(n, n, dtype=torch.bool))
+        assert rel(C.cpu()[lo], ref[lo]) < 2e-6
+        assert torch.equal(C.cpu()[~lo], C0[~lo])          # upper part untouched
+    else:
+        assert rel(C, ref) < 2e-6
+
+
+def test_gemm_big_split_k_deterministic_and_batched(ops):
+    # few tiles, long k: split-K runs (workspace) and must be bit-reproducible and equal to no-split within f32 rounding
+    g = torch.Generator().manual_seed(5)
+    A = torch.randn(3, 256, 4096, generator=g).to(DEV)
+    B = torch.randn(3, 256, 4096, generator=g).to(DEV)
+    outs = []
+    for _ in range(3):
+        C = torch.zeros(3, 256, 256, device=DEV)
+        ops.gemm_big(A, B, C)
+        outs.append(C.clone())
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
+    C1 = torch.zeros(3, 256, 256, device=DEV)
+    ops.gemm_big(A, B, C1, split=False)
+    ref = torch.bmm(A.double().cpu(), B.double().cpu().transpose(1, 2))
+    assert rel(outs[0], ref) < 2e-6 and rel(C1, ref) < 2e-6
 
 
 def test_chol_inv_blocked_not_pd_reports_global_column(ops):
@@ -326,3 +398,56 @@ def test_normal_rng(ops):
     ops.counter_add_(cnt, 1)
     ops.normal_(again, seed=1234, counter=cnt)
     assert not torch.equal(out, again)
+
+
+@pytest.mark.parametrize("n,batch", [(1, 1), (2, 3), (5, 2), (33, 2), (64, 1), (65, 1), (200, 1), (300, 2)])
+def test_syevj(ops, n, batch):
+    # Jacobi eigensolver (eig.hip) vs LAPACK eigh: eigenvalues ascending, V orthonormal, V diag(w) V^T = A
+    g = torch.Generator().manual_seed(n * 31 + batch)
+    G = torch.randn(batch, n, n, generator=g, dtype=F64)
+    A = (G + G.transpose(1, 2)) / 2
+    A[0] += torch.diag(torch.linspace(0, 3, n, dtype=F64))
+    w, V = ops.syevj(A.to(DEV))
+    w, V = w.cpu(), V.cpu()
+    wr = torch.linalg.eigvalsh(A)
+    scale = float(A.norm())
+    assert float((w - wr).abs().max()) <= 1e-13 * scale
+    eye = torch.eye(n, dtype=F64).expand(batch, n, n)
+    assert float((V.transpose(1, 2) @ V - eye).abs().max()) < 1e-12
+    assert float((V @ torch.diag_embed(w) @ V.transpose(1, 2) - A).abs().max()) < 1e-12 * scale
+
+
+def test_syevj_degenerate_and_kernel_matrix(ops):
+    # repeated eigenvalues (identity block) and an ill-conditioned Gibbs kernel matrix of the legacy simulation size
+    A = torch.zeros(100, 100, dtype=F64)
+    A[:50, :50] = torch.eye(50, dtype=F64)
+    A[50:, 50:] = 2 * torch.eye(50, dtype=F64)
+    w, V = ops.syevj(A.to(DEV))
+    assert torch.equal(w.cpu(), torch.cat([torch.ones(50, dtype=F64), 2 * torch.ones(50, dtype=F64)]))
+    x = torch.linspace(0, 1, 200, dtype=F64).view(-1, 1)
+    ell = 0.05 + 0.1 * x.view(-1)
+    K = O.Nonstationary_RBF_cov(x, ell1=ell)
+    w, V = ops.syevj(K.to(DEV))
+    wr = torch.linalg.eigvalsh(K)
+    assert float((w.cpu() - wr).abs().max()) <= 1e-13 * float(K.norm())
+    assert float((V.cpu() @ torch.diag(w.cpu()) @ V.cpu().t() - K).abs().max()) < 1e-12 * float(K.norm())
+
+
+@pytest.mark.parametrize("P,N", [(2, 200), (3, 70)])
+def test_kronecker_gaussian_legacy_sizes(ops, P, N):
+    # kron_inv / kron_logdet / multivariate_normal_logpdf0 and the dense logpdf2 on the HIP path vs the oracle
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.Utility import kronecker_operation as KO
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.Utility import distributions as DI
+    g = torch.Generator().manual_seed(P * N)
+    Lb = torch.randn(P, P, generator=g, dtype=F64)
+    Bm = Lb @ Lb.t() + 0.5 * torch.eye(P, dtype=F64)
+    x = torch.linspace(0, 1, N, dtype=F64).view(-1, 1)
+    K = torch.exp(-(x - x.t()) ** 2 / 0.05) + 1e-6 * torch.eye(N, dtype=F64)
+    y = torch.randn(P * N, generator=g, dtype=F64)
+    mu = torch.zeros(P * N, dtype=F64)
+    s2 = torch.tensor(0.3, dtype=F64)
+    assert float(KO.kron_logdet(s2, Bm, K)) == pytest.approx(float(O.kron_logdet(s2, Bm, K)), rel=1e-11)
+    assert rel(KO.kron_inv(s2, Bm, K), O.kron_inv(s2, Bm, K)) < 1e-10
+    lp = float(DI.multivariate_normal_logpdf0(y, mu, Bm, K, s2))
+    assert lp == pytest.approx(float(O.multivariate_normal_logpdf0(y, mu, Bm, K, s2)), rel=1e-10)
+    assert float(DI.multivariate_normal_logpdf2(y, mu, Bm, K, s2)) == pytest.approx(lp, rel=1e-9)
