@@ -37,6 +37,7 @@ struct BigGemmArgs {
   float alpha, beta;
   int tiles_m, tiles_n, tiles;   // tiles per batch item (lower tiles only with OUT_LOWER)
   int ksplit;
+  int streamk;              // 1: stream-K partition over a persistent grid (batch 1, uniform k)
   float* ws; int32_t* counters;
 };
 
@@ -44,21 +45,9 @@ __device__ inline float4 ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
-__global__ __launch_bounds__(256) void gemm_big_kernel(BigGemmArgs g) {
-  extern __shared__ __attribute__((aligned(16))) float big_smem[];
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wr = w >> 1, wc = w & 1;
-  const int S = g.ksplit;
-
-  // XCD-aware block order: hardware places block b on XCD b % 8; give each XCD a contiguous run
-  int bid = blockIdx.x;
-  const int nb = gridDim.x;
-  if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);
-  const int tile = bid / S, split = bid - tile * S;
-  const int64_t bat = blockIdx.y;
-  int tm, tn;
-  if (g.flags & NMGP_OUT_LOWER) {   // row-major over the lower triangle of the tile grid
+// Lower-triangle tile index -> (tile row, tile column), row-major over the lower triangle.
+__device__ inline void tile_coords(const BigGemmArgs& g, int tile, int& tm, int& tn) {
+  if (g.flags & NMGP_OUT_LOWER) {
     tm = (int)((sqrtf(8.0f * (float)tile + 1.0f) - 1.0f) * 0.5f);
     while ((tm + 1) * (tm + 2) / 2 <= tile) ++tm;
     while (tm * (tm + 1) / 2 > tile) --tm;
@@ -67,21 +56,26 @@ __global__ __launch_bounds__(256) void gemm_big_kernel(BigGemmArgs g) {
     tm = tile / g.tiles_n;
     tn = tile - tm * g.tiles_n;
   }
-  const int i0 = tm * BBM, j0 = tn * BBN;
+}
+
+// Structurally nonzero k range of a tile (triangular operands), in whole k-tiles from kbeg.
+__device__ inline void tile_krange(const BigGemmArgs& g, int i0, int j0, int& kbeg, int& kend) {
+  kbeg = 0;
+  kend = g.k;
+  if (g.flags & NMGP_A_LOWER) kend = min(kend, i0 + BBM);
+  if (g.flags & NMGP_B_UPPER) kend = min(kend, j0 + BBN);
+  if (g.flags & NMGP_B_LOWER) kbeg = max(kbeg, j0);
+  kbeg = (kbeg / BBK) * BBK;
+}
+
+// acc += A[i0:i0+128, kt0:kt1] op(B)[kt0:kt1, j0:j0+128] (kend bounds the masks).
+__device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, float* big_smem, int64_t bat, int i0, int j0,
+                                             int kend, int kt0, int kt1, f32x16 (&acc)[2][2]) {
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 1, wc = w & 1;
   const int fl = g.flags;
   const bool aLo = fl & NMGP_A_LOWER, bUp = fl & NMGP_B_UPPER, bLo = fl & NMGP_B_LOWER;
-
-  // this tile's structurally nonzero k range, in whole k-tiles, then this split's share
-  int kbeg = 0, kend = g.k;
-  if (aLo) kend = min(kend, i0 + BBM);
-  if (bUp) kend = min(kend, j0 + BBN);
-  if (bLo) kbeg = max(kbeg, j0);
-  kbeg = (kbeg / BBK) * BBK;
-  const int nkt = kend > kbeg ? (kend - kbeg + BBK - 1) / BBK : 0;
-  const int chunk = (nkt + S - 1) / S;
-  const int kt0 = kbeg + min(split * chunk, nkt) * BBK;
-  const int kt1 = min(kend, kbeg + min((split + 1) * chunk, nkt) * BBK);
-
   const float* Ab = g.A + bat * g.sAb;
   const float* Bb = g.B + bat * g.sBb;
   const __amdgpu_buffer_rsrc_t rA = make_rsrc(Ab, ((int64_t)(g.m - 1) * g.lda + g.k) * 4);
@@ -113,7 +107,10 @@ __global__ __launch_bounds__(256) void gemm_big_kernel(BigGemmArgs g) {
         rb[q] = ld4(rB, (uint32_t)((kr * g.ldb + j0 + jc) * 4));
       }
     }
-    // element masks only on k-tiles that straddle a triangle's diagonal or the k tail
+  };
+  auto store_lds = [&](float* st, int kt) {
+    // element masks (applied here, after the current k-tile's MFMAs: masking in load() made the
+    // compiler wait for the global loads before them) only on k-tiles that straddle a triangle's diagonal or the k tail
     const bool need = (kt + BBK > kend) || (aLo && kt + BBK - 1 > i0) || (bUp && kt + BBK - 1 > j0) ||
                       (bLo && kt < j0 + BBN - 1);
     if (need) {
@@ -144,8 +141,6 @@ __global__ __launch_bounds__(256) void gemm_big_kernel(BigGemmArgs g) {
         }
       }
     }
-  };
-  auto store_lds = [&](float* st) {
     float* As = st;
     float* Bs = st + BBM * BP;
 #pragma unroll
@@ -163,17 +158,9 @@ __global__ __launch_bounds__(256) void gemm_big_kernel(BigGemmArgs g) {
     }
   };
 
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
-
   if (kt0 < kt1) {
     load(kt0);
-    store_lds(big_smem);
+    store_lds(big_smem, kt0);
     __syncthreads();
     int st = 0;
     const int ko = 16 * (lane >> 5), rl = lane & 31;
@@ -199,81 +186,93 @@ __global__ __launch_bounds__(256) void gemm_big_kernel(BigGemmArgs g) {
         acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
         acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
       }
-      if (more) store_lds(big_smem + (st ^ 1) * BSTAGE);
+      if (more) store_lds(big_smem + (st ^ 1) * BSTAGE, kt + BBK);
       lds_barrier();
       st ^= 1;
     }
   }
+}
 
-  // split-K: publish, last arriver combines in chunk order
-  if (S > 1) {
-    __shared__ int s_last;
-    const int64_t slot0 = ((bat * g.tiles + tile) * (int64_t)S) * BSLOT;
-    const __amdgpu_buffer_rsrc_t rws = make_rsrc(g.ws + slot0, (int64_t)S * BSLOT * 4);
-    {
-      const uint32_t off = (uint32_t)(((int64_t)split * BSLOT + t * 64) * 4);
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            u32x4g v;
-            v[0] = __float_as_uint(acc[a][b][4 * q + 0]);
-            v[1] = __float_as_uint(acc[a][b][4 * q + 1]);
-            v[2] = __float_as_uint(acc[a][b][4 * q + 2]);
-            v[3] = __float_as_uint(acc[a][b][4 * q + 3]);
-            __builtin_amdgcn_raw_buffer_store_b128(v, rws, off + ((a * 2 + b) * 4 + q) * 16, 0, 16 /* sc1 */);
-          }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int32_t* ctr = g.counters + bat * g.tiles + tile;
-    if (t == 0) {
-      const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = (old == S - 1);
-      if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = last;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    f32x16 sum[2][2];
+// Publish this workgroup's partial tile (slot `mine`) write-through, count arrivals on `ctr`;
+// the last of the `S` contributors sums all partials in contributor order (its own from
+// registers) into acc and returns true.  slot_of(c) gives contributor c's slot.
+template <typename SlotOf>
+__device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S, int32_t* ctr, SlotOf slot_of,
+                                            f32x16 (&acc)[2][2]) {
+  __shared__ int s_last;
+  const int t = threadIdx.x;
+  {
+    const __amdgpu_buffer_rsrc_t rws = make_rsrc(g.ws + (int64_t)slot_of(me) * BSLOT, (int64_t)BSLOT * 4);
+    const uint32_t off = (uint32_t)(t * 64 * 4);
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sum[a][b][r] = 0.0f;
-    for (int c = 0; c < S; ++c) {
-      if (c == split) {
+        for (int q = 0; q < 4; ++q) {
+          u32x4g v;
+          v[0] = __float_as_uint(acc[a][b][4 * q + 0]);
+          v[1] = __float_as_uint(acc[a][b][4 * q + 1]);
+          v[2] = __float_as_uint(acc[a][b][4 * q + 2]);
+          v[3] = __float_as_uint(acc[a][b][4 * q + 3]);
+          __builtin_amdgcn_raw_buffer_store_b128(v, rws, off + ((a * 2 + b) * 4 + q) * 16, 0, 16 /* sc1 */);
+        }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (old == S - 1);
+    if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = last;
+  }
+  __syncthreads();
+  const bool last = s_last;
+  __syncthreads();   // s_last is reused by the next tile of a stream-K workgroup
+  if (!last) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  f32x16 sum[2][2];
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < 2; ++a)
 #pragma unroll
-          for (int b = 0; b < 2; ++b) sum[a][b] += acc[a][b];
-        continue;
-      }
-      const uint32_t off = (uint32_t)(((int64_t)c * BSLOT + t * 64) * 4);
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sum[a][b][r] = 0.0f;
+  for (int c = 0; c < S; ++c) {
+    if (c == me) {
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const u32x4g v = __builtin_amdgcn_raw_buffer_load_b128(rws, off + ((a * 2 + b) * 4 + q) * 16, 0, 16);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) sum[a][b][4 * q + e] += __uint_as_float(v[e]);
-          }
+        for (int b = 0; b < 2; ++b) sum[a][b] += acc[a][b];
+      continue;
     }
+    const __amdgpu_buffer_rsrc_t rws = make_rsrc(g.ws + (int64_t)slot_of(c) * BSLOT, (int64_t)BSLOT * 4);
+    const uint32_t off = (uint32_t)(t * 64 * 4);
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) acc[a][b] = sum[a][b];
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const u32x4g v = __builtin_amdgcn_raw_buffer_load_b128(rws, off + ((a * 2 + b) * 4 + q) * 16, 0, 16);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sum[a][b][4 * q + e] += __uint_as_float(v[e]);
+        }
   }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = sum[a][b];
+  return true;
+}
 
-  // epilogue: C = alpha * acc + beta * C on the stored part
+// C = alpha * acc + beta * C on the stored part of the tile.
+__device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, int i0, int j0, f32x16 (&acc)[2][2]) {
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 1, wc = w & 1;
   float* Cb = g.C + bat * g.sCb;
-  const bool lower = fl & NMGP_OUT_LOWER;
+  const bool lower = g.flags & NMGP_OUT_LOWER;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -289,6 +288,88 @@ __global__ __launch_bounds__(256) void gemm_big_kernel(BigGemmArgs g) {
           *c = v;
         }
       }
+}
+
+__device__ inline void zero_acc(f32x16 (&acc)[2][2]) {
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+}
+
+__global__ __launch_bounds__(256, 2) void gemm_big_kernel(BigGemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float big_smem[];
+  // XCD-aware block order: hardware places block b on XCD b % 8; give each XCD a contiguous run
+  int bid = blockIdx.x;
+  const int nb = gridDim.x;
+  if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);
+  const int64_t bat = blockIdx.y;
+  f32x16 acc[2][2];
+
+  // One work segment per pass: a (tile, k-tile range).  Data-parallel / split-K grids run one
+  // pass.  Stream-K (batch 1, every tile the same k range): workgroup w owns iterations
+  // [lo(w), lo(w+1)) of the flattened (tile, k-tile) space, lo(w) = floor(w I / G), so every
+  // workgroup does the same MFMA work whatever the tile count; a tile cut by a range boundary is
+  // finished by the last of its contributors, summing partials in k order (deterministic).
+  const bool sk = g.streamk;
+  const int S = g.ksplit;
+  const int nkt_u = (g.k + BBK - 1) / BBK;
+  const int64_t I = (int64_t)g.tiles * nkt_u, G = nb;
+  auto lo = [&](int64_t w) { return (w * I) / G; };
+  auto wg_of = [&](int64_t i) { return (int)(((i + 1) * G - 1) / I); };
+  int64_t it = sk ? lo(bid) : 0;
+  const int64_t end = sk ? lo(bid + 1) : 1;
+  while (it < end) {
+    int tile, kt0, kt1, kend, nparts = 1, me = 0, c0 = 0;
+    int64_t step;
+    if (sk) {
+      tile = (int)(it / nkt_u);
+      const int ka = (int)(it - (int64_t)tile * nkt_u);
+      const int kb = (int)min((int64_t)nkt_u, (int64_t)ka + (end - it));
+      kend = g.k;
+      kt0 = ka * BBK;
+      kt1 = min(g.k, kb * BBK);
+      step = kb - ka;
+      if (ka > 0 || kb < nkt_u) {
+        c0 = wg_of((int64_t)tile * nkt_u);
+        nparts = wg_of((int64_t)tile * nkt_u + nkt_u - 1) - c0 + 1;
+        me = bid - c0;
+      }
+    } else {
+      tile = bid / S;
+      const int split = bid - tile * S;
+      int tm0, tn0, kbeg;
+      tile_coords(g, tile, tm0, tn0);
+      tile_krange(g, tm0 * BBM, tn0 * BBN, kbeg, kend);
+      const int nkt = kend > kbeg ? (kend - kbeg + BBK - 1) / BBK : 0;
+      const int chunk = (nkt + S - 1) / S;
+      kt0 = kbeg + min(split * chunk, nkt) * BBK;
+      kt1 = min(kend, kbeg + min((split + 1) * chunk, nkt) * BBK);
+      nparts = S;
+      me = split;
+      step = 1;
+    }
+    int tm, tn;
+    tile_coords(g, tile, tm, tn);
+    const int i0 = tm * BBM, j0 = tn * BBN;
+    zero_acc(acc);
+    big_mainloop(g, big_smem, bat, i0, j0, kend, kt0, kt1, acc);
+    bool store = true;
+    if (nparts > 1) {
+      const int64_t slot0 = (bat * g.tiles + tile) * (int64_t)S;
+      auto slot_of = [&](int c) -> int64_t {
+        if (!sk) return slot0 + c;
+        const int wgc = c0 + c;
+        return 2 * wgc + ((lo(wgc) / nkt_u) == tile ? 0 : 1);
+      };
+      int32_t* ctr = sk ? g.counters + c0 : g.counters + bat * g.tiles + tile;
+      store = big_combine(g, me, nparts, ctr, slot_of, acc);
+    }
+    if (store) big_epilogue(g, bat, i0, j0, acc);
+    it += step;
+  }
 }
 
 // Partial slots the split-K path may use per call (workspace = slots * 64 KB + counters).
@@ -323,10 +404,16 @@ int gemm_big_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int b
   g.tiles_m = (m + BBM - 1) / BBM;
   g.tiles_n = (n + BBN - 1) / BBN;
   g.tiles = (flags & NMGP_OUT_LOWER) ? g.tiles_m * (g.tiles_m + 1) / 2 : g.tiles_m * g.tiles_n;
-  int S = 1;
+  int S = 1, sk = 0;
   const int64_t total = (int64_t)g.tiles * batch;
   const int nkt = (k + BBK - 1) / BBK;
-  if (ws && total < 2 * cu_count() && nkt >= 8) {
+  const int P = 2 * cu_count();   // co-resident workgroups (the two LDS stages admit 2 per CU)
+  const bool uniform_k = !(flags & (NMGP_A_LOWER | NMGP_B_UPPER | NMGP_B_LOWER));
+  const int64_t dp_slots = ((total + P - 1) / P) * P;
+  if (ws && batch == 1 && uniform_k && P <= kBigSlots / 2 && (double)total / (double)dp_slots < 0.9 &&
+      total * nkt >= 8LL * P) {
+    sk = 1;   // stream-K: 2 partial slots per workgroup, one arrival counter per workgroup
+  } else if (ws && total < 2 * cu_count() && nkt >= 8) {
     S = (int)((2 * cu_count() + total - 1) / total);
     S = min(S, nkt / 4);
     S = min(S, 16);
@@ -334,6 +421,7 @@ int gemm_big_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int b
     if (total > kBigSlots) S = 1;
   }
   g.ksplit = S;
+  g.streamk = sk;
   g.ws = (float*)ws;
   g.counters = ws ? (int32_t*)((char*)ws + (size_t)kBigSlots * BSLOT * sizeof(float)) : nullptr;
   static bool attr = false;
@@ -342,7 +430,8 @@ int gemm_big_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int b
     (void)hipFuncSetAttribute((const void*)gemm_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL(gemm_big_kernel, dim3((unsigned)(g.tiles * S), (unsigned)batch), dim3(256), lds, s, g);
+  const unsigned grid = sk ? (unsigned)P : (unsigned)(g.tiles * S);
+  hipLaunchKernelGGL(gemm_big_kernel, dim3(grid, (unsigned)batch), dim3(256), lds, s, g);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }

@@ -246,6 +246,33 @@ def test_gemm_big_split_k_deterministic_and_batched(ops):
     assert rel(outs[0], ref) < 2e-6 and rel(C1, ref) < 2e-6
 
 
+@pytest.mark.parametrize("kind,n,k", [("syrk", 2048, 1024), ("gemm", 640, 8192), ("syrk", 1000, 4000)])
+def test_gemm_big_stream_k(ops, kind, n, k):
+    # batch-1 problems whose tile grid would leave most of the chip idle run stream-K (equal k-tile
+    # ranges per workgroup, cut tiles combined in k order): bit-reproducible, fp64-accurate, and
+    # the SYRK leaves the strict upper triangle untouched
+    g = torch.Generator().manual_seed(n + k)
+    A = (torch.rand(n, k, generator=g) * 2 - 1).to(DEV)
+    B = A if kind == "syrk" else (torch.rand(n, k, generator=g) * 2 - 1).to(DEV)
+    C0 = torch.randn(n, n, generator=g).to(DEV)
+    flags = 16 if kind == "syrk" else 0
+    outs = []
+    for _ in range(3):
+        C = C0.clone()
+        ops.gemm_big(A, B, C, flags=flags, alpha=-1.0, beta=1.0)
+        outs.append(C)
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
+    ref = C0.double() - A.double() @ B.double().t()
+    C1 = C0.clone()
+    ops.gemm_big(A, B, C1, flags=flags, alpha=-1.0, beta=1.0, split=False)
+    if kind == "syrk":
+        lo = torch.tril(torch.ones(n, n, dtype=torch.bool, device=DEV))
+        assert rel(outs[0][lo], ref[lo]) < 2e-6 and rel(C1[lo], ref[lo]) < 2e-6
+        assert torch.equal(outs[0][~lo], C0[~lo])
+    else:
+        assert rel(outs[0], ref) < 2e-6 and rel(C1, ref) < 2e-6
+
+
 def test_chol_inv_blocked_not_pd_reports_global_column(ops):
     A = _spd(400, 2, 9)
     bad = A.clone()
