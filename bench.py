@@ -52,6 +52,79 @@ def epoch_batches(xs, ys, rng):
     return out
 
 
+def stress_cholesky(dev, reps=5):
+    """BASELINE.json configs[4] beside the headline: one SPD M=4096 fp32 matrix (A = G G^T / M + I,
+    G ~ N(0,1), seed 0) factored by the blocked right-looking potrf (nmgp_potrf_blocked_f32), and its
+    dominant kernel -- the trailing-update SYRK on the 128x128 f32 MFMA kernel -- timed alone at
+    n = k = 4096.  GFLOP/s counts M^3/3 for the factorization and n(n+1)k for the SYRK (lower half).
+    The CPU figure is torch.linalg.cholesky (LAPACK spotrf: what the reference calls through
+    torch.cholesky, code/utils.py:40) on this host's cores."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import hip_ops as H
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L
+    Mst = 4096
+    g = torch.Generator(device=dev).manual_seed(0)
+    G = torch.randn(Mst, Mst, generator=g, dtype=torch.float64, device=dev)
+    A0 = (G @ G.t() / Mst + torch.eye(Mst, dtype=torch.float64, device=dev)).float().contiguous()
+    W = A0.clone()
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        W.copy_(A0)
+        H.potrf_blocked_(W, info=info)
+    torch.cuda.current_stream().wait_stream(s)
+
+    def graph_ms(body):
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            for _ in range(reps):
+                body()
+        gr.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        gr.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    def fac():
+        W.copy_(A0)
+        H.potrf_blocked_(W, info=info)
+
+    t_fac = graph_ms(fac)
+    assert int(info.item()) == 0, "stress potrf reported a non-positive pivot"
+    idx = torch.arange(0, Mst, 16, device=dev)
+    Ld = W.double()
+    resid = float((Ld[idx] @ Ld.t() - A0.double()[idx]).norm() / A0.double()[idx].norm())
+    del Ld
+    t_fac -= graph_ms(lambda: W.copy_(A0))     # the per-rep restore copy is not factorization time
+    # the trailing-update SYRK alone at n = k = 4096 (stream-K over the lower tiles)
+    X = (torch.rand(Mst, Mst, generator=g, device=dev) * 2 - 1)
+    C = torch.zeros(Mst, Mst, device=dev)
+    ws = H.big_workspace(dev, L.lib().nmgp_gemm_big_workspace_size())
+    t_syrk = graph_ms(lambda: H.gemm_big(X, X, C, flags=L.OUT_LOWER, alpha=-1.0, beta=1.0, ws=ws))
+    syrk_tf = Mst * (Mst + 1.0) * Mst / (t_syrk * 1e-3) / 1e12
+    del G, X, C
+    # CPU: LAPACK spotrf through torch on the host cores, one call (about 0.1-1 s)
+    Ac = A0.cpu()
+    torch.linalg.cholesky(Ac[:512, :512])
+    t0 = time.time()
+    torch.linalg.cholesky(Ac)
+    t_cpu = time.time() - t0
+    f = Mst ** 3 / 3.0
+    return {"workload": "stress: one SPD M=4096 fp32 matrix (BASELINE.json configs[4])",
+            "kernel": "nmgp_potrf_blocked_f32 (128-wide fused leaves, panel GEMM, lookahead, side-stream SYRK)",
+            "potrf_ms": round(t_fac, 4), "gflops": round(f / (t_fac * 1e-3) / 1e9, 1),
+            "residual": resid,
+            "syrk": {"kernel": "gemm_big_kernel (128x128 f32 MFMA, stream-K)", "n": Mst, "k": Mst,
+                     "ms": round(t_syrk, 4), "achieved_tflops": round(syrk_tf, 2), "peak_tflops": 157.3,
+                     "frac": round(syrk_tf / 157.3, 4)},
+            "cpu": {"potrf_ms": round(1e3 * t_cpu, 2), "gflops": round(f / t_cpu / 1e9, 1),
+                    "cores": torch.get_num_threads(), "kind": "torch.linalg.cholesky (LAPACK spotrf)"},
+            "speedup_vs_cpu": round(t_cpu * 1e3 / t_fac, 1)}
+
+
 class PhaseTimer:
     """HIP events around every launch of an eager step (same stream as the kernels)."""
 
@@ -126,6 +199,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-breakdown", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP graph (launch every kernel from Python)")
+    ap.add_argument("--no-stress", action="store_true", help="skip the M=4096 stress Cholesky line (configs[4])")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -251,6 +325,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds, xs, ys, z)
 
+    stress = None
+    if rank == 0 and world == 1 and not args.no_stress:
+        stress = stress_cholesky(dev)
+
     if rank == 0:
         rec = {"metric": "DSVI ELBO iterations/sec (PM2.5-shaped, fp64, 1 iteration = fwd+bwd+Adam on B=2000)",
                "value": round(value, 3), "unit": "it/s", "n_gpus": world, "steps": args.steps,
@@ -260,7 +338,8 @@ def main():
                           "D_outputs": D, "M_inducing": M, "minibatch_rows": B, "N_observations": D * N_LOC,
                           "global_batch": B * world, "parallelism": f"dp{world}" if world > 1 else "single",
                           "hip_graph": graph is not None},
-               "roofline": roofline, "cpu_baseline": cpu, "cholesky": chol, "phase_ms": breakdown,
+               "roofline": roofline, "cpu_baseline": cpu, "cholesky": chol, "cholesky_stress": stress,
+               "phase_ms": breakdown,
                "final_loss": loss_val}
         if cpu is not None:
             rec["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)

@@ -89,6 +89,10 @@ _SIGS = {
     "nmgp_chol_inv_batched_f64": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "nmgp_chol_inv_batched_f32": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "nmgp_chol_inv_workspace_size_f32": (c_i64, [c_i64, c_i64]),
+    "nmgp_potrf_blocked_workspace_size_f32": (c_i64, [c_i64]),
+    "nmgp_potrf_blocked_workspace_size_f64": (c_i64, [c_i64]),
+    "nmgp_potrf_blocked_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "nmgp_potrf_blocked_f64": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "nmgp_chol_inv_batched_ws_f32": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64,
                                              c_vp]),
     "nmgp_syevj_workspace_size_f64": (c_i64, [c_i64]),

@@ -16,6 +16,7 @@
 #include "common.hpp"
 
 #include <cstdlib>
+#include <mutex>
 #include <type_traits>
 
 namespace nmgp {
@@ -922,11 +923,11 @@ static bool use_two_role(int n, int64_t batch) { return n >= 32 && n <= 256 && b
 
 template <typename T>
 static int chol_inv_small(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx, int64_t sX, int64_t batch,
-                          int32_t* info, hipStream_t s, int col_off, int info_first) {
+                          int32_t* info, hipStream_t s, int col_off, int info_first, bool two_role = true) {
   const int nt = (n + 15) >> 4, ntiles = nt * (nt + 1) / 2;
   const size_t sm = chol_inv_smem<T>(n);
   if constexpr (std::is_same<T, double>::value) {
-    if (use_two_role(n, batch) && !getenv("NMGP_CHOL_FUSED1")) {
+    if (two_role && use_two_role(n, batch) && !getenv("NMGP_CHOL_FUSED1")) {
       if (ntiles <= RW * 3)
         chol_inv2_go<3>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
       else if (ntiles <= RW * 5)
@@ -1090,6 +1091,143 @@ static int chol_inv_launch(T* A, int64_t n, int64_t lda, int64_t sA, T* X, int64
   return chol_inv_small<T>(A, (int)n, lda, sA, X, ldx, sX, batch, info, s, 0, 1);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Large single-matrix Cholesky (the M=4096 stress configuration; LAPACK potrf semantics, upper
+// triangle zeroed): right-looking, 128-wide block columns, one step of lookahead on two streams.
+// Step j (rows/columns below block j: n2):
+//   main:  [L_jj, X_jj] = fused leaf(A_jj)                      (register-resident, one workgroup)
+//          L_j = A_j X_jj^T                                      (panel GEMM, A_j staged in P)
+//          A(:, j+1) -= L_j L_j(0:128)^T                         (lookahead: next block column)
+//   side:  A(j+2:, j+2:) -= L_j(128:) L_j(128:)^T                (trailing SYRK, lower tiles only)
+// The trailing SYRK of step j runs while the main stream factors block j+1 (leaf + panel); the
+// lookahead update of step j+1 (which writes block column j+2) waits for it.  Everything else is
+// stream-ordered.  f32 products run on the 128x128 MFMA kernel (stream-K where the tile grid
+// would not fill the chip; one split-K workspace per stream), f64 on the 64x64 f64 MFMA kernel.
+constexpr int PNB = 128;
+
+struct PotrfSide {
+  hipStream_t side = nullptr;
+  hipEvent_t ev_main = nullptr, ev_side = nullptr;
+};
+
+static int potrf_side_ctx(PotrfSide*& out) {
+  static PotrfSide ctx[64];
+  static std::mutex mu;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return NMGP_ERR_LAUNCH;
+  std::lock_guard<std::mutex> lk(mu);
+  PotrfSide& c = ctx[dev];
+  if (c.side == nullptr) {
+    if (hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking) != hipSuccess) return NMGP_ERR_LAUNCH;
+    if (hipEventCreateWithFlags(&c.ev_main, hipEventDisableTiming) != hipSuccess) return NMGP_ERR_LAUNCH;
+    if (hipEventCreateWithFlags(&c.ev_side, hipEventDisableTiming) != hipSuccess) return NMGP_ERR_LAUNCH;
+  }
+  out = &c;
+  return NMGP_OK;
+}
+
+static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+template <typename T>
+static size_t potrf_blocked_ws(int64_t n) {
+  const int64_t nblk = (n + PNB - 1) / PNB;
+  size_t b = al256((size_t)nblk * PNB * PNB * sizeof(T)) + al256((size_t)n * PNB * sizeof(T));
+  if (std::is_same<T, float>::value) b += 2 * al256(gemm_big_ws_bytes());
+  return b;
+}
+
+// C(m x nn) = alpha * A(m x k, row stride lda) op(B) + beta * C, op(B)(k, c) = B[c * ldb + k]
+template <typename T>
+static int pgemm(const T* A, int64_t lda, const T* B, int64_t ldb, T* C, int64_t ldc, int m, int nn, int k, int flags,
+                 double alpha, double beta, void* bigws, hipStream_t s) {
+  if constexpr (std::is_same<T, float>::value) {
+    return gemm_big_f32(A, lda, B, ldb, 1, C, ldc, 1, m, nn, k, flags, (float)alpha, (float)beta, 0, 0, 0, 1, bigws,
+                        s);
+  } else {
+    nmgp_gemm_desc d = gdesc(A, lda, 1, B, 1, ldb, C, ldc, 1, m, nn, k, flags, alpha, beta, 0, 0, 0, 1);
+    return gemm_single<T>(d, s);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void zero_upper_kernel(T* A, int n, int64_t lda) {
+  const int i = blockIdx.x;
+  for (int j = i + 1 + (int)threadIdx.x; j < n; j += 256) A[(int64_t)i * lda + j] = (T)0;
+}
+
+template <typename T>
+static int potrf_blocked(T* A, int n, int64_t lda, int32_t* info, void* ws, hipStream_t s) {
+  PotrfSide* ctx = nullptr;
+  int rc = potrf_side_ctx(ctx);
+  if (rc != NMGP_OK) return rc;
+  const int nblk = (n + PNB - 1) / PNB;
+  char* w = (char*)ws;
+  T* Xd = (T*)w;
+  w += al256((size_t)nblk * PNB * PNB * sizeof(T));
+  T* P = (T*)w;
+  w += al256((size_t)n * PNB * sizeof(T));
+  void* ws_main = nullptr;
+  void* ws_side = nullptr;
+  if (std::is_same<T, float>::value) {
+    ws_main = w;
+    ws_side = w + al256(gemm_big_ws_bytes());
+  }
+  bool side_used = false;
+  for (int jb = 0; jb < nblk; ++jb) {
+    const int j0 = jb * PNB, nbj = min(PNB, n - j0), r0 = j0 + nbj, n2 = n - r0;
+    T* Ajj = A + (int64_t)j0 * lda + j0;
+    T* Xj = Xd + (int64_t)jb * PNB * PNB;
+    if ((rc = chol_inv_small<T>(Ajj, nbj, lda, 0, Xj, PNB, 0, 1, info, s, j0, jb == 0, false)) != NMGP_OK) return rc;
+    if (n2 == 0) break;
+    T* Lj = A + (int64_t)r0 * lda + j0;   // block column j below the diagonal block
+    // f32: one 128-wide tile column, no split-K (B is triangular), so each workgroup reads its rows
+    // of A_j in full before it overwrites them -- the panel runs in place.  The f64 kernel's 64-wide
+    // tiles would let one workgroup overwrite rows another is still reading: staged through P.
+    const T* Aj = Lj;
+    int64_t ldaj = lda;
+    if (!std::is_same<T, float>::value) {
+      if ((rc = block_copy<T>(Lj, lda, 0, P, PNB, 0, n2, nbj, 1, s)) != NMGP_OK) return rc;
+      Aj = P;
+      ldaj = PNB;
+    }
+    if ((rc = pgemm<T>(Aj, ldaj, Xj, PNB, Lj, lda, n2, nbj, nbj, NMGP_B_UPPER, 1.0, 0.0, ws_main, s)) != NMGP_OK)
+      return rc;
+    const int c1 = min(PNB, n2), n3 = n2 - c1;
+    // the trailing SYRK of step j-1 wrote block column j+1: the lookahead update must follow it
+    if (side_used && hipStreamWaitEvent(s, ctx->ev_side, 0) != hipSuccess) return NMGP_ERR_LAUNCH;
+    if ((rc = pgemm<T>(Lj, lda, Lj, lda, A + (int64_t)r0 * lda + r0, lda, n2, c1, nbj, 0, -1.0, 1.0, ws_main, s)) !=
+        NMGP_OK)
+      return rc;
+    if (n3 > 0) {
+      if (hipEventRecord(ctx->ev_main, s) != hipSuccess) return NMGP_ERR_LAUNCH;
+      if (hipStreamWaitEvent(ctx->side, ctx->ev_main, 0) != hipSuccess) return NMGP_ERR_LAUNCH;
+      const T* Lb = Lj + (int64_t)c1 * lda;
+      T* C = A + (int64_t)(r0 + c1) * lda + (r0 + c1);
+      if ((rc = pgemm<T>(Lb, lda, Lb, lda, C, lda, n3, n3, nbj, NMGP_OUT_LOWER, -1.0, 1.0, ws_side, ctx->side)) !=
+          NMGP_OK)
+        return rc;
+      if (hipEventRecord(ctx->ev_side, ctx->side) != hipSuccess) return NMGP_ERR_LAUNCH;
+      side_used = true;
+    }
+  }
+  if (side_used && hipStreamWaitEvent(s, ctx->ev_side, 0) != hipSuccess) return NMGP_ERR_LAUNCH;
+  hipLaunchKernelGGL(zero_upper_kernel<T>, dim3((unsigned)n), dim3(256), 0, s, A, n, lda);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
+
+template <typename T>
+static int potrf_blocked_launch(T* A, int64_t n, int64_t lda, int32_t* info, void* ws, int64_t ws_bytes,
+                                hipStream_t s) {
+  if (A == nullptr) return -1;
+  if (n < 0 || n > (1 << 20)) return -2;
+  if (lda < n) return -3;
+  if (info == nullptr) return -4;
+  if (n == 0) return NMGP_OK;
+  if (ws == nullptr || ws_bytes < (int64_t)potrf_blocked_ws<T>(n)) return -5;
+  return potrf_blocked<T>(A, (int)n, lda, info, ws, s);
+}
+
 }  // namespace nmgp
 
 extern "C" {
@@ -1122,5 +1260,13 @@ int nmgp_chol_inv_batched_ws_f32(float* A, int64_t n, int64_t lda, int64_t sA, f
                                  int64_t b, int32_t* info, void* ws, int64_t ws_bytes, hipStream_t s) {
   if (ws != nullptr && ws_bytes < nmgp_chol_inv_workspace_size_f32(n, b)) return -11;
   return nmgp::chol_inv_launch<float>(A, n, lda, sA, X, ldx, sX, b, info, s, ws);
+}
+int64_t nmgp_potrf_blocked_workspace_size_f32(int64_t n) { return n > 0 ? (int64_t)nmgp::potrf_blocked_ws<float>(n) : 0; }
+int64_t nmgp_potrf_blocked_workspace_size_f64(int64_t n) { return n > 0 ? (int64_t)nmgp::potrf_blocked_ws<double>(n) : 0; }
+int nmgp_potrf_blocked_f32(float* A, int64_t n, int64_t lda, int32_t* info, void* ws, int64_t ws_bytes, hipStream_t s) {
+  return nmgp::potrf_blocked_launch<float>(A, n, lda, info, ws, ws_bytes, s);
+}
+int nmgp_potrf_blocked_f64(double* A, int64_t n, int64_t lda, int32_t* info, void* ws, int64_t ws_bytes, hipStream_t s) {
+  return nmgp::potrf_blocked_launch<double>(A, n, lda, info, ws, ws_bytes, s);
 }
 }

@@ -266,13 +266,40 @@ __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S,
   return true;
 }
 
-// C = alpha * acc + beta * C on the stored part of the tile.
+// C = alpha * acc + beta * C on the stored part of the tile.  With beta != 0 all 64 C values of a
+// lane are loaded before the first store (one round trip instead of 64 serialized load->store
+// pairs: the compiler cannot move a C load above a C store it may alias).
 __device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, int i0, int j0, f32x16 (&acc)[2][2]) {
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = w >> 1, wc = w & 1;
   float* Cb = g.C + bat * g.sCb;
   const bool lower = g.flags & NMGP_OUT_LOWER;
+  if (g.beta != 0.0f) {
+    f32x16 cv[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int i = i0 + 64 * wr + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int j = j0 + 64 * wc + 32 * b + (lane & 31);
+          const bool ok = i < g.m && j < g.n && (!lower || j <= i);
+          cv[a][b][r] = ok ? __builtin_nontemporal_load(Cb + (int64_t)i * g.sCi + (int64_t)j * g.sCj) : 0.0f;
+        }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[a][b][r] = g.alpha * acc[a][b][r] + g.beta * cv[a][b][r];
+  } else {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[a][b] *= g.alpha;
+  }
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -281,12 +308,7 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, 
       for (int r = 0; r < 16; ++r) {
         const int i = i0 + 64 * wr + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         const int j = j0 + 64 * wc + 32 * b + (lane & 31);
-        if (i < g.m && j < g.n && (!lower || j <= i)) {
-          float* c = Cb + (int64_t)i * g.sCi + (int64_t)j * g.sCj;
-          float v = g.alpha * acc[a][b][r];
-          if (g.beta != 0.0f) v += g.beta * *c;
-          *c = v;
-        }
+        if (i < g.m && j < g.n && (!lower || j <= i)) Cb[(int64_t)i * g.sCi + (int64_t)j * g.sCj] = acc[a][b][r];
       }
 }
 

@@ -249,10 +249,12 @@ def trtri(Lm, out=None):
 _WS = {}
 
 
-def big_workspace(device, nbytes):
-    """Zero-filled device workspace of the split-K GEMM paths, one per device, grown on demand (the
-    kernels leave its counters zero again, so it is reused by every call in stream order)."""
-    key = torch.device(device).index or 0
+def big_workspace(device, nbytes, tag="gemm"):
+    """Zero-filled device workspace of the split-K GEMM paths, one per (device, layout tag), grown on
+    demand (the kernels leave its counters zero again, so it is reused by every call in stream
+    order).  Layouts differ per tag (the blocked potrf puts its own counters elsewhere), so callers
+    with different layouts never share one."""
+    key = (torch.device(device).index or 0, tag)
     ws = _WS.get(key)
     if ws is None or ws.numel() < nbytes:
         ws = torch.zeros(int(nbytes), dtype=torch.uint8, device=device)
@@ -286,6 +288,26 @@ def chol_inv_(A, out=None, info=None, ws=None):
     L.check(fn(ctypes.c_void_p(A.data_ptr()), n, n, n * n, ctypes.c_void_p(out.data_ptr()), n, n * n, batch,
                ctypes.c_void_p(info.data_ptr()), L.stream_handle()), "chol_inv")
     return out, info
+
+
+def potrf_blocked_(A, info=None, ws=None):
+    """In-place lower Cholesky of ONE large SPD matrix A (n, n) on the blocked right-looking path with
+    lookahead (include/nmgp_hip.h nmgp_potrf_blocked_*); strictly upper part zeroed.  Returns info
+    (int32 (1,), first non-positive pivot column, 1-based, as LAPACK potrf)."""
+    L.require_device(A, "A")
+    assert A.dim() == 2 and A.shape[0] == A.shape[1] and A.is_contiguous()
+    n = A.shape[0]
+    if info is None:
+        info = torch.zeros(1, dtype=torch.int32, device=A.device)
+    lib = L.lib()
+    sfx = _sfx(A.dtype)
+    need = getattr(lib, "nmgp_potrf_blocked_workspace_size_" + sfx)(n)
+    if ws is None:
+        ws = big_workspace(A.device, need, tag="potrf")
+    L.check(getattr(lib, "nmgp_potrf_blocked_" + sfx)(ctypes.c_void_p(A.data_ptr()), n, n,
+                                                      ctypes.c_void_p(info.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+                                                      ws.numel(), L.stream_handle()), "potrf_blocked")
+    return info
 
 
 def gemm_big(A, B, C, *, b_kcontig=True, flags=0, alpha=1.0, beta=0.0, ctrans=False, ws=None, split=True):

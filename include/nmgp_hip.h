@@ -124,6 +124,21 @@ int nmgp_chol_inv_batched_ws_f32(float* A, int64_t n, int64_t lda, int64_t strid
                                  int64_t strideX, int64_t batch, int32_t* info, void* ws, int64_t ws_bytes,
                                  hipStream_t stream);
 
+/* Single large SPD matrix (the M=4096 stress configuration, BASELINE.json configs[4]): blocked
+ * right-looking Cholesky, A <- L in place (strictly upper part zeroed), info as potrf (first
+ * non-positive pivot column, 1-based).  Replaces torch.cholesky / LAPACK potrf on one K_uu + jitter
+ * (code/utils.py:32-40, 343-344; SIM_code/Utility/kernels.py:64 for the legacy kernels).
+ * 128-wide fused leaves, panel GEMM against the leaf's inverse, one block column of lookahead, and the
+ * trailing SYRK on a library-owned side stream joined back to `stream` through events (capturable
+ * into a graph).  ws: nmgp_potrf_blocked_workspace_size_*(n) bytes, zero-filled once before first use
+ * (the split-K counters are left zero again).                                                   */
+int64_t nmgp_potrf_blocked_workspace_size_f32(int64_t n);
+int64_t nmgp_potrf_blocked_workspace_size_f64(int64_t n);
+int nmgp_potrf_blocked_f32(float* A, int64_t n, int64_t lda, int32_t* info, void* ws, int64_t ws_bytes,
+                           hipStream_t stream);
+int nmgp_potrf_blocked_f64(double* A, int64_t n, int64_t lda, int32_t* info, void* ws, int64_t ws_bytes,
+                           hipStream_t stream);
+
 /* ------------------------------------------------------------------ large-tile f32 GEMM / SYRK
  * C(i,j) = alpha * sum_k A[i*lda + k] * op(B)(k,j) + beta * C[i*sCi + j*sCj], batched with strides
  * sAb/sBb/sCb; op(B)(k,j) = B[j*ldb + k] (b_kcontig = 1) or B[k*ldb + j] (0).  flags: NMGP_A_LOWER,

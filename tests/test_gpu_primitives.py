@@ -273,6 +273,48 @@ def test_gemm_big_stream_k(ops, kind, n, k):
         assert rel(outs[0], ref) < 2e-6 and rel(C1, ref) < 2e-6
 
 
+@pytest.mark.parametrize("n", [130, 300, 1000, 2048])
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+def test_potrf_blocked(ops, n, dt):
+    # large single-matrix blocked Cholesky with lookahead (stress path): fp64-accurate residual,
+    # strictly upper part zero, graph replay bit-identical to the eager call
+    A = _spd(n, 1, n + 1)[0]
+    Ad = A.to(dt).to(DEV).contiguous()
+    W = Ad.clone()
+    info = ops.potrf_blocked_(W)
+    torch.cuda.synchronize()
+    assert int(info.item()) == 0
+    Ld = W.double().cpu()
+    assert torch.equal(torch.triu(Ld, 1), torch.zeros_like(Ld))
+    tol = 1e-12 if dt == torch.float64 else 2e-6
+    assert float((Ld @ Ld.t() - A).norm() / A.norm()) < tol
+    assert rel(Ld, torch.linalg.cholesky(A)) < (1e-10 if dt == torch.float64 else 1e-4)
+    G = Ad.clone()
+    inf2 = torch.zeros(1, dtype=torch.int32, device=DEV)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.potrf_blocked_(G, info=inf2)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        G.copy_(Ad)
+        ops.potrf_blocked_(G, info=inf2)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(G, W)
+
+
+def test_potrf_blocked_not_pd(ops):
+    # first failing pivot reported as a global 1-based column, inside a later block
+    A = _spd(400, 1, 3)[0]
+    A[333, 333] = -50.0
+    W = A.to(DEV).contiguous()
+    info = ops.potrf_blocked_(W)
+    ref = torch.linalg.cholesky_ex(A).info
+    assert int(info.item()) == int(ref.item()) == 334
+
+
 def test_chol_inv_blocked_not_pd_reports_global_column(ops):
     A = _spd(400, 2, 9)
     bad = A.clone()
