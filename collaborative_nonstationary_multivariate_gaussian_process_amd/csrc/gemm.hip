@@ -36,6 +36,7 @@ struct GemmArgs {
   int nprob;
   int coop;  // whole grid co-resident: split-K chunks combine cooperatively
   const int32_t* seg;
+  const int32_t* dyn_start;   // device tile plan (nprob + 1) or nullptr: static tile_start
   nmgp_gemm_desc inl;
 };
 
@@ -362,20 +363,22 @@ __device__ inline void mainloop_general(const nmgp_gemm_desc& d, const Tile& tl,
   }
 }
 
+// One output tile (or split-K chunk) `tile` of the launch: problem lookup, k-loop, epilogue.
 template <typename T, bool GROUPED>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args, const nmgp_gemm_desc* __restrict__ descs) {
-  // ONE shared array (a second __shared__ object can make hipcc wait vmcnt(0) in the k-loop)
-  __shared__ T smem[2 * LDS_T + 2];
+__device__ __forceinline__ void gemm_body(const GemmArgs& args, const nmgp_gemm_desc* __restrict__ descs, T* smem,
+                                          int tile) {
   int* s_last = (int*)(smem + 2 * LDS_T);
   GEMM_STAMP(0);
   GEMM_STAMPB(0);
-  int tile = blockIdx.x;
   int idx = 0;
+  const int32_t* dyn = args.dyn_start;
   if (GROUPED) {
+    // problem = last one whose first tile <= tile (problems with no tiles share the next start)
     int lo = 0, hi = args.nprob - 1;
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (descs[mid].tile_start <= tile) lo = mid; else hi = mid - 1;
+      const int st = dyn ? dyn[mid] : descs[mid].tile_start;
+      if (st <= tile) lo = mid; else hi = mid - 1;
     }
     idx = lo;
   }
@@ -388,7 +391,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args, const nmgp_gem
     d.B = (const char*)d.B + b * d.sB_b * (int64_t)sizeof(T);
     d.C = (char*)d.C + b * d.sC_b * (int64_t)sizeof(T);
   }
-  tile -= d.tile_start;
+  tile -= (GROUPED && dyn) ? dyn[idx] : d.tile_start;
   const int ksplit = d.ksplit > 1 ? d.ksplit : 1;
   const int ks = tile % ksplit;
   tile /= ksplit;
@@ -630,6 +633,64 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args, const nmgp_gem
   GEMM_STAMPB(3);
 }
 
+// Static grids run one tile per workgroup.  With a device tile plan (args.dyn_start, written by
+// gemm_plan_kernel from the segment table just before) the grid is a fixed number of workgroups
+// striding over the tiles that exist for this minibatch: row-segmented problems (rows of one
+// output) launch no workgroups for the rows other outputs own.
+template <typename T, bool GROUPED>
+__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs args, const nmgp_gemm_desc* __restrict__ descs) {
+  // ONE shared array (a second __shared__ object can make hipcc wait vmcnt(0) in the k-loop)
+  __shared__ T smem[2 * LDS_T + 2];
+  if constexpr (!GROUPED) {
+    gemm_body<T, false>(args, descs, smem, blockIdx.x);
+    return;
+  }
+  const int total = args.dyn_start ? args.dyn_start[args.nprob] : (int)gridDim.x;
+  for (int tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    gemm_body<T, GROUPED>(args, descs, smem, tile);
+    __syncthreads();
+  }
+}
+
+// Tile plan of a grouped launch for this minibatch: dyn_start[p] = first tile of problem p with
+// row-segmented problems sized by their actual segment (<= the static tiles_m), dyn_start[nprob] =
+// total.  One workgroup, block-wide exclusive scan in chunks of 256 problems.
+__global__ __launch_bounds__(256) void gemm_plan_kernel(const nmgp_gemm_desc* __restrict__ descs, int nprob,
+                                                        const int32_t* __restrict__ seg, int32_t* dyn_start) {
+  __shared__ int buf[256];
+  __shared__ int carry;
+  const int t = threadIdx.x;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < nprob; base += 256) {
+    const int p = base + t;
+    int v = 0;
+    if (p < nprob) {
+      const nmgp_gemm_desc& d = descs[p];
+      int tm = d.tiles_m;
+      if (d.row_seg >= 0 && seg != nullptr) {
+        const int span = d.seg_span > 0 ? d.seg_span : 1;
+        const int m = seg[d.row_seg + span] - seg[d.row_seg];
+        tm = min(tm, max(0, (m + GBM - 1) / GBM));
+      }
+      v = tm * d.tiles_n * (d.ksplit > 1 ? d.ksplit : 1);
+    }
+    buf[t] = v;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {   // Hillis-Steele inclusive scan
+      const int add = t >= off ? buf[t - off] : 0;
+      __syncthreads();
+      buf[t] += add;
+      __syncthreads();
+    }
+    if (p < nprob) dyn_start[p] = carry + buf[t] - v;
+    __syncthreads();
+    if (t == 255) carry += buf[255];
+    __syncthreads();
+  }
+  if (t == 0) dyn_start[nprob] = carry;
+}
+
 // Extra dynamic LDS per workgroup (experiment knob NMGP_GEMM_LDS_RESERVE=bytes, applied to grids of at
 // most NMGP_GEMM_LDS_RESERVE_MAXWG workgroups): reserving LDS forces one workgroup per CU.
 static size_t lds_reserve(int wgs) {
@@ -673,8 +734,34 @@ static int launch_grouped(const nmgp_gemm_desc* d_desc, int nprob, int total_til
   a.nprob = nprob;
   a.coop = total_tiles <= coresident_wgs<T>() ? 1 : 0;
   a.seg = d_seg;
+  a.dyn_start = nullptr;
   a.inl = nmgp_gemm_desc{};
   hipLaunchKernelGGL((gemm_kernel<T, true>), dim3(total_tiles), dim3(256), lds_reserve(total_tiles), s, a, d_desc);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
+
+// Grouped launch sized on device: plan kernel (tiles of this minibatch's segments) + a grid of
+// `grid` workgroups striding over them.  Split-K combines by last arriver (no co-residency waits).
+template <typename T>
+static int launch_grouped_dyn(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles, const int32_t* d_seg,
+                              int32_t* d_plan, int grid, hipStream_t s) {
+  if (d_desc == nullptr) return -1;
+  if (nprob <= 0) return -2;
+  if (total_tiles < 0) return -3;
+  if (d_plan == nullptr) return -5;
+  if (total_tiles == 0) return NMGP_OK;
+  if (grid <= 0 || grid > total_tiles) grid = total_tiles;
+  hipLaunchKernelGGL(gemm_plan_kernel, dim3(1), dim3(256), 0, s, d_desc, nprob, d_seg, d_plan);
+  NMGP_CHECK_LAUNCH();
+  GemmArgs a;
+  a.descs = d_desc;
+  a.nprob = nprob;
+  a.coop = 0;
+  a.seg = d_seg;
+  a.dyn_start = d_plan;
+  a.inl = nmgp_gemm_desc{};
+  hipLaunchKernelGGL((gemm_kernel<T, true>), dim3(grid), dim3(256), lds_reserve(grid), s, a, d_desc);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
@@ -694,6 +781,7 @@ static int launch_single(const nmgp_gemm_desc* h, const int32_t* d_seg, hipStrea
   a.nprob = 1;
   a.coop = 0;
   a.seg = d_seg;
+  a.dyn_start = nullptr;
   a.inl = d;
   hipLaunchKernelGGL((gemm_kernel<T, false>), dim3(d.tiles_m * d.tiles_n, d.batch > 1 ? d.batch : 1), dim3(256), 0, s,
                      a, (const nmgp_gemm_desc*)nullptr);
@@ -717,6 +805,14 @@ int64_t nmgp_sizeof_dsvi_args(void) { return (int64_t)sizeof(nmgp_dsvi_args); }
 
 int nmgp_gemm_grouped_f64(const nmgp_gemm_desc* d, int np, int tt, const int32_t* seg, hipStream_t s) {
   return nmgp::launch_grouped<double>(d, np, tt, seg, s);
+}
+int nmgp_gemm_grouped_dyn_f64(const nmgp_gemm_desc* d, int np, int tt, const int32_t* seg, int32_t* plan, int grid,
+                              hipStream_t s) {
+  return nmgp::launch_grouped_dyn<double>(d, np, tt, seg, plan, grid, s);
+}
+int nmgp_gemm_grouped_dyn_f32(const nmgp_gemm_desc* d, int np, int tt, const int32_t* seg, int32_t* plan, int grid,
+                              hipStream_t s) {
+  return nmgp::launch_grouped_dyn<float>(d, np, tt, seg, plan, grid, s);
 }
 int nmgp_gemm_grouped_f32(const nmgp_gemm_desc* d, int np, int tt, const int32_t* seg, hipStream_t s) {
   return nmgp::launch_grouped<float>(d, np, tt, seg, s);

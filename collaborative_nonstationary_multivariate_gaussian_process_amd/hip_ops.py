@@ -82,7 +82,7 @@ def _auto_ksplit(k_eff, group_tiles, work_per_wg):
 class GemmGroup:
     """A fixed list of GEMM problems launched as ONE grouped kernel (descriptors uploaded once)."""
 
-    def __init__(self, descs, device, dtype, seg=None, target_wgs=512):
+    def __init__(self, descs, device, dtype, seg=None, target_wgs=512, dyn_plan=True):
         """Split-K is chosen per problem so that the launch has ~target_wgs workgroups when the
         outputs alone are too few tiles (the M x B x M products P^T R with K = B)."""
         self.dtype = dtype
@@ -126,6 +126,17 @@ class GemmGroup:
         self.descs = list(descs)
         raw = bytes(memoryview(arr).cast("B"))
         self.dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+        # row-segmented problems (rows of one output) are sized on device per minibatch: a plan
+        # kernel + a grid of about the expected tile count striding over the tiles that exist
+        # (only where the static grid is mostly idle workgroups: the plan launch costs more than it
+        # saves on the PM2.5 shape, D=5; at HCP, D=50, it removes ~95% of the quad-form workgroups)
+        self.plan, self.grid = None, 0
+        if seg is not None and dyn_plan and any(d.row_seg >= 0 for d in descs):
+            ksp = {id(d): max(d.ksplit, 1) for d in descs}
+            expect = sum(eff[order[i]][0] * ksp[id(d)] for i, d in enumerate(descs))
+            if dyn_plan == "force" or (t >= 16384 and expect < 0.5 * t):
+                self.plan = torch.zeros(len(descs) + 1, dtype=torch.int32, device=device)
+                self.grid = int(min(t, max(256, min(4096, round(1.15 * expect)))))
 
     def macs(self, seg=None):
         return sum(desc_macs(d, seg) for d in self.descs)
@@ -135,6 +146,11 @@ class GemmGroup:
             return
         s = stream if stream is not None else L.stream_handle()
         segp = ctypes.c_void_p(self.seg.data_ptr()) if self.seg is not None else None
+        if self.plan is not None:
+            fn = getattr(L.lib(), "nmgp_gemm_grouped_dyn_" + _sfx(self.dtype))
+            L.check(fn(ctypes.c_void_p(self.dev.data_ptr()), self.n, self.total, segp,
+                       ctypes.c_void_p(self.plan.data_ptr()), self.grid, s), "gemm_grouped_dyn")
+            return
         fn = getattr(L.lib(), "nmgp_gemm_grouped_" + _sfx(self.dtype))
         L.check(fn(ctypes.c_void_p(self.dev.data_ptr()), self.n, self.total, segp, s), "gemm_grouped")
 

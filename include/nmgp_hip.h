@@ -86,6 +86,15 @@ int nmgp_gemm_grouped_f64(const nmgp_gemm_desc* d_desc, int nprob, int total_til
                           const int32_t* d_seg, hipStream_t stream);
 int nmgp_gemm_grouped_f32(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles,
                           const int32_t* d_seg, hipStream_t stream);
+/* The same sized on device for this minibatch: a one-workgroup plan kernel turns the segment table
+ * into per-problem first tiles (row-segmented problems get ceil(segment rows / 64) row tiles instead
+ * of the static tiles_m), written to plan[0..nprob] (caller buffer of nprob + 1 int32), then `grid`
+ * workgroups (<= total_tiles; <= 0: total_tiles) stride over the planned tiles.  Same results as the
+ * static launch; no workgroups are dispatched for rows other outputs own (HCP: D=50 segments).   */
+int nmgp_gemm_grouped_dyn_f64(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles, const int32_t* d_seg,
+                              int32_t* plan, int grid, hipStream_t stream);
+int nmgp_gemm_grouped_dyn_f32(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles, const int32_t* d_seg,
+                              int32_t* plan, int grid, hipStream_t stream);
 /* one problem passed by value (host descriptor; tiles fields are filled internally)          */
 int nmgp_gemm_f64(const nmgp_gemm_desc* h_desc, const int32_t* d_seg, hipStream_t stream);
 int nmgp_gemm_f32(const nmgp_gemm_desc* h_desc, const int32_t* d_seg, hipStream_t stream);

@@ -102,6 +102,41 @@ def test_gemm_kblocks_and_segments_grouped(ops):
     assert rel(out3, ref3) < 1e-14
 
 
+@pytest.mark.parametrize("dt", [F64, torch.float32])
+def test_gemm_grouped_device_plan(ops, dt):
+    """Row-segmented groups sized on device (plan kernel + grid-stride tiles) equal the static launch
+    bit for bit, including an empty segment, a segment longer than the static estimate and split-K."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L
+    g = torch.Generator().manual_seed(11)
+    D, B, M = 6, 900, 96
+    W = torch.randn(D, B, M, generator=g, dtype=F64).to(dt).to(DEV)
+    S = torch.randn(D, M, M, generator=g, dtype=F64).to(dt).to(DEV)
+    seg = torch.tensor([0, 0, 610, 700, 701, 840, 900], dtype=torch.int32, device=DEV)   # segment 0 empty
+    outs = []
+    for dyn in (False, True):
+        out = torch.full((B, M), 2.0, dtype=dt, device=DEV)
+        out2 = torch.zeros(D, M, M, dtype=dt, device=DEV)
+        descs = [ops.gemm_desc(out, W, S, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), row_seg=d,
+                               offs=(d * B * M, d * M * M, 0), alpha=0.5, beta=1.0) for d in range(D)]
+        # out2[d] = W[d][rows of segment d]^T W[d][same rows]  (k over the segment: split-K)
+        descs += [ops.gemm_desc(out2, W, W, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), k_seg=d,
+                                offs=(d * B * M, d * B * M, d * M * M)) for d in range(D)]
+        grp = ops.GemmGroup(descs, DEV, dt, seg=seg, dyn_plan="force" if dyn else False)
+        assert (grp.plan is not None) == dyn
+        grp()
+        grp()
+        outs.append((out.clone(), out2.clone()))
+    assert torch.equal(outs[0][1], outs[1][1])
+    Wc, Sc, sc = W.double().cpu(), S.double().cpu(), seg.cpu().tolist()
+    ref = torch.full((B, M), 2.0, dtype=F64)
+    for d in range(D):
+        r0, r1 = sc[d], sc[d + 1]
+        for _ in range(2):
+            ref[r0:r1] = 0.5 * (Wc[d][r0:r1] @ Sc[d]) + ref[r0:r1]
+    tol = 1e-13 if dt == F64 else 2e-6
+    assert rel(outs[1][0], ref) < tol and torch.equal(outs[0][0], outs[1][0])
+
+
 @pytest.mark.parametrize("K", [600, 2000, 4099])
 def test_gemm_split_k_deterministic(ops, K):
     """Long-k products P^T R (few output tiles) take the split-K path; results are bit-identical
