@@ -460,7 +460,9 @@ class DsviEngine:
             ("recon", "row", row(getattr(lib, "nmgp_dsvi_recon_" + self.sfx)), "main"),
             ("sig", "main", "recon"),
             ("bwd_w", "gemm", gemm("bwd_w"), "main"),
-            # L-bar / mu-bar gradient rows: after the KL L-bar (their first writer, same stream) and recon
+            # L-bar / mu-bar gradient rows: after the KL L-bar (their first writer, same stream) and recon.
+            # (Deferring them until after bwd_w, to leave it the whole chip, measured 2% slower: the
+            # main chain after bwd_w is latency-bound either way.)
             ("wait", "side", "recon"),
             ("bwd_lbar", "gemm", gemm("bwd_lbar"), "side"),
             ("sig", "side", "lbar_done"),

@@ -129,12 +129,12 @@ class GemmGroup:
         # row-segmented problems (rows of one output) are sized on device per minibatch: a plan
         # kernel + a grid of about the expected tile count striding over the tiles that exist
         # (only where the static grid is mostly idle workgroups: the plan launch costs more than it
-        # saves on the PM2.5 shape, D=5; at HCP, D=50, it removes ~95% of the quad-form workgroups)
+        # saves on small grids; PM2.5 quad / bwd_w: +2-3% it/s; HCP, D=50: ~95% of the quad-form workgroups removed)
         self.plan, self.grid = None, 0
         if seg is not None and dyn_plan and any(d.row_seg >= 0 for d in descs):
             ksp = {id(d): max(d.ksplit, 1) for d in descs}
             expect = sum(eff[order[i]][0] * ksp[id(d)] for i, d in enumerate(descs))
-            if dyn_plan == "force" or (t >= 16384 and expect < 0.5 * t):
+            if dyn_plan == "force" or (t >= int(os.environ.get("NMGP_DYN_MIN_TILES", 1024)) and expect < 0.5 * t):
                 self.plan = torch.zeros(len(descs) + 1, dtype=torch.int32, device=device)
                 self.grid = int(min(t, max(256, min(4096, round(1.15 * expect)))))
 
