@@ -363,7 +363,7 @@ def syevj(A):
     V = torch.empty_like(A)
     lib = L.lib()
     need = lib.nmgp_syevj_workspace_size_f64(n)
-    ws = big_workspace(A.device, need) if need > 0 else None
+    ws = big_workspace(A.device, need, tag="syevj") if need > 0 else None
     L.check(lib.nmgp_syevj_batched_f64(ctypes.c_void_p(A.data_ptr()), n, n, n * n, batch,
                                        ctypes.c_void_p(w.data_ptr()), n, ctypes.c_void_p(V.data_ptr()), n, n * n,
                                        ctypes.c_void_p(ws.data_ptr()) if ws is not None else None,

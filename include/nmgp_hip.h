@@ -148,6 +148,19 @@ int nmgp_potrf_blocked_f32(float* A, int64_t n, int64_t lda, int32_t* info, void
 int nmgp_potrf_blocked_f64(double* A, int64_t n, int64_t lda, int32_t* info, void* ws, int64_t ws_bytes,
                            hipStream_t stream);
 
+/* ------------------------------------------------------------------ symmetric eigensolver
+ * W[b] = eigenvalues of the symmetric A[b] (ascending, as torch.linalg.eigh / torch.symeig), V[b] =
+ * eigenvectors as columns (V[i*ldv + j] = component i of vector j).  Replaces torch.symeig(B) /
+ * torch.symeig(K) in kron_inv / kron_logdet (code/SIM_code/Utility/kronecker_operation.py:45,47,66,
+ * 67) and multivariate_normal_logpdf0/1 (code/SIM_code/Utility/distributions.py:37,40,67,70).
+ * Parallel cyclic Jacobi: n <= 64 one workgroup per matrix in LDS; larger n block Jacobi on 64x64
+ * pair sub-problems with a device convergence flag (asynchronous, graph-capturable).  A is not
+ * modified.  ws: nmgp_syevj_workspace_size_f64(n) bytes (no zero-fill needed).                  */
+int64_t nmgp_syevj_workspace_size_f64(int64_t n);
+int nmgp_syevj_batched_f64(const double* A, int64_t n, int64_t lda, int64_t strideA, int64_t batch, double* W,
+                           int64_t strideW, double* V, int64_t ldv, int64_t strideV, void* ws, int64_t ws_bytes,
+                           hipStream_t stream);
+
 /* ------------------------------------------------------------------ large-tile f32 GEMM / SYRK
  * C(i,j) = alpha * sum_k A[i*lda + k] * op(B)(k,j) + beta * C[i*sCi + j*sCj], batched with strides
  * sAb/sBb/sCb; op(B)(k,j) = B[j*ldb + k] (b_kcontig = 1) or B[k*ldb + j] (0).  flags: NMGP_A_LOWER,
