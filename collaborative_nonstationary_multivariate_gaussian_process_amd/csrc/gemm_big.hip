@@ -36,6 +36,10 @@ struct BigGemmArgs {
   int b_kcontig;            // 1: op(B)(k,j) = B[j*ldb + k]; 0: op(B)(k,j) = B[k*ldb + j]
   float alpha, beta;
   int tiles_m, tiles_n, tiles;   // tiles per batch item (lower tiles only with OUT_LOWER)
+  const int64_t* offA;      // per-batch element offsets (device arrays) instead of bat * sAb / sBb / sCb
+  const int64_t* offB;
+  const int64_t* offC;
+  float diag_add;           // added to C(i, i) after the update (Sigma = L L^T + jitter I)
   int ksplit;
   int streamk;              // 1: stream-K partition over a persistent grid (batch 1, uniform k)
   float* ws; int32_t* counters;
@@ -76,8 +80,8 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, float* big_sm
   const int wr = w >> 1, wc = w & 1;
   const int fl = g.flags;
   const bool aLo = fl & NMGP_A_LOWER, bUp = fl & NMGP_B_UPPER, bLo = fl & NMGP_B_LOWER;
-  const float* Ab = g.A + bat * g.sAb;
-  const float* Bb = g.B + bat * g.sBb;
+  const float* Ab = g.A + (g.offA ? g.offA[bat] : bat * g.sAb);
+  const float* Bb = g.B + (g.offB ? g.offB[bat] : bat * g.sBb);
   const __amdgpu_buffer_rsrc_t rA = make_rsrc(Ab, ((int64_t)(g.m - 1) * g.lda + g.k) * 4);
   const __amdgpu_buffer_rsrc_t rB =
       g.b_kcontig ? make_rsrc(Bb, ((int64_t)(g.n - 1) * g.ldb + g.k) * 4)
@@ -273,8 +277,9 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, 
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = w >> 1, wc = w & 1;
-  float* Cb = g.C + bat * g.sCb;
+  float* Cb = g.C + (g.offC ? g.offC[bat] : bat * g.sCb);
   const bool lower = g.flags & NMGP_OUT_LOWER;
+  const bool tril = g.flags & NMGP_OUT_TRIL;
   if (g.beta != 0.0f) {
     f32x16 cv[2][2];
 #pragma unroll
@@ -308,7 +313,12 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, 
       for (int r = 0; r < 16; ++r) {
         const int i = i0 + 64 * wr + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         const int j = j0 + 64 * wc + 32 * b + (lane & 31);
-        if (i < g.m && j < g.n && (!lower || j <= i)) Cb[(int64_t)i * g.sCi + (int64_t)j * g.sCj] = acc[a][b][r];
+        if (i < g.m && j < g.n && (!lower || j <= i)) {
+          float v = acc[a][b][r];
+          if (i == j) v += g.diag_add;
+          if (tril && j > i) v = 0.0f;
+          Cb[(int64_t)i * g.sCi + (int64_t)j * g.sCj] = v;
+        }
       }
 }
 
@@ -412,13 +422,16 @@ static int cu_count() {
 // C(i,j) = alpha * sum_k A[i*lda + k] * op(B)(k,j) + beta * C(i,j), batched over `batch` problems.
 // ws: gemm_big_ws_bytes() of device memory whose counter part is zero (the kernel leaves it zero),
 // or nullptr (no split-K).
-int gemm_big_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C, int64_t sCi,
-                 int64_t sCj, int m, int n, int k, int flags, float alpha, float beta, int64_t sAb, int64_t sBb,
-                 int64_t sCb, int batch, void* ws, hipStream_t s) {
+static int gemm_big_f32_ex(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C,
+                           int64_t sCi, int64_t sCj, int m, int n, int k, int flags, float alpha, float beta,
+                           int64_t sAb, int64_t sBb, int64_t sCb, const int64_t* offA, const int64_t* offB,
+                           const int64_t* offC, float diag_add, int batch, void* ws, hipStream_t s) {
   if (m <= 0 || n <= 0 || batch <= 0) return NMGP_OK;
   if ((flags & NMGP_OUT_LOWER) && m != n) return -1;
   BigGemmArgs g;
   g.A = A; g.B = B; g.C = C;
+  g.offA = offA; g.offB = offB; g.offC = offC;
+  g.diag_add = diag_add;
   g.lda = lda; g.ldb = ldb; g.sCi = sCi; g.sCj = sCj;
   g.sAb = sAb; g.sBb = sBb; g.sCb = sCb;
   g.m = m; g.n = n; g.k = k; g.flags = flags; g.b_kcontig = b_kcontig;
@@ -458,6 +471,13 @@ int gemm_big_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int b
   return NMGP_OK;
 }
 
+int gemm_big_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C, int64_t sCi,
+                 int64_t sCj, int m, int n, int k, int flags, float alpha, float beta, int64_t sAb, int64_t sBb,
+                 int64_t sCb, int batch, void* ws, hipStream_t s) {
+  return gemm_big_f32_ex(A, lda, B, ldb, b_kcontig, C, sCi, sCj, m, n, k, flags, alpha, beta, sAb, sBb, sCb, nullptr,
+                         nullptr, nullptr, 0.0f, batch, ws, s);
+}
+
 }  // namespace nmgp
 
 extern "C" {
@@ -475,5 +495,23 @@ int nmgp_gemm_big_f32(const float* A, int64_t lda, const float* B, int64_t ldb, 
   if (batch < 0 || batch > 65535) return -18;
   return nmgp::gemm_big_f32(A, lda, B, ldb, b_kcontig, C, sCi, sCj, m, n, k, flags, (float)alpha, (float)beta, sAb,
                             sBb, sCb, batch, ws, s);
+}
+int nmgp_gemm_big_offsets_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C,
+                              int64_t sCi, int64_t sCj, int m, int n, int k, int flags, double alpha, double beta,
+                              double diag_add, const int64_t* offA, const int64_t* offB, const int64_t* offC,
+                              int batch, void* ws, hipStream_t s) {
+  if (A == nullptr) return -1;
+  if (lda < k) return -2;
+  if (B == nullptr) return -3;
+  if (C == nullptr) return -6;
+  if (m < 0) return -9;
+  if (n < 0) return -10;
+  if (k < 0) return -11;
+  if (offA == nullptr) return -16;
+  if (offB == nullptr) return -17;
+  if (offC == nullptr) return -18;
+  if (batch < 0 || batch > 65535) return -19;
+  return nmgp::gemm_big_f32_ex(A, lda, B, ldb, b_kcontig, C, sCi, sCj, m, n, k, flags, (float)alpha, (float)beta, 0, 0,
+                               0, offA, offB, offC, (float)diag_add, batch, ws, s);
 }
 }

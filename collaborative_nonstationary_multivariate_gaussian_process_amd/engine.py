@@ -10,6 +10,7 @@ Reference path replaced: NMGP.forward + loss.backward() (code/nmgp_dsvi.py:157-3
 NMGP.compute_ELBO (code/nmgp_dsvi.py:303-404) and the Adam step (:777, :854).
 """
 import ctypes
+import os
 import math
 
 import numpy as np
@@ -197,6 +198,16 @@ class DsviEngine:
             d5.append(xs(FV))
             p["xs_side"] = G([xs(f) for f in range(FV)])
         p["inv3"] = G(d5)
+        if self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0":
+            # HCP / ECoG shapes: the D+Q factor products are 1000s of M x M triangular products --
+            # the 128x128 f32 MFMA kernel at per-factor parameter offsets instead of 64x64 grouped tiles
+            offs_f, slots = fac_off[:FV], [f * MM for f in range(FV)]
+            p["syrk_side"] = H.BigBatch(th, th, self.Afac, offs_f, offs_f, slots, M, M, M, lda=M, ldb=M,
+                                        b_kcontig=True, flags=L.A_LOWER | L.B_UPPER | L.OUT_LOWER,
+                                        diag_add=self.jitter)
+            if not elbo_mode:
+                p["xs_side"] = H.BigBatch(self.Cinv, th, self.Xs, slots, offs_f, slots, M, M, M, lda=M, ldb=M,
+                                          b_kcontig=False, flags=L.A_LOWER | L.B_LOWER | L.OUT_TRIL)
         # F6: P_k = K12_k Ainv_k (k = t,0,1) ; Y_t, Y_0, Y_1
         d6 = [g(self.P, self.K12, self.Ainv, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), offs=(k * BM, k * MM, k * BM),
                 **rows_all) for k in range(3)]

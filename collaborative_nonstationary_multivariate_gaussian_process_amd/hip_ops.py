@@ -306,6 +306,38 @@ def chol_inv_(A, out=None, info=None, ws=None):
     return out, info
 
 
+class BigBatch:
+    """`batch` same-shape f32 products at per-problem element offsets on the 128x128 MFMA kernel
+    (nmgp_gemm_big_offsets_f32): C_b = alpha A_b op(B_b) + beta C_b (+ diag_add on the diagonal),
+    A_b = A + offA[b] (m x k, row stride lda), op(B_b)(k, j) = B_b[j*ldb + k] (b_kcontig) or
+    B_b[k*ldb + j], C_b = C + offC[b] with strides (sCi, sCj).  Offsets are uploaded once; a call
+    is one launch (graph-capturable)."""
+
+    def __init__(self, A, B, C, offA, offB, offC, m, n, k, *, lda, ldb, b_kcontig, sC=None, flags=0, alpha=1.0,
+                 beta=0.0, diag_add=0.0):
+        for t_, nm in ((A, "A"), (B, "B"), (C, "C")):
+            L.require_device(t_, nm)
+            assert t_.dtype == torch.float32
+        dev = A.device
+        self.A, self.B, self.C = A, B, C
+        self.off = [torch.tensor(list(o), dtype=torch.int64, device=dev) for o in (offA, offB, offC)]
+        self.batch = len(offA)
+        assert len(offB) == self.batch and len(offC) == self.batch
+        self.args = (m, n, k, lda, ldb, b_kcontig, sC if sC is not None else (n, 1), flags, alpha, beta, diag_add)
+
+    def __call__(self, stream=None):
+        if self.batch == 0:
+            return
+        m, n, k, lda, ldb, bk, (sCi, sCj), flags, alpha, beta, dadd = self.args
+        s = stream if stream is not None else L.stream_handle()
+        vp = ctypes.c_void_p
+        L.check(L.lib().nmgp_gemm_big_offsets_f32(vp(self.A.data_ptr()), lda, vp(self.B.data_ptr()), ldb,
+                                                  1 if bk else 0, vp(self.C.data_ptr()), sCi, sCj, m, n, k, flags,
+                                                  alpha, beta, dadd, vp(self.off[0].data_ptr()),
+                                                  vp(self.off[1].data_ptr()), vp(self.off[2].data_ptr()), self.batch,
+                                                  None, s), "gemm_big_offsets")
+
+
 def potrf_blocked_(A, info=None, ws=None):
     """In-place lower Cholesky of ONE large SPD matrix A (n, n) on the blocked right-looking path with
     lookahead (include/nmgp_hip.h nmgp_potrf_blocked_*); strictly upper part zeroed.  Returns info

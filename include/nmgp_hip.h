@@ -173,6 +173,15 @@ int64_t nmgp_gemm_big_workspace_size(void);
 int nmgp_gemm_big_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C,
                       int64_t sCi, int64_t sCj, int m, int n, int k, int flags, double alpha, double beta,
                       int64_t sAb, int64_t sBb, int64_t sCb, int batch, void* ws, hipStream_t stream);
+/* The same for `batch` problems at arbitrary element offsets (device int64 arrays offA/offB/offC:
+ * problem b uses A + offA[b], B + offB[b], C + offC[b]) -- the D + Q variational factors of the
+ * engine, which sit at non-uniform offsets of the parameter vector (the live i >= j blocks of the dense
+ * D x D Sigma_U layout).  NMGP_OUT_TRIL stores zeros above the diagonal; diag_add is added to C(i,i)
+ * (Sigma_f = tril(S_f) tril(S_f)^T + jitter I, code/nmgp_dsvi.py:172-177, code/utils.py:343-344).  */
+int nmgp_gemm_big_offsets_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C,
+                              int64_t sCi, int64_t sCj, int m, int n, int k, int flags, double alpha, double beta,
+                              double diag_add, const int64_t* offA, const int64_t* offB, const int64_t* offC,
+                              int batch, void* ws, hipStream_t stream);
 
 /* ------------------------------------------------------------------ pairwise kernel builder
  * mode RBF:   K = scale2 * exp(-0.5 * ||x/ls - z/ls||^2)          (code/utils.py:91-94)

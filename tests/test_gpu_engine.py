@@ -186,3 +186,28 @@ def test_fp32_hcp_like_step_trains():
     assert model._theta.dtype == torch.float32
     assert np.all(np.isfinite(L)) and len(L) == 40
     assert L[-5:].mean() < L[:5].mean()
+
+
+def test_fp32_big_side_products_match_grouped(monkeypatch):
+    """M >= 512 fp32 engines run the D+Q factor products (Sigma_f = tril(S_f) tril(S_f)^T + jitter,
+    Xs_f = C_f^-1 L_f) on the 128x128 kernel at per-factor offsets; same loss and gradients as the
+    64x64 grouped path within fp32 rounding (D=3, M=512, device noise, HCP-style length scales)."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP
+    rng = np.random.default_rng(12)
+    D, n, M = 3, 300, 512
+    X = [np.sort(rng.uniform(0, 1, n)).reshape(-1, 1) for _ in range(D)]
+    Y = [np.sin(6 * x + d) + 0.3 * rng.standard_normal(x.shape) for d, x in enumerate(X)]
+    res = []
+    for big in ("1", "0"):
+        monkeypatch.setenv("NMGP_BIG_SIDE", big)
+        model = NMGP(number_observations=D * n, dim_outputs=D, Z=np.linspace(0, 1, M), seed=22,
+                     device="cuda:0", noise="device", dtype=torch.float32)
+        for k in ["length_scales_tildeell_log", "length_scales_L0_log", "length_scales_L1_log"]:
+            getattr(model, k).data.fill_(float(np.log(3.0 / M)))
+        loss = model(X, Y)
+        loss.backward()
+        torch.cuda.synchronize()
+        res.append((float(loss), torch.cat([p.grad.reshape(-1).double() for p in model.parameters()]).cpu()))
+    assert np.isfinite(res[0][0])
+    assert res[0][0] == pytest.approx(res[1][0], rel=1e-4)
+    assert _rel(res[0][1], res[1][1]) < 1e-3

@@ -350,6 +350,37 @@ def test_potrf_blocked_not_pd(ops):
     assert int(info.item()) == int(ref.item()) == 334
 
 
+def test_gemm_big_offsets_batch(ops):
+    # per-problem element offsets (non-uniform), OUT_TRIL zeroing, diag_add, OUT_LOWER + B_UPPER SYRK form
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L
+    g = torch.Generator().manual_seed(21)
+    M, nb = 300, 5
+    pool = torch.randn(9 * M * M, generator=g)
+    offs = [0, 3 * M * M + 17, M * M + 5, 7 * M * M, 5 * M * M + 1]
+    P = pool.to(DEV)
+    C = torch.full((nb, M, M), 7.0, device=DEV)
+    cs = [b * M * M for b in range(nb)]
+    syrk = ops.BigBatch(P, P, C, offs, offs, cs, M, M, M, lda=M, ldb=M, b_kcontig=True,
+                        flags=L.A_LOWER | L.B_UPPER | L.OUT_LOWER, diag_add=0.25)
+    syrk()
+    lo = torch.tril(torch.ones(M, M, dtype=torch.bool))
+    for b, o in enumerate(offs):
+        S = torch.tril(pool[o:o + M * M].reshape(M, M).double())
+        ref = S @ S.t() + 0.25 * torch.eye(M, dtype=F64)
+        got = C[b].cpu()
+        assert rel(got[lo], ref[lo]) < 2e-6 and torch.all(got[~lo] == 7.0)
+    X = torch.full((nb, M, M), 3.0, device=DEV)
+    xs = ops.BigBatch(C, P, X, cs, offs, cs, M, M, M, lda=M, ldb=M, b_kcontig=False,
+                      flags=L.A_LOWER | L.B_LOWER | L.OUT_TRIL)
+    xs()
+    for b, o in enumerate(offs):
+        A = torch.tril(C[b].cpu().double())
+        Bm = torch.tril(pool[o:o + M * M].reshape(M, M).double())
+        ref = A @ Bm
+        got = X[b].cpu()
+        assert rel(got, ref) < 2e-6 and torch.all(got[~lo] == 0)
+
+
 def test_chol_inv_blocked_not_pd_reports_global_column(ops):
     A = _spd(400, 2, 9)
     bad = A.clone()
