@@ -34,12 +34,17 @@ struct BigGemmArgs {
   int64_t sAb, sBb, sCb;
   int m, n, k, flags;
   int b_kcontig;            // 1: op(B)(k,j) = B[j*ldb + k]; 0: op(B)(k,j) = B[k*ldb + j]
+  int a_kcontig;            // 1: op(A)(i,k) = A[i*lda + k]; 0: op(A)(i,k) = A[k*lda + i]
   float alpha, beta;
   int tiles_m, tiles_n, tiles;   // tiles per batch item (lower tiles only with OUT_LOWER)
   const int64_t* offA;      // per-batch element offsets (device arrays) instead of bat * sAb / sBb / sCb
   const int64_t* offB;
   const int64_t* offC;
   float diag_add;           // added to C(i, i) after the update (Sigma = L L^T + jitter I)
+  // NMGP_EPI: C += gamma * rs[i] * E(i, j) (E(i, j) = 0 above the diagonal with NMGP_EPI_E_LOWER)
+  const float* E; const int64_t* offE; int64_t sEi, sEj;
+  const float* RS; const int64_t* offRS;
+  float gamma;
   int ksplit;
   int streamk;              // 1: stream-K partition over a persistent grid (batch 1, uniform k)
   float* ws; int32_t* counters;
@@ -69,36 +74,52 @@ __device__ inline void tile_krange(const BigGemmArgs& g, int i0, int j0, int& kb
   if (g.flags & NMGP_A_LOWER) kend = min(kend, i0 + BBM);
   if (g.flags & NMGP_B_UPPER) kend = min(kend, j0 + BBN);
   if (g.flags & NMGP_B_LOWER) kbeg = max(kbeg, j0);
+  if (g.flags & NMGP_A_UPPER) kbeg = max(kbeg, i0);
   kbeg = (kbeg / BBK) * BBK;
 }
 
-// acc += A[i0:i0+128, kt0:kt1] op(B)[kt0:kt1, j0:j0+128] (kend bounds the masks).
+// acc += A[i0:i0+128, kt0:kt1] op(B)[kt0:kt1, j0:j0+128] (kend bounds the masks).  AK / BK: operand
+// layouts (k-contiguous or not) as compile-time variants, so each kernel carries one loader per operand.
+template <bool AK, bool BK, int MODE>
 __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, float* big_smem, int64_t bat, int i0, int j0,
                                              int kend, int kt0, int kt1, f32x16 (&acc)[2][2]) {
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = w >> 1, wc = w & 1;
   const int fl = g.flags;
-  const bool aLo = fl & NMGP_A_LOWER, bUp = fl & NMGP_B_UPPER, bLo = fl & NMGP_B_LOWER;
-  const float* Ab = g.A + (g.offA ? g.offA[bat] : bat * g.sAb);
-  const float* Bb = g.B + (g.offB ? g.offB[bat] : bat * g.sBb);
-  const __amdgpu_buffer_rsrc_t rA = make_rsrc(Ab, ((int64_t)(g.m - 1) * g.lda + g.k) * 4);
+  const bool aLo = fl & NMGP_A_LOWER, aUp = fl & NMGP_A_UPPER, bUp = fl & NMGP_B_UPPER, bLo = fl & NMGP_B_LOWER;
+  const float* Ab = g.A + (MODE ? g.offA[bat] : bat * g.sAb);
+  const float* Bb = g.B + (MODE ? g.offB[bat] : bat * g.sBb);
+  const __amdgpu_buffer_rsrc_t rA =
+      AK ? make_rsrc(Ab, ((int64_t)(g.m - 1) * g.lda + g.k) * 4)
+                  : make_rsrc(Ab, ((int64_t)(g.k - 1) * g.lda + g.m) * 4);
   const __amdgpu_buffer_rsrc_t rB =
-      g.b_kcontig ? make_rsrc(Bb, ((int64_t)(g.n - 1) * g.ldb + g.k) * 4)
+      BK ? make_rsrc(Bb, ((int64_t)(g.n - 1) * g.ldb + g.k) * 4)
                   : make_rsrc(Bb, ((int64_t)(g.k - 1) * g.ldb + g.n) * 4);
 
-  // loader maps: A and k-contiguous B: row t>>3 (+32q), k 4*(t&7);  j-contiguous B: k t>>5 (+8q), j 4*(t&31)
+  // loader maps: k-contiguous A / B: row t>>3 (+32q), k 4*(t&7)
   const int lr = t >> 3, lk = (t & 7) * 4;
-  const int jr = t >> 5, jc = (t & 31) * 4;
+  // i-contiguous A / j-contiguous B: k = (t & 7) + 8q, i or j = 4 (t >> 3): each k row is read as 128
+  // contiguous bytes by 8 lanes, and the transposed LDS writes of consecutive lanes hit consecutive
+  // banks (2-way at most; a k = t >> 5 map put 8 lanes on one bank)
+  const int jr = t & 7, jc = (t >> 3) * 4;
   float4 ra[4], rb[4];
 
   auto load = [&](int kt) {
+    if constexpr (AK) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t row = i0 + lr + 32 * q;
-      ra[q] = ld4(rA, (uint32_t)((row * g.lda + kt + lk) * 4));
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = i0 + lr + 32 * q;
+        ra[q] = ld4(rA, (uint32_t)((row * g.lda + kt + lk) * 4));
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t kr = kt + jr + 8 * q;
+        ra[q] = ld4(rA, (uint32_t)((kr * g.lda + i0 + jc) * 4));
+      }
     }
-    if (g.b_kcontig) {
+    if constexpr (BK) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int64_t row = j0 + lr + 32 * q;
@@ -116,19 +137,28 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, float* big_sm
     // element masks (applied here, after the current k-tile's MFMAs: masking in load() made the
     // compiler wait for the global loads before them) only on k-tiles that straddle a triangle's diagonal or the k tail
     const bool need = (kt + BBK > kend) || (aLo && kt + BBK - 1 > i0) || (bUp && kt + BBK - 1 > j0) ||
-                      (bLo && kt < j0 + BBN - 1);
+                      (bLo && kt < j0 + BBN - 1) || (aUp && kt < i0 + BBM - 1);
     if (need) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int i = i0 + lr + 32 * q;
         float* a = (float*)&ra[q];
+        if constexpr (AK) {
+          const int i = i0 + lr + 32 * q;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int kk = kt + lk + e;
-          a[e] = keep_if(a[e], kk < kend && (!aLo || kk <= i));
+          for (int e = 0; e < 4; ++e) {
+            const int kk = kt + lk + e;
+            a[e] = keep_if(a[e], kk < kend && (!aLo || kk <= i) && (!aUp || kk >= i));
+          }
+        } else {
+          const int kk = kt + jr + 8 * q;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int i = i0 + jc + e;
+            a[e] = keep_if(a[e], kk < kend && (!aLo || kk <= i) && (!aUp || kk >= i));
+          }
         }
         float* b = (float*)&rb[q];
-        if (g.b_kcontig) {
+        if constexpr (BK) {
           const int j = j0 + lr + 32 * q;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -147,9 +177,18 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, float* big_sm
     }
     float* As = st;
     float* Bs = st + BBM * BP;
+    if constexpr (AK) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) *(float4*)&As[(lr + 32 * q) * BP + lk] = ra[q];
-    if (g.b_kcontig) {
+      for (int q = 0; q < 4; ++q) *(float4*)&As[(lr + 32 * q) * BP + lk] = ra[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float* a = (const float*)&ra[q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) As[(jc + e) * BP + jr + 8 * q] = a[e];
+      }
+    }
+    if constexpr (BK) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) *(float4*)&Bs[(lr + 32 * q) * BP + lk] = rb[q];
     } else {
@@ -270,56 +309,55 @@ __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S,
   return true;
 }
 
-// C = alpha * acc + beta * C on the stored part of the tile.  With beta != 0 all 64 C values of a
-// lane are loaded before the first store (one round trip instead of 64 serialized load->store
-// pairs: the compiler cannot move a C load above a C store it may alias).
+// C = alpha * acc + beta * C (+ diag_add, + the KL epilogue) on the stored part of the tile.  With
+// beta != 0 the 16 C values of one accumulator block are loaded together before its stores (4 round
+// trips per tile instead of 64 serialized load->store pairs: the compiler cannot move a C load above
+// a C store it may alias), which also keeps the epilogue within the 2-waves/SIMD register budget.
+template <int MODE>
 __device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, int i0, int j0, f32x16 (&acc)[2][2]) {
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = w >> 1, wc = w & 1;
-  float* Cb = g.C + (g.offC ? g.offC[bat] : bat * g.sCb);
+  constexpr bool EPI = MODE == 2;
+  float* Cb = g.C + (MODE ? g.offC[bat] : bat * g.sCb);
   const bool lower = g.flags & NMGP_OUT_LOWER;
-  const bool tril = g.flags & NMGP_OUT_TRIL;
-  if (g.beta != 0.0f) {
-    f32x16 cv[2][2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int i = i0 + 64 * wr + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          const int j = j0 + 64 * wc + 32 * b + (lane & 31);
-          const bool ok = i < g.m && j < g.n && (!lower || j <= i);
-          cv[a][b][r] = ok ? __builtin_nontemporal_load(Cb + (int64_t)i * g.sCi + (int64_t)j * g.sCj) : 0.0f;
-        }
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[a][b][r] = g.alpha * acc[a][b][r] + g.beta * cv[a][b][r];
-  } else {
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) acc[a][b] *= g.alpha;
-  }
+  const bool tril = MODE && (g.flags & NMGP_OUT_TRIL);
+  const bool eLo = g.flags & NMGP_EPI_E_LOWER;
+  const float* Eb = EPI ? g.E + (g.offE ? g.offE[bat] : 0) : nullptr;
+  const float* rs = EPI ? g.RS + (g.offRS ? g.offRS[bat] : 0) : nullptr;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < 2; ++b) {
+      const int ib = i0 + 64 * wr + 32 * a + 4 * (lane >> 5);
+      const int j = j0 + 64 * wc + 32 * b + (lane & 31);
+      f32x16 v = acc[a][b] * g.alpha;
+      if (g.beta != 0.0f) {
+        f32x16 cv;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int i = ib + (r & 3) + 8 * (r >> 2);
+          const bool ok = i < g.m && j < g.n && (!lower || j <= i);
+          cv[r] = ok ? __builtin_nontemporal_load(Cb + (int64_t)i * g.sCi + (int64_t)j * g.sCj) : 0.0f;
+        }
+        v += g.beta * cv;
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int i = i0 + 64 * wr + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int j = j0 + 64 * wc + 32 * b + (lane & 31);
+        const int i = ib + (r & 3) + 8 * (r >> 2);
         if (i < g.m && j < g.n && (!lower || j <= i)) {
-          float v = acc[a][b][r];
-          if (i == j) v += g.diag_add;
-          if (tril && j > i) v = 0.0f;
-          Cb[(int64_t)i * g.sCi + (int64_t)j * g.sCj] = v;
+          float x = v[r];
+          if constexpr (MODE == 1) {
+            if (i == j) x += g.diag_add;
+          }
+          if constexpr (EPI) {
+            if (!(eLo && j > i)) x += g.gamma * rs[i] * Eb[(int64_t)i * g.sEi + (int64_t)j * g.sEj];
+          }
+          if (tril && j > i) x = 0.0f;
+          Cb[(int64_t)i * g.sCi + (int64_t)j * g.sCj] = x;
         }
       }
+    }
 }
 
 __device__ inline void zero_acc(f32x16 (&acc)[2][2]) {
@@ -331,6 +369,7 @@ __device__ inline void zero_acc(f32x16 (&acc)[2][2]) {
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
 }
 
+template <bool AK, bool BK, int MODE>
 __global__ __launch_bounds__(256, 2) void gemm_big_kernel(BigGemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) float big_smem[];
   // XCD-aware block order: hardware places block b on XCD b % 8; give each XCD a contiguous run
@@ -387,7 +426,7 @@ __global__ __launch_bounds__(256, 2) void gemm_big_kernel(BigGemmArgs g) {
     tile_coords(g, tile, tm, tn);
     const int i0 = tm * BBM, j0 = tn * BBN;
     zero_acc(acc);
-    big_mainloop(g, big_smem, bat, i0, j0, kend, kt0, kt1, acc);
+    big_mainloop<AK, BK, MODE>(g, big_smem, bat, i0, j0, kend, kt0, kt1, acc);
     bool store = true;
     if (nparts > 1) {
       const int64_t slot0 = (bat * g.tiles + tile) * (int64_t)S;
@@ -399,7 +438,7 @@ __global__ __launch_bounds__(256, 2) void gemm_big_kernel(BigGemmArgs g) {
       int32_t* ctr = sk ? g.counters + c0 : g.counters + bat * g.tiles + tile;
       store = big_combine(g, me, nparts, ctr, slot_of, acc);
     }
-    if (store) big_epilogue(g, bat, i0, j0, acc);
+    if (store) big_epilogue<MODE>(g, bat, i0, j0, acc);
     it += step;
   }
 }
@@ -422,16 +461,28 @@ static int cu_count() {
 // C(i,j) = alpha * sum_k A[i*lda + k] * op(B)(k,j) + beta * C(i,j), batched over `batch` problems.
 // ws: gemm_big_ws_bytes() of device memory whose counter part is zero (the kernel leaves it zero),
 // or nullptr (no split-K).
+struct BigEpi {
+  int a_kcontig = 1;
+  const float* E = nullptr; const int64_t* offE = nullptr; int64_t sEi = 0, sEj = 0;
+  const float* RS = nullptr; const int64_t* offRS = nullptr;
+  float gamma = 0.0f;
+};
+
 static int gemm_big_f32_ex(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C,
                            int64_t sCi, int64_t sCj, int m, int n, int k, int flags, float alpha, float beta,
                            int64_t sAb, int64_t sBb, int64_t sCb, const int64_t* offA, const int64_t* offB,
-                           const int64_t* offC, float diag_add, int batch, void* ws, hipStream_t s) {
+                           const int64_t* offC, float diag_add, int batch, void* ws, hipStream_t s,
+                           const BigEpi& ep = BigEpi()) {
   if (m <= 0 || n <= 0 || batch <= 0) return NMGP_OK;
   if ((flags & NMGP_OUT_LOWER) && m != n) return -1;
   BigGemmArgs g;
   g.A = A; g.B = B; g.C = C;
   g.offA = offA; g.offB = offB; g.offC = offC;
   g.diag_add = diag_add;
+  g.a_kcontig = ep.a_kcontig;
+  g.E = ep.E; g.offE = ep.offE; g.sEi = ep.sEi; g.sEj = ep.sEj;
+  g.RS = ep.RS; g.offRS = ep.offRS; g.gamma = ep.gamma;
+  if ((flags & NMGP_EPI) && (ep.E == nullptr || ep.RS == nullptr)) return -1;
   g.lda = lda; g.ldb = ldb; g.sCi = sCi; g.sCj = sCj;
   g.sAb = sAb; g.sBb = sBb; g.sCb = sCb;
   g.m = m; g.n = n; g.k = k; g.flags = flags; g.b_kcontig = b_kcontig;
@@ -443,7 +494,7 @@ static int gemm_big_f32_ex(const float* A, int64_t lda, const float* B, int64_t 
   const int64_t total = (int64_t)g.tiles * batch;
   const int nkt = (k + BBK - 1) / BBK;
   const int P = 2 * cu_count();   // co-resident workgroups (the two LDS stages admit 2 per CU)
-  const bool uniform_k = !(flags & (NMGP_A_LOWER | NMGP_B_UPPER | NMGP_B_LOWER));
+  const bool uniform_k = !(flags & (NMGP_A_LOWER | NMGP_A_UPPER | NMGP_B_UPPER | NMGP_B_LOWER));
   const int64_t dp_slots = ((total + P - 1) / P) * P;
   if (ws && batch == 1 && uniform_k && P <= kBigSlots / 2 && (double)total / (double)dp_slots < 0.9 &&
       total * nkt >= 8LL * P) {
@@ -459,14 +510,42 @@ static int gemm_big_f32_ex(const float* A, int64_t lda, const float* B, int64_t 
   g.streamk = sk;
   g.ws = (float*)ws;
   g.counters = ws ? (int32_t*)((char*)ws + (size_t)kBigSlots * BSLOT * sizeof(float)) : nullptr;
-  static bool attr = false;
   const size_t lds = 2 * BSTAGE * sizeof(float);
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
+  const dim3 gd(sk ? (unsigned)P : (unsigned)(g.tiles * S), (unsigned)batch);
+  const bool epi = flags & NMGP_EPI;
+  auto go = [&](auto kern) {
+    static bool attr = false;   // one per instantiation
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr = true;
+    }
+    hipLaunchKernelGGL(kern, gd, dim3(256), lds, s, g);
+  };
+  const bool offs = offA != nullptr;
+  if (offs && (offB == nullptr || offC == nullptr)) return -1;
+  if (!offs && (diag_add != 0.0f || (flags & NMGP_OUT_TRIL))) return -1;   // those live in the offsets variants
+  if (epi) {
+    if (!offs || g.a_kcontig || g.b_kcontig) return -1;   // only the KL L-bar form (both operands transposed)
+    go(gemm_big_kernel<false, false, 2>);
+  } else if (offs) {
+    if (g.a_kcontig && g.b_kcontig)
+      go(gemm_big_kernel<true, true, 1>);
+    else if (g.a_kcontig)
+      go(gemm_big_kernel<true, false, 1>);
+    else if (g.b_kcontig)
+      go(gemm_big_kernel<false, true, 1>);
+    else
+      go(gemm_big_kernel<false, false, 1>);
+  } else {
+    if (g.a_kcontig && g.b_kcontig)
+      go(gemm_big_kernel<true, true, 0>);
+    else if (g.a_kcontig)
+      go(gemm_big_kernel<true, false, 0>);
+    else if (g.b_kcontig)
+      go(gemm_big_kernel<false, true, 0>);
+    else
+      go(gemm_big_kernel<false, false, 0>);
   }
-  const unsigned grid = sk ? (unsigned)P : (unsigned)(g.tiles * S);
-  hipLaunchKernelGGL(gemm_big_kernel, dim3(grid, (unsigned)batch), dim3(256), lds, s, g);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
@@ -513,5 +592,31 @@ int nmgp_gemm_big_offsets_f32(const float* A, int64_t lda, const float* B, int64
   if (batch < 0 || batch > 65535) return -19;
   return nmgp::gemm_big_f32_ex(A, lda, B, ldb, b_kcontig, C, sCi, sCj, m, n, k, flags, (float)alpha, (float)beta, 0, 0,
                                0, offA, offB, offC, (float)diag_add, batch, ws, s);
+}
+int nmgp_gemm_big_offsets_epi_f32(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb,
+                                  int b_kcontig, float* C, int64_t sCi, int64_t sCj, int m, int n, int k, int flags,
+                                  double alpha, double beta, double diag_add, const int64_t* offA,
+                                  const int64_t* offB, const int64_t* offC, const float* E, const int64_t* offE,
+                                  int64_t sEi, int64_t sEj, const float* RS, const int64_t* offRS, double gamma,
+                                  int batch, void* ws, hipStream_t s) {
+  if (A == nullptr) return -1;
+  if (B == nullptr) return -4;
+  if (C == nullptr) return -7;
+  if (m < 0) return -10;
+  if (n < 0) return -11;
+  if (k < 0) return -12;
+  if (lda < (a_kcontig ? k : m)) return -2;
+  if (offA == nullptr) return -17;
+  if (offB == nullptr) return -18;
+  if (offC == nullptr) return -19;
+  if ((flags & NMGP_EPI) && (E == nullptr || offE == nullptr)) return -20;
+  if ((flags & NMGP_EPI) && (RS == nullptr || offRS == nullptr)) return -24;
+  if (batch < 0 || batch > 65535) return -27;
+  nmgp::BigEpi ep;
+  ep.a_kcontig = a_kcontig ? 1 : 0;
+  ep.E = E; ep.offE = offE; ep.sEi = sEi; ep.sEj = sEj;
+  ep.RS = RS; ep.offRS = offRS; ep.gamma = (float)gamma;
+  return nmgp::gemm_big_f32_ex(A, lda, B, ldb, b_kcontig, C, sCi, sCj, m, n, k, flags, (float)alpha, (float)beta, 0, 0,
+                               0, offA, offB, offC, (float)diag_add, batch, ws, s, ep);
 }
 }

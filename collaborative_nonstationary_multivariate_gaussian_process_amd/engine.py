@@ -286,6 +286,14 @@ class DsviEngine:
         p["bwd_R"] = G(d18[:3])
         p["kl_abar"] = G(d18[3:7])
         p["kl_lbar"] = G(d18[7:])
+        if self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0":
+            # KL L-bar of all NF factors: -C_f^-T Xs_f + diag(1/C_ii^2) L_f on the 128x128 kernel
+            slots = [f * MM for f in range(NF)]
+            p["kl_lbar"] = H.BigBatch(self.Cinv, self.Xs, gr, slots, slots, fac_off, M, M, M, lda=M, ldb=M,
+                                      a_kcontig=False, b_kcontig=False,
+                                      flags=L.A_UPPER | L.B_LOWER | L.OUT_TRIL | L.EPI_E_LOWER, alpha=-1.0, beta=1.0,
+                                      epi=(th, fac_off, (M, 1), fb, [NF + 4 * M + prior_of[f] * M for f in range(NF)],
+                                           1.0))
         # B4: Abar_k -= 1/2 Y_k diag(sel_k) Y_k^T
         ybase = [D * M, (D + 1) * M, (D + 1 + D * D) * M, 0]
         ncol = [1, D * D, D * D, D]

@@ -308,34 +308,50 @@ def chol_inv_(A, out=None, info=None, ws=None):
 
 class BigBatch:
     """`batch` same-shape f32 products at per-problem element offsets on the 128x128 MFMA kernel
-    (nmgp_gemm_big_offsets_f32): C_b = alpha A_b op(B_b) + beta C_b (+ diag_add on the diagonal),
-    A_b = A + offA[b] (m x k, row stride lda), op(B_b)(k, j) = B_b[j*ldb + k] (b_kcontig) or
-    B_b[k*ldb + j], C_b = C + offC[b] with strides (sCi, sCj).  Offsets are uploaded once; a call
-    is one launch (graph-capturable)."""
+    (nmgp_gemm_big_offsets_epi_f32): C_b = alpha op(A_b) op(B_b) + beta C_b (+ diag_add on the diagonal)
+    (+ gamma rs_b(i) E_b(i, j) with `epi`).  op(A_b)(i, k) = A_b[i*lda + k] (a_kcontig) or
+    A_b[k*lda + i]; op(B_b)(k, j) = B_b[j*ldb + k] (b_kcontig) or B_b[k*ldb + j]; X_b = X + offX[b].
+    epi = (E, offE, (sEi, sEj), RS, offRS, gamma).  Offsets are uploaded once; a call is one launch
+    (graph-capturable)."""
 
-    def __init__(self, A, B, C, offA, offB, offC, m, n, k, *, lda, ldb, b_kcontig, sC=None, flags=0, alpha=1.0,
-                 beta=0.0, diag_add=0.0):
+    def __init__(self, A, B, C, offA, offB, offC, m, n, k, *, lda, ldb, b_kcontig, a_kcontig=True, sC=None,
+                 flags=0, alpha=1.0, beta=0.0, diag_add=0.0, epi=None):
         for t_, nm in ((A, "A"), (B, "B"), (C, "C")):
             L.require_device(t_, nm)
             assert t_.dtype == torch.float32
         dev = A.device
         self.A, self.B, self.C = A, B, C
-        self.off = [torch.tensor(list(o), dtype=torch.int64, device=dev) for o in (offA, offB, offC)]
+        i64 = lambda o: torch.tensor(list(o), dtype=torch.int64, device=dev)
+        self.off = [i64(o) for o in (offA, offB, offC)]
         self.batch = len(offA)
         assert len(offB) == self.batch and len(offC) == self.batch
-        self.args = (m, n, k, lda, ldb, b_kcontig, sC if sC is not None else (n, 1), flags, alpha, beta, diag_add)
+        self.epi = None
+        if epi is not None:
+            E, offE, (sEi, sEj), RS, offRS, gamma = epi
+            assert E.dtype == torch.float32 and RS.dtype == torch.float32
+            assert len(offE) == self.batch and len(offRS) == self.batch
+            self.epi = (E, i64(offE), sEi, sEj, RS, i64(offRS), gamma)
+            flags |= L.EPI
+        self.args = (m, n, k, lda, a_kcontig, ldb, b_kcontig, sC if sC is not None else (n, 1), flags, alpha, beta,
+                     diag_add)
 
     def __call__(self, stream=None):
         if self.batch == 0:
             return
-        m, n, k, lda, ldb, bk, (sCi, sCj), flags, alpha, beta, dadd = self.args
+        m, n, k, lda, ak, ldb, bk, (sCi, sCj), flags, alpha, beta, dadd = self.args
         s = stream if stream is not None else L.stream_handle()
         vp = ctypes.c_void_p
-        L.check(L.lib().nmgp_gemm_big_offsets_f32(vp(self.A.data_ptr()), lda, vp(self.B.data_ptr()), ldb,
-                                                  1 if bk else 0, vp(self.C.data_ptr()), sCi, sCj, m, n, k, flags,
-                                                  alpha, beta, dadd, vp(self.off[0].data_ptr()),
-                                                  vp(self.off[1].data_ptr()), vp(self.off[2].data_ptr()), self.batch,
-                                                  None, s), "gemm_big_offsets")
+        if self.epi is not None:
+            E, oE, sEi, sEj, RS, oRS, gamma = self.epi
+            ep = (vp(E.data_ptr()), vp(oE.data_ptr()), sEi, sEj, vp(RS.data_ptr()), vp(oRS.data_ptr()), gamma)
+        else:
+            ep = (None, None, 0, 0, None, None, 0.0)
+        L.check(L.lib().nmgp_gemm_big_offsets_epi_f32(vp(self.A.data_ptr()), lda, 1 if ak else 0,
+                                                      vp(self.B.data_ptr()), ldb, 1 if bk else 0,
+                                                      vp(self.C.data_ptr()), sCi, sCj, m, n, k, flags, alpha, beta,
+                                                      dadd, vp(self.off[0].data_ptr()), vp(self.off[1].data_ptr()),
+                                                      vp(self.off[2].data_ptr()), *ep, self.batch, None, s),
+                "gemm_big_offsets_epi")
 
 
 def potrf_blocked_(A, info=None, ws=None):

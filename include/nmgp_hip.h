@@ -182,6 +182,17 @@ int nmgp_gemm_big_offsets_f32(const float* A, int64_t lda, const float* B, int64
                               int64_t sCi, int64_t sCj, int m, int n, int k, int flags, double alpha, double beta,
                               double diag_add, const int64_t* offA, const int64_t* offB, const int64_t* offC,
                               int batch, void* ws, hipStream_t stream);
+/* General form: op(A)(i,k) = A[i*lda + k] (a_kcontig = 1) or A[k*lda + i] (0), NMGP_A_UPPER allowed,
+ * and with NMGP_EPI (+ NMGP_EPI_E_LOWER) the epilogue adds gamma * RS_b[i] * E_b(i, j), E_b = E + offE[b]
+ * with strides (sEi, sEj), RS_b = RS + offRS[b]: the KL L-bar of every variational factor,
+ * -C^-T (C^-1 L) + diag(1/C_ii^2) L (code/utils.py:339-351 and its autograd), for all D + Q + 1
+ * factors in one launch.                                                                        */
+int nmgp_gemm_big_offsets_epi_f32(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb,
+                                  int b_kcontig, float* C, int64_t sCi, int64_t sCj, int m, int n, int k, int flags,
+                                  double alpha, double beta, double diag_add, const int64_t* offA,
+                                  const int64_t* offB, const int64_t* offC, const float* E, const int64_t* offE,
+                                  int64_t sEi, int64_t sEj, const float* RS, const int64_t* offRS, double gamma,
+                                  int batch, void* ws, hipStream_t stream);
 
 /* ------------------------------------------------------------------ pairwise kernel builder
  * mode RBF:   K = scale2 * exp(-0.5 * ||x/ls - z/ls||^2)          (code/utils.py:91-94)

@@ -379,6 +379,23 @@ def test_gemm_big_offsets_batch(ops):
         ref = A @ Bm
         got = X[b].cpu()
         assert rel(got, ref) < 2e-6 and torch.all(got[~lo] == 0)
+    # KL L-bar form: G_b = -tril(C_b)^T tril(X_b) + G_b + diag-scaled E_b (lower), upper zeroed
+    Gd = torch.randn(nb, M, M, generator=g).to(DEV)
+    G0 = Gd.clone()
+    RS = torch.randn(3 * M, generator=g).to(DEV)
+    offr = [(b % 3) * M for b in range(nb)]
+    kl = ops.BigBatch(C, X, Gd, cs, cs, cs, M, M, M, lda=M, ldb=M, a_kcontig=False, b_kcontig=False,
+                      flags=L.A_UPPER | L.B_LOWER | L.OUT_TRIL | L.EPI_E_LOWER, alpha=-1.0, beta=1.0,
+                      epi=(P, offs, (M, 1), RS, offr, 1.0))
+    kl()
+    for b, o in enumerate(offs):
+        A = torch.tril(C[b].cpu().double())
+        Xb = torch.tril(X[b].cpu().double())
+        E = torch.tril(pool[o:o + M * M].reshape(M, M).double())
+        rs = RS.cpu().double()[offr[b]:offr[b] + M]
+        ref = torch.tril(-A.t() @ Xb + G0[b].cpu().double() + rs[:, None] * E)
+        got = Gd[b].cpu()
+        assert rel(got, ref) < 2e-6 and torch.all(got[~lo] == 0)
 
 
 def test_chol_inv_blocked_not_pd_reports_global_column(ops):
