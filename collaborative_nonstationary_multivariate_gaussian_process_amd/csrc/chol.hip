@@ -991,6 +991,8 @@ int gemm_big_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int b
                  int64_t sCj, int m, int n, int k, int flags, float alpha, float beta, int64_t sAb, int64_t sBb,
                  int64_t sCb, int batch, void* ws, hipStream_t s);
 size_t gemm_big_ws_bytes();
+int potrf_step_f32(float* P, float* C, const float* X, int64_t lda, int n2, int nb, int c1, int32_t* flag,
+                   hipStream_t s);
 
 // f32 recursion (same algebra as chol_inv_rec below) with the products on the 128x128 MFMA kernel
 // of gemm_big.hip, split-K into `ws` where the tile grid would not fill the chip.
@@ -1096,8 +1098,9 @@ static int chol_inv_launch(T* A, int64_t n, int64_t lda, int64_t sA, T* X, int64
 // triangle zeroed): right-looking, 128-wide block columns, one step of lookahead on two streams.
 // Step j (rows/columns below block j: n2):
 //   main:  [L_jj, X_jj] = fused leaf(A_jj)                      (register-resident, one workgroup)
-//          L_j = A_j X_jj^T                                      (panel GEMM, A_j staged in P)
+//          L_j = A_j X_jj^T                                      (panel GEMM)
 //          A(:, j+1) -= L_j L_j(0:128)^T                         (lookahead: next block column)
+//          (f32: both in one launch, potrf_step_kernel; f64: two GEMMs, A_j staged in P)
 //   side:  A(j+2:, j+2:) -= L_j(128:) L_j(128:)^T                (trailing SYRK, lower tiles only)
 // The trailing SYRK of step j runs while the main stream factors block j+1 (leaf + panel); the
 // lookahead update of step j+1 (which writes block column j+2) waits for it.  Everything else is
@@ -1132,7 +1135,7 @@ template <typename T>
 static size_t potrf_blocked_ws(int64_t n) {
   const int64_t nblk = (n + PNB - 1) / PNB;
   size_t b = al256((size_t)nblk * PNB * PNB * sizeof(T)) + al256((size_t)n * PNB * sizeof(T));
-  if (std::is_same<T, float>::value) b += 2 * al256(gemm_big_ws_bytes());
+  if (std::is_same<T, float>::value) b += 2 * al256(gemm_big_ws_bytes()) + 256;   // + step-kernel flag
   return b;
 }
 
@@ -1168,9 +1171,11 @@ static int potrf_blocked(T* A, int n, int64_t lda, int32_t* info, void* ws, hipS
   w += al256((size_t)n * PNB * sizeof(T));
   void* ws_main = nullptr;
   void* ws_side = nullptr;
+  int32_t* step_flag = nullptr;
   if (std::is_same<T, float>::value) {
     ws_main = w;
     ws_side = w + al256(gemm_big_ws_bytes());
+    step_flag = (int32_t*)((char*)ws_side + al256(gemm_big_ws_bytes()));
   }
   bool side_used = false;
   for (int jb = 0; jb < nblk; ++jb) {
@@ -1180,24 +1185,26 @@ static int potrf_blocked(T* A, int n, int64_t lda, int32_t* info, void* ws, hipS
     if ((rc = chol_inv_small<T>(Ajj, nbj, lda, 0, Xj, PNB, 0, 1, info, s, j0, jb == 0, false)) != NMGP_OK) return rc;
     if (n2 == 0) break;
     T* Lj = A + (int64_t)r0 * lda + j0;   // block column j below the diagonal block
-    // f32: one 128-wide tile column, no split-K (B is triangular), so each workgroup reads its rows
-    // of A_j in full before it overwrites them -- the panel runs in place.  The f64 kernel's 64-wide
-    // tiles would let one workgroup overwrite rows another is still reading: staged through P.
-    const T* Aj = Lj;
-    int64_t ldaj = lda;
-    if (!std::is_same<T, float>::value) {
-      if ((rc = block_copy<T>(Lj, lda, 0, P, PNB, 0, n2, nbj, 1, s)) != NMGP_OK) return rc;
-      Aj = P;
-      ldaj = PNB;
-    }
-    if ((rc = pgemm<T>(Aj, ldaj, Xj, PNB, Lj, lda, n2, nbj, nbj, NMGP_B_UPPER, 1.0, 0.0, ws_main, s)) != NMGP_OK)
-      return rc;
     const int c1 = min(PNB, n2), n3 = n2 - c1;
-    // the trailing SYRK of step j-1 wrote block column j+1: the lookahead update must follow it
-    if (side_used && hipStreamWaitEvent(s, ctx->ev_side, 0) != hipSuccess) return NMGP_ERR_LAUNCH;
-    if ((rc = pgemm<T>(Lj, lda, Lj, lda, A + (int64_t)r0 * lda + r0, lda, n2, c1, nbj, 0, -1.0, 1.0, ws_main, s)) !=
-        NMGP_OK)
-      return rc;
+    if constexpr (std::is_same<T, float>::value) {
+      // panel + lookahead in one launch (gemm_big.hip potrf_step_kernel: one 128-wide tile column,
+      // each workgroup reads its rows of A_j in full before overwriting them -- in place).  The
+      // trailing SYRK of step j-1 wrote block column j+1, so the launch follows it.
+      if (side_used && hipStreamWaitEvent(s, ctx->ev_side, 0) != hipSuccess) return NMGP_ERR_LAUNCH;
+      if ((rc = potrf_step_f32(Lj, A + (int64_t)r0 * lda + r0, Xj, lda, n2, nbj, c1, step_flag, s)) != NMGP_OK)
+        return rc;
+    } else {
+      // the f64 kernel's 64-wide tiles would let one workgroup overwrite rows another is still
+      // reading: the panel is staged through P
+      if ((rc = block_copy<T>(Lj, lda, 0, P, PNB, 0, n2, nbj, 1, s)) != NMGP_OK) return rc;
+      if ((rc = pgemm<T>(P, PNB, Xj, PNB, Lj, lda, n2, nbj, nbj, NMGP_B_UPPER, 1.0, 0.0, ws_main, s)) != NMGP_OK)
+        return rc;
+      // the trailing SYRK of step j-1 wrote block column j+1: the lookahead update must follow it
+      if (side_used && hipStreamWaitEvent(s, ctx->ev_side, 0) != hipSuccess) return NMGP_ERR_LAUNCH;
+      if ((rc = pgemm<T>(Lj, lda, Lj, lda, A + (int64_t)r0 * lda + r0, lda, n2, c1, nbj, 0, -1.0, 1.0, ws_main, s)) !=
+          NMGP_OK)
+        return rc;
+    }
     if (n3 > 0) {
       if (hipEventRecord(ctx->ev_main, s) != hipSuccess) return NMGP_ERR_LAUNCH;
       if (hipStreamWaitEvent(ctx->side, ctx->ev_main, 0) != hipSuccess) return NMGP_ERR_LAUNCH;

@@ -50,8 +50,9 @@ struct BigGemmArgs {
   float* ws; int32_t* counters;
 };
 
+template <int AUX = 0>
 __device__ inline float4 ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX));
 }
 
 // Lower-triangle tile index -> (tile row, tile column), row-major over the lower triangle.
@@ -80,7 +81,7 @@ __device__ inline void tile_krange(const BigGemmArgs& g, int i0, int j0, int& kb
 
 // acc += A[i0:i0+128, kt0:kt1] op(B)[kt0:kt1, j0:j0+128] (kend bounds the masks).  AK / BK: operand
 // layouts (k-contiguous or not) as compile-time variants, so each kernel carries one loader per operand.
-template <bool AK, bool BK, int MODE>
+template <bool AK, bool BK, int MODE, int AUX = 0>
 __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, float* big_smem, int64_t bat, int i0, int j0,
                                              int kend, int kt0, int kt1, f32x16 (&acc)[2][2]) {
   const int t = threadIdx.x, lane = t & 63;
@@ -110,26 +111,26 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, float* big_sm
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int64_t row = i0 + lr + 32 * q;
-        ra[q] = ld4(rA, (uint32_t)((row * g.lda + kt + lk) * 4));
+        ra[q] = ld4<AUX>(rA, (uint32_t)((row * g.lda + kt + lk) * 4));
       }
     } else {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int64_t kr = kt + jr + 8 * q;
-        ra[q] = ld4(rA, (uint32_t)((kr * g.lda + i0 + jc) * 4));
+        ra[q] = ld4<AUX>(rA, (uint32_t)((kr * g.lda + i0 + jc) * 4));
       }
     }
     if constexpr (BK) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int64_t row = j0 + lr + 32 * q;
-        rb[q] = ld4(rB, (uint32_t)((row * g.ldb + kt + lk) * 4));
+        rb[q] = ld4<AUX>(rB, (uint32_t)((row * g.ldb + kt + lk) * 4));
       }
     } else {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int64_t kr = kt + jr + 8 * q;
-        rb[q] = ld4(rB, (uint32_t)((kr * g.ldb + j0 + jc) * 4));
+        rb[q] = ld4<AUX>(rB, (uint32_t)((kr * g.ldb + j0 + jc) * 4));
       }
     }
   };
@@ -441,6 +442,96 @@ __global__ __launch_bounds__(256, 2) void gemm_big_kernel(BigGemmArgs g) {
     if (store) big_epilogue<MODE>(g, bat, i0, j0, acc);
     it += step;
   }
+}
+
+// ------------------------------------------------------------------ blocked potrf: panel + lookahead
+// One launch per block step j of the blocked Cholesky (chol.hip potrf_blocked, f32): workgroup i owns
+// row tile i (128 rows) below the diagonal block.
+//   1. L_i = A_i X_jj^T                 (k = nb; in place: the workgroup reads its rows in full first)
+//      stored write-through (sc1); workgroup 0's tile L_0 (the rows of block column j+1) is published
+//      with a flag once its stores drained.
+//   2. every workgroup waits for the flag, then A(rows i, block column j+1) -= L_i L_0^T, its operands
+//      read back with sc1 loads (L_i: its own write-through stores; L_0: workgroup 0's).
+// The flag is reset by the last workgroup to finish reading, so graph replays start from zero.  Only
+// workgroup 0 is waited on and it is dispatched first, so the grid need not be co-resident.
+struct PotrfStepArgs {
+  float* P;            // panel: A(r0, j0), rows n2, row stride lda (becomes L_j)
+  float* C;            // lookahead target: A(r0, r0)
+  const float* X;      // X_jj = L_jj^{-1}, ld PNB
+  int64_t lda;
+  int n2, nb, c1;
+  int32_t* flag;       // [0] published flag, [1] readers done
+};
+
+__global__ __launch_bounds__(256, 2) void potrf_step_kernel(PotrfStepArgs pa) {
+  extern __shared__ __attribute__((aligned(16))) float big_smem[];
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int i0 = blockIdx.x * BBM;
+  f32x16 acc[2][2];
+  // 1. panel tile
+  BigGemmArgs g{};
+  g.A = pa.P; g.lda = pa.lda; g.B = pa.X; g.ldb = 128; g.C = pa.P; g.sCi = pa.lda; g.sCj = 1;
+  g.m = pa.n2; g.n = pa.nb; g.k = pa.nb; g.flags = NMGP_B_UPPER; g.alpha = 1.0f; g.beta = 0.0f;
+  zero_acc(acc);
+  big_mainloop<true, true, 0>(g, big_smem, 0, i0, 0, pa.nb, 0, pa.nb, acc);
+  {
+    const __amdgpu_buffer_rsrc_t rC = make_rsrc(pa.P, ((int64_t)(pa.n2 - 1) * pa.lda + pa.nb) * 4);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int i = i0 + 64 * wr + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int j = 64 * wc + 32 * b + (lane & 31);
+          if (i < pa.n2 && j < pa.nb)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][r]), rC,
+                                                  (uint32_t)(((int64_t)i * pa.lda + j) * 4), 0, 16 /* sc1 */);
+        }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (blockIdx.x == 0 && t == 0) __hip_atomic_store(pa.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t == 0) {
+    // bounded: a lost publisher must not hang the GPU (the result is then wrong, not stuck)
+    for (int spin = 0; spin < (1 << 26); ++spin) {
+      if (__hip_atomic_load(pa.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // 2. lookahead: A(rows i, block column j+1) -= L_i L_0^T
+  BigGemmArgs g2{};
+  g2.A = pa.P; g2.lda = pa.lda; g2.B = pa.P; g2.ldb = pa.lda; g2.C = pa.C; g2.sCi = pa.lda; g2.sCj = 1;
+  g2.m = pa.n2; g2.n = pa.c1; g2.k = pa.nb; g2.flags = 0; g2.alpha = -1.0f; g2.beta = 1.0f;
+  zero_acc(acc);
+  big_mainloop<true, true, 0, 16>(g2, big_smem, 0, i0, 0, pa.nb, 0, pa.nb, acc);
+  if (t == 0) {
+    const int old = __hip_atomic_fetch_add(pa.flag + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (int)gridDim.x - 1) {   // every reader is past its loads of L_0: re-arm for the next launch
+      __hip_atomic_store(pa.flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(pa.flag + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  big_epilogue<0>(g2, 0, i0, 0, acc);
+}
+
+int potrf_step_f32(float* P, float* C, const float* X, int64_t lda, int n2, int nb, int c1, int32_t* flag,
+                   hipStream_t s) {
+  if (n2 <= 0) return NMGP_OK;
+  PotrfStepArgs pa{P, C, X, lda, n2, nb, c1, flag};
+  const size_t lds = 2 * BSTAGE * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)potrf_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(potrf_step_kernel, dim3((unsigned)((n2 + BBM - 1) / BBM)), dim3(256), lds, s, pa);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
 }
 
 // Partial slots the split-K path may use per call (workspace = slots * 64 KB + counters).
