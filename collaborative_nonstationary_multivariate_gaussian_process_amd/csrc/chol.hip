@@ -366,9 +366,19 @@ template <> __device__ inline void sqrt_recip<double>(double d, double& s, doubl
   const double e = fma(-s, y1, 1.0);
   inv = fma(y1, e, y1);
 }
+// f32 pivots: the same corrected rsq sequence as f64 (8 FMA-pipe ops after v_rsq) instead of IEEE
+// sqrtf + division.  A bare rsq (1 ulp, s = d * rsq) moved the fp32 engine's gradient by 4.5% on the
+// ill-conditioned mid fixture (cond(K22 + 1e-4 I) ~ 1e5): the pivots must round like sqrt.
 template <> __device__ inline void sqrt_recip<float>(float d, float& s, float& inv) {
-  s = sqrtf(d);
-  inv = 1.0f / s;
+  const float y0 = __builtin_amdgcn_rsqf(d);
+  const float h = d * y0;
+  const float r = fmaf(-h, y0, 1.0f);
+  const float y1 = fmaf(0.5f * y0, r, y0);
+  const float s0 = d * y1;
+  const float rr = fmaf(-s0, s0, d);
+  s = fmaf(rr, 0.5f * y1, s0);
+  const float e = fmaf(-s, y1, 1.0f);
+  inv = fmaf(y1, e, y1);
 }
 
 template <typename T, int NTPW>
