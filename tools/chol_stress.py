@@ -73,6 +73,17 @@ for M in sizes:
         assert int(infop.item()) == 0
         Lp = Wp.double()
         resp = float((Lp[idx] @ Lp.t() - A64[idx]).norm() / A64[idx].norm())
+        # the same launches issued eagerly (no graph): one hardware queue per stream
+        torch.cuda.synchronize()
+        ee = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ee[0].record()
+        for _ in range(reps):
+            Wp.copy_(A0)
+            H.potrf_blocked_(Wp, info=infop)
+        ee[1].record()
+        torch.cuda.synchronize()
+        mse = ee[0].elapsed_time(ee[1]) / reps - (e[2].elapsed_time(e[3])) / reps
+        print(f"M={M} {str(dt)[6:]:8s} potrf    {mse:8.3f} ms  eager launches (no graph)", flush=True)
         print(f"M={M} {str(dt)[6:]:8s} potrf    {msp:8.3f} ms  {M ** 3 / 3.0 / msp / 1e9:7.2f} TF/s (M^3/3)  "
               f"|LL^T-A|/|A| {resp:.2e}  [blocked right-looking, lookahead]", flush=True)
         print(f"M={M} {str(dt)[6:]:8s} chol+inv {ms:8.3f} ms  {f2 / ms / 1e9:7.2f} TF/s (2M^3/3)  "
