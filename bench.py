@@ -289,6 +289,12 @@ def main():
         per_name, per_kind = timer.summary(nrep)
         seg_host = host_batches[(nrep - 1) % nb][3]
         gemm_flops = 2.0 * sum(g.macs(seg_host) for _, g in eng.gemm_groups())
+        gemm_by_launch = {}
+        for nm, grp in eng.gemm_groups():
+            if hasattr(grp, "macs") and nm in per_name:
+                gf = 2.0 * grp.macs(seg_host) / 1e9
+                gemm_by_launch[nm] = {"ms": round(per_name[nm], 4), "gflop": round(gf, 4),
+                                      "tflops": round(gf / per_name[nm], 2) if per_name[nm] > 0 else None}
         gemm_ms = per_kind.get("gemm", 0.0)
         n_gemm = sum(1 for it in eng._sched if len(it) > 1 and it[1] == "gemm")
         achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12
@@ -345,6 +351,7 @@ def main():
             rec["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
         if breakdown is not None:
             rec["phase_ms_by_launch"] = breakdown_names
+            rec["gemm_by_launch"] = gemm_by_launch
         print(json.dumps(rec))
     if world > 1:
         dist.destroy_process_group()

@@ -491,11 +491,19 @@ class DsviEngine:
             ("bwd_build", "pairwise_bwd", pw("bwd_build"), "main"),
             ("tbwd", "row", row(getattr(lib, "nmgp_dsvi_tbwd_" + self.sfx)), "main"),
             ("bwd_t1", "gemm", gemm("bwd_t1"), "main"),
+            # after bwd_t1 the t-prior chain (bwd_t2 -> builder backward) and the v-factor Cholesky
+            # backward (vbwd -> bwd_v1 -> bwd_v2, reading vbar and the Gibbs partials) share no buffer:
+            # the v chain runs on the side stream (after bwd_lbar there, which keeps the order of the
+            # sqrt_v gradient accumulation fixed: kl_lbar, bwd_lbar, bwd_v2)
+            ("sig", "main", "t1"),
+            ("wait", "side", "t1"),
+            ("vbwd", "row", row(getattr(lib, "nmgp_dsvi_vbwd_" + self.sfx)), "side"),
+            ("bwd_v1", "gemm", gemm("bwd_v1"), "side"),
+            ("bwd_v2", "gemm", gemm("bwd_v2"), "side"),
+            ("sig", "side", "v_done"),
             ("bwd_t2", "gemm", gemm("bwd_t2"), "main"),
             ("bwd_tbuild", "pairwise_bwd", pw("bwd_tbuild"), "main"),
-            ("vbwd", "row", row(getattr(lib, "nmgp_dsvi_vbwd_" + self.sfx)), "main"),
-            ("bwd_v1", "gemm", gemm("bwd_v1"), "main"),
-            ("bwd_v2", "gemm", gemm("bwd_v2"), "main"),
+            ("wait", "main", "v_done"),
             ("wait", "main", "lbar_done"),
             ("finalize", "row", row(getattr(lib, "nmgp_dsvi_finalize_" + self.sfx)), "main"),
         ]
