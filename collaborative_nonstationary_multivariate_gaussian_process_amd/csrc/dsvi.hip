@@ -476,15 +476,34 @@ __global__ __launch_bounds__(256) void dsvi_vbwd_kernel(Args a) {
   }
   __syncthreads();
   const T* Cv = (const T*)a.Afac + (int64_t)(a.NF - 1) * M * M;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int i0 = blockIdx.x * VBW_ROWS;
-  for (int r = wv; r < VBW_ROWS; r += 4) {
-    const int i = i0 + r;
-    T s = 0;
-    if (i < M)
-      for (int k = i + lane; k < M; k += 64) s += Cv[(int64_t)k * M + i] * vbs[k];
-    s = wave_sum(s);
-    if (lane == 0) wrow[r] = s;
+  {
+    // w_i = sum_{k >= i} C_v[k][i] vbar[k] for the block's VBW_ROWS rows: thread t walks rows k of
+    // C_v and reads the VBW_ROWS consecutive entries (i0 .. i0+7) of each (one contiguous segment per
+    // row; a wave per i with lanes over k touched 64 cache lines per load), then one block reduction
+    // per i in a fixed order
+    T sp[VBW_ROWS];
+#pragma unroll
+    for (int r = 0; r < VBW_ROWS; ++r) sp[r] = 0;
+    for (int k = i0 + (int)threadIdx.x; k < M; k += blockDim.x) {
+      const T vk = vbs[k];
+      const T* row = Cv + (int64_t)k * M + i0;
+#pragma unroll
+      for (int r = 0; r < VBW_ROWS; ++r)
+        if (i0 + r <= k) sp[r] += row[r] * vk;
+    }
+    T* red = wrow + VBW_ROWS;   // 4 waves x VBW_ROWS partials
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int r = 0; r < VBW_ROWS; ++r) {
+      const T v = wave_sum(sp[r]);
+      if (lane == 0) red[wv * VBW_ROWS + r] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < VBW_ROWS) {
+      const int r = threadIdx.x;
+      wrow[r] = ((red[r] + red[VBW_ROWS + r]) + red[2 * VBW_ROWS + r]) + red[3 * VBW_ROWS + r];
+    }
   }
   __syncthreads();
   const T* zv = (const T*)a.noise;
@@ -890,7 +909,7 @@ template <typename T> static int dsvi_tbwd(const Args* a, hipStream_t s) {
 }
 template <typename T> static int dsvi_vbwd(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
-  const size_t sm = (size_t)2 * a->M * sizeof(T);
+  const size_t sm = (size_t)(a->M + 5 * VBW_ROWS) * sizeof(T);   // vbar | w rows | 4 x VBW_ROWS wave partials
   hipLaunchKernelGGL(dsvi_vbwd_kernel<T>, dim3((a->M + VBW_ROWS - 1) / VBW_ROWS), dim3(256), sm, s, *a);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
