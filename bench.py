@@ -206,10 +206,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # one process per GPU (rank LOCAL_RANK on cuda:LOCAL_RANK, RCCL).  NMGP_DIST_BACKEND=gloo with more
+    # ranks than devices is the rehearsal mode for a one-GPU box (ranks share cuda:0); never the
+    # measured configuration.
+    backend = os.environ.get("NMGP_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend != "nccl" and ndev > 0:
+        local = local % ndev
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
