@@ -191,6 +191,7 @@ class DsviEngine:
                          flags=L.A_LOWER | L.B_LOWER | L.OUT_TRIL, offs=(f * MM, fac_off[f], f * MM))
         p["syrk"] = G([syrk(FV)])
         p["syrk_side"] = G([syrk(f) for f in range(FV)])
+        p["syrk_all"] = G([syrk(f) for f in range(FV + 1)])   # training step: Sigma_v with the others
         # F5: prior inverses t,0,1 and Xs_f = Cinv_f L_f (KL gradient)
         d5 = [g(self.Ainv, self.Cinv, self.Cinv, M, M, M, (1, M, 0), (M, 1, 0), (M, 1), flags=L.A_UPPER | L.B_LOWER,
                 offs=((NF + k) * MM, (NF + k) * MM, k * MM)) for k in range(3)]
@@ -438,15 +439,26 @@ class DsviEngine:
 
         need_side = (not elbo_mode) or with_kl
         steps = []
+        # (fp64 engines only: in fp32 Sigma_v's summation order shows through ell_Z = exp(v), so fp32
+        # engines keep forming it exactly as the reference-checked grouped single launch does)
+        v_on_side = need_side and not elbo_mode and self.dt == torch.float64
         if need_side:
-            steps += [("sig", "main", "fork"), ("wait", "side", "fork"),
-                      ("syrk_side", "gemm", gemm("syrk_side"), "side"),
-                      ("chol_side", "chol", chol(0, FV), "side")]
+            steps += [("sig", "main", "fork"), ("wait", "side", "fork")]
+            if v_on_side:
+                # Sigma_v is formed with the other factors on the side stream (one launch), beside the
+                # RBF builders on the main stream, instead of a second dependent launch there
+                steps += [("syrk_all", "gemm", gemm("syrk_all"), "side"), ("sig", "side", "syrk")]
+            else:
+                steps.append(("syrk_side", "gemm", gemm("syrk_side"), "side"))
+            steps.append(("chol_side", "chol", chol(0, FV), "side"))
             if not elbo_mode:
                 steps.append(("xs_side", "gemm", gemm("xs_side"), "side"))
+        steps.append(("build_rbf", "pairwise", pw("build_rbf"), "main"))
+        if v_on_side:
+            steps.append(("wait", "main", "syrk"))
+        else:
+            steps.append(("syrk", "gemm", gemm("syrk"), "main"))
         steps += [
-            ("build_rbf", "pairwise", pw("build_rbf"), "main"),
-            ("syrk", "gemm", gemm("syrk"), "main"),
             ("chol", "chol", chol(FV, 4), "main"),
             ("inv3", "gemm", gemm("inv3"), "main"),
             ("proj3", "gemm", gemm("proj3"), "main"),
