@@ -107,7 +107,7 @@ _SIGS = {
                                           c_int, c_dbl, c_dbl, c_dbl, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "nmgp_gemm_big_offsets_epi_f32": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_int, c_vp, c_i64, c_i64, c_int, c_int,
                                               c_int, c_int, c_dbl, c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
-                                              c_i64, c_vp, c_vp, c_dbl, c_int, c_vp, c_vp]),
+                                              c_i64, c_vp, c_vp, c_dbl, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "nmgp_pairwise_f64": (c_int, [c_vp, c_int, c_int, c_vp]),
     "nmgp_pairwise_f32": (c_int, [c_vp, c_int, c_int, c_vp]),
     "nmgp_pairwise_single_f64": (c_int, [ctypes.POINTER(PairwiseDesc), c_vp]),

@@ -45,6 +45,10 @@ struct BigGemmArgs {
   const float* E; const int64_t* offE; int64_t sEi, sEj;
   const float* RS; const int64_t* offRS;
   float gamma;
+  // per-problem k range from the minibatch segment table (offsets variants): problem b runs
+  // k in [seg[kseg[b]], seg[kseg[b] + kspan[b]]) -- rows of the outputs it sums over
+  const int32_t* seg; const int32_t* kseg; const int32_t* kspan;
+  int koff;
   int ksplit;
   int streamk;              // 1: stream-K partition over a persistent grid (batch 1, uniform k)
   float* ws; int32_t* counters;
@@ -89,8 +93,8 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, float* big_sm
   const int wr = w >> 1, wc = w & 1;
   const int fl = g.flags;
   const bool aLo = fl & NMGP_A_LOWER, aUp = fl & NMGP_A_UPPER, bUp = fl & NMGP_B_UPPER, bLo = fl & NMGP_B_LOWER;
-  const float* Ab = g.A + (MODE ? g.offA[bat] : bat * g.sAb);
-  const float* Bb = g.B + (MODE ? g.offB[bat] : bat * g.sBb);
+  const float* Ab = g.A + (MODE ? g.offA[bat] : bat * g.sAb) + (AK ? (int64_t)g.koff : (int64_t)g.koff * g.lda);
+  const float* Bb = g.B + (MODE ? g.offB[bat] : bat * g.sBb) + (BK ? (int64_t)g.koff : (int64_t)g.koff * g.ldb);
   const __amdgpu_buffer_rsrc_t rA =
       AK ? make_rsrc(Ab, ((int64_t)(g.m - 1) * g.lda + g.k) * 4)
                   : make_rsrc(Ab, ((int64_t)(g.k - 1) * g.lda + g.m) * 4);
@@ -379,6 +383,14 @@ __global__ __launch_bounds__(256, 2) void gemm_big_kernel(BigGemmArgs g) {
   if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);
   const int64_t bat = blockIdx.y;
   f32x16 acc[2][2];
+  if constexpr (MODE != 0) {
+    if (g.kseg != nullptr) {
+      const int s0 = g.kseg[bat];
+      const int k0 = g.seg[s0], k1 = g.seg[s0 + g.kspan[bat]];
+      g.k = max(0, k1 - k0);
+      g.koff = k0;
+    }
+  }
 
   // One work segment per pass: a (tile, k-tile range).  Data-parallel / split-K grids run one
   // pass.  Stream-K (batch 1, every tile the same k range): workgroup w owns iterations
@@ -557,6 +569,7 @@ struct BigEpi {
   const float* E = nullptr; const int64_t* offE = nullptr; int64_t sEi = 0, sEj = 0;
   const float* RS = nullptr; const int64_t* offRS = nullptr;
   float gamma = 0.0f;
+  const int32_t* seg = nullptr; const int32_t* kseg = nullptr; const int32_t* kspan = nullptr;
 };
 
 static int gemm_big_f32_ex(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C,
@@ -573,6 +586,8 @@ static int gemm_big_f32_ex(const float* A, int64_t lda, const float* B, int64_t 
   g.a_kcontig = ep.a_kcontig;
   g.E = ep.E; g.offE = ep.offE; g.sEi = ep.sEi; g.sEj = ep.sEj;
   g.RS = ep.RS; g.offRS = ep.offRS; g.gamma = ep.gamma;
+  g.seg = ep.seg; g.kseg = ep.kseg; g.kspan = ep.kspan; g.koff = 0;
+  if (ep.kseg != nullptr && (offA == nullptr || ep.seg == nullptr || ep.kspan == nullptr)) return -1;
   if ((flags & NMGP_EPI) && (ep.E == nullptr || ep.RS == nullptr)) return -1;
   g.lda = lda; g.ldb = ldb; g.sCi = sCi; g.sCj = sCj;
   g.sAb = sAb; g.sBb = sBb; g.sCb = sCb;
@@ -689,7 +704,8 @@ int nmgp_gemm_big_offsets_epi_f32(const float* A, int64_t lda, int a_kcontig, co
                                   double alpha, double beta, double diag_add, const int64_t* offA,
                                   const int64_t* offB, const int64_t* offC, const float* E, const int64_t* offE,
                                   int64_t sEi, int64_t sEj, const float* RS, const int64_t* offRS, double gamma,
-                                  int batch, void* ws, hipStream_t s) {
+                                  const int32_t* seg, const int32_t* kseg, const int32_t* kspan, int batch,
+                                  void* ws, hipStream_t s) {
   if (A == nullptr) return -1;
   if (B == nullptr) return -4;
   if (C == nullptr) return -7;
@@ -702,11 +718,13 @@ int nmgp_gemm_big_offsets_epi_f32(const float* A, int64_t lda, int a_kcontig, co
   if (offC == nullptr) return -19;
   if ((flags & NMGP_EPI) && (E == nullptr || offE == nullptr)) return -20;
   if ((flags & NMGP_EPI) && (RS == nullptr || offRS == nullptr)) return -24;
-  if (batch < 0 || batch > 65535) return -27;
+  if (batch < 0 || batch > 65535) return -30;
   nmgp::BigEpi ep;
   ep.a_kcontig = a_kcontig ? 1 : 0;
   ep.E = E; ep.offE = offE; ep.sEi = sEi; ep.sEj = sEj;
   ep.RS = RS; ep.offRS = offRS; ep.gamma = (float)gamma;
+  if (kseg != nullptr && (seg == nullptr || kspan == nullptr)) return -26;
+  ep.seg = seg; ep.kseg = kseg; ep.kspan = kspan;
   return nmgp::gemm_big_f32_ex(A, lda, B, ldb, b_kcontig, C, sCi, sCj, m, n, k, flags, (float)alpha, (float)beta, 0, 0,
                                0, offA, offB, offC, (float)diag_add, batch, ws, s, ep);
 }

@@ -266,7 +266,21 @@ class DsviEngine:
                          offs=(typ * BM, j * BM, sU + (i * D + j) * MM), k_seg=i))
             d17.append(g(gr, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1), beta=1.0,
                          offs=(typ * BM, (D + j) * B, muU + (i * D + j) * M), k_seg=i))
-        p["bwd_lbar"] = G(d17)
+        if not (self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0"):
+            p["bwd_lbar"] = G(d17)
+        else:
+            # the D + Q L-bar products P^T W (k over each factor's row segment) on the 128x128 kernel,
+            # the M x 1 mu-bar products stay one grouped launch
+            bw_w = H.BigBatch(self.P, self.WG, gr, [3 * BM] * D, [d * BM for d in range(D)],
+                              [sW + d * MM for d in range(D)], M, M, B, lda=M, ldb=M, a_kcontig=False,
+                              b_kcontig=False, flags=L.OUT_TRIL, beta=1.0,
+                              kseg=(seg, list(range(D)), [D - d for d in range(D)]))
+            bw_u = H.BigBatch(self.P, self.WP, gr, [(2 if i == j else 1) * BM for (i, j) in pairs],
+                              [j * BM for (i, j) in pairs], [sU + (i * D + j) * MM for (i, j) in pairs], M, M, B,
+                              lda=M, ldb=M, a_kcontig=False, b_kcontig=False, flags=L.OUT_TRIL, beta=1.0,
+                              kseg=(seg, [i for (i, j) in pairs], [1] * len(pairs)))
+            mu = G([dd for dd in d17 if dd.n == 1])
+            p["bwd_lbar"] = H.Seq([bw_w, bw_u, mu])
         # B3: R_k = Pbar_k Ainv_k (G,0,1) ; Abar_k = Cinv^T diag(delta) Cinv ; KL L-bar
         d18 = [g(self.R, self.Pbar, self.Ainv, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), offs=(k * BM, k * MM, k * BM),
                  **rows_all) for k in (3, 1, 2)]

@@ -315,7 +315,7 @@ class BigBatch:
     (graph-capturable)."""
 
     def __init__(self, A, B, C, offA, offB, offC, m, n, k, *, lda, ldb, b_kcontig, a_kcontig=True, sC=None,
-                 flags=0, alpha=1.0, beta=0.0, diag_add=0.0, epi=None):
+                 flags=0, alpha=1.0, beta=0.0, diag_add=0.0, epi=None, kseg=None):
         for t_, nm in ((A, "A"), (B, "B"), (C, "C")):
             L.require_device(t_, nm)
             assert t_.dtype == torch.float32
@@ -332,6 +332,13 @@ class BigBatch:
             assert len(offE) == self.batch and len(offRS) == self.batch
             self.epi = (E, i64(offE), sEi, sEj, RS, i64(offRS), gamma)
             flags |= L.EPI
+        # kseg = (seg, [segment index per problem], [segment span per problem]): per-problem k range
+        self.kseg = None
+        if kseg is not None:
+            seg, ks, sp = kseg
+            assert seg.dtype == torch.int32 and len(ks) == self.batch and len(sp) == self.batch
+            i32 = lambda o: torch.tensor(list(o), dtype=torch.int32, device=dev)
+            self.kseg = (seg, i32(ks), i32(sp))
         self.args = (m, n, k, lda, a_kcontig, ldb, b_kcontig, sC if sC is not None else (n, 1), flags, alpha, beta,
                      diag_add)
 
@@ -346,12 +353,24 @@ class BigBatch:
             ep = (vp(E.data_ptr()), vp(oE.data_ptr()), sEi, sEj, vp(RS.data_ptr()), vp(oRS.data_ptr()), gamma)
         else:
             ep = (None, None, 0, 0, None, None, 0.0)
+        kp = tuple(vp(t_.data_ptr()) for t_ in self.kseg) if self.kseg is not None else (None, None, None)
         L.check(L.lib().nmgp_gemm_big_offsets_epi_f32(vp(self.A.data_ptr()), lda, 1 if ak else 0,
                                                       vp(self.B.data_ptr()), ldb, 1 if bk else 0,
                                                       vp(self.C.data_ptr()), sCi, sCj, m, n, k, flags, alpha, beta,
                                                       dadd, vp(self.off[0].data_ptr()), vp(self.off[1].data_ptr()),
-                                                      vp(self.off[2].data_ptr()), *ep, self.batch, None, s),
+                                                      vp(self.off[2].data_ptr()), *ep, *kp, self.batch, None, s),
                 "gemm_big_offsets_epi")
+
+
+class Seq:
+    """Launch callables one after another on the same stream (a composite schedule item)."""
+
+    def __init__(self, parts):
+        self.parts = list(parts)
+
+    def __call__(self, stream=None):
+        for p_ in self.parts:
+            p_(stream)
 
 
 def potrf_blocked_(A, info=None, ws=None):

@@ -186,13 +186,16 @@ int nmgp_gemm_big_offsets_f32(const float* A, int64_t lda, const float* B, int64
  * and with NMGP_EPI (+ NMGP_EPI_E_LOWER) the epilogue adds gamma * RS_b[i] * E_b(i, j), E_b = E + offE[b]
  * with strides (sEi, sEj), RS_b = RS + offRS[b]: the KL L-bar of every variational factor,
  * -C^-T (C^-1 L) + diag(1/C_ii^2) L (code/utils.py:339-351 and its autograd), for all D + Q + 1
- * factors in one launch.                                                                        */
+ * factors in one launch.  kseg != NULL: problem b sums k over [seg[kseg[b]], seg[kseg[b] + kspan[b]])
+ * of the device segment table (A and B advanced to that k), the rows of the outputs it covers -- the
+ * L-bar products P^T W of the quadratic forms (code/nmgp_dsvi.py:227-258 and their autograd).    */
 int nmgp_gemm_big_offsets_epi_f32(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb,
                                   int b_kcontig, float* C, int64_t sCi, int64_t sCj, int m, int n, int k, int flags,
                                   double alpha, double beta, double diag_add, const int64_t* offA,
                                   const int64_t* offB, const int64_t* offC, const float* E, const int64_t* offE,
                                   int64_t sEi, int64_t sEj, const float* RS, const int64_t* offRS, double gamma,
-                                  int batch, void* ws, hipStream_t stream);
+                                  const int32_t* seg, const int32_t* kseg, const int32_t* kspan, int batch,
+                                  void* ws, hipStream_t stream);
 
 /* ------------------------------------------------------------------ pairwise kernel builder
  * mode RBF:   K = scale2 * exp(-0.5 * ||x/ls - z/ls||^2)          (code/utils.py:91-94)

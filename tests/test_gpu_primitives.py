@@ -398,6 +398,32 @@ def test_gemm_big_offsets_batch(ops):
         assert rel(got, ref) < 2e-6 and torch.all(got[~lo] == 0)
 
 
+def test_gemm_big_kseg_batch(ops):
+    # per-problem k ranges from a device segment table (L-bar products P^T W over each factor's rows),
+    # transposed operands, OUT_TRIL + beta accumulate; an empty segment leaves C (lower) unchanged
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L
+    g = torch.Generator().manual_seed(31)
+    Bn, M, D = 700, 200, 4
+    P = torch.randn(Bn, M, generator=g).to(DEV)
+    W = torch.randn(3, Bn, M, generator=g).to(DEV)
+    seg = torch.tensor([0, 250, 250, 600, 700], dtype=torch.int32, device=DEV)   # segment 1 empty
+    probs = [(0, 1, 0), (1, 1, 1), (2, 2, 2), (3, 1, 0), (0, 4, 2)]            # (seg index, span, W slice)
+    C0 = torch.randn(len(probs), M, M, generator=g).to(DEV)
+    C = C0.clone()
+    op = ops.BigBatch(P, W, C, [0] * len(probs), [w * Bn * M for (_, _, w) in probs],
+                      [b * M * M for b in range(len(probs))], M, M, Bn, lda=M, ldb=M, a_kcontig=False,
+                      b_kcontig=False, flags=L.OUT_TRIL, beta=1.0,
+                      kseg=(seg, [s_ for (s_, _, _) in probs], [sp for (_, sp, _) in probs]))
+    op()
+    sc = seg.cpu().tolist()
+    lo = torch.tril(torch.ones(M, M, dtype=torch.bool))
+    for b, (s_, sp, w) in enumerate(probs):
+        k0, k1 = sc[s_], sc[s_ + sp]
+        ref = torch.tril(C0[b].cpu().double() + P[k0:k1].cpu().double().t() @ W[w, k0:k1].cpu().double())
+        got = C[b].cpu()
+        assert rel(got, ref) < 2e-6 and torch.all(got[~lo] == 0)
+
+
 def test_chol_inv_blocked_not_pd_reports_global_column(ops):
     A = _spd(400, 2, 9)
     bad = A.clone()
