@@ -74,10 +74,10 @@ def stress_cholesky(dev, reps=5):
         H.potrf_blocked_(W, info=info)
     torch.cuda.current_stream().wait_stream(s)
 
-    def graph_ms(body):
+    def graph_ms(body, n=reps):
         gr = torch.cuda.CUDAGraph()
         with torch.cuda.graph(gr):
-            for _ in range(reps):
+            for _ in range(n):
                 body()
         gr.replay()
         torch.cuda.synchronize()
@@ -86,7 +86,7 @@ def stress_cholesky(dev, reps=5):
         gr.replay()
         e1.record()
         torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / reps
+        return e0.elapsed_time(e1) / n
 
     def fac():
         W.copy_(A0)
@@ -103,7 +103,7 @@ def stress_cholesky(dev, reps=5):
     X = (torch.rand(Mst, Mst, generator=g, device=dev) * 2 - 1)
     C = torch.zeros(Mst, Mst, device=dev)
     ws = H.big_workspace(dev, L.lib().nmgp_gemm_big_workspace_size())
-    t_syrk = graph_ms(lambda: H.gemm_big(X, X, C, flags=L.OUT_LOWER, alpha=-1.0, beta=1.0, ws=ws))
+    t_syrk = graph_ms(lambda: H.gemm_big(X, X, C, flags=L.OUT_LOWER, alpha=-1.0, beta=1.0, ws=ws), n=20)
     syrk_tf = Mst * (Mst + 1.0) * Mst / (t_syrk * 1e-3) / 1e12
     del G, X, C
     # CPU: LAPACK spotrf through torch on the host cores, one call (about 0.1-1 s)
