@@ -143,6 +143,8 @@ _SIGS = {
     "nmgp_normal_f64": (c_int, [c_vp, c_i64, c_u64, c_vp, c_i64, c_vp]),
     "nmgp_normal_f32": (c_int, [c_vp, c_i64, c_u64, c_vp, c_i64, c_vp]),
     "nmgp_counter_add": (c_int, [c_vp, c_i64, c_vp]),
+    "nmgp_step_begin_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_u64, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "nmgp_step_begin_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_u64, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "nmgp_batch_gather_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_vp]),
     "nmgp_batch_gather_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,

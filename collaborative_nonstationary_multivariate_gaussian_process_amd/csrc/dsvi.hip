@@ -835,11 +835,9 @@ __device__ inline void philox_round(uint32_t (&c)[4], uint32_t (&k)[2]) {
   k[1] += 0xBB67AE85u;
 }
 
+// normals 4t .. 4t+3 of the Philox-4x32-10 stream (key = seed, counter = (t, base)), Box-Muller
 template <typename T>
-__global__ void normal_kernel(T* out, int64_t n, uint64_t seed, const int64_t* counter, int64_t offset) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t * 4 >= n) return;
-  const uint64_t base = (uint64_t)(counter ? counter[0] : 0) + (uint64_t)offset;
+__device__ inline void normal_quad(T* out, int64_t n, uint64_t seed, uint64_t base, int64_t t) {
   uint32_t c[4] = {(uint32_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)base, (uint32_t)(base >> 32)};
   uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
 #pragma unroll
@@ -854,6 +852,48 @@ __global__ void normal_kernel(T* out, int64_t n, uint64_t seed, const int64_t* c
 #pragma unroll
   for (int q = 0; q < 4; ++q)
     if (t * 4 + q < n) out[t * 4 + q] = (T)z[q];
+}
+
+template <typename T>
+__global__ void normal_kernel(T* out, int64_t n, uint64_t seed, const int64_t* counter, int64_t offset) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t * 4 >= n) return;
+  normal_quad<T>(out, n, seed, (uint64_t)(counter ? counter[0] : 0) + (uint64_t)offset, t);
+}
+
+// Start of a graph-replayed training step in ONE launch (was: minibatch gather, Philox noise, noise
+// counter advance, gradient zeroing -- four dependent launches): block 0 gathers the minibatch and
+// advances the batch counter; every block draws its share of the noise from the counter value it read
+// at entry and zeroes its share of the gradient; the last block to finish advances the noise counter
+// (so every block has read it) and re-arms the arrival word.  Same values as the separate kernels.
+template <typename T>
+__global__ __launch_bounds__(256) void step_begin_kernel(const T* Xb, const T* Yb, const int32_t* Ib,
+                                                         const int32_t* Sb, int64_t B, int64_t nseg, int64_t nbatch,
+                                                         int64_t* bctr, T* x, T* y, int32_t* ro, int32_t* seg,
+                                                         T* noise, int64_t nnoise, uint64_t seed, int64_t* nctr,
+                                                         int32_t* done, T* grad, int64_t ngrad) {
+  const uint64_t base = (uint64_t)nctr[0];
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t q = tid; q * 4 < nnoise; q += stride) normal_quad<T>(noise, nnoise, seed, base, q);
+  for (int64_t i = tid; i < ngrad; i += stride) grad[i] = (T)0;
+  if (blockIdx.x == 0) {
+    const int64_t b = bctr[0] % nbatch;
+    for (int64_t i = threadIdx.x; i < B; i += blockDim.x) {
+      x[i] = Xb[b * B + i];
+      y[i] = Yb[b * B + i];
+      ro[i] = Ib[b * B + i];
+    }
+    for (int64_t i = threadIdx.x; i < nseg; i += blockDim.x) seg[i] = Sb[b * nseg + i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (blockIdx.x == 0) bctr[0] += 1;
+    const int old = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (int)gridDim.x - 1) {
+      nctr[0] += 1;
+      __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 static inline unsigned blocks_rows(int B) { return (unsigned)((B + 3) / 4); }
@@ -992,6 +1032,27 @@ int nmgp_normal_f64(double* out, int64_t n, uint64_t seed, const int64_t* counte
 int nmgp_normal_f32(float* out, int64_t n, uint64_t seed, const int64_t* counter, int64_t offset, hipStream_t s) {
   return nmgp::normal_launch<float>(out, n, seed, counter, offset, s);
 }
+#define NMGP_STEP_BEGIN(T, sfx)                                                                                 \
+  int nmgp_step_begin_##sfx(const T* Xb, const T* Yb, const int32_t* Ib, const int32_t* Sb, int64_t B, int64_t nseg, \
+                            int64_t nbatch, int64_t* bctr, T* x, T* y, int32_t* ro, int32_t* seg, T* noise,          \
+                            int64_t nnoise, uint64_t seed, int64_t* nctr, int32_t* done, T* grad, int64_t ngrad,      \
+                            hipStream_t s) {                                                                         \
+    if (!Xb || !Yb || !Ib || !Sb) return -1;                                                                        \
+    if (B <= 0 || nseg <= 0 || nbatch <= 0) return -5;                                                              \
+    if (!bctr) return -8;                                                                                           \
+    if (!x || !y || !ro || !seg) return -9;                                                                         \
+    if (!noise || nnoise < 0 || !nctr || !done) return -13;                                                         \
+    if (!grad || ngrad < 0) return -18;                                                                             \
+    const int64_t work = std::max((nnoise + 3) / 4, ngrad);                                                         \
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 1024));            \
+    hipLaunchKernelGGL(nmgp::step_begin_kernel<T>, dim3(blocks), dim3(256), 0, s, Xb, Yb, Ib, Sb, B, nseg, nbatch,   \
+                       bctr, x, y, ro, seg, noise, nnoise, seed, nctr, done, grad, ngrad);                           \
+    NMGP_CHECK_LAUNCH();                                                                                            \
+    return NMGP_OK;                                                                                                 \
+  }
+NMGP_STEP_BEGIN(double, f64)
+NMGP_STEP_BEGIN(float, f32)
+#undef NMGP_STEP_BEGIN
 int nmgp_batch_gather_f64(const double* Xb, const double* Yb, const int32_t* Ib, const int32_t* Sb, int64_t B,
                           int64_t nseg, int64_t nbatch, int64_t* ctr, double* x, double* y, int32_t* ro, int32_t* seg,
                           hipStream_t s) {

@@ -411,6 +411,20 @@ class DsviEngine:
                                                                                         self.seg)), s),
                 "batch_gather")
 
+    def begin_step(self, seed, counter, stream=None):
+        """Gather + device noise + noise-counter advance + gradient zeroing in one launch
+        (nmgp_step_begin_*); the forward_backward that follows must not zero the gradient again."""
+        Xb, Yb, Ib, Sb, ctr = self._dataset
+        if getattr(self, "_begin_done", None) is None:
+            self._begin_done = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        s = L.stream_handle() if stream is None else stream
+        vp = ctypes.c_void_p
+        L.check(getattr(L.lib(), "nmgp_step_begin_" + self.sfx)(
+            *(vp(t.data_ptr()) for t in (Xb, Yb, Ib, Sb)), self.B, self.D + 1, Xb.shape[0], vp(ctr.data_ptr()),
+            *(vp(t.data_ptr()) for t in (self.x, self.y, self.row_out, self.seg)), vp(self.noise.data_ptr()),
+            self.noise.numel(), ctypes.c_uint64(seed), vp(counter.data_ptr()), vp(self._begin_done.data_ptr()),
+            vp(self._grad.data_ptr()), self._grad.numel(), s), "step_begin")
+
     def device_noise(self, seed, counter):
         H.normal_(self.noise, seed, counter=counter)   # dtype-dispatched Philox normals
 
@@ -580,13 +594,14 @@ class DsviEngine:
             else:
                 fn(s_side if where == "side" else s_main)
 
-    def forward_backward(self, stream=None, timer=None):
+    def forward_backward(self, stream=None, timer=None, zero_grad=True):
         """Enqueue -SELBO (self.out[0]) and all gradients (into the bound grad vector)."""
         key = ("fb", self._theta.data_ptr(), self._grad.data_ptr(), self.frozen_mask, self.N)
         if getattr(self, "_sched_key", None) != key:
             self._sched = self._schedule(0)
             self._sched_key = key
-        self._grad.zero_()
+        if zero_grad:
+            self._grad.zero_()
         self._run(self._sched, stream, timer)
         return self.out
 

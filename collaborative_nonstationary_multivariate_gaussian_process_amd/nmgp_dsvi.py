@@ -331,6 +331,11 @@ class DsviTrainer:
         """[Minibatch gather if a dataset is bound] + noise (device Philox unless host noise was
         loaded) + fused forward/backward."""
         mdl = self.model
+        if getattr(eng, "_dataset", None) is not None and noise is None and timer is None:
+            # one launch: gather + Philox noise + counter advance + gradient zeroing
+            eng.begin_step(mdl._noise_seed, mdl._noise_counter)
+            eng.forward_backward(zero_grad=False)
+            return eng.out[0]
         if getattr(eng, "_dataset", None) is not None:
             eng.gather_batch()
         if noise is None:

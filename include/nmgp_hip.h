@@ -333,6 +333,19 @@ int nmgp_counter_add(int64_t* counter, int64_t inc, hipStream_t stream);
  * b = (*batch_counter) % nbatch of pre-split, output-grouped batches (Xb/Yb (nbatch,B) f64, Ib
  * (nbatch,B) int32 row->output, Sb (nbatch,nseg) int32 segment table) into the engine's inputs
  * and then advances *batch_counter -- one launch, graph-capturable, no host work per step.      */
+/* Start of one training step in a single launch: the minibatch gather of nmgp_batch_gather_* (batch
+ * (*bctr) % nbatch, bctr advanced), nnoise Philox normals exactly as nmgp_normal_*(noise, nnoise, seed,
+ * nctr, 0) with *nctr advanced by one afterwards, and grad[0:ngrad] = 0 -- the DataLoader draw
+ * (code/nmgp_dsvi.py:829-837), optimizer.zero_grad() (:830) and the step's torch.randn draws
+ * (code/utils.py:123, 226, 234).  done: one int32, zero before first use (left zero).            */
+int nmgp_step_begin_f64(const double* Xb, const double* Yb, const int32_t* Ib, const int32_t* Sb, int64_t B,
+                        int64_t nseg, int64_t nbatch, int64_t* bctr, double* x, double* y, int32_t* row_out,
+                        int32_t* seg, double* noise, int64_t nnoise, uint64_t seed, int64_t* nctr, int32_t* done,
+                        double* grad, int64_t ngrad, hipStream_t stream);
+int nmgp_step_begin_f32(const float* Xb, const float* Yb, const int32_t* Ib, const int32_t* Sb, int64_t B,
+                        int64_t nseg, int64_t nbatch, int64_t* bctr, float* x, float* y, int32_t* row_out,
+                        int32_t* seg, float* noise, int64_t nnoise, uint64_t seed, int64_t* nctr, int32_t* done,
+                        float* grad, int64_t ngrad, hipStream_t stream);
 int nmgp_batch_gather_f64(const double* Xb, const double* Yb, const int32_t* Ib, const int32_t* Sb, int64_t B,
                           int64_t nseg, int64_t nbatch, int64_t* batch_counter, double* x, double* y,
                           int32_t* row_out, int32_t* seg, hipStream_t stream);

@@ -213,3 +213,40 @@ def test_fp32_big_side_products_match_grouped(monkeypatch):
     assert np.isfinite(res[0][0])
     assert res[0][0] == pytest.approx(res[1][0], rel=1e-4)
     assert _rel(res[0][1], res[1][1]) < 1e-3
+
+
+def test_step_begin_matches_separate_launches():
+    """nmgp_step_begin (one launch) == batch gather + Philox noise + noise-counter advance + grad
+    zeroing as separate launches: bit-identical minibatch, segment table, noise, counters."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.engine import DsviEngine
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import hip_ops as Hx
+    D, M, B, nb = 3, 24, 150, 3
+    eng = DsviEngine(D, M, B, np.linspace(0, 1, M))
+    theta = torch.zeros(eng.nparam, dtype=torch.float64, device="cuda")
+    grad = torch.full_like(theta, 7.0)
+    eng.bind(theta, grad)
+    g = torch.Generator().manual_seed(3)
+    Xb = torch.rand(nb, B, generator=g, dtype=torch.float64).cuda()
+    Yb = torch.randn(nb, B, generator=g, dtype=torch.float64).cuda()
+    Ib = torch.sort(torch.randint(0, D, (nb, B), generator=g), dim=1).values.to(torch.int32).cuda()
+    Sb = torch.stack([torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(torch.bincount(r, minlength=D), 0)])
+                      for r in Ib.cpu().long()]).to(torch.int32).cuda()
+    bctr = eng.bind_dataset(Xb, Yb, Ib, Sb)
+    nctr = torch.zeros(1, dtype=torch.int64, device="cuda")
+    outs = []
+    for fused in (False, True):
+        bctr.fill_(1)
+        nctr.fill_(5)
+        grad.fill_(7.0)
+        if fused:
+            eng.begin_step(1234, nctr)
+        else:
+            eng.gather_batch()
+            eng.device_noise(1234, nctr)
+            Hx.counter_add_(nctr, 1)
+            grad.zero_()
+        torch.cuda.synchronize()
+        outs.append([t.clone() for t in (eng.x, eng.y, eng.row_out, eng.seg, eng.noise, bctr, nctr, grad)])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert int(outs[1][5]) == 2 and int(outs[1][6]) == 6 and int(eng._begin_done.item()) == 0
