@@ -1044,7 +1044,7 @@ int nmgp_normal_f32(float* out, int64_t n, uint64_t seed, const int64_t* counter
     if (!noise || nnoise < 0 || !nctr || !done) return -13;                                                         \
     if (!grad || ngrad < 0) return -18;                                                                             \
     const int64_t work = std::max((nnoise + 3) / 4, ngrad);                                                         \
-    const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 1024));            \
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 256));             \
     hipLaunchKernelGGL(nmgp::step_begin_kernel<T>, dim3(blocks), dim3(256), 0, s, Xb, Yb, Ib, Sb, B, nseg, nbatch,   \
                        bctr, x, y, ro, seg, noise, nnoise, seed, nctr, done, grad, ngrad);                           \
     NMGP_CHECK_LAUNCH();                                                                                            \
