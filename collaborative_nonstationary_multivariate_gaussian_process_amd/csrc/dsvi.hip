@@ -875,7 +875,16 @@ __global__ __launch_bounds__(256) void step_begin_kernel(const T* Xb, const T* Y
   const uint64_t base = (uint64_t)nctr[0];
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t q = tid; q * 4 < nnoise; q += stride) normal_quad<T>(noise, nnoise, seed, base, q);
-  for (int64_t i = tid; i < ngrad; i += stride) grad[i] = (T)0;
+  if ((((uintptr_t)grad) & 15) == 0) {      // 16-byte stores
+    constexpr int V = 16 / (int)sizeof(T);
+    struct alignas(16) Z { T e[V]; };
+    const Z z{};
+    const int64_t nv = ngrad / V;
+    for (int64_t i = tid; i < nv; i += stride) ((Z*)grad)[i] = z;
+    for (int64_t i = nv * V + tid; i < ngrad; i += stride) grad[i] = (T)0;
+  } else {
+    for (int64_t i = tid; i < ngrad; i += stride) grad[i] = (T)0;
+  }
   if (blockIdx.x == 0) {
     const int64_t b = bctr[0] % nbatch;
     for (int64_t i = threadIdx.x; i < B; i += blockDim.x) {
