@@ -74,6 +74,7 @@ HYP_LOG = 1
 
 _SIGS = {
     "nmgp_version": (c_int, []),
+    "nmgp_device_status": (c_int, [ctypes.POINTER(ctypes.c_uint32), c_int]),
     "nmgp_sizeof_gemm_desc": (c_i64, []),
     "nmgp_sizeof_pairwise_desc": (c_i64, []),
     "nmgp_sizeof_pairwise_bwd_desc": (c_i64, []),
@@ -183,6 +184,26 @@ def exported_symbols():
 def check(rc, what):
     if rc != 0:
         raise HipError(f"{what} failed with status {rc}")
+
+
+STATUS_BITS = {1: "two-role Cholesky: the inverse workgroup gave up waiting for its factor workgroup",
+               2: "grouped GEMM: a cooperative split-K chunk gave up waiting for a peer",
+               4: "blocked potrf: a step workgroup gave up waiting for the panel publisher"}
+
+
+def device_status(clear=True):
+    """OR of the device status words (include/nmgp_hip.h NMGP_STATUS_*); synchronises the device."""
+    v = ctypes.c_uint32(0)
+    check(lib().nmgp_device_status(ctypes.byref(v), 1 if clear else 0), "device_status")
+    return int(v.value)
+
+
+def check_device_status():
+    """Raise if a bounded inter-workgroup spin gave up since the last check (results untrustworthy)."""
+    st = device_status(clear=True)
+    if st:
+        what = "; ".join(msg for bit, msg in STATUS_BITS.items() if st & bit)
+        raise HipError(f"device status 0x{st:x}: {what} -- the results since the last check are not valid")
 
 
 def stream_handle(device=None):

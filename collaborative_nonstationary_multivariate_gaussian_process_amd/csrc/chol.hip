@@ -745,11 +745,16 @@ __device__ __attribute__((always_inline)) inline void chol2_trtri_role(double* A
   for (int kb = 0; kb < nt; ++kb) {
     const int nrow = NR - kb * 16;
     if (t == 0) {
+      bool seen = false;
       for (int spin = 0; spin < (1 << 26); ++spin) {
         const unsigned long long f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (f >= kFlagTag + (unsigned long long)(kb + 1) && f <= kFlagTag + (unsigned long long)nt) break;
+        if (f >= kFlagTag + (unsigned long long)(kb + 1) && f <= kFlagTag + (unsigned long long)nt) {
+          seen = true;
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
       }
+      if (!seen) spin_gave_up(NMGP_STATUS_CHOL_SPIN);   // surfaced by nmgp_device_status()
     }
     CHOL_STAMP1(kb, 0);
     __syncthreads();
@@ -1244,6 +1249,8 @@ static int potrf_blocked_launch(T* A, int64_t n, int64_t lda, int32_t* info, voi
   if (ws == nullptr || ws_bytes < (int64_t)potrf_blocked_ws<T>(n)) return -5;
   return potrf_blocked<T>(A, (int)n, lda, info, ws, s);
 }
+
+NMGP_TU_STATUS_ACCESSOR(chol)
 
 }  // namespace nmgp
 

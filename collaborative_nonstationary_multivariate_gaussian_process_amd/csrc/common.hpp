@@ -161,6 +161,30 @@ template <> __device__ inline float keep_if<float>(float v, bool ok) {
   return __builtin_bit_cast(float, __builtin_bit_cast(unsigned int, v) & (ok ? ~0u : 0u));
 }
 
+// Device status word of this translation unit: a bounded inter-workgroup spin that gives up sets its
+// bit (NMGP_STATUS_* in nmgp_hip.h) instead of failing silently.  Each .hip file has its own copy
+// (internal linkage, no relocatable device code); nmgp_device_status() ORs and clears them all.
+static __device__ unsigned int g_nmgp_status;
+__device__ inline void spin_gave_up(unsigned int bit) {
+  __hip_atomic_fetch_or(&g_nmgp_status, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Host accessor of the TU's status word (read, then optionally clear).  Synchronous: called only at
+// the caller's existing sync points.
+#define NMGP_TU_STATUS_ACCESSOR(name)                                                        \
+  int nmgp_tu_status_##name(unsigned int* v, int clear) {                                  \
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(nmgp::g_nmgp_status), sizeof(unsigned int), 0,    \
+                            hipMemcpyDeviceToHost) != hipSuccess)                           \
+      return NMGP_ERR_LAUNCH;                                                               \
+    if (clear && *v) {                                                                      \
+      const unsigned int z = 0;                                                             \
+      if (hipMemcpyToSymbol(HIP_SYMBOL(nmgp::g_nmgp_status), &z, sizeof(unsigned int), 0,   \
+                            hipMemcpyHostToDevice) != hipSuccess)                           \
+        return NMGP_ERR_LAUNCH;                                                             \
+    }                                                                                       \
+    return NMGP_OK;                                                                         \
+  }
+
 template <typename T> __device__ inline T dexp(T x) { return exp(x); }
 template <> __device__ inline float dexp<float>(float x) { return expf(x); }
 template <typename T> __device__ inline T dlog(T x) { return log(x); }

@@ -992,10 +992,29 @@ static int batch_gather(const T* Xb, const T* Yb, const int32_t* Ib, const int32
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
+// status words of the kernel files with bounded inter-workgroup spins (common.hpp)
+int nmgp_tu_status_gemm(unsigned int* v, int clear);
+int nmgp_tu_status_gemm_big(unsigned int* v, int clear);
+int nmgp_tu_status_chol(unsigned int* v, int clear);
 }  // namespace nmgp
 
 extern "C" {
-#define NMGP_DSVI_ENTRY(name)                                                                     \
+int nmgp_device_status(uint32_t* out, int clear) {
+  if (!out) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return NMGP_ERR_LAUNCH;
+  unsigned int acc = 0;
+  int (*const parts[])(unsigned int*, int) = {nmgp::nmgp_tu_status_gemm, nmgp::nmgp_tu_status_gemm_big,
+                                              nmgp::nmgp_tu_status_chol};
+  for (auto fn : parts) {
+    unsigned int v = 0;
+    const int rc = fn(&v, clear);
+    if (rc != NMGP_OK) return rc;
+    acc |= v;
+  }
+  *out = acc;
+  return NMGP_OK;
+}
+#define NMGP_DSVI_ENTRY(name)                                                                  \
   int nmgp_dsvi_##name##_f64(const Args* a, hipStream_t s) { return nmgp::dsvi_##name<double>(a, s); } \
   int nmgp_dsvi_##name##_f32(const Args* a, hipStream_t s) { return nmgp::dsvi_##name<float>(a, s); }
 NMGP_DSVI_ENTRY(hyper)

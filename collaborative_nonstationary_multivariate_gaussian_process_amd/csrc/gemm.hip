@@ -542,10 +542,15 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, const nmgp_gemm_
       if (t == 0) {
         __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // bounded spin: a lost peer must not hang the GPU (the result is then wrong, not stuck)
+        bool seen = false;
         for (int spin = 0; spin < (1 << 24); ++spin) {
-          if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ksplit) break;
+          if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ksplit) {
+            seen = true;
+            break;
+          }
           __builtin_amdgcn_s_sleep(1);
         }
+        if (!seen) spin_gave_up(NMGP_STATUS_GEMM_SPIN);   // surfaced by nmgp_device_status()
       }
       __syncthreads();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the poll
@@ -793,6 +798,8 @@ static int launch_single(const nmgp_gemm_desc* h, const int32_t* d_seg, hipStrea
 template <typename T> int gemm_single(const nmgp_gemm_desc& d, hipStream_t s) { return launch_single<T>(&d, nullptr, s); }
 template int gemm_single<double>(const nmgp_gemm_desc&, hipStream_t);
 template int gemm_single<float>(const nmgp_gemm_desc&, hipStream_t);
+
+NMGP_TU_STATUS_ACCESSOR(gemm)
 
 }  // namespace nmgp
 

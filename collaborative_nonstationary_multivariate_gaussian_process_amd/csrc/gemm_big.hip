@@ -508,10 +508,15 @@ __global__ __launch_bounds__(256, 2) void potrf_step_kernel(PotrfStepArgs pa) {
   if (blockIdx.x == 0 && t == 0) __hip_atomic_store(pa.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (t == 0) {
     // bounded: a lost publisher must not hang the GPU (the result is then wrong, not stuck)
+    bool seen = false;
     for (int spin = 0; spin < (1 << 26); ++spin) {
-      if (__hip_atomic_load(pa.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+      if (__hip_atomic_load(pa.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+        seen = true;
+        break;
+      }
       __builtin_amdgcn_s_sleep(1);
     }
+    if (!seen) spin_gave_up(NMGP_STATUS_POTRF_SPIN);   // surfaced by nmgp_device_status()
   }
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -662,6 +667,8 @@ int gemm_big_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int b
   return gemm_big_f32_ex(A, lda, B, ldb, b_kcontig, C, sCi, sCj, m, n, k, flags, alpha, beta, sAb, sBb, sCb, nullptr,
                          nullptr, nullptr, 0.0f, batch, ws, s);
 }
+
+NMGP_TU_STATUS_ACCESSOR(gemm_big)
 
 }  // namespace nmgp
 

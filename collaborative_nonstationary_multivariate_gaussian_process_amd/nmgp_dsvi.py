@@ -20,6 +20,7 @@ import torch
 from torch.nn import Parameter
 from torch.utils.data import DataLoader, Dataset
 
+from . import _lib as Lb
 from . import distributed as DD
 from . import hip_ops as H
 from .engine import DsviEngine, HYPER_NAMES, PARAM_NAMES, param_layout
@@ -101,16 +102,9 @@ class NMGP(Model):
         super().__init__()
         if dtype not in (torch.float64, torch.float32):
             raise ValueError("dtype must be torch.float64 or torch.float32")
-        self.dtype_ = dtype
-        self.device_ = torch.device(device) if device is not None else _default_device()
+        D = dim_outputs
         Zt = torch.as_tensor(Z).detach().to(F64).reshape(-1, 1)
-        self.Z = Zt.to(self.device_)
-        self.M = int(Zt.shape[0])
-        self.N = number_observations
-        self.D = dim_outputs
-        self.batch_size = minibatch_size
-        self.noise = noise
-        D, M = self.D, self.M
+        M = int(Zt.shape[0])
         # reference initialisation order on the CPU generator (code/nmgp_dsvi.py:115-155)
         torch.random.manual_seed(seed)
         init = {}
@@ -120,25 +114,56 @@ class NMGP(Model):
         init["sqrt_v"] = 0.1 * torch.randn(M, M).to(F64) if sqrt_v is None else torch.from_numpy(np.asarray(sqrt_v)).to(F64)
         init["mu_U"] = 0.1 * torch.randn(D, D, M).to(F64) if mu_U is None else torch.from_numpy(np.asarray(mu_U)).to(F64)
         init["sqrt_U"] = 0.1 * torch.randn(D, D, M, M).to(F64) if sqrt_U is None else torch.from_numpy(np.asarray(sqrt_U)).to(F64)
-        self.sigma2_g = 1
         hyper0 = [0., -4., 0., -4., 0., -4., -2.]
         for k, v in zip(HYPER_NAMES, hyper0):
             init[k] = torch.tensor(v, dtype=F64)
+        self._setup(number_observations, D, Zt, minibatch_size, noise, dtype,
+                    torch.device(device) if device is not None else _default_device(), seed, init=init)
+
+    def _setup(self, N, D, Zt, batch_size, noise, dtype, device, seed, init=None, theta=None):
+        """Allocate the flat parameter vector on `device` and register the 13 parameters as views of it
+        (from per-parameter `init` tensors, or from an already flat host `theta`)."""
+        self.dtype_ = dtype
+        self.device_ = device
+        self.Z = Zt.to(self.device_)
+        self.M = int(Zt.shape[0])
+        self.N = N
+        self.D = D
+        self.batch_size = batch_size
+        self.noise = noise
+        self.sigma2_g = 1
+        M = self.M
         self._offs, n = param_layout(D, M)
-        self._theta = torch.zeros(n, dtype=dtype, device=self.device_)
+        if theta is not None:
+            assert theta.numel() == n
+            self._theta = theta.to(device=self.device_, dtype=dtype).contiguous()
+        else:
+            self._theta = torch.zeros(n, dtype=dtype, device=self.device_)
         self._grad = torch.zeros(n, dtype=dtype, device=self.device_)
         self._grad_views = []
         for k in PARAM_NAMES:
             o, shp = self._offs[k]
             cnt = int(np.prod(shp)) if shp else 1
             view = self._theta[o:o + cnt].view(shp)
-            view.copy_(init[k].reshape(shp))
+            if init is not None:
+                view.copy_(init[k].reshape(shp))
             setattr(self, k, Parameter(view))
             self._grad_views.append(self._grad[o:o + cnt].view(shp))
         self._engines = {}
         self._batch = None
         self._noise_seed = seed
         self._noise_counter = torch.zeros(1, dtype=torch.int64, device=self.device_)
+
+    def __reduce__(self):
+        """Picklable like the reference's NMGP objects (the drivers pickle whole models,
+        code/NMGP_PM25.py:101-106): the flat parameter vector travels through the host; engines
+        (device workspaces) are rebuilt on first use after loading."""
+        state = {"N": self.N, "D": self.D, "Z": self.Z.detach().cpu(), "batch_size": self.batch_size,
+                 "noise": self.noise, "dtype": str(self.dtype_).replace("torch.", ""),
+                 "device": str(self.device_), "seed": self._noise_seed,
+                 "noise_counter": int(self._noise_counter.cpu()[0]), "theta": self._theta.detach().cpu(),
+                 "requires_grad": {k: bool(getattr(self, k).requires_grad) for k in PARAM_NAMES}}
+        return (_rebuild_nmgp, (state,))
 
     # ------------------------------------------------------------------------------ plumbing
     def _frozen_mask(self):
@@ -155,6 +180,14 @@ class NMGP(Model):
             if p.data_ptr() != self._theta.data_ptr() + o * self._theta.element_size():
                 raise RuntimeError(f"parameter {k} no longer aliases the flat device vector "
                                    "(re-assigning .data is not supported; use .data.copy_)")
+
+    def check_numerics(self, engines=None):
+        """Synchronise and raise like the reference would: torch.linalg.LinAlgError when a Cholesky
+        factor was not positive-definite (the reference's torch.cholesky raises, code/utils.py:46,
+        347-348), HipError when a bounded inter-workgroup spin gave up."""
+        Lb.check_device_status()
+        for eng in (engines if engines is not None else self._engines.values()):
+            eng.check_info()
 
     def engine(self, B, N=None):
         eng = self._engines.get(B)
@@ -196,8 +229,8 @@ class NMGP(Model):
         eng.load_batch(x, y, sizes, noise=noise, index=index)
         self._batch = (eng, noise)
         loss = _DsviObjective.apply(self, *[getattr(self, k) for k in PARAM_NAMES])
+        self.check_numerics([eng])          # a non-PD factor raises here, as torch.cholesky would
         if verbose:
-            torch.cuda.synchronize()
             print("forward+backward (fused) costs {}s".format(time.time() - t1))
         return loss
 
@@ -234,6 +267,8 @@ class NMGP(Model):
             acc += out[1]
             if s == n_sample - 1:
                 kl = out[2] + out[3] + out[4]
+        if out is not None:
+            self.check_numerics([eng])
         if world == 1:
             return (acc / n_sample - out[2] - out[3] - out[4]).detach().clone()
         return DD.combine_elbo(acc, kl, n_sample, group=group, device=self.device_).detach().clone()
@@ -242,6 +277,23 @@ class NMGP(Model):
         """code/nmgp_dsvi.py:666-722: posterior-mean prediction (returns a tensor)."""
         from . import predict
         return predict.predict_mean(self, inputs_list, index)
+
+
+def _rebuild_nmgp(state):
+    """Unpickle an NMGP (see NMGP.__reduce__) onto its saved device, or the current one."""
+    dev = torch.device(state["device"])
+    if dev.type != "cuda":
+        dev = _default_device()
+    elif not torch.cuda.is_available():
+        raise RuntimeError("unpickling an NMGP needs a HIP device; there is no CPU fallback")
+    m = NMGP.__new__(NMGP)
+    torch.nn.Module.__init__(m)
+    m._setup(state["N"], state["D"], state["Z"], state["batch_size"], state["noise"],
+             getattr(torch, state["dtype"]), dev, state["seed"], theta=state["theta"])
+    for k, rg in state["requires_grad"].items():
+        getattr(m, k).requires_grad = rg
+    m._noise_counter.fill_(int(state["noise_counter"]))
+    return m
 
 
 # ==================================================================================== module-level API
@@ -309,23 +361,50 @@ class DsviTrainer:
         self.graphs = {}
 
     def load_optimizer_state(self, sd):
-        """Adopt a torch.optim.Adam state_dict (model.pt) for the flat vector."""
+        """Adopt a torch.optim.Adam state_dict (model.pt, code/nmgp_dsvi.py:792) for the flat vector,
+        as Optimizer.load_state_dict does: the checkpoint's lr / betas / eps replace the constructor's;
+        per-parameter exp_avg / exp_avg_sq are restored.  The flat-vector Adam keeps ONE step counter,
+        so states whose parameters were stepped a different number of times (or a mix of stepped and
+        never-stepped trainable parameters) are rejected rather than bias-corrected wrongly.  Frozen
+        parameters (requires_grad False) keep zero moments: torch skips them (grad None), and a
+        nonzero exp_avg would otherwise keep moving them."""
+        groups = sd.get("param_groups") or []
+        if groups:
+            g0 = groups[0]
+            self.lr = float(g0.get("lr", self.lr))
+            self.betas = tuple(float(b) for b in g0.get("betas", self.betas))
+            self.eps = float(g0.get("eps", self.eps))
         state = sd.get("state", {})
         if not state:
             return
         m = self.model
-        steps = []
+        # saved parameter ids in registration order: 0..12 (current torch) or the object ids an older
+        # torch wrote (code/notebook/model.pt); Optimizer.load_state_dict maps them by position
+        ids = list(groups[0]["params"]) if groups and "params" in groups[0] else list(range(len(PARAM_NAMES)))
+        if len(ids) != len(PARAM_NAMES):
+            raise ValueError(f"optimizer state lists {len(ids)} parameters, NMGP has {len(PARAM_NAMES)}")
+        steps, missing = set(), []
         for idx, name in enumerate(PARAM_NAMES):
-            st = state.get(idx)
-            if st is None:
-                continue
+            pid = ids[idx]
+            st = state.get(pid, state.get(str(pid)))
+            trainable = getattr(m, name).requires_grad
             o, shp = m._offs[name]
             n = int(np.prod(shp)) if shp else 1
-            self.m[o:o + n] = st["exp_avg"].reshape(-1).to(F64)
-            self.v[o:o + n] = st["exp_avg_sq"].reshape(-1).to(F64)
-            steps.append(int(st["step"]))
+            if st is None:
+                if trainable:
+                    missing.append(name)
+                continue
+            if not trainable:
+                continue
+            self.m[o:o + n] = st["exp_avg"].reshape(-1).to(self.m.dtype)
+            self.v[o:o + n] = st["exp_avg_sq"].reshape(-1).to(self.v.dtype)
+            steps.add(int(float(st["step"])))
+        if len(steps) > 1 or (steps and missing):
+            raise NotImplementedError(
+                f"optimizer state with per-parameter step counts {sorted(steps)} (never stepped: {missing}); "
+                "the flat-vector Adam keeps one shared step counter")
         if steps:
-            self.step_count.fill_(max(steps))
+            self.step_count.fill_(steps.pop())
 
     def grad_step(self, eng, noise=None, timer=None):
         """[Minibatch gather if a dataset is bound] + noise (device Philox unless host noise was
@@ -356,15 +435,27 @@ class DsviTrainer:
         return loss
 
     def capture(self, eng, include_update=True):
-        """Capture noise -> forward -> backward (-> Adam) of `eng` into one HIP graph."""
+        """Capture [gather +] noise -> forward -> backward (-> Adam) of `eng` into one HIP graph.
+
+        The warm-up runs (lazy attributes, descriptor uploads) happen outside the capture and
+        without the Adam update; the noise counter and the bound dataset's batch counter they
+        advance are restored afterwards, so capturing leaves parameters, optimizer state and the
+        random stream exactly as they were (the first replay is the first real step)."""
         mdl = self.model
         body = self.step if include_update else self.grad_step
+        cur = torch.cuda.current_stream(mdl.device_)
+        saved = [(mdl._noise_counter, mdl._noise_counter.clone())]
+        ds = getattr(eng, "_dataset", None)
+        if ds is not None:
+            saved.append((ds[4], ds[4].clone()))
         s = torch.cuda.Stream(device=mdl.device_)
-        s.wait_stream(torch.cuda.current_stream(mdl.device_))
+        s.wait_stream(cur)
         with torch.cuda.stream(s):
-            for _ in range(2):                       # warm-up (lazy attrs, plan upload) outside capture
-                body(eng)
-        torch.cuda.current_stream(mdl.device_).wait_stream(s)
+            for _ in range(2):
+                self.grad_step(eng)
+        cur.wait_stream(s)
+        for t, v in saved:
+            t.copy_(v)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             body(eng)
@@ -372,23 +463,146 @@ class DsviTrainer:
         return g
 
 
+class _IndexData(Dataset):
+    """Row indices 0..n-1.  A DataLoader over it with the same length, batch size, shuffle flag and
+    generator draws exactly the permutation the reference's DataLoader(trainData(X, Y, I)) draws
+    (code/nmgp_dsvi.py:816-817): the sampler only sees len(dataset).  __getitems__ hands the whole
+    index list to collate in one call instead of collating B scalar rows."""
+
+    def __init__(self, n):
+        self.n = int(n)
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        return i
+
+    def __getitems__(self, idx):
+        return idx
+
+
+def _index_batch(idx):
+    return torch.as_tensor(idx, dtype=torch.long)
+
+
+def _index_loader(n, batch_size, generator=None):
+    return DataLoader(_IndexData(n), batch_size=batch_size, shuffle=True, generator=generator,
+                      collate_fn=_index_batch)
+
+
+class _DevicePipeline:
+    """the training loop's input pipeline on the device (noise="device").
+
+    The training set stays in HBM.  Per epoch the host draws the DataLoader's index permutation
+    (same draws as the reference's loader); the minibatches are gathered, grouped by output in
+    vec2list order (a stable sort on the output id) and segment-tabled on the device, written into
+    the buffers bound to the engine (`DsviEngine.bind_dataset`), and each step then starts with ONE
+    `nmgp_step_begin` launch (gather + Philox noise + counter advance + gradient zeroing).  With a
+    graph the whole step is one replay; there is no host synchronisation per step -- losses stay on
+    the device and the per-step wall clock comes from HIP events.  A ragged last minibatch gets its
+    own engine (its own B) and buffers."""
+
+    def __init__(self, model, trainer, X, Y, I, batch_size, rank, world, use_graph, include_update):
+        self.model, self.trainer = model, trainer
+        dev = model.device_
+        self.dt = model.dtype_
+        self.D = model.D
+        self.X = X.to(dev, self.dt)
+        self.Y = Y.to(dev, self.dt)
+        self.I = I.to(dev).long()
+        self.bs, self.rank, self.world = batch_size, rank, world
+        self.use_graph, self.include_update = use_graph, include_update
+        self.slots = {}           # B -> dict(eng, bufs, counter, graph)
+        self.ar = torch.arange(self.D + 1, device=dev)
+
+    def _slot(self, B, nb):
+        sl = self.slots.get(B)
+        if sl is not None and sl["nb"] == nb:
+            return sl
+        dev = self.model.device_
+        eng = self.model.engine(B)
+        bufs = (torch.empty(nb, B, dtype=self.dt, device=dev), torch.empty(nb, B, dtype=self.dt, device=dev),
+                torch.empty(nb, B, dtype=torch.int32, device=dev), torch.empty(nb, self.D + 1, dtype=torch.int32,
+                                                                                device=dev))
+        ctr = eng.bind_dataset(*bufs)
+        sl = {"eng": eng, "bufs": bufs, "ctr": ctr, "graph": None, "nb": nb}
+        self.slots[B] = sl
+        return sl
+
+    def _fill(self, sl, idx):
+        """idx (nb, B) row indices on the device -> output-grouped batches in the bound buffers."""
+        Ib = self.I[idx]
+        order = torch.sort(Ib, dim=1, stable=True).indices
+        idx = idx.gather(1, order)
+        Ib = Ib.gather(1, order)
+        Xb, Yb, Ibuf, Sb = sl["bufs"]
+        Xb.copy_(self.X[idx])
+        Yb.copy_(self.Y[idx])
+        Ibuf.copy_(Ib)
+        Sb.copy_(torch.searchsorted(Ib, self.ar.expand(Ib.shape[0], -1).contiguous()))
+        sl["ctr"].zero_()
+
+    def epoch(self, index_batches):
+        """Upload one epoch; returns the ordered list of (slot) to step, one entry per minibatch."""
+        dev = self.model.device_
+        rows = []
+        for b in index_batches:
+            if self.world > 1:
+                if b.numel() < self.world:       # every rank skips the same short global batch
+                    continue
+                b = b[DD.rank_slice(b.numel(), self.rank, self.world)]
+            rows.append(b)
+        plan, groups = [], {}
+        for b in rows:
+            groups.setdefault(b.numel(), []).append(b)
+        for B, bl in groups.items():
+            sl = self._slot(B, len(bl))
+            self._fill(sl, torch.stack(bl).to(dev, non_blocking=True))
+        for b in rows:
+            plan.append(self.slots[b.numel()])
+        return plan
+
+    def step(self, sl):
+        tr = self.trainer
+        if self.use_graph:
+            if sl["graph"] is None:
+                sl["graph"] = tr.capture(sl["eng"], include_update=self.include_update)
+            sl["graph"].replay()
+        elif self.include_update:
+            tr.step(sl["eng"])
+        else:
+            tr.grad_step(sl["eng"])
+        return sl["eng"]
+
+
 def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=None, fix_hyperpars=True,
               mu_v=None, mu_W=None, mu_U=None, sqrt_v=None, sqrt_W=None, sqrt_U=None, lr=0.01, itnum=1000,
               do_stop_criterion=False, seed=22, verbose=False, PATH="model.pt", continuous_training=False,
               show_ELBO=True, save_model=False, X_test_list=None, Y_test_list=None, device=None, noise="torch",
-              use_graph=False, n_elbo_sample=1000, distributed=False, group=None, dtype=F64):
+              use_graph=None, n_elbo_sample=1000, distributed=False, group=None, dtype=F64, check_every=64):
     """code/nmgp_dsvi.py:758-909 on the MI355X.
 
     Returns (model, loss_list, time_list), or (model, loss_list, rmse_test_list, time_list) when
     X_test_list is given -- as the reference.  Extra keyword-only knobs (defaults keep reference
-    behaviour): device, noise ("torch" = reference RNG stream | "device"), use_graph (replay the
-    step as a HIP graph; needs noise="device"), n_elbo_sample (compute_ELBO samples),
-    distributed (data-parallel over the ranks of `group`: every rank draws the same global
-    minibatch of batch_size * world rows -- the seeded DataLoader permutation -- trains on its
-    contiguous slice, and the gradients are averaged with one all-reduce before the replicated
-    Adam step; the reported loss is the rank mean; compute_ELBO shards its samples).
+    behaviour): device, noise ("torch" = the reference RNG stream, replayable sample for sample |
+    "device" = on-device Philox and the on-device input pipeline of SURVEY f4), use_graph (replay
+    each step as one HIP graph; default: on for noise="device", impossible for "torch"),
+    n_elbo_sample (compute_ELBO samples), distributed (data-parallel over the ranks of `group`:
+    every rank draws the same global minibatch of batch_size * world rows from an identically
+    seeded DataLoader generator, trains on its contiguous slice, and the gradients are averaged
+    with one all-reduce before the replicated Adam step; global batches with fewer rows than
+    ranks are skipped on every rank; the reported loss is the rank mean; compute_ELBO shards its
+    samples), check_every (noise="device": steps between the host checks of the Cholesky info /
+    device status -- the only synchronisations of the loop besides verbose / test / ELBO output).
+    A non-positive-definite factor raises torch.linalg.LinAlgError, as the reference's
+    torch.cholesky does.
     """
     rank, world = DD.world_info(group) if distributed else (0, 1)
+    if use_graph is None:
+        use_graph = noise == "device"
+    if use_graph and noise != "device":
+        raise ValueError("use_graph=True needs noise='device' (host RNG cannot be replayed)")
     X_train_vec = np.concatenate(X_train_list)
     Y_train_vec = np.concatenate(Y_train_list)
     train_index = np.concatenate([np.ones_like(Y_train_list[i]) * i for i in range(dim_outputs)]).astype(int)
@@ -403,54 +617,97 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
     _apply_hyperpars(model, hyperpars, fix_hyperpars, continuous_training, PATH, opt_state)
     trainer = DsviTrainer(model, lr)
     trainer.load_optimizer_state(opt_state)
-    train_loader = DataLoader(trainData(X, Y, I), batch_size=batch_size * world, shuffle=True)
-    loss_list, time_list = [], []
+    # data parallel: the loader's permutation must be identical on every rank and independent of
+    # the per-rank torch.randn draws (noise="torch" draws B_r-sized vectors from the global stream)
+    gen = None
+    if world > 1:
+        gen = torch.Generator()
+        gen.manual_seed(int(seed) + 0x5eed)
+    N_train = X_train_vec.shape[0]
     if X_test_list is not None:
         rmse_test_list = []
         Y_test_vec = np.concatenate(Y_test_list)
-    if use_graph and noise != "device":
-        raise ValueError("use_graph=True needs noise='device' (host RNG cannot be replayed)")
     Q = dim_outputs * (dim_outputs + 1) // 2
-    ts = time.time()
-    epoch = 0
+    pipe = None
+    if noise == "device":
+        pipe = _DevicePipeline(model, trainer, X.reshape(-1), Y.reshape(-1), I.reshape(-1), batch_size, rank, world,
+                               use_graph, include_update=(world == 1))
+        loader = _index_loader(N_train, batch_size * world, gen)
+    else:
+        loader = DataLoader(trainData(X, Y, I), batch_size=batch_size * world, shuffle=True, generator=gen)
+    loss_list, time_list = [], []
     losses_dev = []
+    events = []
+    ts = time.time()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    epoch = 0
+    nstep = 0
+
+    def _sync_check():
+        torch.cuda.synchronize(model.device_)
+        model.check_numerics()
+
     for epoch in range(itnum):
         batch = 0
-        for X_batch, Y_batch, I_batch in train_loader:
-            batch += 1
-            if world > 1:                               # this rank's slice of the global minibatch
-                sl = DD.rank_slice(X_batch.shape[0], rank, world)
-                X_batch, Y_batch, I_batch = X_batch[sl], Y_batch[sl], I_batch[sl]
-            X_bl, Y_bl = vec2list(X_batch, Y_batch, I_batch, dim=dim_outputs)
-            model._assert_views()
-            x, y, sizes = model._prepare(X_bl, Y_bl)
-            B = sum(sizes)
-            eng = model.engine(B)
-            nz = model._torch_noise(B, Q) if noise == "torch" else None
-            eng.load_batch(x, y, sizes, noise=nz)
-            if use_graph:
-                g = trainer.graphs.get(id(eng)) or trainer.capture(eng, include_update=(world == 1))
-                g.replay()
-                loss = eng.out[0]
-            elif world == 1:
-                loss = trainer.step(eng, noise=nz)
-            else:
-                loss = trainer.grad_step(eng, noise=nz)
-            if world > 1:
-                DD.allreduce_mean_(model._grad, group)
-                trainer.update()
-                loss = DD.allreduce_mean_(loss.clone().reshape(1), group)[0]
-            losses_dev.append(loss.clone())
-            torch.cuda.synchronize(model.device_)
-            time_list.append(time.time() - ts)
-            if X_test_list is not None:
-                est = predict_Y(model, X_test_list)
-                rmse_test_list.append(np.sqrt(np.mean((est[:, None] - Y_test_vec) ** 2)))
-            if verbose:
-                print("epoch: {}/{}, batch: {}/{}, loss: {}".format(epoch, itnum, batch,
-                                                                   X_train_vec.shape[0] / batch_size, float(loss)))
+        if pipe is not None:
+            for sl in pipe.epoch(list(loader)):
+                batch += 1
+                eng = pipe.step(sl)
+                if world > 1:
+                    DD.allreduce_mean_(model._grad, group)
+                    trainer.update()
+                losses_dev.append(eng.out[0].clone())
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                events.append(ev)
+                nstep += 1
+                if check_every and nstep % check_every == 0:
+                    _sync_check()
+                if X_test_list is not None:
+                    est = predict_Y(model, X_test_list)
+                    rmse_test_list.append(np.sqrt(np.mean((est[:, None] - Y_test_vec) ** 2)))
+                if verbose:
+                    print("epoch: {}/{}, batch: {}/{}, loss: {}".format(epoch, itnum, batch, N_train / batch_size,
+                                                                       float(losses_dev[-1])))
+        else:
+            for X_batch, Y_batch, I_batch in loader:
+                if world > 1:                               # this rank's slice of the global minibatch
+                    if X_batch.shape[0] < world:            # every rank skips the same short global batch
+                        continue
+                    sl = DD.rank_slice(X_batch.shape[0], rank, world)
+                    X_batch, Y_batch, I_batch = X_batch[sl], Y_batch[sl], I_batch[sl]
+                batch += 1
+                X_bl, Y_bl = vec2list(X_batch, Y_batch, I_batch, dim=dim_outputs)
+                model._assert_views()
+                x, y, sizes = model._prepare(X_bl, Y_bl)
+                B = sum(sizes)
+                eng = model.engine(B)
+                nz = model._torch_noise(B, Q)
+                eng.load_batch(x, y, sizes, noise=nz)
+                if world == 1:
+                    loss = trainer.step(eng, noise=nz)
+                else:
+                    loss = trainer.grad_step(eng, noise=nz)
+                    DD.allreduce_mean_(model._grad, group)
+                    trainer.update()
+                losses_dev.append(loss.clone())
+                torch.cuda.synchronize(model.device_)
+                eng.check_info()
+                time_list.append(time.time() - ts)
+                nstep += 1
+                if X_test_list is not None:
+                    est = predict_Y(model, X_test_list)
+                    rmse_test_list.append(np.sqrt(np.mean((est[:, None] - Y_test_vec) ** 2)))
+                if verbose:
+                    print("epoch: {}/{}, batch: {}/{}, loss: {}".format(epoch, itnum, batch, N_train / batch_size,
+                                                                       float(loss)))
         if do_stop_criterion and epoch % 5 == 4 and epoch > 5:
-            la = np.array([float(v) for v in losses_dev])
+            # (data parallel: decided on the rank-mean losses, so every rank stops at the same epoch)
+            recent = torch.stack([l.reshape(()) for l in losses_dev[-batch * 6:]]).to(torch.float64)
+            if world > 1:
+                DD.allreduce_mean_(recent, group)
+            la = recent.cpu().numpy()
             if la[-batch:].sum() > la[-batch * 6:-batch * 5].sum():
                 print("Stop criteria is satisfied.")
                 break
@@ -458,12 +715,19 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
             elbo = model.compute_ELBO(X_list, Y_list, n_sample=n_elbo_sample, distributed=distributed, group=group)
             print("epoch: {}, ELBO: {}".format(epoch + 1, float(elbo)))
             print(print_mem(epoch + 1))
+    _sync_check()
+    if events:
+        time_list = [ev0.elapsed_time(e) / 1e3 for e in events]     # device completion of each step
     print("training takes {}s".format(time.time() - ts))
-    loss_list = [np.array(float(v)) for v in losses_dev]
+    if losses_dev:
+        lv = torch.stack([l.reshape(()) for l in losses_dev]).to(torch.float64)
+        if world > 1:
+            DD.allreduce_mean_(lv, group)        # the rank mean of every step's loss, one collective
+        loss_list = [np.array(v) for v in lv.cpu().numpy()]
     if save_model:
         torch.save({"epoch": epoch, "model_state_dict": {k: v.detach().cpu() for k, v in model.state_dict().items()},
-                    "optimizer_state_dict": _adam_state_dict(model, trainer, lr),
-                    "loss": torch.tensor(float(losses_dev[-1]) if losses_dev else float("nan"))}, PATH)
+                    "optimizer_state_dict": _adam_state_dict(model, trainer),
+                    "loss": torch.tensor(float(loss_list[-1]) if loss_list else float("nan"))}, PATH)
     if show_ELBO:
         elbo = model.compute_ELBO(X_list, Y_list, n_sample=n_elbo_sample, distributed=distributed, group=group)
         print("epoch: {}, ELBO: {}".format(epoch + 1, float(elbo)))
@@ -473,7 +737,8 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
     return model, loss_list, time_list
 
 
-def _adam_state_dict(model, trainer, lr):
+def _adam_state_dict(model, trainer):
+    """torch.optim.Adam.state_dict() layout for the flat-vector optimizer (code/nmgp_dsvi.py:897)."""
     state = {}
     step = float(trainer.step_count.cpu())
     for idx, name in enumerate(PARAM_NAMES):
@@ -483,7 +748,8 @@ def _adam_state_dict(model, trainer, lr):
         n = int(np.prod(shp)) if shp else 1
         state[idx] = {"step": torch.tensor(step), "exp_avg": trainer.m[o:o + n].reshape(shp).cpu(),
                       "exp_avg_sq": trainer.v[o:o + n].reshape(shp).cpu()}
-    return {"state": state, "param_groups": [{"lr": lr, "betas": (0.9, 0.999), "eps": 1e-8, "weight_decay": 0,
+    return {"state": state, "param_groups": [{"lr": trainer.lr, "betas": tuple(trainer.betas), "eps": trainer.eps,
+                                              "weight_decay": 0,
                                               "amsgrad": False, "params": list(range(len(PARAM_NAMES)))}]}
 
 

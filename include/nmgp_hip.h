@@ -28,6 +28,17 @@ extern "C" {
 
 /* ------------------------------------------------------------------ library info */
 int nmgp_version(void);
+
+/* Device status word.  Kernels that hand data between workgroups of one launch wait on peers with
+ * BOUNDED spins (a lost peer must not hang the GPU); a spin that gives up sets one of these bits
+ * instead of failing silently.  nmgp_device_status() ORs the words of every kernel file into *out
+ * (host memory) and clears them when `clear` != 0.  It synchronises with the device: call it at a
+ * point where the caller syncs anyway (the Python layer does so with the Cholesky `info` check).
+ * Any nonzero bit means the results of the launches since the last check are not trustworthy.     */
+#define NMGP_STATUS_CHOL_SPIN  1u   /* two-role Cholesky: the inverse role lost its factor role    */
+#define NMGP_STATUS_GEMM_SPIN  2u   /* grouped GEMM: a cooperative split-K chunk lost a peer       */
+#define NMGP_STATUS_POTRF_SPIN 4u   /* blocked potrf step: the panel publisher never arrived       */
+int nmgp_device_status(uint32_t* out, int clear);
 /* sizeof of the descriptor structs below (host code checks its own layout against these) */
 int64_t nmgp_sizeof_gemm_desc(void);
 int64_t nmgp_sizeof_pairwise_desc(void);

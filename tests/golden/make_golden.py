@@ -271,6 +271,24 @@ def case_modelpt():
     save("modelpt_forward", {**pack_inputs({"N": 200, "seed": 123}, X_list, Y_list, z, params, noise), **out})
 
 
+def case_modelpt_file():
+    """The shipped checkpoint code/notebook/model.pt, loaded weights-only and re-saved as plain tensors
+    (same dict layout: epoch, model_state_dict, optimizer_state_dict with the old torch's object-id
+    keys, loss) so the GPU box -- where the reference tree does not exist -- can load it through
+    NMGP.load_state_dict / the optimizer-state path."""
+    ck = torch.load(os.path.join(REF, "code", "notebook", "model.pt"), weights_only=True, map_location="cpu")
+    out = {"epoch": int(ck["epoch"]), "loss": ck["loss"].detach().clone(),
+           "model_state_dict": {k: v.detach().clone() for k, v in ck["model_state_dict"].items()},
+           "optimizer_state_dict": {
+               "state": {int(k): {"step": torch.tensor(float(v["step"])), "exp_avg": v["exp_avg"].detach().clone(),
+                                  "exp_avg_sq": v["exp_avg_sq"].detach().clone()}
+                         for k, v in ck["optimizer_state_dict"]["state"].items()},
+               "param_groups": [dict(g) for g in ck["optimizer_state_dict"]["param_groups"]]}}
+    path = os.path.join(OUT, "model_pt.pt")
+    torch.save(out, path)
+    print(f"wrote {path}  ({os.path.getsize(path) / 1024:.1f} KiB)")
+
+
 def synth_case(D, M, sizes, seed, mu_v0, hyper):
     rng = np.random.default_rng(seed)
     X_list = [np.sort(rng.uniform(0, 1, n))[:, None] for n in sizes]
@@ -316,6 +334,60 @@ def case_pm25():
     keep = {k: v for k, v in params.items() if k not in ("sqrt_W", "sqrt_U", "sqrt_v")}
     d = pack_inputs({"N": 10000}, X_list, Y_list, z, keep, noise)
     save("pm25_forward", {**d, **small})
+
+
+def _grad_digest(out):
+    """Per-parameter gradient norms + a strided sample of every gradient (big fixtures)."""
+    small = {"loss": out["loss"]}
+    for k in PARAM_NAMES:
+        g = out["grad_" + k]
+        small["gnorm_" + k] = np.linalg.norm(g.reshape(-1))
+        small["gsample_" + k] = g.reshape(-1)[:: max(1, g.size // 997)]
+    return small
+
+
+def case_hcp_like():
+    """HCP-shaped at a size the reference finishes on the CPU: D=8 outputs,
+    M=512 inducing points, B=5000 rows (625 per output), N=50000, length scales 3/M of the input
+    range (cond(K22 + 1e-4 I) moderate), NMGP(seed=22) initialisation.  The fp32 engine
+    is gated against this fp64 reference at SURVEY §8c's fp32 tolerances."""
+    D, M, sizes = 8, 512, [625] * 8
+    rng = np.random.default_rng(21)
+    X_list = [np.sort(rng.uniform(0, 1, n))[:, None] for n in sizes]
+    Y_list = [(np.sin(6 * x + 0.5 * d) + 0.3 * rng.standard_normal(x.shape)) for d, x in enumerate(X_list)]
+    z = np.linspace(0, 1, M)
+    m = build_model(50000, D, z, seed=22)
+    ls = float(np.log(3.0 / M))
+    for k in ["length_scales_tildeell_log", "length_scales_L0_log", "length_scales_L1_log"]:
+        getattr(m, k).data.fill_(ls)
+    params = model_params(m)
+    noise = forward_noise(rng, D, M, sum(sizes))
+    out = run_forward(m, X_list, Y_list, noise, full=False)
+    keep = {k: v for k, v in params.items() if k not in ("sqrt_W", "sqrt_U", "sqrt_v")}
+    d = pack_inputs({"N": 50000}, X_list, Y_list, z, keep, noise)
+    save("hcp_like_forward", {**d, **_grad_digest(out)})
+
+
+def case_driver_hyper():
+    """The reference drivers' own hyper-parameters (code/NMGP_PM25.py:63-64): length-scale logs 10
+    and mu_v = 1 on an hour-indexed axis (z = linspace(0, t_max, M), t_max = 5000 h), where the RBF
+    priors are nearly rank one and only the 1e-4 jitter keeps K22 positive-definite."""
+    D, M, sizes = 3, 64, [190, 210, 200]
+    rng = np.random.default_rng(31)
+    t_max = 5000.0
+    X_list = [np.sort(rng.uniform(0, t_max, n))[:, None] for n in sizes]
+    Y_list = [(np.sin(x / 700.0 + d) + 0.3 * rng.standard_normal(x.shape)) for d, x in enumerate(X_list)]
+    z = np.linspace(0, t_max, M)
+    m = build_model(6000, D, z, params={"mu_v": np.ones(M), "mu_W": None, "mu_U": None, "sqrt_v": None,
+                                        "sqrt_W": None, "sqrt_U": None, **{k: 0.0 for k in PARAM_NAMES[6:]}},
+                    seed=22)
+    for k, v in {"length_scales_L0_log": 10., "length_scales_L1_log": 10., "length_scales_tildeell_log": 10.,
+                 "sigma2_tildeell_log": 0., "sigma2_L0_log": 0., "sigma2_L1_log": 0., "sigma2_err_log": -2.}.items():
+        getattr(m, k).data.fill_(v)
+    params = model_params(m)
+    noise = forward_noise(rng, D, M, sum(sizes))
+    out = run_forward(m, X_list, Y_list, noise, full=False)
+    save("driver_hyper_forward", {**pack_inputs({"N": 6000}, X_list, Y_list, z, params, noise), **out})
 
 
 def case_elbo():
@@ -538,3 +610,6 @@ if __name__ == "__main__":
     case_legacy()
     case_inference()
     case_sample()
+    case_modelpt_file()
+    case_hcp_like()
+    case_driver_hyper()

@@ -170,27 +170,31 @@ def test_legacy_kernels_and_kronecker_vs_golden():
 
 
 def test_device_noise_graph_step_is_finite_and_matches_eager():
-    """The HIP-graph replay of a full step equals the eager step (same Philox stream)."""
+    """The HIP-graph replay of a full step equals the eager step (same Philox stream), and capturing
+    the graph has no side effects: k replays after the capture == k eager steps."""
     from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP, DsviTrainer
     g = G.load("mid_forward")
     xs, ys = G.split_lists(g)
-    res = []
-    for use_graph in (False, True):
-        m = _model_from(g, 3, 64, 4096, noise="device")
-        tr = DsviTrainer(m, lr=0.01)
-        eng = m.engine(sum(len(x) for x in xs))
-        eng.load_batch(g["x"], g["y"], [len(x) for x in xs])
-        if use_graph:
-            gr = tr.capture(eng)              # 2 warm-up steps + capture
-            gr.replay()
-        else:
-            for _ in range(3):
-                tr.step(eng)
-        torch.cuda.synchronize()
-        res.append((float(eng.out[0]), m._theta.clone()))
-    assert np.isfinite(res[0][0])
-    assert res[0][0] == pytest.approx(res[1][0], rel=1e-12)
-    assert _rel(res[1][1], res[0][1]) < 1e-12
+    for k in (1, 3):
+        res = []
+        for use_graph in (False, True):
+            m = _model_from(g, 3, 64, 4096, noise="device")
+            tr = DsviTrainer(m, lr=0.01)
+            eng = m.engine(sum(len(x) for x in xs))
+            eng.load_batch(g["x"], g["y"], [len(x) for x in xs])
+            if use_graph:
+                gr = tr.capture(eng)              # warm-up + capture: no parameter / RNG change
+                for _ in range(k):
+                    gr.replay()
+            else:
+                for _ in range(k):
+                    tr.step(eng)
+            torch.cuda.synchronize()
+            res.append((float(eng.out[0]), m._theta.clone(), int(tr.step_count.item()), int(m._noise_counter.item())))
+        assert np.isfinite(res[0][0])
+        assert res[0][0] == pytest.approx(res[1][0], rel=1e-12)
+        assert _rel(res[1][1], res[0][1]) < 1e-12
+        assert res[0][2] == res[1][2] == k and res[0][3] == res[1][3] == k
 
 
 def test_sample_Y_and_sample_FY_replay_reference_noise():

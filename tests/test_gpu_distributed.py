@@ -92,3 +92,48 @@ def test_data_parallel_inference_keeps_ranks_in_sync():
     assert np.array_equal(t0, t1)
     assert l0 == l1 and len(l0) == 2            # 200 rows / (50 x 2 ranks) = 2 global steps
     assert all(np.isfinite(l0))
+
+
+def _dp_train_ragged(rank):
+    """N % (batch * world) != 0 with the reference RNG (noise='torch'), several epochs: the ragged last
+    global batch splits unevenly, one global batch is shorter than the world and must be skipped on
+    every rank, and the per-rank torch.randn draws must not desynchronise the loader."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import inference
+    from tests import _golden as G
+    g = G.load("toy_elbo")
+    xs, ys = G.split_lists(g)
+    xs = [xs[0], xs[1][:-29]]                      # 171 rows: global batches of 2 x 50 -> 100, 71 (36 / 35)
+    ys = [ys[0], ys[1][:-29]]
+    torch.manual_seed(100 + rank)                  # different global streams per rank on purpose
+    model, losses, _ = inference(xs, ys, g["z"], 50, 2, hyperpars={}, fix_hyperpars=True, lr=0.005, itnum=3,
+                                 show_ELBO=False, device="cuda:0", noise="torch", distributed=True)
+    return model._theta.detach().cpu().numpy(), [float(v) for v in losses]
+
+
+def test_data_parallel_ragged_batches_torch_noise_keep_ranks_in_sync():
+    outs = _run(_dp_train_ragged)
+    (t0, l0), (t1, l1) = outs
+    assert np.array_equal(t0, t1)
+    assert l0 == l1 and len(l0) == 3 * 2           # 2 usable global batches per epoch
+    assert all(np.isfinite(l0))
+
+
+def _dp_train_device_ragged(rank):
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import inference
+    from tests import _golden as G
+    g = G.load("toy_elbo")
+    xs, ys = G.split_lists(g)
+    xs = [xs[0], np.concatenate([xs[1], xs[1][:1] + 1e-3])]     # 201 rows: 100, 100, 1 (skipped on both ranks)
+    ys = [ys[0], np.concatenate([ys[1], ys[1][:1]])]
+    torch.manual_seed(7)
+    model, losses, _ = inference(xs, ys, g["z"], 50, 2, hyperpars={}, fix_hyperpars=True, lr=0.005, itnum=2,
+                                 show_ELBO=False, device="cuda:0", noise="device", distributed=True)
+    return model._theta.detach().cpu().numpy(), [float(v) for v in losses]
+
+
+def test_data_parallel_device_pipeline_ragged_keeps_ranks_in_sync():
+    outs = _run(_dp_train_device_ragged)
+    (t0, l0), (t1, l1) = outs
+    assert np.array_equal(t0, t1)
+    assert l0 == l1 and len(l0) == 2 * 2           # the 1-row global batch is skipped every epoch
+    assert all(np.isfinite(l0))

@@ -308,7 +308,7 @@ def test_gemm_big_stream_k(ops, kind, n, k):
         assert rel(outs[0], ref) < 2e-6 and rel(C1, ref) < 2e-6
 
 
-@pytest.mark.parametrize("n", [130, 300, 1000, 2048])
+@pytest.mark.parametrize("n", [130, 300, 1000, 2048, 4096])
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64])
 def test_potrf_blocked(ops, n, dt):
     # large single-matrix blocked Cholesky with lookahead (stress path): fp64-accurate residual,

@@ -6,7 +6,7 @@ import torch
 from oracle import nmgp_oracle as O
 from tests import _golden as G
 
-FWD_CASES = ["toy_forward", "modelpt_forward", "mid_forward"]
+FWD_CASES = ["toy_forward", "modelpt_forward", "mid_forward", "driver_hyper_forward"]
 
 
 def _rel(a, b):
@@ -46,10 +46,13 @@ def test_modelpt_known_answer_with_reference_rng():
     assert float(loss) == pytest.approx(float(g["loss"]), rel=1e-13)
 
 
-def test_pm25_shape_scalars():
-    g = G.load("pm25_forward")
+@pytest.mark.parametrize("case,D,M", [("pm25_forward", 5, 256), ("hcp_like_forward", 8, 512)])
+def test_big_shape_digests(case, D, M):
+    """Loss, per-parameter gradient norms and strided gradient samples of the PM2.5-shaped and the
+    HCP-like (D=8, M=512, B=5000) reference runs."""
+    g = G.load(case)
     xs, ys = G.split_lists(g)
-    p = G.params(g, D=5, M=256, requires_grad=True)
+    p = G.params(g, D=D, M=M, requires_grad=True)
     loss, _ = O.forward(p, xs, ys, g["z"], float(g["N"]), O.TapeNoise(g["noise"]))
     loss.backward()
     assert float(loss) == pytest.approx(float(g["loss"]), rel=1e-11)
