@@ -62,7 +62,7 @@ class DsviArgs(ctypes.Structure):
                 ("rowbuf", c_vp), ("facbuf", c_vp), ("red", c_vp), ("out", c_vp),
                 ("gib_row", c_vp), ("gib_col", c_vp), ("scal_part", c_vp), ("phi", c_vp),
                 ("info", c_vp), ("n_ct", c_int), ("n_rt", c_int), ("n_rt22", c_int), ("nblk_rows", c_int),
-                ("scal_off", c_i64 * 8)]
+                ("scal_off", c_i64 * 8), ("T", c_vp)]
 
 
 # flags (include/nmgp_hip.h)
@@ -144,6 +144,8 @@ _SIGS = {
     "nmgp_normal_f64": (c_int, [c_vp, c_i64, c_u64, c_vp, c_i64, c_vp]),
     "nmgp_normal_f32": (c_int, [c_vp, c_i64, c_u64, c_vp, c_i64, c_vp]),
     "nmgp_counter_add": (c_int, [c_vp, c_i64, c_vp]),
+    "nmgp_convert_f32_to_f64": (c_int, [c_vp, c_vp, c_i64, c_vp]),
+    "nmgp_convert_f64_to_f32": (c_int, [c_vp, c_vp, c_i64, c_vp]),
     "nmgp_step_begin_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_u64, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "nmgp_step_begin_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_u64, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "nmgp_batch_gather_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,

@@ -103,13 +103,13 @@ __global__ __launch_bounds__(256) void dsvi_trow_kernel(Args a) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= B) return;
   const T* Pt = (const T*)a.P + (int64_t)r * M;       // slot 0 = t
-  const T* Kt = (const T*)a.K12 + (int64_t)r * M;
+  const T* Tt = (const T*)a.T + (int64_t)r * M;       // K_t12 C_t^-T: rowsum(P o K12) = ||T_row||^2
   const T* v = (const T*)a.v;
   T mean = 0, q = 0;
   for (int c = lane; c < M; c += 64) {
-    const T p = Pt[c];
-    mean += p * v[c];
-    q += p * Kt[c];
+    const T tt = Tt[c];
+    mean += Pt[c] * v[c];
+    q += tt * tt;
   }
   mean = wave_sum(mean);
   q = wave_sum(q);
@@ -156,6 +156,11 @@ __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
   const T* K0 = K12 + 1 * BM + (int64_t)r * M;
   const T* P1 = P + 2 * BM + (int64_t)r * M;
   const T* K1 = K12 + 2 * BM + (int64_t)r * M;
+  // Nystrom variances rowsum(P o K12) as ||K12 C2^-T||^2 per row: a sum of squares instead of the
+  // cancellation 1 - rowsum(P o K12) of an explicit-inverse product (fp32 on smooth priors)
+  const T* TG = (const T*)a.T + 3 * BM + (int64_t)r * M;
+  const T* T0 = (const T*)a.T + 1 * BM + (int64_t)r * M;
+  const T* T1 = (const T*)a.T + 2 * BM + (int64_t)r * M;
   T* WG = (T*)a.WG;
   T* WP = (T*)a.WP;
   const T* muW = th + a.off_muW;
@@ -166,9 +171,9 @@ __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
   {
     T q[3] = {0, 0, 0};
     for (int c = t; c < M; c += 256) {
-      q[0] += PG[c] * KG[c];
-      q[1] += P0[c] * K0[c];
-      q[2] += P1[c] * K1[c];
+      q[0] += TG[c] * TG[c];
+      q[1] += T0[c] * T0[c];
+      q[2] += T1[c] * T1[c];
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -800,6 +805,25 @@ static void adam_launch(T* th, const T* g, T* m, T* v, int64_t n, const int64_t*
 
 __global__ void counter_add_kernel(int64_t* c, int64_t inc) { c[0] += inc; }
 
+// Element-wise precision conversion (grid-strided): fp32 engines factor their four GP priors in fp64
+// (engine.py), the explicit-inverse projections K12 (K22 + 1e-4 I)^-1 of smooth priors lose ~cond*eps
+// in an fp32 factorization.
+template <typename S, typename D>
+__global__ __launch_bounds__(256) void convert_kernel(const S* __restrict__ src, D* __restrict__ dst, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = (D)src[i];
+}
+template <typename S, typename D>
+static int convert_launch(const S* src, D* dst, int64_t n, hipStream_t s) {
+  if (!src) return -1;
+  if (!dst) return -2;
+  if (n <= 0) return NMGP_OK;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL((convert_kernel<S, D>), dim3((unsigned)blocks), dim3(256), 0, s, src, dst, n);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
+
 // ------------------------------------------------------------------------------------ batch gather
 // One block: every thread reads the batch index first, the copy is grid-strided over the block,
 // then (after a barrier) thread 0 advances the counter for the next step.
@@ -1090,6 +1114,12 @@ int nmgp_batch_gather_f32(const float* Xb, const float* Yb, const int32_t* Ib, c
                           int64_t nseg, int64_t nbatch, int64_t* ctr, float* x, float* y, int32_t* ro, int32_t* seg,
                           hipStream_t s) {
   return nmgp::batch_gather<float>(Xb, Yb, Ib, Sb, B, nseg, nbatch, ctr, x, y, ro, seg, s);
+}
+int nmgp_convert_f32_to_f64(const float* src, double* dst, int64_t n, hipStream_t s) {
+  return nmgp::convert_launch<float, double>(src, dst, n, s);
+}
+int nmgp_convert_f64_to_f32(const double* src, float* dst, int64_t n, hipStream_t s) {
+  return nmgp::convert_launch<double, float>(src, dst, n, s);
 }
 int nmgp_counter_add(int64_t* c, int64_t inc, hipStream_t s) {
   if (!c) return -1;

@@ -58,7 +58,7 @@ def vtvlcm(cfg, data, M, batchsize, lr, itnum, do_inference, do_test, res_dir, i
     z = np.linspace(0, dd.t_max, num=M)
     dim_outputs = len(dd.X_list)
     batch_size = dd.X_train_vec.shape[0] if batchsize == 0 else batchsize
-    path = os.path.join(res_dir, data, "prediction_res_M{}_B{}.pickle".format(M, batchsize))
+    path = None if res_dir is None else os.path.join(res_dir, data, "prediction_res_M{}_B{}.pickle".format(M, batchsize))
     if do_inference:
         ls = cfg["length_scale_log"]
         hyperpars = {"length_scales_L0_log": ls, "length_scales_L1_log": ls, "length_scales_tildeell_log": ls}
@@ -80,5 +80,7 @@ def vtvlcm(cfg, data, M, batchsize, lr, itnum, do_inference, do_test, res_dir, i
             with open(path, "wb") as res:
                 pickle.dump(list(out), res)
         return tuple(out)
+    if path is None:
+        raise ValueError("do_inference=False reloads an earlier run's result pickle: res_dir must be given")
     with open(path, "rb") as res:          # do_inference=False: reload the results of an earlier run
         return tuple(pickle.load(res))

@@ -81,6 +81,7 @@ class DsviEngine:
         self.Ainv = e(4, M, M)
         self.K12 = e(4, B, M)
         self.P = e(4, B, M)
+        self.T = e(4, B, M)             # K12 C2^-T per prior: Nystrom variances ||T_row||^2, P = T C2^-1
         self.Pbar = e(4, B, M)
         self.R = e(4, B, M)
         self.Abar = e(4, M, M)
@@ -110,6 +111,14 @@ class DsviEngine:
         self.scal_part = e(2 * int(self.scal_off[-1]))
         self.phi = e(M, M)
         self.info = torch.zeros(NF + 4, dtype=torch.int32, device=self.dev)
+        # fp32 engines factor the four GP priors (t, L0, L1, G) in fp64 and round L, L^-1 back: the
+        # explicit-inverse projections K12 (K22 + 1e-4 I)^-1 of smooth priors otherwise lose
+        # ~cond(K22) * eps32 (HCP-like fixture: P_G off by 40% with an fp32 factorization, 5e-4 with
+        # an fp64 one -- DESIGN.md §5).  NMGP_PRIOR_FP64=0 turns it off (A/B only).
+        self.prior64 = dtype == F32 and os.environ.get("NMGP_PRIOR_FP64", "1") != "0"
+        if self.prior64:
+            self.pri_A64 = torch.zeros(4, M, M, dtype=F64, device=self.dev)
+            self.pri_X64 = torch.zeros(4, M, M, dtype=F64, device=self.dev)
         # selection weights for the -1/2 Y diag(sel) Y^T prior adjoint (static)
         sel = np.zeros((4, D * D))
         for i in range(D):
@@ -148,7 +157,7 @@ class DsviEngine:
         a.off_muU, a.off_sU, a.off_hyp = o["mu_U"][0], o["sqrt_U"][0], o["sigma2_tildeell_log"][0]
         for name in ["x", "y", "row_out", "seg", "Z", "noise", "Afac", "Cinv", "Ainv", "K12", "P", "Pbar", "R",
                      "Abar", "WG", "WP", "Y", "Xs", "v", "vbar", "ellZ", "ellX", "var_t", "rowbuf", "facbuf",
-                     "red", "out", "gib_row", "gib_col", "scal_part", "phi", "info"]:
+                     "red", "out", "gib_row", "gib_col", "scal_part", "phi", "info", "T"]:
             setattr(a, name, getattr(self, name).data_ptr())
         a.n_ct, a.n_rt, a.n_rt22, a.nblk_rows = self.n_ct, self.n_rt, self.n_rt22, self.nblk
         for i, v in enumerate(self.scal_off):
@@ -195,6 +204,13 @@ class DsviEngine:
         # F5: prior inverses t,0,1 and Xs_f = Cinv_f L_f (KL gradient)
         d5 = [g(self.Ainv, self.Cinv, self.Cinv, M, M, M, (1, M, 0), (M, 1, 0), (M, 1), flags=L.A_UPPER | L.B_LOWER,
                 offs=((NF + k) * MM, (NF + k) * MM, k * MM)) for k in range(3)]
+        # T_k = K12_k C_k^-T (same launch: independent of the inverses); the projections below are
+        # P_k = T_k C_k^-1, i.e. two triangular applications instead of K12 (C^-T C^-1)
+        tproj = lambda k: g(self.T, self.K12, self.Cinv, B, M, M, (M, 1, 0), (1, M, 0), (M, 1), flags=L.B_UPPER,
+                            offs=(k * BM, (NF + k) * MM, k * BM), **rows_all)
+        pproj = lambda k: g(self.P, self.T, self.Cinv, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), flags=L.B_LOWER,
+                            offs=(k * BM, (NF + k) * MM, k * BM), **rows_all)
+        d5 += [tproj(k) for k in range(3)]
         if not elbo_mode:
             d5.append(xs(FV))
             p["xs_side"] = G([xs(f) for f in range(FV)])
@@ -210,8 +226,7 @@ class DsviEngine:
                 p["xs_side"] = H.BigBatch(self.Cinv, th, self.Xs, slots, offs_f, slots, M, M, M, lda=M, ldb=M,
                                           b_kcontig=False, flags=L.A_LOWER | L.B_LOWER | L.OUT_TRIL)
         # F6: P_k = K12_k Ainv_k (k = t,0,1) ; Y_t, Y_0, Y_1
-        d6 = [g(self.P, self.K12, self.Ainv, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), offs=(k * BM, k * MM, k * BM),
-                **rows_all) for k in range(3)]
+        d6 = [pproj(k) for k in range(3)]
         d6 += [g(self.Y, self.Ainv, th, M, 1, M, (M, 1, 0), (1, M, 0), (1, M), offs=(0, muv, D * M)),
                g(self.Y, self.Ainv, th, M, D * D, M, (M, 1, 0), (1, M, 0), (1, M), offs=(MM, muU, (D + 1) * M)),
                g(self.Y, self.Ainv, th, M, D * D, M, (M, 1, 0), (1, M, 0), (1, M),
@@ -223,9 +238,8 @@ class DsviEngine:
                             diag_add=self.jitter),
             H.pairwise_desc(self.K12[3], self.x, self.Z, mode=L.GIBBS, ellX=self.ellX, ellZ=self.ellZ)], dev)
         p["invG"] = G([g(self.Ainv, self.Cinv, self.Cinv, M, M, M, (1, M, 0), (M, 1, 0), (M, 1),
-                         flags=L.A_UPPER | L.B_LOWER, offs=((NF + 3) * MM, (NF + 3) * MM, 3 * MM))])
-        p["projG"] = G([g(self.P, self.K12, self.Ainv, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1),
-                          offs=(3 * BM, 3 * MM, 3 * BM), **rows_all),
+                         flags=L.A_UPPER | L.B_LOWER, offs=((NF + 3) * MM, (NF + 3) * MM, 3 * MM)), tproj(3)])
+        p["projG"] = G([pproj(3),
                         g(self.Y, self.Ainv, th, M, D, M, (M, 1, 0), (1, M, 0), (1, M), offs=(3 * MM, muW, 0))])
         # F14: quadratic-form factors W = P L on the rows that use them
         d14 = []
@@ -465,6 +479,32 @@ class DsviEngine:
                                                                    vp(Ci + first * MM * es), M, MM, count,
                                                                    vp(info + first * 4), s), "chol_inv")
 
+        if self.prior64:
+            conv_up, conv_dn = lib.nmgp_convert_f32_to_f64, lib.nmgp_convert_f64_to_f32
+            chol64 = lib.nmgp_chol_inv_batched_f64
+            A64, X64 = self.pri_A64.data_ptr(), self.pri_X64.data_ptr()
+            es = self.Afac.element_size()
+
+            def chol_prior(k0, cnt, v_too=False):
+                # slots NF + k0 .. NF + k0 + cnt - 1: up-convert K22 + lam I, fp64 factor + inverse, round
+                # L and L^-1 back into the fp32 slots (info as the fp32 kernel reports it)
+                f32 = chol(FV, 1) if v_too else None
+                n = cnt * MM
+
+                def run(s):
+                    if f32 is not None:
+                        f32(s)
+                    src = vp(Af + (NF + k0) * MM * es)
+                    L.check(conv_up(src, vp(A64 + k0 * MM * 8), n, s), "convert")
+                    L.check(chol64(vp(A64 + k0 * MM * 8), M, M, MM, vp(X64 + k0 * MM * 8), M, MM, cnt,
+                                   vp(info + (NF + k0) * 4), s), "chol_inv f64 prior")
+                    L.check(conv_dn(vp(A64 + k0 * MM * 8), src, n, s), "convert")
+                    L.check(conv_dn(vp(X64 + k0 * MM * 8), vp(Ci + (NF + k0) * MM * es), n, s), "convert")
+                return run
+            chol_main, chol_g = chol_prior(0, 3, v_too=True), chol_prior(3, 1)
+        else:
+            chol_main, chol_g = chol(FV, 4), chol(NF + 3, 1)
+
         need_side = (not elbo_mode) or with_kl
         steps = []
         # (fp64 engines only: in fp32 Sigma_v's summation order shows through ell_Z = exp(v), so fp32
@@ -487,13 +527,13 @@ class DsviEngine:
         else:
             steps.append(("syrk", "gemm", gemm("syrk"), "main"))
         steps += [
-            ("chol", "chol", chol(FV, 4), "main"),
+            ("chol", "chol", chol_main, "main"),
             ("inv3", "gemm", gemm("inv3"), "main"),
             ("proj3", "gemm", gemm("proj3"), "main"),
             ("v", "row", row(getattr(lib, "nmgp_dsvi_hyper_" + self.sfx)), "main"),
             ("trow", "row", row(getattr(lib, "nmgp_dsvi_trow_" + self.sfx)), "main"),
             ("build_gibbs", "pairwise", pw("build_gibbs"), "main"),
-            ("chol_G", "chol", chol(NF + 3, 1), "main"),
+            ("chol_G", "chol", chol_g, "main"),
             ("invG", "gemm", gemm("invG"), "main"),
             ("projG", "gemm", gemm("projG"), "main"),
         ]

@@ -306,6 +306,9 @@ typedef struct nmgp_dsvi_args {
   int32_t* info;
   int32_t n_ct, n_rt, n_rt22, nblk_rows;
   int64_t scal_off[8];        /* tile offsets of the RBF backward problems L0_12,L0_22,L1_12,L1_22,t12,t22 */
+  void* T;                    /* (4, B, M) K12 C2^-T per prior (t,0,1,G): the Nystrom variance
+                                 rowsum(P o K12) is formed as ||T_row||^2 (no cancellation-prone
+                                 explicit-inverse product) and P = T C2^-1                       */
 } nmgp_dsvi_args;
 
 int nmgp_dsvi_hyper_f64(const nmgp_dsvi_args* a, hipStream_t s);      /* hyper values + v sample   */
@@ -339,6 +342,12 @@ int nmgp_normal_f64(double* out, int64_t n, uint64_t seed, const int64_t* counte
 int nmgp_normal_f32(float* out, int64_t n, uint64_t seed, const int64_t* counter, int64_t offset,
                     hipStream_t stream);
 int nmgp_counter_add(int64_t* counter, int64_t inc, hipStream_t stream);
+/* Element-wise precision conversion dst[i] = (dst type) src[i] (round to nearest for f64 -> f32).
+ * fp32 engines (HCP / ECoG shapes) factor the four GP priors K22 + 1e-4 I in fp64: the fp32
+ * explicit-inverse projections K12 (K22 + 1e-4 I)^-1 of code/utils.py:117-119 otherwise lose
+ * ~cond(K22) * eps.                                                            */
+int nmgp_convert_f32_to_f64(const float* src, double* dst, int64_t n, hipStream_t stream);
+int nmgp_convert_f64_to_f32(const double* src, float* dst, int64_t n, hipStream_t stream);
 /* On-device minibatch pipeline (replaces the host DataLoader + vec2list split of
  * code/nmgp_dsvi.py:816-837 for a dataset resident in HBM): copies minibatch
  * b = (*batch_counter) % nbatch of pre-split, output-grouped batches (Xb/Yb (nbatch,B) f64, Ib

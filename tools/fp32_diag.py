@@ -1,0 +1,50 @@
+"""fp32 vs fp64 engine on a golden fixture, intermediate by intermediate (numerics triage tool)."""
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from oracle import nmgp_oracle as O  # noqa: E402
+from tests import _golden as G  # noqa: E402
+from collaborative_nonstationary_multivariate_gaussian_process_amd.engine import DsviEngine  # noqa: E402
+
+
+def run(case, D, M, dt, big_side="1"):
+    import os
+    os.environ["NMGP_BIG_SIDE"] = big_side
+    g = G.load(case)
+    p = G.params(g, D=D, M=M)
+    sizes = [int(s) for s in g["sizes"]]
+    eng = DsviEngine(D, M, sum(sizes), g["z"], dtype=dt)
+    theta = torch.cat([p[k].reshape(-1) for k in O.PARAM_NAMES]).to("cuda", dt)
+    grad = torch.zeros_like(theta)
+    eng.bind(theta, grad, frozen_mask=0, N=float(g["N"]))
+    eng.load_batch(g["x"], g["y"], sizes, noise=g["noise"])
+    eng.forward_backward()
+    torch.cuda.synchronize()
+    eng.check_info()
+    return g, eng, grad
+
+
+def rel(a, b):
+    a, b = a.double().reshape(-1).cpu(), b.double().reshape(-1).cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-300))
+
+
+case, D, M = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+g, e64, g64 = run(case, D, M, torch.float64)
+print("fp64 loss", float(e64.out[0]), "golden", float(g["loss"]), "rel", abs(float(e64.out[0]) - float(g["loss"])) / abs(float(g["loss"])))
+print("fp64 parts R, KLW, KLv, KLU", [float(v) for v in e64.out[1:5]])
+for bs in ("1", "0"):
+    _, e32, g32 = run(case, D, M, torch.float32, bs)
+    print(f"--- fp32 (big_side={bs}) loss", float(e32.out[0]), "rel vs fp64", abs(float(e32.out[0]) - float(e64.out[0])) / abs(float(e64.out[0])))
+    print("fp32 parts", [float(v) for v in e32.out[1:5]])
+    for name in ["v", "ellZ", "var_t", "ellX", "Ainv", "K12", "P", "WG", "WP", "Cinv", "Afac", "Y"]:
+        a, b = getattr(e32, name), getattr(e64, name)
+        print(f"  {name:6s} rel {rel(a, b):.3e}")
+    for k in range(4):
+        print(f"  P[{k}] rel {rel(e32.P[k], e64.P[k]):.3e}  K12[{k}] rel {rel(e32.K12[k], e64.K12[k]):.3e}  Ainv[{k}] {rel(e32.Ainv[k], e64.Ainv[k]):.3e}")
+    vt32, vt64 = e32.var_t.double().cpu(), e64.var_t.double().cpu()
+    print("  var_t fp64 min/median", float(vt64.min()), float(vt64.median()), " abs err max", float((vt32 - vt64).abs().max()))
+    print("  grad rel-norm", rel(g32, g64))
