@@ -152,11 +152,26 @@ class PhaseTimer:
         return per_name, per_kind
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(seconds, xs, ys, z):
     """The oracle (reference op for op: per-pair LU solves, dense D x D Sigma_U, torch autograd,
     Adam) on the same PM2.5-shaped minibatch, on this host's cores; bounded to ~`seconds`."""
     from oracle import nmgp_oracle as O
-    nthreads = min(16, os.cpu_count() or 1)
+    # the host cores this process may run on (on the GPU box: the job's CPU share; os.cpu_count()
+    # reports the whole machine there), capped by OMP_NUM_THREADS when the launcher sets it
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    nthreads = max(1, min(avail, omp) if omp > 0 else avail)
     torch.set_num_threads(nthreads)
     p = O.new_params(D, M, seed=22)
     for k in ["length_scales_tildeell_log", "length_scales_L0_log", "length_scales_L1_log"]:
@@ -185,6 +200,9 @@ def cpu_baseline(seconds, xs, ys, z):
             break
     steady = times[1:]
     return {"value": round(1.0 / float(np.mean(steady)), 4), "unit": "it/s", "cores": nthreads, "kind": "port",
+            "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count(), "affinity_cpus": avail,
+            "oracle_vs_reference": "oracle/reference CPU time 0.957 on the build container, interleaved medians "
+                                   "(profiles/r02_cpu_oracle_vs_reference.json, tools/cpu_baseline_check.py)",
             "sample": f"{len(steady)} timed DSVI iterations (after 1 warm-up) of the oracle "
                       f"(torch-CPU fp64 restatement of code/nmgp_dsvi.py:157-301 + autograd + Adam) on the same "
                       f"D=5, M=256, B=2000 config; mean {1000 * float(np.mean(steady)):.1f} ms/it"}
