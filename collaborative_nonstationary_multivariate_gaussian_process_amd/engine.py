@@ -233,9 +233,12 @@ class DsviEngine:
                  offs=(2 * MM, muU, (D + 1 + D * D) * M))]
         p["proj3"] = G(d6)
         # F9: Gibbs builders (K_G22 + lam I into the G prior slot, K_G12)
-        p["build_gibbs"] = H.PairwiseGroup([
+        # K_G22 + lam I needs only ell_Z (the v sample) and feeds chol_G on the main chain; K_G12 also needs
+        # ell_X (the t-row) and is built on the second side stream beside chol_G
+        p["build_g22"] = H.PairwiseGroup([
             H.pairwise_desc(self.Afac[NF + 3], self.Z, self.Z, mode=L.GIBBS, ellX=self.ellZ, ellZ=self.ellZ,
-                            diag_add=self.jitter),
+                            diag_add=self.jitter)], dev)
+        p["build_g12"] = H.PairwiseGroup([
             H.pairwise_desc(self.K12[3], self.x, self.Z, mode=L.GIBBS, ellX=self.ellX, ellZ=self.ellZ)], dev)
         p["invG"] = G([g(self.Ainv, self.Cinv, self.Cinv, M, M, M, (1, M, 0), (M, 1, 0), (M, 1),
                          flags=L.A_UPPER | L.B_LOWER, offs=((NF + 3) * MM, (NF + 3) * MM, 3 * MM)), tproj(3)])
@@ -356,7 +359,8 @@ class DsviEngine:
             bw.append(H.pairwise_bwd_desc(self.Z, self.Z, None, self.Abar, mode=L.RBF, ld=M, hyp=th, hyp_off=hoff,
                                           hyp_log=True, scal_part=self.scal_part,
                                           offs=(0, k * MM, 0, 0, 0, 2 * int(so[2 * q + 1]))))
-        p["bwd_build"] = H.PairwiseBwdGroup(bw[:2], dev)      # G12, G22 (feeds the t chain)
+        p["bwd_build12"] = H.PairwiseBwdGroup(bw[:1], dev)    # G12: ell_X adjoints (feeds the t chain)
+        p["bwd_build22"] = H.PairwiseBwdGroup(bw[1:2], dev)   # G22: ell_Z adjoints (v chain only)
         p["bwd_build_L"] = H.PairwiseBwdGroup(bw[2:], dev)    # L0_*, L1_* (hyper-parameter partials only)
         # B7: t chain
         p["bwd_t1"] = G([g(self.R, self.Pbar, self.Ainv, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), offs=(0, 0, 0),
@@ -526,14 +530,23 @@ class DsviEngine:
             steps.append(("wait", "main", "syrk"))
         else:
             steps.append(("syrk", "gemm", gemm("syrk"), "main"))
+        # forward chain: chol -> v -> K_G22 -> chol_G -> invG -> projG.  The t-prior projections, the
+        # t-row (ell_X) and K_G12 run on the second side stream beside v / K_G22 / chol_G: they are
+        # needed only from invG on (T_G = K_G12 C_G^-T)
         steps += [
             ("chol", "chol", chol_main, "main"),
-            ("inv3", "gemm", gemm("inv3"), "main"),
-            ("proj3", "gemm", gemm("proj3"), "main"),
+            ("sig", "main", "chol"), ("wait", "side2", "chol"),
+            ("inv3", "gemm", gemm("inv3"), "side2"),
+            ("proj3", "gemm", gemm("proj3"), "side2"),
             ("v", "row", row(getattr(lib, "nmgp_dsvi_hyper_" + self.sfx)), "main"),
-            ("trow", "row", row(getattr(lib, "nmgp_dsvi_trow_" + self.sfx)), "main"),
-            ("build_gibbs", "pairwise", pw("build_gibbs"), "main"),
+            ("sig", "main", "v"),
+            ("build_g22", "pairwise", pw("build_g22"), "main"),
+            ("wait", "side2", "v"),
+            ("trow", "row", row(getattr(lib, "nmgp_dsvi_trow_" + self.sfx)), "side2"),
+            ("build_g12", "pairwise", pw("build_g12"), "side2"),
+            ("sig", "side2", "g12"),
             ("chol_G", "chol", chol_g, "main"),
+            ("wait", "main", "g12"),
             ("invG", "gemm", gemm("invG"), "main"),
             ("projG", "gemm", gemm("projG"), "main"),
         ]
@@ -571,11 +584,18 @@ class DsviEngine:
             ("sig", "side", "lbar_done"),
             ("sig", "main", "bwd_w"),
         ]
+        # G prior: R_G -> the K_G12 builder backward (ell_X adjoints) stays on the main chain; the prior
+        # adjoint Abar_G -= P_G^T R_G and the K_G22 builder backward (ell_Z adjoints: the v chain only)
+        # run on the second side stream
         steps += [
             ("bwd_R", "gemm", gemm("bwd_R"), "main"),
-            ("wait", "main", "kl_done"),
-            ("bwd_pr", "gemm", gemm("bwd_pr"), "main"),
-            ("bwd_build", "pairwise_bwd", pw("bwd_build"), "main"),
+            ("sig", "main", "R_G"),
+            ("bwd_build12", "pairwise_bwd", pw("bwd_build12"), "main"),
+            ("wait", "side2", "R_G"),
+            ("wait", "side2", "kl_done"),
+            ("bwd_pr", "gemm", gemm("bwd_pr"), "side2"),
+            ("bwd_build22", "pairwise_bwd", pw("bwd_build22"), "side2"),
+            ("sig", "side2", "g22"),
             # the L0 / L1 prior adjoints feed only their hyper-parameter partials (scal_part slots and
             # row-coefficient rows of their own): side stream, after the KL parts of Abar (same stream).
             # A/B on the box: +2% it/s against one 3-prior launch of each on the main stream.
@@ -593,6 +613,7 @@ class DsviEngine:
             # sqrt_v gradient accumulation fixed: kl_lbar, bwd_lbar, bwd_v2)
             ("sig", "main", "t1"),
             ("wait", "side", "t1"),
+            ("wait", "side", "g22"),
             ("vbwd", "row", row(getattr(lib, "nmgp_dsvi_vbwd_" + self.sfx)), "side"),
             ("bwd_v1", "gemm", gemm("bwd_v1"), "side"),
             ("bwd_v2", "gemm", gemm("bwd_v2"), "side"),
@@ -601,6 +622,7 @@ class DsviEngine:
             ("bwd_tbuild", "pairwise_bwd", pw("bwd_tbuild"), "main"),
             ("wait", "main", "v_done"),
             ("wait", "main", "lbar_done"),
+            ("wait", "main", "g22"),             # explicit join of the second side stream (graph capture)
             ("finalize", "row", row(getattr(lib, "nmgp_dsvi_finalize_" + self.sfx)), "main"),
         ]
         return steps
@@ -611,14 +633,16 @@ class DsviEngine:
         if timer is None:
             if getattr(self, "_side", None) is None:
                 self._side = torch.cuda.Stream(device=self.dev)
-            s_side = ctypes.c_void_p(self._side.cuda_stream)
+                self._side2 = torch.cuda.Stream(device=self.dev)
+            streams = {"main": main, "side": self._side, "side2": self._side2}
+            handles = {k: ctypes.c_void_p(v.cuda_stream) for k, v in streams.items()}
         events = {}
         for item in steps:
             if item[0] in ("sig", "wait"):
                 if timer is not None:
                     continue                       # timed runs are serial on one stream
                 _, who, tag = item
-                st = main if who == "main" else self._side
+                st = streams[who]
                 if item[0] == "sig":
                     ev = torch.cuda.Event()
                     ev.record(st)
@@ -632,7 +656,7 @@ class DsviEngine:
                 fn(s_main)
                 timer.stop(name, kind)
             else:
-                fn(s_side if where == "side" else s_main)
+                fn(handles[where])
 
     def forward_backward(self, stream=None, timer=None, zero_grad=True):
         """Enqueue -SELBO (self.out[0]) and all gradients (into the bound grad vector)."""
