@@ -550,6 +550,9 @@ class DsviEngine:
             ("invG", "gemm", gemm("invG"), "main"),
             ("projG", "gemm", gemm("projG"), "main"),
         ]
+        if os.environ.get("NMGP_SIDE2_FWD", "1") == "0":
+            steps = self._remap(steps, 0, len(steps), "side2", "main")
+        n_fwd = len(steps)
         if elbo_mode:
             steps.append(("quad", "gemm", gemm("quad"), "main"))
             if need_side:
@@ -588,11 +591,14 @@ class DsviEngine:
         # adjoint Abar_G -= P_G^T R_G and the K_G22 builder backward (ell_Z adjoints: the v chain only)
         # run on the second side stream
         steps += [
+            # (the second side stream synchronises with the main stream only: a side <-> side2 event
+            # edge made hipGraph instantiation crash on this stack; the KL prior adjoints are long done
+            # when bwd_R finishes, so the main stream's wait on them costs nothing)
             ("bwd_R", "gemm", gemm("bwd_R"), "main"),
+            ("wait", "main", "kl_done"),
             ("sig", "main", "R_G"),
             ("bwd_build12", "pairwise_bwd", pw("bwd_build12"), "main"),
             ("wait", "side2", "R_G"),
-            ("wait", "side2", "kl_done"),
             ("bwd_pr", "gemm", gemm("bwd_pr"), "side2"),
             ("bwd_build22", "pairwise_bwd", pw("bwd_build22"), "side2"),
             ("sig", "side2", "g22"),
@@ -611,9 +617,9 @@ class DsviEngine:
             # backward (vbwd -> bwd_v1 -> bwd_v2, reading vbar and the Gibbs partials) share no buffer:
             # the v chain runs on the side stream (after bwd_lbar there, which keeps the order of the
             # sqrt_v gradient accumulation fixed: kl_lbar, bwd_lbar, bwd_v2)
+            ("wait", "main", "g22"),
             ("sig", "main", "t1"),
             ("wait", "side", "t1"),
-            ("wait", "side", "g22"),
             ("vbwd", "row", row(getattr(lib, "nmgp_dsvi_vbwd_" + self.sfx)), "side"),
             ("bwd_v1", "gemm", gemm("bwd_v1"), "side"),
             ("bwd_v2", "gemm", gemm("bwd_v2"), "side"),
@@ -622,10 +628,24 @@ class DsviEngine:
             ("bwd_tbuild", "pairwise_bwd", pw("bwd_tbuild"), "main"),
             ("wait", "main", "v_done"),
             ("wait", "main", "lbar_done"),
-            ("wait", "main", "g22"),             # explicit join of the second side stream (graph capture)
             ("finalize", "row", row(getattr(lib, "nmgp_dsvi_finalize_" + self.sfx)), "main"),
         ]
+        if os.environ.get("NMGP_SIDE2_BWD", "1") == "0":
+            steps = self._remap(steps, n_fwd, len(steps), "side2", "main")
         return steps
+
+    @staticmethod
+    def _remap(steps, lo, hi, frm, to):
+        """Run the items [lo, hi) of `frm` on stream `to` instead (A/B of stream placements)."""
+        out = []
+        for i, it in enumerate(steps):
+            if lo <= i < hi:
+                if it[0] in ("sig", "wait") and it[1] == frm:
+                    it = (it[0], to, it[2])
+                elif len(it) == 4 and it[3] == frm:
+                    it = (it[0], it[1], it[2], to)
+            out.append(it)
+        return out
 
     def _run(self, steps, stream, timer):
         main = stream if stream is not None else torch.cuda.current_stream(self.dev)
