@@ -525,6 +525,34 @@ __global__ __launch_bounds__(256) void dsvi_vbwd_kernel(Args a) {
   }
 }
 
+// ------------------------------------------------------------------------------------ mu gradients
+// KL mean gradients A2^{-1} mu (Y) into the mu_W / mu_U gradient rows (live pairs j <= i only) and
+// mu_v += vbar + Y_t: one grid-strided element-wise pass, launched on the side stream after the last
+// writers of those rows (the mu-bar products of bwd_lbar and the v backward), off the main chain.
+template <typename T>
+__global__ __launch_bounds__(256) void dsvi_mugrad_kernel(Args a) {
+  const int D = a.D, M = a.M;
+  T* __restrict__ gw = (T*)a.grad;
+  const T* __restrict__ Y = (const T*)a.Y;
+  const T* __restrict__ vbar = (const T*)a.vbar + M;   // completed by the v-backward kernel
+  const int64_t DM = (int64_t)D * M, DDM = (int64_t)D * D * M;
+  const int64_t yu0 = (int64_t)(D + 1) * M, yu1 = yu0 + DDM;
+  const int64_t n = DM + M + DDM, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    if (i < DM) {
+      gw[a.off_muW + i] = gw[a.off_muW + i] + Y[i];
+    } else if (i < DM + M) {
+      const int64_t c = i - DM;
+      gw[a.off_muv + c] += vbar[c] + Y[DM + c];
+    } else {
+      const int64_t idx = i - DM - M;
+      const int ij = (int)(idx / M);
+      const int pi = ij / D, pj = ij - pi * D;
+      if (pj <= pi) gw[a.off_muU + idx] = gw[a.off_muU + idx] + Y[(pi == pj ? yu1 : yu0) + idx];
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------ finalize
 template <typename T>
 __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
@@ -668,43 +696,7 @@ __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
     gs[6] = e;                            // sigma2_err_log
     for (int k = 0; k < 7; ++k) g[a.off_hyp + k] = (a.frozen_mask >> k & 1) ? (T)0 : gs[k];
   }
-  // KL mean gradients A2^{-1} mu (Y) and mu_v += vbar: element-wise, batches of 4 strides with all
-  // loads issued before the stores (restrict: g does not alias Y / vbar)
-  T* __restrict__ gw = g;
-  const T* __restrict__ Y = (const T*)a.Y;
-  const T* __restrict__ vbar = (const T*)a.vbar + M;   // completed by the v-backward kernel
-  const int DM = D * M;
-  for (int i0 = t; i0 < DM; i0 += 4096) {
-    T gv[4], yv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = min(i0 + u * 1024, DM - 1);
-      gv[u] = gw[a.off_muW + i];
-      yv[u] = Y[i];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (i0 + u * 1024 < DM) gw[a.off_muW + i0 + u * 1024] = gv[u] + yv[u];
-  }
-  for (int c = t; c < M; c += 1024) gw[a.off_muv + c] += vbar[c] + Y[(int64_t)DM + c];
-  const int64_t yu0 = (int64_t)(D + 1) * M, yu1 = yu0 + (int64_t)D * D * M;
-  const int DDM = D * D * M;
-  for (int i0 = t; i0 < DDM; i0 += 4096) {
-    T gv[4], yv[4];
-    bool live[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int idx = min(i0 + u * 1024, DDM - 1);
-      const int ij = idx / M;
-      const int i = ij / D, j = ij - i * D;
-      live[u] = j <= i && i0 + u * 1024 < DDM;
-      gv[u] = gw[a.off_muU + idx];
-      yv[u] = Y[(i == j ? yu1 : yu0) + idx];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (live[u]) gw[a.off_muU + i0 + u * 1024] = gv[u] + yv[u];
-  }
+  // (the KL mean gradients A2^{-1} mu and mu_v += vbar are added by dsvi_mugrad_kernel on the side stream)
 #ifdef NMGP_FIN_TRACE
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -987,6 +979,14 @@ template <typename T> static int dsvi_vbwd(const Args* a, hipStream_t s) {
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
+template <typename T> static int dsvi_mugrad(const Args* a, hipStream_t s) {
+  CHECK_ARGS(a);
+  const int64_t n = (int64_t)a->D * a->M + a->M + (int64_t)a->D * a->D * a->M;
+  hipLaunchKernelGGL(dsvi_mugrad_kernel<T>, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 2048)), dim3(256), 0, s,
+                     *a);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
 template <typename T> static int dsvi_finalize(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
   if (a->M > 16384) return -2;
@@ -1049,6 +1049,7 @@ NMGP_DSVI_ENTRY(delta)
 NMGP_DSVI_ENTRY(tbwd)
 NMGP_DSVI_ENTRY(vbwd)
 NMGP_DSVI_ENTRY(finalize)
+NMGP_DSVI_ENTRY(mugrad)
 #undef NMGP_DSVI_ENTRY
 int nmgp_adam_f64(double* th, const double* g, double* m, double* v, int64_t n, int64_t* step, double lr,
                   double b1, double b2, double eps, hipStream_t s) {

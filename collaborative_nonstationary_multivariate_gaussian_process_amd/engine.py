@@ -364,8 +364,10 @@ class DsviEngine:
         p["bwd_build_L"] = H.PairwiseBwdGroup(bw[2:], dev)    # L0_*, L1_* (hyper-parameter partials only)
         # B7: t chain
         p["bwd_t1"] = G([g(self.R, self.Pbar, self.Ainv, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), offs=(0, 0, 0),
-                           **rows_all),
-                         g(self.vbar, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1),
+                           **rows_all)])
+        # vbar[0:M] = P_t^T tbar: the v backward's only input from the t chain -- its own launch on the
+        # side stream right after the t-row backward, so the v chain does not wait for R_t
+        p["bwd_vt"] = G([g(self.vbar, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1),
                            offs=(0, (2 * D + 3) * B, 0), k_seg=0, seg_span=D)])
         p["bwd_t2"] = G([g(self.Abar, self.P, self.R, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), alpha=-1.0, beta=1.0,
                            offs=(0, 0, 0), k_seg=0, seg_span=D)])
@@ -612,18 +614,21 @@ class DsviEngine:
         ]
         steps += [
             ("tbwd", "row", row(getattr(lib, "nmgp_dsvi_tbwd_" + self.sfx)), "main"),
-            ("bwd_t1", "gemm", gemm("bwd_t1"), "main"),
-            # after bwd_t1 the t-prior chain (bwd_t2 -> builder backward) and the v-factor Cholesky
-            # backward (vbwd -> bwd_v1 -> bwd_v2, reading vbar and the Gibbs partials) share no buffer:
-            # the v chain runs on the side stream (after bwd_lbar there, which keeps the order of the
-            # sqrt_v gradient accumulation fixed: kl_lbar, bwd_lbar, bwd_v2)
+            # after the t-row backward the t-prior chain (bwd_t1 -> bwd_t2 -> builder backward) and the
+            # v-factor Cholesky backward (P_t^T tbar -> vbwd -> bwd_v1 -> bwd_v2, reading vbar and the
+            # Gibbs partials) share no buffer: the v chain runs on the side stream (after bwd_lbar there,
+            # which keeps the order of the sqrt_v gradient accumulation fixed: kl_lbar, bwd_lbar,
+            # bwd_v2), followed by the KL mean gradients of the mu rows
             ("wait", "main", "g22"),
-            ("sig", "main", "t1"),
-            ("wait", "side", "t1"),
+            ("sig", "main", "tb"),
+            ("wait", "side", "tb"),
+            ("bwd_vt", "gemm", gemm("bwd_vt"), "side"),
             ("vbwd", "row", row(getattr(lib, "nmgp_dsvi_vbwd_" + self.sfx)), "side"),
             ("bwd_v1", "gemm", gemm("bwd_v1"), "side"),
             ("bwd_v2", "gemm", gemm("bwd_v2"), "side"),
+            ("mugrad", "row", row(getattr(lib, "nmgp_dsvi_mugrad_" + self.sfx)), "side"),
             ("sig", "side", "v_done"),
+            ("bwd_t1", "gemm", gemm("bwd_t1"), "main"),
             ("bwd_t2", "gemm", gemm("bwd_t2"), "main"),
             ("bwd_tbuild", "pairwise_bwd", pw("bwd_tbuild"), "main"),
             ("wait", "main", "v_done"),

@@ -319,6 +319,7 @@ int nmgp_dsvi_delta_f64(const nmgp_dsvi_args* a, hipStream_t s);      /* prior d
 int nmgp_dsvi_tbwd_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* t-row backward            */
 int nmgp_dsvi_vbwd_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* v backward -> Phi         */
 int nmgp_dsvi_finalize_f64(const nmgp_dsvi_args* a, hipStream_t s);   /* loss + scalar gradients   */
+int nmgp_dsvi_mugrad_f64(const nmgp_dsvi_args* a, hipStream_t s);     /* KL mean gradients of mu_W / mu_v / mu_U */
 /* fp32 twins (HCP / ECoG-shaped configurations): same arguments, every buffer float */
 int nmgp_dsvi_hyper_f32(const nmgp_dsvi_args* a, hipStream_t s);
 int nmgp_dsvi_trow_f32(const nmgp_dsvi_args* a, hipStream_t s);
@@ -328,6 +329,7 @@ int nmgp_dsvi_delta_f32(const nmgp_dsvi_args* a, hipStream_t s);
 int nmgp_dsvi_tbwd_f32(const nmgp_dsvi_args* a, hipStream_t s);
 int nmgp_dsvi_vbwd_f32(const nmgp_dsvi_args* a, hipStream_t s);
 int nmgp_dsvi_finalize_f32(const nmgp_dsvi_args* a, hipStream_t s);
+int nmgp_dsvi_mugrad_f32(const nmgp_dsvi_args* a, hipStream_t s);
 
 /* ------------------------------------------------------------------ optimiser / RNG
  * torch.optim.Adam update (code/nmgp_dsvi.py:777,854) on a flat parameter vector; step is a
