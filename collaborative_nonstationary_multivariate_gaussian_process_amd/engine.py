@@ -605,12 +605,13 @@ class DsviEngine:
             ("bwd_build22", "pairwise_bwd", pw("bwd_build22"), "side2"),
             ("sig", "side2", "g22"),
             # the L0 / L1 prior adjoints feed only their hyper-parameter partials (scal_part slots and
-            # row-coefficient rows of their own): side stream, after the KL parts of Abar (same stream).
-            # A/B on the box: +2% it/s against one 3-prior launch of each on the main stream.
-            ("wait", "side", "bwd_w"),
-            ("bwd_R_L", "gemm", gemm("bwd_R_L"), "side"),
-            ("bwd_pr_L", "gemm", gemm("bwd_pr_L"), "side"),
-            ("bwd_build_L", "pairwise_bwd", pw("bwd_build_L"), "side"),
+            # row-coefficient rows of their own): second side stream after the G prior adjoint (R_G was
+            # signalled after bwd_w and the KL parts of Abar), so the v chain on the side stream does not
+            # queue behind them
+            ("bwd_R_L", "gemm", gemm("bwd_R_L"), "side2"),
+            ("bwd_pr_L", "gemm", gemm("bwd_pr_L"), "side2"),
+            ("bwd_build_L", "pairwise_bwd", pw("bwd_build_L"), "side2"),
+            ("sig", "side2", "L_done"),
         ]
         steps += [
             ("tbwd", "row", row(getattr(lib, "nmgp_dsvi_tbwd_" + self.sfx)), "main"),
@@ -633,6 +634,7 @@ class DsviEngine:
             ("bwd_tbuild", "pairwise_bwd", pw("bwd_tbuild"), "main"),
             ("wait", "main", "v_done"),
             ("wait", "main", "lbar_done"),
+            ("wait", "main", "L_done"),
             ("finalize", "row", row(getattr(lib, "nmgp_dsvi_finalize_" + self.sfx)), "main"),
         ]
         if os.environ.get("NMGP_SIDE2_BWD", "1") == "0":
