@@ -51,7 +51,7 @@ class PairwiseBwdDesc(ctypes.Structure):
 
 class DsviArgs(ctypes.Structure):
     _fields_ = [("D", c_int), ("M", c_int), ("B", c_int), ("Q", c_int), ("NF", c_int), ("elbo_mode", c_int),
-                ("frozen_mask", c_int), ("pad0_", c_int), ("N_over_B", c_dbl), ("jitter", c_dbl),
+                ("frozen_mask", c_int), ("pair_packed", c_int), ("N_over_B", c_dbl), ("jitter", c_dbl),
                 ("theta", c_vp), ("grad", c_vp),
                 ("off_muW", c_i64), ("off_sW", c_i64), ("off_muv", c_i64), ("off_sv", c_i64), ("off_muU", c_i64),
                 ("off_sU", c_i64), ("off_hyp", c_i64),

@@ -29,6 +29,15 @@ __device__ inline void pair_ij(int q, int& i, int& j) {
   i = r;
   j = q - r * (r + 1) / 2;
 }
+// Block index of coefficient pair (i, j <= i) in mu_U / sqrt_U / Y_0 / Y_1: the reference's dense
+// D x D layout, or the packed Q-pair layout (engine.param_layout)
+__device__ inline int64_t pair_blk(const nmgp_dsvi_args& a, int i, int j) {
+  return a.pair_packed ? (int64_t)i * (i + 1) / 2 + j : (int64_t)i * a.D + j;
+}
+__device__ inline int64_t pair_cols(const nmgp_dsvi_args& a) {
+  return a.pair_packed ? (int64_t)a.Q : (int64_t)a.D * a.D;
+}
+
 // Variational factor order: f < D latent functions W_f | D <= f < D+Q coefficient pairs (i,j) in
 // (i, j<=i) order | f = D+Q (= NF-1) the length-scale process v.  Prior slot of factor f:
 // 0 = t (v), 1 = L0 (off-diagonal pairs), 2 = L1 (diagonal pairs), 3 = G (W).
@@ -188,7 +197,7 @@ __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
     const T* wg = WG + (int64_t)s * BM + (int64_t)r * M;
     const T* wp = WP + (int64_t)s * BM + (int64_t)r * M;
     const T* mw = muW + (int64_t)s * M;
-    const T* mu = muU + ((int64_t)pi * D + pj) * M;
+    const T* mu = muU + pair_blk(a, pi, pj) * M;
     T d4[4] = {0, 0, 0, 0};
     for (int c = t; c < M; c += 256) {
       const T x = wg[c], y = wp[c];
@@ -312,9 +321,9 @@ __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
     for (int d = 0; d <= o; ++d) acc += sv[2 * D + d] * muW[(int64_t)d * M + c];
     PbG[c] = acc;
     acc = -c0 * K0[c];
-    for (int j = 0; j < o; ++j) acc += sv[3 * D + j] * muU[((int64_t)o * D + j) * M + c];
+    for (int j = 0; j < o; ++j) acc += sv[3 * D + j] * muU[pair_blk(a, o, j) * M + c];
     Pb0[c] = acc;
-    Pb1[c] = sv[3 * D + o] * muU[((int64_t)o * D + o) * M + c] - c1 * K1[c];
+    Pb1[c] = sv[3 * D + o] * muU[pair_blk(a, o, o) * M + c] - c1 * K1[c];
   }
 }
 
@@ -326,7 +335,7 @@ template <typename T> __device__ inline const T* fac_S(const Args& a, int f) {
   if (f == a.NF - 1) return th + a.off_sv;
   int i, j;
   pair_ij(f - a.D, i, j);
-  return th + a.off_sU + ((int64_t)i * a.D + j) * MM;
+  return th + a.off_sU + pair_blk(a, i, j) * MM;
 }
 template <typename T> __device__ inline const T* fac_mu(const Args& a, int f) {
   const T* th = (const T*)a.theta;
@@ -334,7 +343,7 @@ template <typename T> __device__ inline const T* fac_mu(const Args& a, int f) {
   if (f == a.NF - 1) return th + a.off_muv;
   int i, j;
   pair_ij(f - a.D, i, j);
-  return th + a.off_muU + ((int64_t)i * a.D + j) * a.M;
+  return th + a.off_muU + pair_blk(a, i, j) * a.M;
 }
 template <typename T> __device__ inline const T* fac_y(const Args& a, int f) {
   const T* Y = (const T*)a.Y;
@@ -343,8 +352,8 @@ template <typename T> __device__ inline const T* fac_y(const Args& a, int f) {
   if (f == a.NF - 1) return Y + (int64_t)D * M;
   int i, j;
   pair_ij(f - D, i, j);
-  const int64_t base = (int64_t)(D + 1) * M + (i == j ? (int64_t)D * D * M : 0);
-  return Y + base + ((int64_t)i * D + j) * M;
+  const int64_t base = (int64_t)(D + 1) * M + (i == j ? pair_cols(a) * M : 0);
+  return Y + base + pair_blk(a, i, j) * M;
 }
 
 // KL per factor, parallel over (factor, 16-row slab): 16 lanes per row sum tril(S)_i. squared
@@ -352,7 +361,7 @@ template <typename T> __device__ inline const T* fac_y(const Args& a, int f) {
 // each block leaves 4 partial sums in klpart[f][slab], summed in slab order by the finalize kernel.
 constexpr int KL_ROWS = 16;
 template <typename T> __device__ inline T* kl_part(const Args& a) {
-  return (T*)a.facbuf + a.NF + 8 * (int64_t)a.M + 4 * (int64_t)a.D * a.D + (int64_t)a.NF * a.M;
+  return (T*)a.facbuf + a.NF + 8 * (int64_t)a.M + 4 * pair_cols(a) + (int64_t)a.NF * a.M;
 }
 
 template <typename T>
@@ -385,7 +394,7 @@ __global__ __launch_bounds__(256) void dsvi_kl_kernel(Args a) {
     ld2 = dlog(c2);
     t2 = a1 / (c2 * c2);
     t3 = fac_mu<T>(a, f)[i] * fac_y<T>(a, f)[i];
-    T* ev = fb + NF + 8 * (int64_t)M + 4 * (int64_t)D * D + (int64_t)f * M;
+    T* ev = fb + NF + 8 * (int64_t)M + 4 * pair_cols(a) + (int64_t)f * M;
     ev[i] = (T)0.5 - (T)0.5 * a1 / (c2 * c2);   // d KL / d C2_ii * C2_ii / 2 + 1/2
   }
   // rows of this block in order: lane 0 of each 16-lane group holds one row's terms
@@ -415,7 +424,7 @@ __global__ __launch_bounds__(256) void dsvi_delta_kernel(Args a) {
   if (i >= M) return;
   T* fb = (T*)a.facbuf;
   const T* C2 = (const T*)a.Afac + (int64_t)(NF + k) * MM;
-  const T* ev = fb + NF + 8 * (int64_t)M + 4 * (int64_t)D * D;
+  const T* ev = fb + NF + 8 * (int64_t)M + 4 * pair_cols(a);
   T dl = 0;
   for (int f = 0; f < NF; ++f)
     if (prior_of(f, D) == k) dl += ev[(int64_t)f * M + i];
@@ -535,7 +544,7 @@ __global__ __launch_bounds__(256) void dsvi_mugrad_kernel(Args a) {
   T* __restrict__ gw = (T*)a.grad;
   const T* __restrict__ Y = (const T*)a.Y;
   const T* __restrict__ vbar = (const T*)a.vbar + M;   // completed by the v-backward kernel
-  const int64_t DM = (int64_t)D * M, DDM = (int64_t)D * D * M;
+  const int64_t DM = (int64_t)D * M, DDM = pair_cols(a) * M;
   const int64_t yu0 = (int64_t)(D + 1) * M, yu1 = yu0 + DDM;
   const int64_t n = DM + M + DDM, stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -547,7 +556,13 @@ __global__ __launch_bounds__(256) void dsvi_mugrad_kernel(Args a) {
     } else {
       const int64_t idx = i - DM - M;
       const int ij = (int)(idx / M);
-      const int pi = ij / D, pj = ij - pi * D;
+      int pi, pj;
+      if (a.pair_packed) {
+        pair_ij(ij, pi, pj);
+      } else {
+        pi = ij / D;
+        pj = ij - pi * D;
+      }
       if (pj <= pi) gw[a.off_muU + idx] = gw[a.off_muU + idx] + Y[(pi == pj ? yu1 : yu0) + idx];
     }
   }
@@ -981,7 +996,7 @@ template <typename T> static int dsvi_vbwd(const Args* a, hipStream_t s) {
 }
 template <typename T> static int dsvi_mugrad(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
-  const int64_t n = (int64_t)a->D * a->M + a->M + (int64_t)a->D * a->D * a->M;
+  const int64_t n = (int64_t)a->D * a->M + a->M + (a->pair_packed ? (int64_t)a->Q : (int64_t)a->D * a->D) * a->M;
   hipLaunchKernelGGL(dsvi_mugrad_kernel<T>, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 2048)), dim3(256), 0, s,
                      *a);
   NMGP_CHECK_LAUNCH();

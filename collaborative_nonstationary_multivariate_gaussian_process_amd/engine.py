@@ -33,9 +33,19 @@ PARAM_NAMES = ["mu_W", "sqrt_W", "mu_v", "sqrt_v", "mu_U", "sqrt_U",
 HYPER_NAMES = PARAM_NAMES[6:]
 
 
-def param_layout(D, M):
-    """Offsets (elements) of the 13 parameters inside the flat theta vector, registration order."""
-    shapes = [(D, M), (D, M, M), (M,), (M, M), (D, D, M), (D, D, M, M)] + [()] * 7
+def param_layout(D, M, packed=False):
+    """Offsets (elements) of the 13 parameters inside the flat theta vector, registration order.
+
+    packed=False: the reference's dense layout, mu_U (D, D, M) and sqrt_U (D, D, M, M) with all D^2
+    coefficient blocks (code/nmgp_dsvi.py:136-143).  packed=True: only the Q = D(D+1)/2 live pairs
+    (i, j <= i) in (i, j) order, mu_U (Q, M) and sqrt_U (Q, M, M) -- the dead upper blocks never
+    receive a gradient, and at the ECoG shape (D=128, M=1024) the dense layout is
+    69 GB per copy of sqrt_U in fp32 against 35 GB packed."""
+    Q = D * (D + 1) // 2
+    if packed:
+        shapes = [(D, M), (D, M, M), (M,), (M, M), (Q, M), (Q, M, M)] + [()] * 7
+    else:
+        shapes = [(D, M), (D, M, M), (M,), (M, M), (D, D, M), (D, D, M, M)] + [()] * 7
     offs, o = {}, 0
     for name, shp in zip(PARAM_NAMES, shapes):
         n = int(np.prod(shp)) if shp else 1
@@ -51,7 +61,10 @@ def pair_list(D):
 class DsviEngine:
     """Workspace + launch schedule of one DSVI step for fixed (D, M, B)."""
 
-    def __init__(self, D, M, B, z, device="cuda", jitter=JITTER, dtype=F64):
+    def __init__(self, D, M, B, z, device="cuda", jitter=JITTER, dtype=F64, packed=False, factor_ws=None):
+        """packed: the parameter vector uses the packed pair layout of param_layout.  factor_ws: the
+        (Afac, Cinv, Xs) factor workspaces of another engine of the same (D, M, dtype) to share (they
+        hold no state between steps; a model's engines never run concurrently)."""
         if not torch.cuda.is_available():
             raise RuntimeError("DsviEngine needs a HIP device; there is no CPU fallback")
         if dtype not in (F64, F32):
@@ -64,8 +77,10 @@ class DsviEngine:
         self.NF = D + 1 + self.Q
         self.dev = torch.device(device)
         self.jitter = jitter
-        self.offs, self.nparam = param_layout(D, M)
+        self.packed = bool(packed)
+        self.offs, self.nparam = param_layout(D, M, packed=self.packed)
         Q, NF = self.Q, self.NF
+        self.NPC = Q if self.packed else D * D     # pair columns of mu_U / Y_0 / Y_1 / sel
         e = lambda *shape: torch.zeros(*shape, dtype=self.dt, device=self.dev)
         self.Z = torch.as_tensor(np.asarray(z, np.float64).reshape(-1, 1), device=self.dev).to(self.dt).contiguous()
         assert self.Z.shape[0] == M
@@ -76,8 +91,13 @@ class DsviEngine:
         self.seg = torch.zeros(D + 1, dtype=torch.int32, device=self.dev)
         self.noise = e(M + B + Q * B)
         # factors
-        self.Afac = e(NF + 4, M, M)
-        self.Cinv = e(NF + 4, M, M)
+        if factor_ws is not None:
+            self.Afac, self.Cinv, self.Xs = factor_ws
+            assert self.Afac.shape == (NF + 4, M, M) and self.Afac.dtype == self.dt
+        else:
+            self.Afac = e(NF + 4, M, M)
+            self.Cinv = e(NF + 4, M, M)
+            self.Xs = e(NF, M, M)
         self.Ainv = e(4, M, M)
         self.K12 = e(4, B, M)
         self.P = e(4, B, M)
@@ -87,15 +107,14 @@ class DsviEngine:
         self.Abar = e(4, M, M)
         self.WG = e(D, B, M)
         self.WP = e(D, B, M)
-        self.Y = e(D + 1 + 2 * D * D, M)
-        self.Xs = e(NF, M, M)
+        self.Y = e(D + 1 + 2 * self.NPC, M)
         self.T2 = e(M, M)
         self.v, self.ellZ = e(M), e(M)
         self.vbar = e(2 * M)            # [0:M] P_t^T tbar (GEMM), [M:2M] completed by the v-backward kernel
         self.ellX, self.var_t = e(B), e(B)
         self.rowbuf = e(2 * D + 5, B)
         # KL per factor | delta/w vectors (8M) | selection weights (4D^2) | e_f rows (NF M) | KL slab partials
-        self.facbuf = e(NF + 8 * M + 4 * D * D + NF * M + NF * ((M + 15) // 16) * 4)
+        self.facbuf = e(NF + 8 * M + 4 * self.NPC + NF * M + NF * ((M + 15) // 16) * 4)
         self.nblk = B                       # recon partials: one per row; then (B+3)//4 t-row partials
         self.red = e(4 * B + (B + 3) // 4)
         self.out = e(8)
@@ -120,14 +139,21 @@ class DsviEngine:
             self.pri_A64 = torch.zeros(4, M, M, dtype=F64, device=self.dev)
             self.pri_X64 = torch.zeros(4, M, M, dtype=F64, device=self.dev)
         # selection weights for the -1/2 Y diag(sel) Y^T prior adjoint (static)
-        sel = np.zeros((4, D * D))
+        sel = np.zeros((4, self.NPC))
         for i in range(D):
             for j in range(i + 1):
-                sel[2 if i == j else 1, i * D + j] = 1.0
+                sel[2 if i == j else 1, self.pidx(i, j)] = 1.0
         base = NF + 8 * M
-        self.facbuf[base:base + 4 * D * D] = torch.from_numpy(sel.reshape(-1)).to(self.dev)
+        self.facbuf[base:base + 4 * self.NPC] = torch.from_numpy(sel.reshape(-1)).to(self.dev)
         self._theta = None
         self._plans = {}
+
+    def pidx(self, i, j):
+        """Block index of coefficient pair (i, j) in mu_U / sqrt_U (dense i*D + j, or packed)."""
+        return i * (i + 1) // 2 + j if self.packed else i * self.D + j
+
+    def factor_workspace(self):
+        return (self.Afac, self.Cinv, self.Xs)
 
     # ------------------------------------------------------------------------------------ binding
     def bind(self, theta, grad, frozen_mask=0, N=None):
@@ -149,6 +175,7 @@ class DsviEngine:
         D, M, B = self.D, self.M, self.B
         a.D, a.M, a.B, a.Q, a.NF = D, M, B, self.Q, self.NF
         a.elbo_mode, a.frozen_mask = elbo_mode, self.frozen_mask
+        a.pair_packed = 1 if self.packed else 0
         a.N_over_B = float(self.N) / float(B)
         a.jitter = self.jitter
         a.theta, a.grad = self._theta.data_ptr(), self._grad.data_ptr()
@@ -176,7 +203,9 @@ class DsviEngine:
         muW, muv, muU, hyp = o["mu_W"][0], o["mu_v"][0], o["mu_U"][0], o["sigma2_tildeell_log"][0]
         pairs = pair_list(D)
         # factor order: W (D) | pairs (Q) | v  -> v and the 3 static priors are contiguous slots NF-1..NF+2
-        fac_off = [sW + d * MM for d in range(D)] + [sU + (i * D + j) * MM for (i, j) in pairs] + [sv]
+        pq = self.pidx
+        NPC = self.NPC
+        fac_off = [sW + d * MM for d in range(D)] + [sU + pq(i, j) * MM for (i, j) in pairs] + [sv]
         prior_of = [3] * D + [2 if i == j else 1 for (i, j) in pairs] + [0]
         FV = NF - 1
         dev, seg = self.dev, self.seg
@@ -228,9 +257,9 @@ class DsviEngine:
         # F6: P_k = K12_k Ainv_k (k = t,0,1) ; Y_t, Y_0, Y_1
         d6 = [pproj(k) for k in range(3)]
         d6 += [g(self.Y, self.Ainv, th, M, 1, M, (M, 1, 0), (1, M, 0), (1, M), offs=(0, muv, D * M)),
-               g(self.Y, self.Ainv, th, M, D * D, M, (M, 1, 0), (1, M, 0), (1, M), offs=(MM, muU, (D + 1) * M)),
-               g(self.Y, self.Ainv, th, M, D * D, M, (M, 1, 0), (1, M, 0), (1, M),
-                 offs=(2 * MM, muU, (D + 1 + D * D) * M))]
+               g(self.Y, self.Ainv, th, M, NPC, M, (M, 1, 0), (1, M, 0), (1, M), offs=(MM, muU, (D + 1) * M)),
+               g(self.Y, self.Ainv, th, M, NPC, M, (M, 1, 0), (1, M, 0), (1, M),
+                 offs=(2 * MM, muU, (D + 1 + NPC) * M))]
         p["proj3"] = G(d6)
         # F9: Gibbs builders (K_G22 + lam I into the G prior slot, K_G12)
         # K_G22 + lam I needs only ell_Z (the v sample) and feeds chol_G on the main chain; K_G12 also needs
@@ -254,7 +283,7 @@ class DsviEngine:
             typ = 2 if i == j else 1
             slot, rseg = (j, i) if not elbo_mode else (i, j)
             d14.append(g(self.WP, self.P, th, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), flags=L.B_LOWER,
-                         offs=(typ * BM, sU + (i * D + j) * MM, slot * BM), row_seg=rseg))
+                         offs=(typ * BM, sU + pq(i, j) * MM, slot * BM), row_seg=rseg))
         p["quad"] = G(d14)
         if elbo_mode:
             self._plans[elbo_mode] = p
@@ -264,10 +293,10 @@ class DsviEngine:
                  beta=1.0, offs=(0, sW, 3 * BM), **rows_all)]
         for i in range(D):
             d17.append(g(self.Pbar, self.WP, th, B, M, M, (M, 1, 0), (1, M, 0), (M, 1), flags=L.B_UPPER, beta=1.0,
-                         offs=(i * BM, sU + (i * D + i) * MM, 2 * BM), row_seg=i))
+                         offs=(i * BM, sU + pq(i, i) * MM, 2 * BM), row_seg=i))
             if i > 0:
                 d17.append(g(self.Pbar, self.WP, th, B, M, i * M, (M, 1, BM), (1, M, MM), (M, 1), flags=L.B_UPPER,
-                             kb=(M, M), beta=1.0, offs=(0, sU + (i * D) * MM, 1 * BM), row_seg=i))
+                             kb=(M, M), beta=1.0, offs=(0, sU + pq(i, 0) * MM, 1 * BM), row_seg=i))
         # the P-bar products feed R (main chain); the L-bar / mu-bar products below only accumulate
         # gradient rows, so they run on the side stream beside bwd_R .. bwd_v2
         p["bwd_w"] = G(d17)
@@ -280,9 +309,9 @@ class DsviEngine:
         for (i, j) in pairs:
             typ = 2 if i == j else 1
             d17.append(g(gr, self.P, self.WP, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_TRIL, beta=1.0,
-                         offs=(typ * BM, j * BM, sU + (i * D + j) * MM), k_seg=i))
+                         offs=(typ * BM, j * BM, sU + pq(i, j) * MM), k_seg=i))
             d17.append(g(gr, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1), beta=1.0,
-                         offs=(typ * BM, (D + j) * B, muU + (i * D + j) * M), k_seg=i))
+                         offs=(typ * BM, (D + j) * B, muU + pq(i, j) * M), k_seg=i))
         if not (self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0"):
             p["bwd_lbar"] = G(d17)
         else:
@@ -293,7 +322,7 @@ class DsviEngine:
                               b_kcontig=False, flags=L.OUT_TRIL, beta=1.0,
                               kseg=(seg, list(range(D)), [D - d for d in range(D)]))
             bw_u = H.BigBatch(self.P, self.WP, gr, [(2 if i == j else 1) * BM for (i, j) in pairs],
-                              [j * BM for (i, j) in pairs], [sU + (i * D + j) * MM for (i, j) in pairs], M, M, B,
+                              [j * BM for (i, j) in pairs], [sU + pq(i, j) * MM for (i, j) in pairs], M, M, B,
                               lda=M, ldb=M, a_kcontig=False, b_kcontig=False, flags=L.OUT_TRIL, beta=1.0,
                               kseg=(seg, [i for (i, j) in pairs], [1] * len(pairs)))
             mu = G([dd for dd in d17 if dd.n == 1])
@@ -328,12 +357,12 @@ class DsviEngine:
                                       epi=(th, fac_off, (M, 1), fb, [NF + 4 * M + prior_of[f] * M for f in range(NF)],
                                            1.0))
         # B4: Abar_k -= 1/2 Y_k diag(sel_k) Y_k^T
-        ybase = [D * M, (D + 1) * M, (D + 1 + D * D) * M, 0]
-        ncol = [1, D * D, D * D, D]
+        ybase = [D * M, (D + 1) * M, (D + 1 + NPC) * M, 0]
+        ncol = [1, NPC, NPC, D]
         sel_base = NF + 8 * M
         d19 = []
         for k in range(4):
-            ks = (fb, sel_base + k * D * D) if k in (1, 2) else None
+            ks = (fb, sel_base + k * NPC) if k in (1, 2) else None
             d19.append(g(self.Abar, self.Y, self.Y, M, M, ncol[k], (1, M, 0), (M, 1, 0), (M, 1), alpha=-0.5,
                          beta=1.0, kscale=ks, offs=(ybase[k], ybase[k], k * MM)))
         p["bwd_kly"] = G(d19)

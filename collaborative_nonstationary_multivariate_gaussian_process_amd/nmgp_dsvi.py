@@ -95,36 +95,55 @@ class NMGP(Model):
     """code/nmgp_dsvi.py:99-155: variational parameters + 7 log hyper-parameters."""
 
     def __init__(self, number_observations, dim_outputs, Z, minibatch_size=None, mu_v=None, mu_W=None, mu_U=None,
-                 sqrt_v=None, sqrt_W=None, sqrt_U=None, seed=22, device=None, noise="torch", dtype=F64):
+                 sqrt_v=None, sqrt_W=None, sqrt_U=None, seed=22, device=None, noise="torch", dtype=F64,
+                 pair_layout="auto"):
         """Reference signature plus: ``device``; ``noise`` ("torch": the reference's CPU randn stream,
         "device": Philox on the GPU); ``dtype`` (float64 = the reference's arithmetic; float32 for
-        the HCP / ECoG-shaped configurations, SURVEY §8d, parity gates loss 1e-3 / grad 2e-2)."""
+        the HCP / ECoG-shaped configurations, SURVEY §8d, parity gates loss 1e-3 / grad 2e-2);
+        ``pair_layout`` ("dense": mu_U (D, D, M) and sqrt_U (D, D, M, M) as the reference; "packed":
+        only the Q = D(D+1)/2 live pairs, (Q, M) and (Q, M, M); "auto": packed when the dense sqrt_U
+        would exceed 2^31 elements, e.g. the ECoG shape D=128, M=1024).  state_dict() always exports
+        the reference's dense shapes (dead upper pairs zero) and load_state_dict accepts them.
+
+        Packed-layout initialisation without explicit mu_U / sqrt_U draws the live pairs' 0.1 N(0,1)
+        values on the device (seeded by `seed`): the reference's CPU draw of all D^2 M^2 values is 69
+        GB at the ECoG shape.  Pass mu_U / sqrt_U to reproduce a reference initialisation."""
         super().__init__()
         if dtype not in (torch.float64, torch.float32):
             raise ValueError("dtype must be torch.float64 or torch.float32")
         D = dim_outputs
         Zt = torch.as_tensor(Z).detach().to(F64).reshape(-1, 1)
         M = int(Zt.shape[0])
+        if pair_layout not in ("dense", "packed", "auto"):
+            raise ValueError("pair_layout must be 'dense', 'packed' or 'auto'")
+        packed = pair_layout == "packed" or (pair_layout == "auto" and D * D * M * M > 2 ** 31)
+        dev = torch.device(device) if device is not None else _default_device()
         # reference initialisation order on the CPU generator (code/nmgp_dsvi.py:115-155)
         torch.random.manual_seed(seed)
         init = {}
-        init["mu_W"] = 0.1 * torch.randn(D, M).to(F64) if mu_W is None else torch.from_numpy(np.asarray(mu_W)).to(F64)
-        init["sqrt_W"] = 0.1 * torch.randn(D, M, M).to(F64) if sqrt_W is None else torch.from_numpy(np.asarray(sqrt_W)).to(F64)
-        init["mu_v"] = -4 * torch.ones(M, dtype=F64) if mu_v is None else torch.from_numpy(np.asarray(mu_v)).to(F64)
-        init["sqrt_v"] = 0.1 * torch.randn(M, M).to(F64) if sqrt_v is None else torch.from_numpy(np.asarray(sqrt_v)).to(F64)
-        init["mu_U"] = 0.1 * torch.randn(D, D, M).to(F64) if mu_U is None else torch.from_numpy(np.asarray(mu_U)).to(F64)
-        init["sqrt_U"] = 0.1 * torch.randn(D, D, M, M).to(F64) if sqrt_U is None else torch.from_numpy(np.asarray(sqrt_U)).to(F64)
+        arr = lambda a: torch.from_numpy(np.asarray(a)).to(F64)
+        init["mu_W"] = 0.1 * torch.randn(D, M).to(F64) if mu_W is None else arr(mu_W)
+        init["sqrt_W"] = 0.1 * torch.randn(D, M, M).to(F64) if sqrt_W is None else arr(sqrt_W)
+        init["mu_v"] = -4 * torch.ones(M, dtype=F64) if mu_v is None else arr(mu_v)
+        init["sqrt_v"] = 0.1 * torch.randn(M, M).to(F64) if sqrt_v is None else arr(sqrt_v)
+        if not packed:
+            init["mu_U"] = 0.1 * torch.randn(D, D, M).to(F64) if mu_U is None else arr(mu_U)
+            init["sqrt_U"] = 0.1 * torch.randn(D, D, M, M).to(F64) if sqrt_U is None else arr(sqrt_U)
+        else:
+            init["mu_U"] = None if mu_U is None else _pack_pairs(arr(mu_U), D)
+            init["sqrt_U"] = None if sqrt_U is None else _pack_pairs(arr(sqrt_U), D)
         hyper0 = [0., -4., 0., -4., 0., -4., -2.]
         for k, v in zip(HYPER_NAMES, hyper0):
             init[k] = torch.tensor(v, dtype=F64)
-        self._setup(number_observations, D, Zt, minibatch_size, noise, dtype,
-                    torch.device(device) if device is not None else _default_device(), seed, init=init)
+        self._setup(number_observations, D, Zt, minibatch_size, noise, dtype, dev, seed, init=init, packed=packed)
 
-    def _setup(self, N, D, Zt, batch_size, noise, dtype, device, seed, init=None, theta=None):
+    def _setup(self, N, D, Zt, batch_size, noise, dtype, device, seed, init=None, theta=None, packed=False):
         """Allocate the flat parameter vector on `device` and register the 13 parameters as views of it
-        (from per-parameter `init` tensors, or from an already flat host `theta`)."""
+        (from per-parameter `init` tensors, or from an already flat host `theta`).  init[k] None: the
+        packed pair parameters, drawn on the device (0.1 N(0,1), generator seeded by `seed`)."""
         self.dtype_ = dtype
         self.device_ = device
+        self.packed = bool(packed)
         self.Z = Zt.to(self.device_)
         self.M = int(Zt.shape[0])
         self.N = N
@@ -133,7 +152,7 @@ class NMGP(Model):
         self.noise = noise
         self.sigma2_g = 1
         M = self.M
-        self._offs, n = param_layout(D, M)
+        self._offs, n = param_layout(D, M, packed=self.packed)
         if theta is not None:
             assert theta.numel() == n
             self._theta = theta.to(device=self.device_, dtype=dtype).contiguous()
@@ -146,7 +165,12 @@ class NMGP(Model):
             cnt = int(np.prod(shp)) if shp else 1
             view = self._theta[o:o + cnt].view(shp)
             if init is not None:
-                view.copy_(init[k].reshape(shp))
+                if init[k] is None:
+                    gen = torch.Generator(device=self.device_)
+                    gen.manual_seed(int(seed) * 1000003 + PARAM_NAMES.index(k))
+                    view.copy_(0.1 * torch.randn(shp, generator=gen, device=self.device_, dtype=dtype))
+                else:
+                    view.copy_(init[k].reshape(shp))
             setattr(self, k, Parameter(view))
             self._grad_views.append(self._grad[o:o + cnt].view(shp))
         self._engines = {}
@@ -162,7 +186,8 @@ class NMGP(Model):
                  "noise": self.noise, "dtype": str(self.dtype_).replace("torch.", ""),
                  "device": str(self.device_), "seed": self._noise_seed,
                  "noise_counter": int(self._noise_counter.cpu()[0]), "theta": self._theta.detach().cpu(),
-                 "requires_grad": {k: bool(getattr(self, k).requires_grad) for k in PARAM_NAMES}}
+                 "requires_grad": {k: bool(getattr(self, k).requires_grad) for k in PARAM_NAMES},
+                 "packed": self.packed}
         return (_rebuild_nmgp, (state,))
 
     # ------------------------------------------------------------------------------ plumbing
@@ -181,6 +206,34 @@ class NMGP(Model):
                 raise RuntimeError(f"parameter {k} no longer aliases the flat device vector "
                                    "(re-assigning .data is not supported; use .data.copy_)")
 
+    def mu_U_dense(self):
+        """mu_U in the reference's (D, D, M) layout (zero dead upper pairs in the packed layout)."""
+        return _unpack_pairs(self.mu_U.detach(), self.D) if self.packed else self.mu_U.detach()
+
+    def sqrt_U_pair(self, i, j):
+        """The (M, M) block of coefficient pair (i, j <= i), in either layout."""
+        return self.sqrt_U[i * (i + 1) // 2 + j] if self.packed else self.sqrt_U[i, j]
+
+    def state_dict(self, *args, **kwargs):
+        """The reference's 13 keys with its dense shapes (code/nmgp_dsvi.py:117-155, model.pt)."""
+        sd = super().state_dict(*args, **kwargs)
+        if self.packed:
+            prefix = kwargs.get("prefix", args[1] if len(args) > 1 else "")
+            for k in ("mu_U", "sqrt_U"):
+                sd[prefix + k] = _unpack_pairs(sd[prefix + k].detach(), self.D)
+        return sd
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        if self.packed:
+            state_dict = dict(state_dict)
+            for k in ("mu_U", "sqrt_U"):
+                v = state_dict.get(k)
+                if v is not None and tuple(v.shape[:2]) == (self.D, self.D):
+                    state_dict[k] = _pack_pairs(v, self.D)
+        if assign:
+            raise ValueError("assign=True would detach the parameters from the flat device vector")
+        return super().load_state_dict(state_dict, strict=strict)
+
     def check_numerics(self, engines=None):
         """Synchronise and raise like the reference would: torch.linalg.LinAlgError when a Cholesky
         factor was not positive-definite (the reference's torch.cholesky raises, code/utils.py:46,
@@ -192,8 +245,9 @@ class NMGP(Model):
     def engine(self, B, N=None):
         eng = self._engines.get(B)
         if eng is None:
+            ws = next(iter(self._engines.values())).factor_workspace() if self._engines else None
             eng = DsviEngine(self.D, self.M, B, self.Z.cpu().numpy().reshape(-1), device=self.device_,
-                             dtype=self.dtype_)
+                             dtype=self.dtype_, packed=self.packed, factor_ws=ws)
             self._engines[B] = eng
         eng.bind(self._theta, self._grad, frozen_mask=self._frozen_mask(), N=self.N if N is None else N)
         return eng
@@ -279,6 +333,20 @@ class NMGP(Model):
         return predict.predict_mean(self, inputs_list, index)
 
 
+def _pack_pairs(dense, D):
+    """(D, D, ...) -> (Q, ...): the live pairs (i, j <= i) in (i, j) order."""
+    ii, jj = np.tril_indices(D)
+    return dense[torch.from_numpy(ii), torch.from_numpy(jj)].contiguous()
+
+
+def _unpack_pairs(packed, D):
+    """(Q, ...) -> (D, D, ...) with zero dead (upper) pairs."""
+    out = torch.zeros((D, D) + tuple(packed.shape[1:]), dtype=packed.dtype, device=packed.device)
+    ii, jj = np.tril_indices(D)
+    out[torch.from_numpy(ii).to(packed.device), torch.from_numpy(jj).to(packed.device)] = packed
+    return out
+
+
 def _rebuild_nmgp(state):
     """Unpickle an NMGP (see NMGP.__reduce__) onto its saved device, or the current one."""
     dev = torch.device(state["device"])
@@ -289,7 +357,8 @@ def _rebuild_nmgp(state):
     m = NMGP.__new__(NMGP)
     torch.nn.Module.__init__(m)
     m._setup(state["N"], state["D"], state["Z"], state["batch_size"], state["noise"],
-             getattr(torch, state["dtype"]), dev, state["seed"], theta=state["theta"])
+             getattr(torch, state["dtype"]), dev, state["seed"], theta=state["theta"],
+             packed=state.get("packed", False))
     for k, rg in state["requires_grad"].items():
         getattr(m, k).requires_grad = rg
     m._noise_counter.fill_(int(state["noise_counter"]))
@@ -336,9 +405,7 @@ def _apply_hyperpars(model, hyperpars, fix_hyperpars, continuous_training, PATH,
             model.sigma2_err_log.data.fill_(hyperpars["sigma2_err_log"])
     if continuous_training:
         ck = torch.load(PATH, weights_only=True, map_location="cpu")
-        with torch.no_grad():
-            for k, v in ck["model_state_dict"].items():
-                getattr(model, k).data.copy_(v.to(F64))
+        model.load_state_dict(ck["model_state_dict"])
         optimizer_state.update(ck.get("optimizer_state_dict", {}) or {})
     if fix_hyperpars:
         for name in ["length_scales_tildeell_log", "length_scales_L0_log", "length_scales_L1_log"]:
@@ -396,8 +463,11 @@ class DsviTrainer:
                 continue
             if not trainable:
                 continue
-            self.m[o:o + n] = st["exp_avg"].reshape(-1).to(self.m.dtype)
-            self.v[o:o + n] = st["exp_avg_sq"].reshape(-1).to(self.v.dtype)
+            ea, eq = st["exp_avg"], st["exp_avg_sq"]
+            if m.packed and name in ("mu_U", "sqrt_U") and tuple(ea.shape[:2]) == (m.D, m.D):
+                ea, eq = _pack_pairs(ea, m.D), _pack_pairs(eq, m.D)
+            self.m[o:o + n] = ea.reshape(-1).to(self.m.dtype)
+            self.v[o:o + n] = eq.reshape(-1).to(self.v.dtype)
             steps.add(int(float(st["step"])))
         if len(steps) > 1 or (steps and missing):
             raise NotImplementedError(
@@ -746,8 +816,10 @@ def _adam_state_dict(model, trainer):
             continue
         o, shp = model._offs[name]
         n = int(np.prod(shp)) if shp else 1
-        state[idx] = {"step": torch.tensor(step), "exp_avg": trainer.m[o:o + n].reshape(shp).cpu(),
-                      "exp_avg_sq": trainer.v[o:o + n].reshape(shp).cpu()}
+        ea, eq = trainer.m[o:o + n].reshape(shp), trainer.v[o:o + n].reshape(shp)
+        if model.packed and name in ("mu_U", "sqrt_U"):      # the reference's dense shapes
+            ea, eq = _unpack_pairs(ea, model.D), _unpack_pairs(eq, model.D)
+        state[idx] = {"step": torch.tensor(step), "exp_avg": ea.cpu(), "exp_avg_sq": eq.cpu()}
     return {"state": state, "param_groups": [{"lr": trainer.lr, "betas": tuple(trainer.betas), "eps": trainer.eps,
                                               "weight_decay": 0,
                                               "amsgrad": False, "params": list(range(len(PARAM_NAMES)))}]}

@@ -51,7 +51,7 @@ def predict_mean(model, inputs_list, index=None):
     K022 = rbf(Z, Z, hyp["sigma2_L0_log"], hyp["length_scales_L0_log"])
     K112 = rbf(x, Z, hyp["sigma2_L1_log"], hyp["length_scales_L1_log"])
     K122 = rbf(Z, Z, hyp["sigma2_L1_log"], hyp["length_scales_L1_log"])
-    muU = th["mu_U"].reshape(D * D, M).t().contiguous()                 # (M, D*D)
+    muU = model.mu_U_dense().to(F64).reshape(D * D, M).t().contiguous()   # (M, D*D)
     L0 = _solve_rows(K012, K022, muU)                                   # (B, D*D)
     L1 = _solve_rows(K112, K122, muU)
     KG12 = H.pairwise(x, Z, mode=L.GIBBS, ellX=ellX, ellZ=ellZ)
@@ -116,7 +116,8 @@ def _sampling_setup(model, x):
     dev = model.device_
     D, M = model.D, model.M
     Z = model.Z
-    p = {k: getattr(model, k).detach().to(F64) for k in ["mu_W", "sqrt_W", "mu_v", "sqrt_v", "mu_U", "sqrt_U"]}
+    p = {k: getattr(model, k).detach().to(F64) for k in ["mu_W", "sqrt_W", "mu_v", "sqrt_v"]}
+    p["mu_U"] = model.mu_U_dense().to(F64)
     hyp = {k: float(torch.exp(getattr(model, k).detach().to(F64))) for k in
            ["sigma2_tildeell_log", "length_scales_tildeell_log", "sigma2_L0_log", "length_scales_L0_log",
             "sigma2_L1_log", "length_scales_L1_log", "sigma2_err_log"]}
@@ -149,7 +150,7 @@ def _sampling_setup(model, x):
     for (i, j) in pairs:
         P, base = (P1, b1) if i == j else (P0, b0)
         mus.append(H.matmul(P, p["mu_U"][i, j].reshape(M, 1).contiguous()).reshape(N))
-        PL = H.matmul(P, _tril(p["sqrt_U"][i, j]).contiguous(), maskB=L.B_LOWER)
+        PL = H.matmul(P, _tril(model.sqrt_U_pair(i, j).detach().to(F64)).contiguous(), maskB=L.B_LOWER)
         sds.append(torch.sqrt(base + (PL * PL).sum(1) + JIT))
     st["pairs"], st["pair_mu"], st["pair_sd"] = pairs, torch.stack(mus), torch.stack(sds)   # (Q, N)
     st["lW"] = _tril(p["sqrt_W"]).contiguous()                           # (D, M, M)

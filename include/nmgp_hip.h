@@ -280,7 +280,8 @@ int nmgp_kron_mv_f32(const float* B, int64_t P1, int64_t P2, const float* K, int
  * row / reduction kernels below, all reading one argument block.  See DESIGN.md §4.       */
 typedef struct nmgp_dsvi_args {
   /* sizes */
-  int32_t D, M, B, Q, NF, elbo_mode, frozen_mask, pad0_;
+  int32_t D, M, B, Q, NF, elbo_mode, frozen_mask;
+  int32_t pair_packed;         /* 0: mu_U (D,D,M), sqrt_U (D,D,M,M) as the reference; 1: (Q,M), (Q,M,M) */
   double N_over_B, jitter;
   /* parameters: flat theta in the registration order of code/nmgp_dsvi.py:117-155 */
   const void* theta; void* grad;

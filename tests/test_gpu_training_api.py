@@ -270,3 +270,45 @@ def test_drivers_vtvlcm_run_and_reload(tmp_path):
                                            device="cuda:0", noise="device", dtype=torch.float32)
     assert model._theta.dtype == torch.float32 and len(losses) == 3
     assert float(model.length_scales_tildeell_log) == 5
+
+
+# ------------------------------------------------------------------------------ packed pair layout
+def test_packed_pair_layout_matches_dense():
+    """pair_layout="packed" (the ECoG memory layout: Q live pairs instead of D^2 blocks) gives the same
+    loss and gradients as the reference's dense layout; state_dict exports / accepts dense shapes."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP, DsviTrainer
+    g = G.load("mid_forward")
+    xs, ys = G.split_lists(g)
+    p = G.params(g, D=3, M=64)
+    res = {}
+    for layout in ("dense", "packed"):
+        m = NMGP(4096, 3, g["z"], device="cuda:0", noise="device", pair_layout=layout,
+                 **{k: p[k].numpy() for k in ["mu_W", "sqrt_W", "mu_v", "sqrt_v", "mu_U", "sqrt_U"]})
+        with torch.no_grad():
+            for k in O.PARAM_NAMES[6:]:
+                getattr(m, k).data.fill_(float(p[k]))
+        assert m.packed == (layout == "packed")
+        sd = m.state_dict()
+        assert tuple(sd["sqrt_U"].shape) == (3, 3, 64, 64) and tuple(sd["mu_U"].shape) == (3, 3, 64)
+        eng = m.engine(sum(len(x) for x in xs))
+        eng.load_batch(g["x"], g["y"], [len(x) for x in xs], noise=g["noise"])
+        tr = DsviTrainer(m, lr=0.01)
+        tr.grad_step(eng, noise=g["noise"])
+        torch.cuda.synchronize()
+        eng.check_info()
+        grads = {k: v.clone() for k, v in zip(O.PARAM_NAMES, m._grad_views)}
+        if m.packed:
+            from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import _unpack_pairs
+            grads = {k: (_unpack_pairs(v, 3) if k in ("mu_U", "sqrt_U") else v) for k, v in grads.items()}
+        res[layout] = (float(eng.out[0]), grads, m)
+    (ld, gd, md), (lp, gp, mp) = res["dense"], res["packed"]
+    assert lp == pytest.approx(ld, rel=1e-13)
+    for k in O.PARAM_NAMES:
+        if float(gd[k].norm()) > 0:
+            assert _rel(gp[k], gd[k]) < 1e-12, k
+    # the packed model's dense export holds the live pairs; a dense state_dict loads into it
+    ii, jj = np.tril_indices(3)
+    for k in ("mu_U", "sqrt_U"):
+        assert torch.equal(mp.state_dict()[k][ii, jj], md.state_dict()[k][ii, jj])
+    mp.load_state_dict(md.state_dict())
+    assert torch.equal(mp.sqrt_U.detach(), md.sqrt_U.detach()[ii, jj])
