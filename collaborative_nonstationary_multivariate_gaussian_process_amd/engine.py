@@ -286,6 +286,10 @@ class DsviEngine:
                          offs=(typ * BM, sU + pq(i, j) * MM, slot * BM), row_seg=rseg))
         p["quad"] = G(d14)
         if elbo_mode:
+            # later Monte-Carlo samples of compute_ELBO: the pair factors W_P = P_{0,1} L_ij do not depend
+            # on the sample (the L priors and Sigma_U are fixed within a call) -- only the D latent ones
+            p["quad_W"] = G(d14[:D])
+        if elbo_mode:
             self._plans[elbo_mode] = p
             return p
         # B2: P-bar += W-hat L^T ; L-bar = P^T W-hat ; mu-bar = P^T adjoints
@@ -481,7 +485,7 @@ class DsviEngine:
     def _call(self, fn, a, s):
         L.check(fn(ctypes.byref(a), s), fn.__name__)
 
-    def _schedule(self, elbo_mode, with_kl=True):
+    def _schedule(self, elbo_mode, with_kl=True, cached=False):
         """The ordered launch list of one step.  Items are (name, kind, callable(stream), where) with
         where in {"main", "side"}, plus ("fork",) / ("join",) markers: the D+Q variational factors that
         only the KL terms need are factored on a side stream, overlapping the forward chain."""
@@ -592,6 +596,15 @@ class DsviEngine:
                 steps.append(("kl", "row", row(getattr(lib, "nmgp_dsvi_kl_" + self.sfx)), "main"))
             steps += [("recon", "row", row(getattr(lib, "nmgp_dsvi_recon_" + self.sfx)), "main"),
                       ("finalize", "row", row(getattr(lib, "nmgp_dsvi_finalize_" + self.sfx)), "main")]
+            if cached:
+                # sample-independent work of an earlier sample of the same compute_ELBO call is reused:
+                # the RBF priors t, L0, L1 (builds, factors, inverses, projections P / T / Y), chol(Sigma_v)
+                # and the pair quadratic-form factors W_P; per sample only v, ell_X, the Gibbs prior and
+                # the latent-function factors W_G are recomputed (code/nmgp_dsvi.py:330-376)
+                skip = {"build_rbf", "syrk", "chol", "inv3", "proj3"}
+                steps = [it for it in steps if not (len(it) == 4 and it[0] in skip)]
+                steps = [("quad_W",) + it[1:] if len(it) == 4 and it[0] == "quad" else it for it in steps]
+                steps = [(it[0], it[1], gemm("quad_W"), it[3]) if it[0] == "quad_W" else it for it in steps]
             return steps
         # KL branch on the side stream once all prior factors and Y = A^-1 mu exist (after projG):
         # KL terms, prior-diagonal adjoints, the variational factors' KL L-bar (first writer of those
@@ -725,13 +738,15 @@ class DsviEngine:
         self._run(self._sched, stream, timer)
         return self.out
 
-    def elbo_sample(self, stream=None, with_kl=False):
+    def elbo_sample(self, stream=None, with_kl=False, cached=False):
         """Enqueue one Monte-Carlo sample of compute_ELBO's reconstruction term (self.out[1]);
-        with_kl also evaluates the KL terms from THIS sample's K_G22 (out[2..4])."""
-        key = ("elbo", with_kl, self._theta.data_ptr(), self.frozen_mask, self.N)
+        with_kl also evaluates the KL terms from THIS sample's K_G22 (out[2..4]).  cached: reuse the
+        sample-independent factors of the previous (uncached) sample of the same call -- parameters,
+        data and the factor workspace must be unchanged since then."""
+        key = ("elbo", with_kl, cached, self._theta.data_ptr(), self.frozen_mask, self.N)
         cache = getattr(self, "_elbo_sched", {})
         if key not in cache:
-            cache[key] = self._schedule(1, with_kl)
+            cache[key] = self._schedule(1, with_kl, cached)
             self._elbo_sched = cache
         self._run(cache[key], stream, None)
         return self.out

@@ -371,3 +371,31 @@ def test_hcp_full_size_fp32_step_tracks_fp64():
     print("hcp full size: loss rel", abs(l32 - l64) / abs(l64), "grad rel-norm", _rel(g32, g64))
     assert abs(l32 - l64) / abs(l64) < 1e-3
     assert _rel(g32, g64) < 2e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_cached_elbo_samples_equal_full_samples(dtype):
+    """compute_ELBO's later samples reuse the sample-independent work of the first one (RBF priors,
+    chol(Sigma_v), pair quadratic forms): per-sample reconstruction terms and the last sample's KL are
+    bit-identical to recomputing everything per sample."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.engine import DsviEngine
+    g = G.load("mid_forward")
+    p = G.params(g, D=3, M=64)
+    sizes = [int(s) for s in g["sizes"]]
+    B = sum(sizes)
+    eng = DsviEngine(3, 64, B, g["z"], dtype=dtype)
+    theta = torch.cat([p[k].reshape(-1) for k in O.PARAM_NAMES]).to("cuda", dtype)
+    eng.bind(theta, torch.zeros_like(theta), N=float(g["N"]))
+    per = 64 + B + 6 * B
+    rng = np.random.default_rng(9)
+    noises = [rng.standard_normal(per).astype(np.float32) for _ in range(4)]
+    res = []
+    for cached in (False, True):
+        vals = []
+        for s, nz in enumerate(noises):
+            eng.load_batch(g["x"], g["y"], sizes, noise=nz)
+            out = eng.elbo_sample(with_kl=(s == 3), cached=cached and s > 0)
+            torch.cuda.synchronize()
+            vals.append(float(out[1]))
+        res.append((vals, [float(v) for v in out[2:5]]))
+    assert res[0] == res[1]
