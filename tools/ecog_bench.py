@@ -1,0 +1,112 @@
+"""ECoG-full-shaped configuration (BASELINE.json configs[3]) on one MI355X.
+
+  D = 128 channels (Q = 8256 coefficient pairs), M = 1024 inducing points, N = 50,048 rows (391 per
+  channel), fp32, packed Q-pair layout (pair_layout="packed": 35 GB per copy of the parameters instead
+  of 69 GB dense), device Philox noise.
+
+modes:
+  train  one DSVI iteration (B = 512 rows, forward + backward + Adam) replayed as a HIP graph: it/s.
+         Memory: parameters + gradient + Adam moments 141 GB, factor workspaces 106 GB.
+  elbo   compute_ELBO on all N rows, S Monte-Carlo samples (default 8 = one GPU's share of 64 over 8
+         GPUs): samples/s; the first sample of the call also builds the sample-independent factors
+         (RBF priors, pair quadratic forms), the last one the KL terms (8385 Cholesky factors).
+usage: python tools/ecog_bench.py {train|elbo} [--steps K] [--samples S] [--D 128] [--M 1024] [--rows 391]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def data(D, rows, seed=7):
+    rng = np.random.default_rng(seed)
+    xs = [np.sort(rng.uniform(0, 1, rows)) for _ in range(D)]
+    ys = [np.sin(6 * x + 0.1 * d) + 0.3 * rng.standard_normal(rows) for d, x in enumerate(xs)]
+    return xs, ys
+
+
+def model(D, M, N, dev):
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP
+    t0 = time.time()
+    m = NMGP(number_observations=N, dim_outputs=D, Z=np.linspace(0, 1, M), minibatch_size=512, seed=22, device=dev,
+             noise="device", dtype=torch.float32, pair_layout="packed")
+    for k in ["length_scales_tildeell_log", "length_scales_L0_log", "length_scales_L1_log"]:
+        getattr(m, k).data.fill_(float(np.log(3.0 / M)))
+        getattr(m, k).requires_grad = False
+    return m, time.time() - t0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", choices=["train", "elbo"])
+    ap.add_argument("--D", type=int, default=128)
+    ap.add_argument("--M", type=int, default=1024)
+    ap.add_argument("--rows", type=int, default=391)
+    ap.add_argument("--B", type=int, default=512)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--samples", type=int, default=8)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    D, M = a.D, a.M
+    xs, ys = data(D, a.rows)
+    N = D * a.rows
+    m, t_init = model(D, M, N, dev)
+    rec = {"config": f"ECoG-shaped: D={D}, Q={D * (D + 1) // 2}, M={M}, N={N}, fp32, packed pairs",
+           "init_s": round(t_init, 2), "param_GB": round(m._theta.numel() * 4 / 1e9, 2)}
+    if a.mode == "train":
+        from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import DsviTrainer
+        tr = DsviTrainer(m, lr=0.01)
+        eng = m.engine(a.B)
+        X = np.concatenate(xs); Y = np.concatenate(ys)
+        I = np.concatenate([np.full(a.rows, d) for d in range(D)])
+        rng = np.random.default_rng(3)
+        nb = 4
+        bx, by, bi, bs = [], [], [], []
+        for s in range(nb):
+            idx = rng.choice(N, a.B, replace=False)
+            idx = idx[np.argsort(I[idx], kind="stable")]
+            bx.append(X[idx]); by.append(Y[idx]); bi.append(I[idx])
+            bs.append(np.concatenate([[0], np.cumsum(np.bincount(I[idx], minlength=D))]))
+        f = lambda v, t: torch.tensor(np.stack(v), dtype=t, device=dev)
+        eng.bind_dataset(f(bx, torch.float32), f(by, torch.float32), f(bi, torch.int32), f(bs, torch.int32))
+        t0 = time.time()
+        g = tr.capture(eng)
+        torch.cuda.synchronize()
+        rec["capture_s"] = round(time.time() - t0, 2)
+        g.replay()
+        torch.cuda.synchronize()
+        m.check_numerics()
+        t0 = time.time()
+        for _ in range(a.steps):
+            g.replay()
+        torch.cuda.synchronize()
+        dt = (time.time() - t0) / a.steps
+        m.check_numerics()
+        rec.update({"mode": "train", "B": a.B, "steps": a.steps, "s_per_step": round(dt, 4), "it_per_s": round(1 / dt, 3),
+                    "loss": float(eng.out[0]), "peak_mem_GB": round(torch.cuda.max_memory_allocated() / 1e9, 1)})
+    else:
+        Xl = [torch.from_numpy(x) for x in xs]
+        Yl = [torch.from_numpy(y) for y in ys]
+        t0 = time.time()
+        e1 = m.compute_ELBO(Xl, Yl, n_sample=1)                 # one sample incl. factors + KL (and warm-up)
+        torch.cuda.synchronize()
+        t_one = time.time() - t0
+        t0 = time.time()
+        e = m.compute_ELBO(Xl, Yl, n_sample=a.samples)
+        torch.cuda.synchronize()
+        t_s = time.time() - t0
+        rec.update({"mode": "elbo", "samples": a.samples, "first_call_1_sample_s": round(t_one, 3),
+                    "call_s": round(t_s, 3), "samples_per_s": round(a.samples / t_s, 3), "elbo": float(e),
+                    "elbo_1": float(e1), "peak_mem_GB": round(torch.cuda.max_memory_allocated() / 1e9, 1)})
+    print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
