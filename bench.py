@@ -125,6 +125,43 @@ def stress_cholesky(dev, reps=5):
             "speedup_vs_cpu": round(t_cpu * 1e3 / t_fac, 1)}
 
 
+def elbo_sharded(dev, world, rank, dist, D=128, M=1024, rows=391, samples=64):
+    """North-star's sample-sharded ELBO (BASELINE.json configs[3], ECoG-full shape): compute_ELBO over all
+    N = D * rows observations with `samples` Monte-Carlo samples split round-robin over the ranks
+    (rank r runs samples r, r + W, ...; one scalar all-reduce; the owner of the last sample adds the KL
+    terms).  fp32, packed Q-pair layout, device Philox noise.  Timed after one warm-up call, barrier +
+    synchronize on both sides, max over ranks."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP
+    rng = np.random.default_rng(7)
+    xs = [torch.from_numpy(np.sort(rng.uniform(0, 1, rows))) for _ in range(D)]
+    ys = [torch.sin(6 * x + 0.1 * d) + 0.3 * torch.from_numpy(rng.standard_normal(rows)) for d, x in enumerate(xs)]
+    m = NMGP(number_observations=D * rows, dim_outputs=D, Z=np.linspace(0, 1, M), seed=22, device=dev,
+             noise="device", dtype=torch.float32, pair_layout="packed")
+    for k in ["length_scales_tildeell_log", "length_scales_L0_log", "length_scales_L1_log"]:
+        getattr(m, k).data.fill_(float(np.log(3.0 / M)))
+    m.compute_ELBO(xs, ys, n_sample=world, distributed=world > 1)          # warm-up: plans, first launches
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.time()
+    e = m.compute_ELBO(xs, ys, n_sample=samples, distributed=world > 1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.time() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    out = {"workload": f"compute_ELBO, ECoG-full shape D={D} (Q={D * (D + 1) // 2} pairs), M={M}, N={D * rows}, fp32, "
+                       f"{samples} MC samples sharded over {world} rank(s)",
+           "samples": samples, "ranks": world, "seconds": round(el, 4), "samples_per_s": round(samples / el, 3),
+           "elbo": float(e), "peak_mem_GB": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)}
+    del m
+    torch.cuda.empty_cache()
+    return out
+
+
 class PhaseTimer:
     """HIP events around every launch of an eager step (same stream as the kernels)."""
 
@@ -218,6 +255,8 @@ def main():
     ap.add_argument("--no-breakdown", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP graph (launch every kernel from Python)")
     ap.add_argument("--no-stress", action="store_true", help="skip the M=4096 stress Cholesky line (configs[4])")
+    ap.add_argument("--no-elbo", action="store_true", help="skip the sample-sharded ECoG compute_ELBO leg (configs[3])")
+    ap.add_argument("--elbo-D", type=int, default=128, help="channels of the ELBO leg (default: ECoG-full 128)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -355,6 +394,16 @@ def main():
                 roofline["traffic_unit"] = "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
                 roofline["traffic_source"] = os.path.relpath(summaries[-1], ROOT)
 
+    # free the headline workload before the large ELBO leg
+    elbo = None
+    if not args.no_elbo:
+        del graph, trainer, eng, model, Xb, Yb, Ib, Sb
+        torch.cuda.empty_cache()
+        try:
+            elbo = elbo_sharded(dev, world, rank, dist, D=args.elbo_D)
+        except Exception as exc:                        # reported, never masks the headline line
+            elbo = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds, xs, ys, z)
@@ -373,6 +422,7 @@ def main():
                           "global_batch": B * world, "parallelism": f"dp{world}" if world > 1 else "single",
                           "hip_graph": graph is not None},
                "roofline": roofline, "cpu_baseline": cpu, "cholesky": chol, "cholesky_stress": stress,
+               "elbo_sample_sharded": elbo,
                "phase_ms": breakdown,
                "final_loss": loss_val}
         if cpu is not None:

@@ -102,6 +102,21 @@ def main():
         e = m.compute_ELBO(Xl, Yl, n_sample=a.samples)
         torch.cuda.synchronize()
         t_s = time.time() - t0
+        # per-part costs on the engine: first (uncached) sample, a cached sample, the KL of the last one
+        eng = m._engines[N]
+        parts = {}
+        for name, kw in (("first_sample_s", dict(with_kl=False, cached=False)), ("cached_sample_s", dict(with_kl=False, cached=True)),
+                         ("cached_sample_with_kl_s", dict(with_kl=True, cached=True))):
+            eng.device_noise(1, m._noise_counter)
+            torch.cuda.synchronize()
+            t0 = time.time()
+            eng.elbo_sample(**kw)
+            torch.cuda.synchronize()
+            parts[name] = round(time.time() - t0, 4)
+        rec.update(parts)
+        c, f, k = parts["cached_sample_s"], parts["first_sample_s"], parts["cached_sample_with_kl_s"] - parts["cached_sample_s"]
+        rec["projected_64_samples_s"] = {str(W): round(f + (64 // W - 1) * c + k, 3) for W in (1, 2, 4, 8)}
+        rec["projected_scaling_8"] = round(rec["projected_64_samples_s"]["1"] / rec["projected_64_samples_s"]["8"], 2)
         rec.update({"mode": "elbo", "samples": a.samples, "first_call_1_sample_s": round(t_one, 3),
                     "call_s": round(t_s, 3), "samples_per_s": round(a.samples / t_s, 3), "elbo": float(e),
                     "elbo_1": float(e1), "peak_mem_GB": round(torch.cuda.max_memory_allocated() / 1e9, 1)})
