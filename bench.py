@@ -396,7 +396,9 @@ def main():
 
     # free the headline workload before the large ELBO leg
     elbo = None
+    used_graph = graph is not None
     if not args.no_elbo:
+        used_graph = graph is not None
         del graph, trainer, eng, model, Xb, Yb, Ib, Sb
         torch.cuda.empty_cache()
         try:
@@ -420,7 +422,7 @@ def main():
                "config": {"workload": "PM2.5-shaped synthetic DSVI step (BASELINE.json configs[1])",
                           "D_outputs": D, "M_inducing": M, "minibatch_rows": B, "N_observations": D * N_LOC,
                           "global_batch": B * world, "parallelism": f"dp{world}" if world > 1 else "single",
-                          "hip_graph": graph is not None},
+                          "hip_graph": used_graph},
                "roofline": roofline, "cpu_baseline": cpu, "cholesky": chol, "cholesky_stress": stress,
                "elbo_sample_sharded": elbo,
                "phase_ms": breakdown,
