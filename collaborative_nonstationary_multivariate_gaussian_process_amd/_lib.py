@@ -116,11 +116,13 @@ _SIGS = {
     "nmgp_pairwise_bwd_f64": (c_int, [c_vp, c_int, c_int, c_vp]),
     "nmgp_pairwise_bwd_f32": (c_int, [c_vp, c_int, c_int, c_vp]),
     "nmgp_pairwise_bwd_single_f64": (c_int, [ctypes.POINTER(PairwiseBwdDesc), c_vp]),
+    "nmgp_pairwise_bwd_single_f32": (c_int, [ctypes.POINTER(PairwiseBwdDesc), c_vp]),
     "nmgp_colsum_f64": (c_int, [c_vp, c_i64, c_i64, c_dbl, c_vp, c_vp]),
     "nmgp_colsum_f32": (c_int, [c_vp, c_i64, c_i64, c_dbl, c_vp, c_vp]),
     "nmgp_kron_product_f64": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "nmgp_kron_product_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "nmgp_kron_product_diag_f64": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    "nmgp_kron_product_diag_f32": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "nmgp_kron_mv_f64": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "nmgp_kron_mv_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "nmgp_dsvi_hyper_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),

@@ -85,6 +85,10 @@ int nmgp_kron_product_diag_f64(const double* d1, int64_t n1, const double* d2, i
                                hipStream_t s) {
   return nmgp::kron_product<double>(d1, n1, 1, d2, n2, 1, out, s);
 }
+int nmgp_kron_product_diag_f32(const float* d1, int64_t n1, const float* d2, int64_t n2, float* out,
+                               hipStream_t s) {
+  return nmgp::kron_product<float>(d1, n1, 1, d2, n2, 1, out, s);
+}
 int nmgp_kron_mv_f64(const double* B, int64_t P1, int64_t P2, const double* K, int64_t N1, int64_t N2,
                      const double* y, double* out, double* work, hipStream_t s) {
   return nmgp::kron_mv<double>(B, P1, P2, K, N1, N2, y, out, work, s, nmgp_gemm_f64);

@@ -283,6 +283,13 @@ int nmgp_pairwise_bwd_single_f64(const nmgp_pairwise_bwd_desc* h, hipStream_t s)
   d.tiles = nmgp::pw_tiles(d.n, d.m);
   return nmgp::pwb_launch<double>(nullptr, 1, d.tiles, &d, s);
 }
+int nmgp_pairwise_bwd_single_f32(const nmgp_pairwise_bwd_desc* h, hipStream_t s) {
+  if (!h) return -1;
+  nmgp_pairwise_bwd_desc d = *h;
+  d.tile_start = 0;
+  d.tiles = nmgp::pw_tiles(d.n, d.m);
+  return nmgp::pwb_launch<float>(nullptr, 1, d.tiles, &d, s);
+}
 int nmgp_colsum_f32(const float* a, int64_t rows, int64_t cols, double beta, float* out, hipStream_t s) {
   if (!a) return -1;
   if (!out) return -5;

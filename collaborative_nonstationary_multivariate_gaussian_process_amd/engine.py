@@ -425,20 +425,29 @@ class DsviEngine:
         sizes = [int(s) for s in sizes]
         assert sum(sizes) == B, (sum(sizes), B)
         ids = list(range(len(sizes))) if index is None else [int(i) for i in index]
-        order = sorted(range(len(sizes)), key=lambda k: ids[k])
-        if ids != sorted(ids) or len(set(ids)) != len(ids):
-            raise NotImplementedError("index must list distinct outputs in increasing order")
-        seg = np.zeros(D + 1, np.int32)
-        for k, n in zip(ids, sizes):
-            seg[k + 1] = n
-        seg = np.cumsum(seg).astype(np.int32)
-        row_out = np.repeat(np.arange(D, dtype=np.int32), np.diff(seg))
-        self.x.copy_(torch.as_tensor(np.asarray(x, np.float64).reshape(-1)).to(self.dt))
-        self.y.copy_(torch.as_tensor(np.asarray(y, np.float64).reshape(-1)).to(self.dt))
+        if len(ids) != len(sizes) or any(i < 0 or i >= D for i in ids):
+            raise ValueError(f"index {ids} must give one output id in [0, {D}) per input list")
+        # rows of output j in the reference's row order (code/nmgp_dsvi.py:163-169 with `index`): the
+        # engine addresses outputs as contiguous segments, so rows (and their per-row noise) are put in
+        # output order, stably -- the objective is a sum over rows, invariant to that permutation
+        row_ids = np.repeat(np.asarray(ids, np.int64), sizes)
+        order = np.argsort(row_ids, kind="stable")
+        perm = not np.array_equal(order, np.arange(B))
+        seg = np.concatenate([[0], np.cumsum(np.bincount(row_ids, minlength=D))]).astype(np.int32)
+        row_out = row_ids[order].astype(np.int32)
+        xv = np.asarray(x, np.float64).reshape(-1)
+        yv = np.asarray(y, np.float64).reshape(-1)
+        self.x.copy_(torch.as_tensor(xv[order] if perm else xv).to(self.dt))
+        self.y.copy_(torch.as_tensor(yv[order] if perm else yv).to(self.dt))
         self.seg.copy_(torch.from_numpy(seg))
         self.row_out.copy_(torch.from_numpy(row_out))
         if noise is not None:
-            self.noise.copy_(torch.as_tensor(noise, dtype=F64).reshape(-1).to(self.dt))
+            nz = torch.as_tensor(noise, dtype=F64).reshape(-1)
+            if perm:
+                M, Q = self.M, self.Q
+                o = torch.from_numpy(order)
+                nz = torch.cat([nz[:M], nz[M:M + B][o], nz[M + B:].reshape(Q, B)[:, o].reshape(-1)])
+            self.noise.copy_(nz.to(self.dt))
 
     def bind_dataset(self, Xb, Yb, Ib, Sb, counter=None):
         """Keep an epoch of pre-split minibatches resident in HBM (Xb, Yb (nb, B) engine dtype; Ib (nb, B) int32

@@ -253,6 +253,7 @@ typedef struct nmgp_pairwise_bwd_desc {
 int nmgp_pairwise_bwd_f64(const nmgp_pairwise_bwd_desc* d_desc, int ndesc, int total_tiles, hipStream_t stream);
 int nmgp_pairwise_bwd_f32(const nmgp_pairwise_bwd_desc* d_desc, int ndesc, int total_tiles, hipStream_t stream);
 int nmgp_pairwise_bwd_single_f64(const nmgp_pairwise_bwd_desc* h_desc, hipStream_t stream);
+int nmgp_pairwise_bwd_single_f32(const nmgp_pairwise_bwd_desc* h_desc, hipStream_t stream);
 
 /* Deterministic column sums of a (rows x cols) row-major array: out[j] = beta*out[j] + sum_i a[i*cols+j] */
 int nmgp_colsum_f64(const double* a, int64_t rows, int64_t cols, double beta, double* out, hipStream_t stream);
@@ -271,6 +272,8 @@ int nmgp_kron_mv_f64(const double* B, int64_t P1, int64_t P2, const double* K, i
                      const double* y, double* out, double* work, hipStream_t stream);
 int nmgp_kron_product_f32(const float* t1, int64_t r1, int64_t c1, const float* t2, int64_t r2, int64_t c2,
                           float* out, hipStream_t stream);
+int nmgp_kron_product_diag_f32(const float* d1, int64_t n1, const float* d2, int64_t n2, float* out,
+                               hipStream_t stream);
 int nmgp_kron_mv_f32(const float* B, int64_t P1, int64_t P2, const float* K, int64_t N1, int64_t N2,
                      const float* y, float* out, float* work, hipStream_t stream);
 
