@@ -725,6 +725,9 @@ class DsviEngine:
                     ev = torch.cuda.Event()
                     ev.record(st)
                     events[tag] = ev
+                    hook = getattr(self, "hooks", {}).get(tag)
+                    if hook is not None:           # e.g. start a gradient bucket's all-reduce
+                        hook(ev)
                 else:
                     st.wait_event(events[tag])
                 continue

@@ -137,3 +137,28 @@ def test_data_parallel_device_pipeline_ragged_keeps_ranks_in_sync():
     assert np.array_equal(t0, t1)
     assert l0 == l1 and len(l0) == 2 * 2           # the 1-row global batch is skipped every epoch
     assert all(np.isfinite(l0))
+
+
+def _dp_overlap_vs_single(rank):
+    """The bucketed all-reduce overlapped with the backward (eager step) sums exactly what the single
+    all-reduce after the graph-replayed step sums: identical parameters."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import inference
+    from tests import _golden as G
+    g = G.load("toy_elbo")
+    xs, ys = G.split_lists(g)
+    out = []
+    for use_graph in (False, True):
+        torch.manual_seed(3)
+        model, losses, _ = inference(xs, ys, g["z"], 50, 2, hyperpars={}, fix_hyperpars=True, lr=0.005, itnum=2,
+                                     show_ELBO=False, device="cuda:0", noise="device", distributed=True,
+                                     use_graph=use_graph)
+        out.append((model._theta.detach().cpu().numpy(), [float(v) for v in losses]))
+    return out
+
+
+def test_data_parallel_overlapped_allreduce_equals_single():
+    outs = _run(_dp_overlap_vs_single)
+    for (eager, graph) in outs:
+        assert np.array_equal(eager[0], graph[0])
+        assert eager[1] == graph[1]
+    assert np.array_equal(outs[0][0][0], outs[1][0][0])
