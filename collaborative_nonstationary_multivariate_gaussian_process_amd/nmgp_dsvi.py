@@ -752,7 +752,9 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
                                use_graph, include_update=(world == 1))
         loader = _index_loader(N_train, batch_size * world, gen)
     else:
-        loader = DataLoader(trainData(X, Y, I), batch_size=batch_size * world, shuffle=True, generator=gen)
+        # the reference's DataLoader(trainData(X, Y, I)) draws: same sampler, same global-RNG consumption
+        # (tests/test_host_logic.py), rows gathered by index instead of B per-row fetches + collate
+        loader = _index_loader(N_train, batch_size * world, gen)
     loss_list, time_list = [], []
     losses_dev = []
     events = []
@@ -794,7 +796,8 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
                     print("epoch: {}/{}, batch: {}/{}, loss: {}".format(epoch, itnum, batch, N_train / batch_size,
                                                                        float(losses_dev[-1])))
         else:
-            for X_batch, Y_batch, I_batch in loader:
+            for idx in loader:
+                X_batch, Y_batch, I_batch = X[idx], Y[idx], I[idx]
                 if world > 1:                               # this rank's slice of the global minibatch
                     if X_batch.shape[0] < world:            # every rank skips the same short global batch
                         continue

@@ -1,10 +1,11 @@
 """Capture one DSVI step of the toy fixture into a HIP graph and replay it (schedule A/B probe)."""
+import os
 import sys
 
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from tests import _golden as G  # noqa: E402
 from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP, DsviTrainer  # noqa: E402
 

@@ -4,7 +4,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from oracle import nmgp_oracle as O  # noqa: E402
 from tests import _golden as G  # noqa: E402
 from collaborative_nonstationary_multivariate_gaussian_process_amd.engine import DsviEngine  # noqa: E402

@@ -6,8 +6,8 @@ bench.py measures the headline PM2.5-shaped step; this prints one JSON line per 
   pm25f32 the PM2.5 shape through the fp32 engine (for the fp32/fp64 ratio).
   toy     the shipped toy shape (D=2, M=20, B=200), fp64, graph step (latency floor).
 usage: python tools/bench_configs.py [config ...]   (default: toy pm25f32 hcp)
-Synthetic data (seeded); the ECoG shape (D=128, M=1024: 69 GB of dense Sigma_U parameters plus
-Adam state) needs pair sharding across GPUs (SURVEY §8e axis 3) and is not run here.
+Synthetic data (seeded); the ECoG shape (D=128, M=1024, packed pairs) is measured by
+tools/ecog_bench.py and bench.py's compute_ELBO leg.
 """
 import json
 import math
