@@ -293,8 +293,10 @@ class DsviEngine:
             self._plans[elbo_mode] = p
             return p
         # B2: P-bar += W-hat L^T ; L-bar = P^T W-hat ; mu-bar = P^T adjoints
-        d17 = [g(self.Pbar, self.WG, th, B, M, D * M, (M, 1, BM), (1, M, MM), (M, 1), flags=L.B_UPPER, kb=(M, M),
-                 beta=1.0, offs=(0, sW, 3 * BM), **rows_all)]
+        # rows of output i: P-bar_G += sum_{d <= i} W-hat_d L_d^T (W-hat_d holds only the rows of outputs
+        # >= d, so k runs over the (i + 1) latent blocks that are non-zero there, not all D)
+        d17 = [g(self.Pbar, self.WG, th, B, M, (i + 1) * M, (M, 1, BM), (1, M, MM), (M, 1), flags=L.B_UPPER,
+                 kb=(M, M), beta=1.0, offs=(0, sW, 3 * BM), row_seg=i) for i in range(D)]
         for i in range(D):
             d17.append(g(self.Pbar, self.WP, th, B, M, M, (M, 1, 0), (1, M, 0), (M, 1), flags=L.B_UPPER, beta=1.0,
                          offs=(i * BM, sU + pq(i, i) * MM, 2 * BM), row_seg=i))
@@ -561,9 +563,10 @@ class DsviEngine:
         if need_side:
             steps += [("sig", "main", "fork"), ("wait", "side", "fork")]
             if v_on_side:
-                # Sigma_v is formed with the other factors on the side stream (one launch), beside the
-                # RBF builders on the main stream, instead of a second dependent launch there
-                steps += [("syrk_all", "gemm", gemm("syrk_all"), "side"), ("sig", "side", "syrk")]
+                # Sigma_v first on the side stream (one small latency-kernel launch beside the RBF
+                # builders on the main stream, which waits only for it), then the other factors
+                steps += [("syrk", "gemm", gemm("syrk"), "side"), ("sig", "side", "syrk"),
+                          ("syrk_side", "gemm", gemm("syrk_side"), "side")]
             else:
                 steps.append(("syrk_side", "gemm", gemm("syrk_side"), "side"))
             steps.append(("chol_side", "chol", chol(0, FV), "side"))

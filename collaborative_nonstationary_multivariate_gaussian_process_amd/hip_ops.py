@@ -79,14 +79,81 @@ def _auto_ksplit(k_eff, group_tiles, work_per_wg):
     return 1
 
 
-class GemmGroup:
-    """A fixed list of GEMM problems launched as ONE grouped kernel (descriptors uploaded once)."""
+LAT_TILE = 32       # output tile of the latency kernel (csrc/gemm_lat.hip LTM / LTN)
+LAT_PANEL = 64      # panel alignment the latency kernel needs of k-blocked operands
+LAT_WAVES, LAT_KP = 8, 32   # waves per workgroup and k-panel width (gemm_lat.hip launch config 1)
+_LAT_MODE = os.environ.get("NMGP_GEMM_LAT", "auto")        # "0": never, "force": wherever eligible
+# a workgroup of the latency kernel loads each round of panels (LAT_WAVES x LAT_KP of k) in one go and
+# waits for it; groups that leave more rounds than this per workgroup after split-K (many output tiles
+# AND long k: the P-bar / L-bar products over several latent blocks or the minibatch) stay on the
+# LDS-pipelined tile kernel (per-group A/B on the box: tools/gemm_group_probe.py)
+_LAT_MAX_ROUNDS = int(os.environ.get("NMGP_GEMM_LAT_MAX_ROUNDS", "2"))
 
-    def __init__(self, descs, device, dtype, seg=None, target_wgs=512, dyn_plan=True):
+
+def _lat_split(descs, seg, target_wgs):
+    """Split-K factor per descriptor for the latency kernel and the rounds of k panels a workgroup
+    then still runs: ([ksplit], max rounds)."""
+    nseg = (seg.numel() - 1) if seg is not None else 1
+    frac = lambda d, s_: (max(d.seg_span, 1) / nseg) if s_ >= 0 else 1.0
+    tiles = [-(-max(d.m, 0) // LAT_TILE) * -(-max(d.n, 0) // LAT_TILE) for d in descs]
+    group_tiles = max(1, sum(tiles))
+    ks, worst = [], 0
+    for d in descs:
+        k_eff = max(1, round(max(d.k, 1) * frac(d, d.k_seg)))
+        rounds = -(-(-(-k_eff // LAT_KP)) // LAT_WAVES)
+        k = int(max(1, min(16, rounds, round(target_wgs / group_tiles))))
+        ks.append(k)
+        worst = max(worst, -(-rounds // k))
+    return ks, worst
+
+
+def _lat_eligible(d, esz):
+    """Can gemm_lat.hip run this descriptor?  Non-negative strides, k-blocks that panels never
+    straddle, and operand extents (incl. the rows / k a tile may touch past the problem) addressable
+    by a 32-bit buffer offset."""
+    if d.batch > 1:
+        return False
+    st = (d.sA_i, d.sA_k, d.sA_kb, d.sB_k, d.sB_j, d.sB_kb)
+    if min(st) < 0:
+        return False
+    K = max(d.k, 1)
+    for kb in (d.kbA, d.kbB):
+        if 0 < kb < K and kb % LAT_PANEL:
+            return False
+    kinA = d.kbA if 0 < d.kbA < K else K
+    kinB = d.kbB if 0 < d.kbB < K else K
+    nkbA = -(-K // kinA)
+    nkbB = -(-K // kinB)
+    extA = ((d.m + LAT_TILE) * d.sA_i + (kinA + LAT_PANEL) * d.sA_k + nkbA * d.sA_kb) * esz
+    extB = ((kinB + LAT_PANEL) * d.sB_k + (d.n + LAT_TILE) * d.sB_j + nkbB * d.sB_kb) * esz
+    return max(extA, extB) < 0x7fff0000
+
+
+class GemmGroup:
+    """A fixed list of GEMM problems launched as ONE grouped kernel (descriptors uploaded once).
+
+    Two kernels share the descriptor format: the LDS-staged 64x64 kernel (gemm.hip: long k loops,
+    split-K) and the latency kernel (gemm_lat.hip: 32x32 tiles, the k range split over the waves of
+    a workgroup, operands loaded straight into registers) for groups whose k loops are short -- the
+    B x M x M and M x M x M products of the DSVI step.  `kernel`: "auto" (latency kernel when every
+    problem is eligible and k <= NMGP_GEMM_LAT_KMAX), "tile", "lat"."""
+
+    def __init__(self, descs, device, dtype, seg=None, target_wgs=512, dyn_plan=True, kernel="auto"):
         """Split-K is chosen per problem so that the launch has ~target_wgs workgroups when the
         outputs alone are too few tiles (the M x B x M products P^T R with K = B)."""
         self.dtype = dtype
         self.seg = seg
+        self.lat = False
+        esz = 8 if dtype == _F64 else 4
+        if kernel != "tile" and _LAT_MODE != "0" and descs:
+            ok = all(_lat_eligible(d, esz) for d in descs)
+            if kernel == "lat" and not ok:
+                raise ValueError("GemmGroup(kernel='lat'): a descriptor is not addressable by the latency kernel")
+            short = ok and _lat_split(descs, seg, target_wgs)[1] <= _LAT_MAX_ROUNDS
+            self.lat = ok and (kernel == "lat" or _LAT_MODE == "force" or (short and dtype == _F64))
+        if self.lat:
+            self._init_lat(descs, device, dyn_plan, target_wgs)
+            return
         arr = (L.GemmDesc * len(descs))()
         group_tiles = sum(d.tiles_m * d.tiles_n for d in descs)
         nseg = (seg.numel() - 1) if seg is not None else 1
@@ -138,6 +205,43 @@ class GemmGroup:
                 self.plan = torch.zeros(len(descs) + 1, dtype=torch.int32, device=device)
                 self.grid = int(min(t, max(256, min(4096, round(1.15 * expect)))))
 
+    def _init_lat(self, descs, device, dyn_plan, target_wgs):
+        """Latency-kernel layout: 32x32 tiles; a problem whose k range needs more than one round of
+        panels over the workgroup's waves is split over up to that many workgroups when the group's
+        tiles alone leave the chip idle (workspace + counters as the tile kernel's split-K).
+        Row-segmented groups whose static grid is mostly idle get the device tile plan (the grid stays
+        a multiple of 8 for the XCD mapping)."""
+        nseg = (self.seg.numel() - 1) if self.seg is not None else 1
+        frac = lambda d, s_: (max(d.seg_span, 1) / nseg) if s_ >= 0 else 1.0
+        arr = (L.GemmDesc * len(descs))()
+        ksplits, _ = _lat_split(descs, self.seg, target_wgs)
+        t, expect = 0, 0.0
+        self._ws = []
+        for i, d in enumerate(descs):
+            d.tiles_m = -(-d.m // LAT_TILE) if d.m > 0 else 0
+            d.tiles_n = -(-d.n // LAT_TILE) if d.n > 0 else 0
+            d.ksplit = ksplits[i]
+            nt = d.tiles_m * d.tiles_n
+            if d.ksplit > 1:
+                ws = torch.empty(nt * d.ksplit * LAT_TILE * LAT_TILE, dtype=self.dtype, device=device)
+                ctr = torch.zeros(max(nt, 1), dtype=torch.int32, device=device)
+                self._ws += [ws, ctr]
+                d.ws, d.counters = ws.data_ptr(), ctr.data_ptr()
+            d.tile_start = t
+            t += nt * d.ksplit
+            expect += nt * d.ksplit * frac(d, d.row_seg)
+            arr[i] = d
+        self.total = t
+        self.n = len(descs)
+        self.descs = list(descs)
+        raw = bytes(memoryview(arr).cast("B"))
+        self.dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+        self.plan, self.grid = None, 0
+        if self.seg is not None and dyn_plan and any(d.row_seg >= 0 for d in descs):
+            if dyn_plan == "force" or (t >= int(os.environ.get("NMGP_DYN_MIN_TILES", 1024)) and expect < 0.5 * t):
+                self.plan = torch.zeros(len(descs) + 1, dtype=torch.int32, device=device)
+                self.grid = int(min(-(-t // 8) * 8, max(256, min(8192, 8 * round(1.15 * expect / 8)))))
+
     def macs(self, seg=None):
         return sum(desc_macs(d, seg) for d in self.descs)
 
@@ -146,6 +250,12 @@ class GemmGroup:
             return
         s = stream if stream is not None else L.stream_handle()
         segp = ctypes.c_void_p(self.seg.data_ptr()) if self.seg is not None else None
+        if self.lat:
+            fn = getattr(L.lib(), "nmgp_gemm_grouped_lat_" + _sfx(self.dtype))
+            plan = ctypes.c_void_p(self.plan.data_ptr()) if self.plan is not None else None
+            L.check(fn(ctypes.c_void_p(self.dev.data_ptr()), self.n, self.total, segp, plan, self.grid, s),
+                    "gemm_grouped_lat")
+            return
         if self.plan is not None:
             fn = getattr(L.lib(), "nmgp_gemm_grouped_dyn_" + _sfx(self.dtype))
             L.check(fn(ctypes.c_void_p(self.dev.data_ptr()), self.n, self.total, segp,

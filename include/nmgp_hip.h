@@ -106,6 +106,17 @@ int nmgp_gemm_grouped_dyn_f64(const nmgp_gemm_desc* d_desc, int nprob, int total
                               int32_t* plan, int grid, hipStream_t stream);
 int nmgp_gemm_grouped_dyn_f32(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles, const int32_t* d_seg,
                               int32_t* plan, int grid, hipStream_t stream);
+/* The same descriptors through the latency-oriented kernel (gemm_lat.hip) for groups of short-k
+ * problems: 32x32 output tiles (tiles_m = ceil(m/32), tiles_n = ceil(n/32), tile_start in those
+ * units, ksplit ignored), the k range of a tile split over the waves of its workgroup, operands
+ * loaded straight into MFMA registers.  Requirements: non-negative strides, kbA / kbB either >= k
+ * or a multiple of 64, operand extents below 2 GiB.  plan != NULL: sized on device as
+ * nmgp_gemm_grouped_dyn_* (32-row tiles), `grid` workgroups (rounded up to a multiple of 8).
+ * Same role in the step as nmgp_gemm_grouped_*: code/utils.py:117-146, code/nmgp_dsvi.py:172-258. */
+int nmgp_gemm_grouped_lat_f64(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles, const int32_t* d_seg,
+                              int32_t* plan, int grid, hipStream_t stream);
+int nmgp_gemm_grouped_lat_f32(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles, const int32_t* d_seg,
+                              int32_t* plan, int grid, hipStream_t stream);
 /* one problem passed by value (host descriptor; tiles fields are filled internally)          */
 int nmgp_gemm_f64(const nmgp_gemm_desc* h_desc, const int32_t* d_seg, hipStream_t stream);
 int nmgp_gemm_f32(const nmgp_gemm_desc* h_desc, const int32_t* d_seg, hipStream_t stream);

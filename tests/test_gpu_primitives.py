@@ -137,6 +137,106 @@ def test_gemm_grouped_device_plan(ops, dt):
     assert rel(outs[1][0], ref) < tol and torch.equal(outs[0][0], outs[1][0])
 
 
+@pytest.mark.parametrize("dt", [F64, torch.float32])
+def test_gemm_latency_kernel(ops, dt):
+    """gemm_lat.hip (32x32 tiles, k split over the waves, register-direct operands) on the descriptor
+    features the DSVI step uses: triangular operands whose zero triangles hold inf, k-scaling, the
+    rs(i) E epilogue, diagonal add, beta, OUT_LOWER / OUT_TRIL, transposed operands, k-blocked
+    operands (kb = 64), row / k segments, the device tile plan; repeat launches are bit-identical."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L
+    g = torch.Generator().manual_seed(21)
+    n, B, D, M = 100, 330, 3, 64
+    S = torch.randn(n, n, generator=g, dtype=F64)
+    Sinf = torch.tril(S) + torch.triu(torch.full((n, n), float("inf"), dtype=F64), 1)   # inf above the diagonal
+    s = torch.rand(n, generator=g, dtype=F64)
+    E = torch.randn(n, n, generator=g, dtype=F64)
+    rs = torch.randn(n, generator=g, dtype=F64)
+    C0 = torch.randn(n, n, generator=g, dtype=F64)
+    W = torch.randn(D, B, M, generator=g, dtype=F64)
+    U = torch.randn(D, M, M, generator=g, dtype=F64)
+    seg = torch.tensor([0, 120, 121, 330], dtype=torch.int32)
+    P = torch.randn(1500, M, generator=g, dtype=F64)
+    C40 = torch.randn(M, M, generator=g, dtype=F64)
+    dv = lambda x: x.to(dt).to(DEV)
+    Pd = dv(P)
+    Sd, sd, Ed, rsd, Wd, Ud, segd = dv(Sinf), dv(s), dv(E), dv(rs), dv(W), dv(U), seg.to(DEV)
+    Wc, Uc, Sc = W.to(dt).double(), U.to(dt).double(), torch.tril(S.to(dt).double())
+    results = []
+    for rep in range(2):
+        C1 = dv(C0)
+        C2 = torch.full((n, n), 7.0, dtype=dt, device=DEV)
+        C3 = torch.full((n, n), 7.0, dtype=dt, device=DEV)
+        O1 = torch.zeros(B, M, dtype=dt, device=DEV)
+        O2 = torch.zeros(M, M, dtype=dt, device=DEV)
+        O3 = torch.full((B, M), 3.0, dtype=dt, device=DEV)
+        O4 = dv(C40)
+        descs = [
+            # C1 = 0.5 L diag(s) L^T + 2 C0 - 1.5 diag(rs) tril(E) + 0.25 I   (L = tril(S): A_LOWER, B_UPPER)
+            ops.gemm_desc(C1, Sd, Sd, n, n, n, (n, 1, 0), (1, n, 0), (n, 1),
+                          flags=L.A_LOWER | L.B_UPPER | L.EPI_E_LOWER | L.EPI_RS_NEG, alpha=0.5, beta=2.0,
+                          kscale=(sd, 0), epi=(Ed, 0, (n, 1), (rsd, 0), 1.5), diag_add=0.25),
+            # C2 = tril(L^T L) with zeros above (A = L^T: A_UPPER, B = L: B_LOWER)
+            ops.gemm_desc(C2, Sd, Sd, n, n, n, (1, n, 0), (n, 1, 0), (n, 1), flags=L.A_UPPER | L.B_LOWER | L.OUT_TRIL),
+            # C3 lower part only of L L^T (upper untouched)
+            ops.gemm_desc(C3, Sd, Sd, n, n, n, (n, 1, 0), (1, n, 0), (n, 1), flags=L.A_LOWER | L.B_UPPER | L.OUT_LOWER),
+            # O1 = sum_d W[d] tril(U[d])^T   (k-blocked, kb = M = 64)
+            ops.gemm_desc(O1, Wd, Ud, B, M, D * M, (M, 1, B * M), (1, M, M * M), (M, 1), flags=L.B_UPPER, kb=(M, M)),
+            # O2 = W[1][rows of segments 1..2]^T W[2][same rows]
+            ops.gemm_desc(O2, Wd, Wd, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), k_seg=1, seg_span=2, offs=(B * M, 2 * B * M, 0)),
+            # O3[rows of segment 2] = W[0][seg 2] U[0] + O3
+            ops.gemm_desc(O3, Wd, Ud, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), row_seg=2, beta=1.0),
+            # O4 = C40 - P^T P  (k = 1500: split over workgroups, last-arriver combine)
+            ops.gemm_desc(O4, Pd, Pd, M, M, 1500, (1, M, 0), (M, 1, 0), (M, 1), alpha=-1.0, beta=1.0),
+        ]
+        grp = ops.GemmGroup(descs, DEV, dt, seg=segd, kernel="lat", dyn_plan="force" if rep else False)
+        assert grp.lat and (grp.plan is not None) == bool(rep)
+        assert max(d.ksplit for d in grp.descs) > 1
+        grp()
+        results.append([x.cpu() for x in (C1, C2, C3, O1, O2, O3, O4)])
+    tol = 1e-13 if dt == F64 else 3e-6
+    ref1 = 0.5 * Sc @ torch.diag(s.to(dt).double()) @ Sc.t() + 2 * C0.to(dt).double() \
+        - 1.5 * rs.to(dt).double()[:, None] * torch.tril(E.to(dt).double()) + 0.25 * torch.eye(n, dtype=F64)
+    ref2 = torch.tril(Sc.t() @ Sc)
+    ref3 = torch.tril(Sc @ Sc.t()) + torch.triu(torch.full((n, n), 7.0, dtype=F64), 1)
+    refO1 = sum(Wc[d] @ torch.tril(Uc[d]).t() for d in range(D))
+    refO2 = Wc[1][120:330].t() @ Wc[2][120:330]
+    refO3 = torch.full((B, M), 3.0, dtype=F64)
+    refO3[121:330] += Wc[0][121:330] @ Uc[0]
+    Pc = P.to(dt).double()
+    refO4 = C40.to(dt).double() - Pc.t() @ Pc
+    for got in results:
+        for a, r in zip(got, (ref1, ref2, ref3, refO1, refO2, refO3, refO4)):
+            assert torch.isfinite(a).all() and rel(a, r) < tol
+    for a, b in zip(*results):          # static grid vs device plan: same tiles, same order of sums
+        assert torch.equal(a, b)
+
+
+def test_gemm_latency_kernel_dsvi_step(ops, monkeypatch):
+    """The PM2.5-shaped step (D=5, M=256, B=2000) with the latency kernel on its short-k groups equals
+    the step with every group on the 64x64 tile kernel: loss and whole gradient to rounding."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP, DsviTrainer
+    import collaborative_nonstationary_multivariate_gaussian_process_amd.hip_ops as H
+    D, M, B = 5, 256, 2000
+    rng = np.random.default_rng(3)
+    xs = [torch.from_numpy(np.sort(rng.uniform(0, 1, 400))) for _ in range(D)]
+    ys = [torch.from_numpy(rng.standard_normal(400)) for _ in range(D)]
+    res = {}
+    for mode in ("0", "auto"):
+        monkeypatch.setattr(H, "_LAT_MODE", mode)
+        model = NMGP(number_observations=D * 400, dim_outputs=D, Z=np.linspace(0, 1, M), minibatch_size=B, seed=2,
+                     device=DEV, noise="device")
+        eng = model.engine(B)
+        x, y, sizes = model._prepare(xs, ys)
+        eng.load_batch(x, y, sizes)
+        loss = DsviTrainer(model, 0.01).grad_step(eng)
+        torch.cuda.synchronize()
+        nlat = sum(1 for _, g_ in eng.gemm_groups() if getattr(g_, "lat", False))
+        res[mode] = (float(loss), model._grad.detach().cpu().clone(), nlat)
+    assert res["0"][2] == 0 and res["auto"][2] > 0
+    assert abs(res["auto"][0] - res["0"][0]) <= 1e-12 * abs(res["0"][0])
+    assert rel(res["auto"][1], res["0"][1]) < 1e-11
+
+
 @pytest.mark.parametrize("K", [600, 2000, 4099])
 def test_gemm_split_k_deterministic(ops, K):
     """Long-k products P^T R (few output tiles) take the split-K path; results are bit-identical
@@ -151,7 +251,7 @@ def test_gemm_split_k_deterministic(ops, K):
     for rep in range(3):
         C = C0.clone().to(DEV)
         d = ops.gemm_desc(C, Pd, Rd, M, M, K, (1, M, 0), (M, 1, 0), (M, 1), alpha=-1.0, beta=1.0)
-        grp = ops.GemmGroup([d], DEV, F64)
+        grp = ops.GemmGroup([d], DEV, F64, kernel="tile")
         assert grp.descs[0].ksplit > 1
         grp()
         grp()          # counters were reset by the last arrivers: a second launch is valid too

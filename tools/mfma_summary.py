@@ -1,7 +1,8 @@
 """Summarise a rocprofv3 PMC pass (SQ_VALU_MFMA_BUSY_CYCLES, SQ_BUSY_CU_CYCLES, GRBM_GUI_ACTIVE) per kernel
 and grid size: MFMA utilisation = MFMA-busy SIMD cycles / (active cycles x 4 SIMDs x CUs), where the active
 cycles per XCD are GRBM_GUI_ACTIVE / 8 (rocprofv3 sums it over the 8 XCDs; MI355X_MICROARCH.md, DVFS note).
-usage: python tools/mfma_summary.py <run_counter_collection.csv> <out.json> [--cus 256]"""
+usage: python tools/mfma_summary.py <run_counter_collection.csv> <out.json> [--cus 256] [--by-grid]
+--by-grid: aggregate every dispatch of one (kernel, grid) (graph replays interleave many launches)."""
 import collections
 import csv
 import json
@@ -18,7 +19,15 @@ def main():
         d[x["Counter_Name"]] = d.get(x["Counter_Name"], 0.0) + float(x["Counter_Value"])
     # consecutive MFMA dispatches of one (kernel, grid) form a group: one probe case (warm-up + replays)
     groups = []
+    by_grid = "--by-grid" in sys.argv
+    index = {}
     for (did, name, grid), d in disp.items():
+        if by_grid:
+            if (name, grid) not in index:
+                index[(name, grid)] = len(groups)
+                groups.append([(name, grid), []])
+            groups[index[(name, grid)]][1].append(d)
+            continue
         if d.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) <= 0:
             continue
         if groups and groups[-1][0] == (name, grid):
@@ -36,6 +45,8 @@ def main():
                      "mfma_util": round(busy / (cyc * 4 * cus), 4), "cu_busy": round(cu / (cyc * cus), 4)})
     json.dump({"source": src, "definition": "mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 4 * CUs)",
                "rows": rows}, open(out, "w"), indent=1)
+    if by_grid:
+        rows.sort(key=lambda r: -r["avg_us"] * r["dispatches"])
     for r in rows:
         print(json.dumps(r))
 

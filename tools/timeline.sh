@@ -7,6 +7,6 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/tl_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-stress --no-breakdown > $OUT/b.json 2> $OUT/err.log
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-stress --no-breakdown --no-elbo --no-api > $OUT/b.json 2> $OUT/err.log
 cd $R
 python3 tools/step_timeline.py $(find $OUT -name "*kernel_trace.csv" | head -1) 1 > $OUT/timeline.txt
