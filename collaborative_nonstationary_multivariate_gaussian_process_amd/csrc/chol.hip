@@ -31,7 +31,10 @@ __device__ unsigned long long* g_chol_trace;
   if (threadIdx.x == 0 && blockIdx.x == 0) g_chol_trace[512 + (kb) * 4 + (p)] = wall_clock64()
 #define CHOL_STAMP1(kb, p) \
   if (threadIdx.x == 0 && blockIdx.x == 1) g_chol_trace[256 + (kb) * 4 + (p)] = wall_clock64()
+#define CHOL_STAMPX(i) \
+  if (threadIdx.x == 0) g_chol_trace[1000 + 4 * blockIdx.x + (i)] = wall_clock64()
 #else
+#define CHOL_STAMPX(i)
 #define CHOL_STAMP1(kb, p)
 #define CHOL_STAMP(kb, p)
 #define CHOL_STAMPW(kb, p)
@@ -593,27 +596,41 @@ __device__ __attribute__((always_inline)) inline void chol2_potrf_role(double* A
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int ntiles = nt * (nt + 1) / 2;
+  CHOL_STAMPX(0);
   int ib[NTPW], jb[NTPW];
   acc_t acc[NTPW];
+  // decode every owned tile first, then issue all NTPW x 4 loads unconditionally (out-of-range ones
+  // read 0 through the resource) so they share one memory round trip: loads behind the per-tile
+  // branches went out one tile at a time (13 us of prologue at n = 256)
 #pragma unroll
   for (int u = 0; u < NTPW; ++u) {
     const int tt = w + RW * u;
     ib[u] = -1;
     jb[u] = -1;
-    if (tt < ntiles) {
-      tri_decode(tt, ib[u], jb[u]);
+    if (tt < ntiles) tri_decode(tt, ib[u], jb[u]);
+  }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gr = ib[u] * 16 + Mfma<T>::row(lane, r), gc = jb[u] * 16 + (lane & 15);
-        const T v = Am[(int64_t)min(gr, n - 1) * lda + min(gc, n - 1)];
-        acc[u][r] = (gr < n && gc < n) ? v : (gr == gc ? (T)1 : (T)0);
-      }
+  for (int u = 0; u < NTPW; ++u) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gr = ib[u] * 16 + Mfma<T>::row(lane, r), gc = jb[u] * 16 + (lane & 15);
+      const bool in = ib[u] >= 0 && gr < n && gc < n;
+      acc[u][r] = bload<T>(rAm, in ? (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)) : 0x80000000u);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NTPW; ++u) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gr = ib[u] * 16 + Mfma<T>::row(lane, r), gc = jb[u] * 16 + (lane & 15);
+      if (ib[u] >= 0 && !(gr < n && gc < n)) acc[u][r] = gr == gc ? (T)1 : (T)0;   // padding past n
     }
   }
   int first_fail = 0;
   // strictly-upper block tiles of L are zero (the stores drain while the factorization runs)
   for (int i = w; i < n; i += RW)
     for (int j = ((i >> 4) + 1) * 16 + lane; j < n; j += 64) Am[(int64_t)i * lda + j] = 0;
+  CHOL_STAMPX(1);
   for (int kb = 0; kb < nt; ++kb) {
     CHOL_STAMP(kb, 0);
     const int nrow = NR - kb * 16;
@@ -645,6 +662,7 @@ __device__ __attribute__((always_inline)) inline void chol2_potrf_role(double* A
 #pragma unroll
         for (int c = 0; c < 16; ++c) a[c] = fma(src[c], keep, (ident && c == lr) ? (T)1 : (T)0);
       }
+      CHOL_STAMPW(kb, 0);
       unsigned int bad = 0;
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
@@ -656,6 +674,7 @@ __device__ __attribute__((always_inline)) inline void chol2_potrf_role(double* A
 #pragma unroll
         for (int c = j + 1; c < 16; ++c) a[c] = fma(-a[j], readlane(a[j], c), a[c]);
       }
+      CHOL_STAMPW(kb, 1);
       if (bad && first_fail == 0) {
         const int j0 = __builtin_ctz(bad);
         if (kb * 16 + j0 < n) first_fail = kb * 16 + j0 + 1;
@@ -667,8 +686,14 @@ __device__ __attribute__((always_inline)) inline void chol2_potrf_role(double* A
 #pragma unroll
         for (int c = 0; c < 16; ++c) dst[c] = a[c];
       }
+      CHOL_STAMPW(kb, 2);
     }
+    // the previous step's published stores had this step's spill and panel to drain: the wait is
+    // (nearly) free here, where right after the SYRK it stalled every step for a full write round trip
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
+    if (t == 0 && kb > 0)
+      __hip_atomic_store(flag, kFlagTag + (unsigned long long)kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     CHOL_STAMP(kb, 2);
     // publish L[:, kb] (final output) and L_kk^-1 (= the final X[kb, kb]) write-through
     for (int idx = t; idx < nrow * 16; idx += RW * 64) {
@@ -695,12 +720,12 @@ __device__ __attribute__((always_inline)) inline void chol2_potrf_role(double* A
       }
     }
     CHOL_STAMP(kb, 3);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
-    if (t == 0) __hip_atomic_store(flag, kFlagTag + (unsigned long long)(kb + 1), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+  if (t == 0) __hip_atomic_store(flag, kFlagTag + (unsigned long long)nt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   CHOL_STAMP(nt, 0);
+  CHOL_STAMPX(2);
   if (t == 0 && info) {
     if (info_first) info[mat] = first_fail ? first_fail + col_off : 0;
     else if (first_fail && info[mat] == 0) info[mat] = first_fail + col_off;
@@ -833,6 +858,179 @@ __device__ __attribute__((always_inline)) inline void chol2_trtri_role(double* A
   if (t == 0) __hip_atomic_store(flag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Three workgroups per matrix (f64, 32 <= n <= 256): the factor role as above, and the inverse role
+// split over two workgroups by block-column parity (X[:, jb] and R[:, jb] for jb % 2 == par): the
+// trtri work of a late block step (rows below kb x columns up to kb) grows past the factor's step
+// time on one CU, so a single inverse workgroup fell behind by up to 15 us per step.  Both read the
+// factor role's published L[:, kb] / L_kk^-1; the last of them to finish re-arms the progress word
+// (a second word, X(0, n-2), counts finished consumers; the factor role initialises it).
+constexpr unsigned long long kDoneTag = 0x7ff8d5a1d0e00000ull;
+
+__device__ inline void tri_decode_par(int tp, int par, int& ib, int& jb) {
+  ib = -1;
+  jb = -1;
+  for (int r = par; r < 64; ++r) {           // row r holds (r - par) / 2 + 1 tiles of this parity
+    const int c = (r - par) / 2 + 1;
+    if (tp < c) {
+      ib = r;
+      jb = par + 2 * tp;
+      return;
+    }
+    tp -= c;
+  }
+}
+
+template <int NTPW>
+__device__ __attribute__((always_inline)) inline void chol3_trtri_role(double* Am, double* Xm, int n, int64_t lda,
+                                                                       int64_t ldx, int par, unsigned char* smem_raw) {
+  using T = double;
+  using acc_t = typename Mfma<T>::acc_t;
+  const int nt = (n + 15) >> 4, NR = nt * 16;
+  T* Ps = (T*)smem_raw + NR * CP;
+  T* Xrow = Ps + NR * CP;
+  T* LiT = Xrow + NR * CP;
+  unsigned long long* flag = (unsigned long long*)(Xm + (n - 1));
+  unsigned long long* done = (unsigned long long*)(Xm + (n - 2));
+  const __amdgpu_buffer_rsrc_t rAm = make_rsrc(Am, ((int64_t)(n - 1) * lda + n) * (int64_t)sizeof(T));
+  const __amdgpu_buffer_rsrc_t rXm = make_rsrc(Xm, ((int64_t)(n - 1) * ldx + n) * (int64_t)sizeof(T));
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  int ntp = 0;                                                          // lower tiles of this parity
+  for (int j = par; j < nt; j += 2) ntp += nt - j;
+  int ib[NTPW], jb[NTPW];
+  acc_t acc[NTPW];
+#pragma unroll
+  for (int u = 0; u < NTPW; ++u) {
+    const int tp = w + RW * u;
+    ib[u] = -1;
+    jb[u] = -1;
+    if (tp < ntp) {
+      tri_decode_par(tp, par, ib[u], jb[u]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gr = ib[u] * 16 + Mfma<T>::row(lane, r), gc = jb[u] * 16 + (lane & 15);
+        acc[u][r] = gr == gc ? (T)1 : (T)0;  // R starts as the identity
+      }
+    }
+  }
+  // strictly upper part of X is zero (rows of this parity; the two control words stay)
+  for (int i = 2 * w + par; i < n; i += 2 * RW)
+    for (int j = ((i >> 4) + 1) * 16 + lane; j < n; j += 64)
+      if (i != 0 || j < n - 2) Xm[(int64_t)i * ldx + j] = 0;
+  for (int kb = 0; kb < nt; ++kb) {
+    const int nrow = NR - kb * 16;
+    if (t == 0) {
+      bool seen = false;
+      for (int spin = 0; spin < (1 << 26); ++spin) {
+        const unsigned long long f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (f >= kFlagTag + (unsigned long long)(kb + 1) && f <= kFlagTag + (unsigned long long)nt) {
+          seen = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (!seen) spin_gave_up(NMGP_STATUS_CHOL_SPIN);
+    }
+    CHOL_STAMP1(kb, 0);
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    {
+      constexpr int PER = 256 * 16 / (RW * 64);
+      T v[PER];
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int idx = t + q * RW * 64, lr = idx >> 4, c = idx & 15;
+        const int gr = kb * 16 + lr, gc = kb * 16 + c;
+        const uint32_t off =
+            (idx < nrow * 16 && gr < n && gc < n) ? (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)) : 0x80000000u;
+        v[q] = bload_sc1<T>(rAm, off);
+      }
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int idx = t + q * RW * 64;
+        if (idx < nrow * 16) Ps[(idx >> 4) * CP + (idx & 15)] = v[q];
+      }
+    }
+    if (t < 256) {
+      const int r = t >> 4, c = t & 15;
+      const int gr = kb * 16 + r, gc = kb * 16 + c;
+      const uint32_t off = (gr < n && gc < n) ? (uint32_t)(((int64_t)gr * ldx + gc) * sizeof(T)) : 0x80000000u;
+      T v = bload_sc1<T>(rXm, off);
+      if (gr >= n || gc >= n) v = (gr == gc) ? (T)1 : (T)0;
+      LiT[c * CP + r] = v;
+    }
+    lds_barrier();
+    CHOL_STAMP1(kb, 1);
+    // X[kb, jb] = L_kk^-1 R[kb, jb]   (jb <= kb of this parity)
+#pragma unroll
+    for (int u = 0; u < NTPW; ++u) {
+      if (ib[u] == kb) {
+        const int xj = __builtin_amdgcn_readfirstlane(jb[u] - kb) + kb;
+        acc_t x = {0, 0, 0, 0};
+        if (xj == kb) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) x[r] = LiT[(lane & 15) * CP + Mfma<T>::row(lane, r)];
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) x = Mfma<T>::mma(LiT[Mfma<T>::row(lane, s) * CP + (lane & 15)], acc[u][s], x);
+        }
+        acc[u] = x;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Xrow[(xj * 16 + Mfma<T>::row(lane, r)) * CP + (lane & 15)] = x[r];
+      }
+    }
+    lds_barrier();
+    CHOL_STAMP1(kb, 2);
+    // rows below kb: R[ib, jb] -= L[ib, kb] X[kb, jb]
+#pragma unroll
+    for (int u = 0; u < NTPW; ++u) {
+      if (ib[u] > kb && jb[u] >= 0 && jb[u] <= kb) {
+        const int ra = __builtin_amdgcn_readfirstlane(ib[u] - kb) * 16 + (lane & 15);
+        const int xj = __builtin_amdgcn_readfirstlane(jb[u] - kb) + kb;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int kr = Mfma<T>::row(lane, s);
+          acc[u] = Mfma<T>::mma(-Ps[ra * CP + kr], Xrow[(xj * 16 + kr) * CP + (lane & 15)], acc[u]);
+        }
+      }
+    }
+    const int ncol = kb >= par ? (kb - par) / 2 + 1 : 0;   // own block columns <= kb
+    for (int idx = t; idx < ncol * 256; idx += RW * 64) {
+      const int j = par + 2 * (idx >> 8), k = (idx >> 4) & 15, c = idx & 15;
+      const int gr = kb * 16 + k, gc = j * 16 + c;
+      if (gr < n && gc < n) Xm[(int64_t)gr * ldx + gc] = Xrow[(j * 16 + k) * CP + c];
+    }
+    lds_barrier();
+    CHOL_STAMP1(kb, 3);
+  }
+  CHOL_STAMPX(2);
+  if (t == 0) {
+    // the last consumer re-arms the progress word for the next launch and clears both words
+    const unsigned long long old = __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == kDoneTag + 1ull) {
+      __hip_atomic_store(flag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <int NTPW, int NTPW1>
+__global__ __launch_bounds__(RW * 64) void chol_inv3_kernel(double* A, int n, int64_t lda, int64_t strideA, double* X,
+                                                            int64_t ldx, int64_t strideX, int32_t* info, int col_off,
+                                                            int info_first) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int mat = blockIdx.x / 3, role = blockIdx.x - 3 * mat;
+  double* Am = A + (int64_t)mat * strideA;
+  double* Xm = X + (int64_t)mat * strideX;
+  if (role == 0) {
+    if (threadIdx.x == 0)
+      __hip_atomic_store((unsigned long long*)(Xm + (n - 2)), kDoneTag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    chol2_potrf_role<NTPW>(Am, Xm, n, lda, ldx, info, col_off, info_first, mat, smem_raw);
+  } else {
+    chol3_trtri_role<NTPW1>(Am, Xm, n, lda, ldx, role - 1, smem_raw);
+  }
+}
+
 template <int NTPW>
 __global__ __launch_bounds__(RW * 64) void chol_inv2_kernel(double* A, int n, int64_t lda, int64_t strideA, double* X,
                                                             int64_t ldx, int64_t strideX, int32_t* info, int col_off,
@@ -933,8 +1131,27 @@ static void chol_inv2_go(double* A, int n, int64_t lda, int64_t sA, double* X, i
 }
 
 // Two-role split pays from n = 32 up; its workgroup pairs must be co-resident, so a launch holds at
-// most 128 matrices (256 workgroups, one per CU).
+// most 128 matrices (256 workgroups, one per CU).  The three-role split (inverse over two
+// workgroups) for up to 85 matrices.
 static bool use_two_role(int n, int64_t batch) { return n >= 32 && n <= 256 && batch <= 128; }
+static bool use_three_role(int n, int64_t batch) {
+  static int off = -1;
+  if (off < 0) off = getenv("NMGP_CHOL_TWO_ROLE") ? 1 : 0;
+  return !off && n >= 128 && n <= 256 && batch <= 85;
+}
+
+template <int NTPW, int NTPW1>
+static void chol_inv3_go(double* A, int n, int64_t lda, int64_t sA, double* X, int64_t ldx, int64_t sX, int64_t batch,
+                         int32_t* info, size_t sm, hipStream_t s, int col_off, int info_first) {
+  static bool attr_done = false;
+  if (!attr_done) {
+    (void)hipFuncSetAttribute((const void*)chol_inv3_kernel<NTPW, NTPW1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr_done = true;
+  }
+  hipLaunchKernelGGL((chol_inv3_kernel<NTPW, NTPW1>), dim3((unsigned)(3 * batch)), dim3(RW * 64), sm, s, A, n, lda, sA,
+                     X, ldx, sX, info, col_off, info_first);
+}
 
 template <typename T>
 static int chol_inv_small(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx, int64_t sX, int64_t batch,
@@ -942,6 +1159,14 @@ static int chol_inv_small(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ld
   const int nt = (n + 15) >> 4, ntiles = nt * (nt + 1) / 2;
   const size_t sm = chol_inv_smem<T>(n);
   if constexpr (std::is_same<T, double>::value) {
+    if (two_role && use_three_role(n, batch) && !getenv("NMGP_CHOL_FUSED1")) {
+      if (ntiles <= RW * 9)
+        chol_inv3_go<9, 5>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+      else
+        chol_inv3_go<17, 9>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+      NMGP_CHECK_LAUNCH();
+      return NMGP_OK;
+    }
     if (two_role && use_two_role(n, batch) && !getenv("NMGP_CHOL_FUSED1")) {
       if (ntiles <= RW * 3)
         chol_inv2_go<3>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);

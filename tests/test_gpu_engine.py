@@ -429,3 +429,20 @@ def test_index_argument_any_order_matches_oracle():
     gd = _unflatten(eng, grad)
     whole = _rel(torch.cat([gd[k].reshape(-1) for k in O.PARAM_NAMES]), torch.cat([q[k].grad.reshape(-1) for k in O.PARAM_NAMES]))
     assert whole < 1e-9
+
+
+@pytest.mark.parametrize("case", ["mid_forward", "pm25_forward"])
+def test_step_is_deterministic_run_to_run(case):
+    """The fused step (grouped / latency-kernel GEMMs with their split-K combines, the multi-workgroup
+    Cholesky, every reduction) is bit-reproducible: the same batch twice gives identical loss and
+    gradient bits."""
+    if case not in CASES:
+        pytest.skip(case)
+    g, xs, ys, p, eng, theta, grad = _setup(case)
+    outs = []
+    for _ in range(3):
+        eng.forward_backward()           # (zeroes the gradient first; the host noise stays loaded)
+        torch.cuda.synchronize()
+        outs.append((eng.out.clone().cpu(), grad.clone().cpu()))
+    for o, gr in outs[1:]:
+        assert torch.equal(o[:1], outs[0][0][:1]) and torch.equal(gr, outs[0][1])

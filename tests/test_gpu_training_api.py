@@ -303,9 +303,13 @@ def test_packed_pair_layout_matches_dense():
         res[layout] = (float(eng.out[0]), grads, m)
     (ld, gd, md), (lp, gp, mp) = res["dense"], res["packed"]
     assert lp == pytest.approx(ld, rel=1e-13)
+    # (the layouts order the pair columns differently -- dense (0,0),(0,1),..., packed (0,0),(1,0),(1,1),...
+    # -- so sums over pairs, e.g. the KL mean products over the Y columns, round differently: the scalar
+    # hyper-parameter gradients, sums with cancellation, differ at ~1e-12 relative; the step itself is
+    # bit-reproducible, tests/test_gpu_engine.py::test_step_is_deterministic_run_to_run)
     for k in O.PARAM_NAMES:
         if float(gd[k].norm()) > 0:
-            assert _rel(gp[k], gd[k]) < 1e-12, k
+            assert _rel(gp[k], gd[k]) < 1e-11, k
     # the packed model's dense export holds the live pairs; a dense state_dict loads into it
     ii, jj = np.tril_indices(3)
     for k in ("mu_U", "sqrt_U"):

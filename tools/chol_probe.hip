@@ -99,7 +99,7 @@ int main(int argc, char** argv) {
       int rc = lvl == 0 ? nmgp::chol_inv_small<double>(dA, n, n, (int64_t)n * n, dX, n, (int64_t)n * n, batch, dinfo,
                                                        cs, 0, 1)
                         : nmgp::chol_inv_rec<double>(dA, n, n, (int64_t)n * n, dX, n, (int64_t)n * n, batch, dinfo,
-                                                     cs, 0);
+                                                     cs, 0, nullptr);
       HC(hipStreamEndCapture(cs, &g));
       if (rc != 0) return 5;
       HC(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
@@ -136,6 +136,26 @@ int main(int argc, char** argv) {
           l1 += (r1[1] - r1[0]) * 10.0;
           a1 += (r1[2] - r1[1]) * 10.0;
           c1 += (r1[3] - r1[2]) * 10.0;
+        }
+        {
+          std::vector<unsigned long long> tx(1024);
+          HC(hipMemcpy(tx.data(), dtr, tx.size() * 8, hipMemcpyDeviceToHost));
+          printf("  role 0: prologue (tile loads + zeroing) %.0f ns, loop %.0f ns; inverse workgroups end %.0f / %.0f ns "
+                 "after role 0 starts\n", (tx[1001] - tx[1000]) * 10.0, (tx[1002] - tx[1001]) * 10.0,
+                 (tx[1006] - tx[1000]) * 10.0, (tx[1010] - tx[1000]) * 10.0);
+        }
+        {
+          std::vector<unsigned long long> tw(1024);
+          HC(hipMemcpy(tw.data(), dtr, tw.size() * 8, hipMemcpyDeviceToHost));
+          double a = 0, b = 0, c = 0, d = 0;
+          for (int kb = 0; kb < nt; ++kb) {
+            a += (tw[512 + kb * 4] - tw[kb * 4 + 1]) * 10.0;
+            b += (tw[512 + kb * 4 + 1] - tw[512 + kb * 4]) * 10.0;
+            c += (tw[512 + kb * 4 + 2] - tw[512 + kb * 4 + 1]) * 10.0;
+            d += (tw[kb * 4 + 2] - tw[512 + kb * 4 + 2]) * 10.0;
+          }
+          printf("  role 0 panel (ns, summed): colbuf load %.0f  16-column loop %.0f  LDS write %.0f  wait+barrier+flag %.0f\n",
+                 a, b, c, d);
         }
         printf("  block 1 phases (ns, summed): wait-flag %.0f  load %.0f  X-row %.0f  update+store %.0f  (ends %.0f after "
                "block 0)\n", w1, l1, a1, c1, ((double)t1[256 + (nt - 1) * 4 + 3] - (double)tr[nt * 4]) * 10.0);
