@@ -145,6 +145,8 @@ _SIGS = {
     "nmgp_dsvi_finalize_f32": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_mugrad_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_mugrad_f32": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_prefinal_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_prefinal_f32": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_adam_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_dbl, c_dbl, c_dbl, c_dbl, c_vp]),
     "nmgp_adam_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_dbl, c_dbl, c_dbl, c_dbl, c_vp]),
     "nmgp_normal_f64": (c_int, [c_vp, c_i64, c_u64, c_vp, c_i64, c_vp]),

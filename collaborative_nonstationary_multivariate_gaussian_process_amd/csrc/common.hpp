@@ -151,6 +151,30 @@ template <typename T, int K> __device__ inline void block_sum_n(T (&v)[K], T* sc
   __syncthreads();
 }
 
+// The same K sums with the result valid in thread 0 only (the caller's epilogue runs there): the
+// cross-wave step is one wave, lane k summing value k's 16 wave partials, instead of every thread of
+// the block re-reading all K x 16 partials from LDS (15 us of the finalize kernel at K = 20).
+template <typename T, int K> __device__ inline void block_sum_n0(T (&v)[K], T* scratch) {
+  static_assert(K <= 64, "one lane per value");
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = wave_sum(v[k]);
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) scratch[k * 16 + w] = v[k];
+  }
+  __syncthreads();
+  if (w == 0) {
+    T s = 0;
+    if (lane < K)
+      for (int i = 0; i < nw; ++i) s += scratch[lane * 16 + i];
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = shfl(s, k);
+  }
+  __syncthreads();
+}
+
 // v if ok else +0, bitwise: no load is sunk into a branch (loads of a batch stay in flight together)
 // and a NaN in a masked-off element cannot leak through a multiply.
 template <typename T> __device__ inline T keep_if(T v, bool ok);

@@ -569,6 +569,79 @@ __global__ __launch_bounds__(256) void dsvi_mugrad_kernel(Args a) {
 }
 
 // ------------------------------------------------------------------------------------ finalize
+// The recon row partials and the per-factor KL slabs are final right after recon / the KL kernel,
+// long before the last backward kernels: in training steps dsvi_prefinal_kernel (side stream, after
+// recon) reduces them into out[8..14], and the finalize kernel at the end of the main chain only sums
+// the late partials (t-row backward, the RBF / Gibbs builder backward scalars) and adds those.
+template <typename T>
+__device__ inline void sum_recon_kl(const Args& a, T (&acc)[20], T* klstage) {
+  const int D = a.D, M = a.M, NF = a.NF;
+  const T* rp = (const T*)a.red;
+  const int t = threadIdx.x;
+  constexpr int RU = 4;
+  const int nbr = a.nblk_rows;                                     // recon: one partial per row
+  T rv[RU][4];
+#pragma unroll
+  for (int u = 0; u < RU; ++u) {
+    const int b = min(t + u * 1024, nbr - 1);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) rv[u][k] = rp[b * 4 + k];
+  }
+#pragma unroll
+  for (int u = 0; u < RU; ++u)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] += keep_if(rv[u][k], t + u * 1024 < nbr);
+  for (int b = t + RU * 1024; b < nbr; b += 1024)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] += rp[b * 4 + k];
+  const int nslab = (M + KL_ROWS - 1) / KL_ROWS;
+  const T* kp = kl_part<T>(a);
+  constexpr int CH = 1024;
+  const int fpc = CH / nslab;
+  for (int fb = 0; fb < NF; fb += fpc) {
+    const int nf = min(fpc, NF - fb), base = fb * nslab, n = nf * nslab;
+    if (t < n) {
+      T q[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) q[j] = kp[(int64_t)(base + t) * 4 + j];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) klstage[t * 4 + j] = q[j];
+    }
+    __syncthreads();
+    for (int f = fb + t; f < fb + nf; f += blockDim.x) {
+      T p[4] = {0, 0, 0, 0};
+      for (int sl = 0; sl < nslab; ++sl)
+        for (int j = 0; j < 4; ++j) p[j] += klstage[((f - fb) * nslab + sl) * 4 + j];
+      const T v = p[1] - p[0] + (T)0.5 * (p[2] + p[3] - (T)M);
+      ((T*)a.facbuf)[f] = v;                   // per-factor KL (kept for inspection)
+      // static indices only: a computed index into acc[] put the whole array in scratch memory
+      if (f < D) acc[5] += v;
+      else if (f == NF - 1) acc[6] += v;
+      else acc[7] += v;
+    }
+    __syncthreads();
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(1024) void dsvi_prefinal_kernel(Args a) {
+  __shared__ T red[16 * 20];
+  __shared__ T klstage[1024 * 4];
+  T acc[20];
+#pragma unroll
+  for (int k = 0; k < 20; ++k) acc[k] = 0;
+  sum_recon_kl<T>(a, acc, klstage);
+  T v8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v8[k] = acc[k];
+  block_sum_n0(v8, red);
+  if (threadIdx.x == 0) {
+    T* out = (T*)a.out;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out[8 + k] = v8[k];
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
   // every partial sum of the step in ONE pass: 5 row-block sums, per-factor KL slabs, 12 scalar
@@ -580,23 +653,14 @@ __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
 #ifdef NMGP_FIN_TRACE
   const unsigned long long t0 = wall_clock64();
 #endif
-  const int D = a.D, M = a.M, NF = a.NF;
   const T* rp = (const T*)a.red;
   const int t = threadIdx.x;
   T acc[20];
 #pragma unroll
   for (int k = 0; k < 20; ++k) acc[k] = 0;
-  // Loads are clamped and masked (keep_if) instead of guarded, so the first RU strides of every
-  // partial array are in flight together: one memory round trip instead of one per loop trip.
-  constexpr int RU = 4;
-  const int nbr = a.nblk_rows;                                     // recon: one partial per row
-  T rv[RU][4];
-#pragma unroll
-  for (int u = 0; u < RU; ++u) {
-    const int b = min(t + u * 1024, nbr - 1);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) rv[u][k] = rp[b * 4 + k];
-  }
+  // Loads are clamped and masked (keep_if) instead of guarded, so every partial array's first
+  // strides are in flight together: one memory round trip instead of one per loop trip.
+  const int nbr = a.nblk_rows;
   const int ntb = a.elbo_mode ? 0 : (a.B + 3) / 4;                 // t-row backward: per 4-row block
   const T tv = rp[(int64_t)nbr * 4 + min(t, max(ntb - 1, 0))];
   T sv[6][2][2];
@@ -611,13 +675,6 @@ __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
         sv[p][u][1] = sp[i * 2 + 1];
       }
   }
-#pragma unroll
-  for (int u = 0; u < RU; ++u)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) acc[k] += keep_if(rv[u][k], t + u * 1024 < nbr);
-  for (int b = t + RU * 1024; b < nbr; b += 1024)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) acc[k] += rp[b * 4 + k];
   acc[4] += keep_if(tv, t < ntb);
   for (int b = t + 1024; b < ntb; b += 1024) acc[4] += rp[(int64_t)nbr * 4 + b];
   if (!a.elbo_mode) {
@@ -635,39 +692,18 @@ __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
       }
     }
   }
-  const int nslab = (M + KL_ROWS - 1) / KL_ROWS;
-  const T* kp = kl_part<T>(a);
-  // per-factor KL from its slab partials, summed in slab order; the partials are brought in by
-  // (factor, slab) in parallel chunks that fit LDS, so no thread walks a dependent chain of loads
-  {
-    constexpr int CH = 1024;                     // (factor, slab) pairs per chunk, 4 values each
-    T* stage = klstage;
-    const int fpc = CH / nslab;                  // whole factors per chunk (M <= 16384: fpc >= 1)
-    for (int fb = 0; fb < NF; fb += fpc) {
-      const int nf = min(fpc, NF - fb), base = fb * nslab, n = nf * nslab;
-      if (t < n) {
-        T q[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) q[j] = kp[(int64_t)(base + t) * 4 + j];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) stage[t * 4 + j] = q[j];
-      }
-      __syncthreads();
-      for (int f = fb + t; f < fb + nf; f += blockDim.x) {
-        T p[4] = {0, 0, 0, 0};
-        for (int sl = 0; sl < nslab; ++sl)
-          for (int j = 0; j < 4; ++j) p[j] += stage[((f - fb) * nslab + sl) * 4 + j];
-        const T v = p[1] - p[0] + (T)0.5 * (p[2] + p[3] - (T)M);
-        ((T*)a.facbuf)[f] = v;                   // per-factor KL (kept for inspection)
-        acc[f < D ? 5 : (f == NF - 1 ? 6 : 7)] += v;
-      }
-      __syncthreads();
-    }
-  }
+  // per-factor KL from its slab partials (slab order) and the recon row partials: here only for
+  // compute_ELBO samples; training steps took them from dsvi_prefinal_kernel (added after the sum)
+  if (a.elbo_mode) sum_recon_kl<T>(a, acc, klstage);
 #ifdef NMGP_FIN_TRACE
   const unsigned long long t1 = wall_clock64();
 #endif
-  block_sum_n(acc, red);
+  block_sum_n0(acc, red);        // (valid in thread 0, which writes every output below)
+  if (!a.elbo_mode && threadIdx.x == 0) {
+    const T* pre = (const T*)a.out + 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += pre[k];     // acc[k] holds no early partials here: exact copy
+  }
 #ifdef NMGP_FIN_TRACE
   const unsigned long long t2 = wall_clock64();
 #endif
@@ -1002,6 +1038,13 @@ template <typename T> static int dsvi_mugrad(const Args* a, hipStream_t s) {
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
+template <typename T> static int dsvi_prefinal(const Args* a, hipStream_t s) {
+  CHECK_ARGS(a);
+  if (a->M > 16384) return -2;
+  hipLaunchKernelGGL(dsvi_prefinal_kernel<T>, dim3(1), dim3(1024), 0, s, *a);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
 template <typename T> static int dsvi_finalize(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
   if (a->M > 16384) return -2;
@@ -1064,6 +1107,7 @@ NMGP_DSVI_ENTRY(delta)
 NMGP_DSVI_ENTRY(tbwd)
 NMGP_DSVI_ENTRY(vbwd)
 NMGP_DSVI_ENTRY(finalize)
+NMGP_DSVI_ENTRY(prefinal)
 NMGP_DSVI_ENTRY(mugrad)
 #undef NMGP_DSVI_ENTRY
 int nmgp_adam_f64(double* th, const double* g, double* m, double* v, int64_t n, int64_t* step, double lr,

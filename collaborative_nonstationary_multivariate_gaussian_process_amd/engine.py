@@ -117,7 +117,7 @@ class DsviEngine:
         self.facbuf = e(NF + 8 * M + 4 * self.NPC + NF * M + NF * ((M + 15) // 16) * 4)
         self.nblk = B                       # recon partials: one per row; then (B+3)//4 t-row partials
         self.red = e(4 * B + (B + 3) // 4)
-        self.out = e(8)
+        self.out = e(16)          # [0..4] loss / SELBO_R / KL_W / KL_v / KL_U, [8..14] training pre-sums
         self.n_ct = (M + 63) // 64
         self.n_rt = (B + 31) // 32
         self.n_rt22 = (M + 31) // 32
@@ -639,6 +639,8 @@ class DsviEngine:
             # (Deferring them until after bwd_w, to leave it the whole chip, measured 2% slower: the
             # main chain after bwd_w is latency-bound either way.)
             ("wait", "side", "recon"),
+            # the recon row partials and the KL slabs summed here, off the main chain (finalize adds them)
+            ("prefinal", "row", row(getattr(lib, "nmgp_dsvi_prefinal_" + self.sfx)), "side"),
             ("bwd_lbar", "gemm", gemm("bwd_lbar"), "side"),
             ("sig", "side", "lbar_done"),
             ("sig", "main", "bwd_w"),

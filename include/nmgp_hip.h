@@ -316,7 +316,8 @@ typedef struct nmgp_dsvi_args {
   void* rowbuf;               /* (2D+5, B) per-row adjoints                                     */
   void* facbuf;               /* KL (NF) | delta (4,M) | wvec (4,M) | sel (4,D*D) | e (NF,M)   */
   void* red;                  /* per-block partial sums                                        */
-  void* out;                  /* [0] loss [1] SELBO_R [2] KL_W [3] KL_v [4] KL_U               */
+  void* out;                  /* [0] loss [1] SELBO_R [2] KL_W [3] KL_v [4] KL_U  (16 entries;  */
+                              /* [8..14] training-step pre-sums of nmgp_dsvi_prefinal_*)      */
   void* gib_row; void* gib_col; void* scal_part; void* phi;
   int32_t* info;
   int32_t n_ct, n_rt, n_rt22, nblk_rows;
@@ -335,6 +336,7 @@ int nmgp_dsvi_tbwd_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* t-row b
 int nmgp_dsvi_vbwd_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* v backward -> Phi         */
 int nmgp_dsvi_finalize_f64(const nmgp_dsvi_args* a, hipStream_t s);   /* loss + scalar gradients   */
 int nmgp_dsvi_mugrad_f64(const nmgp_dsvi_args* a, hipStream_t s);     /* KL mean gradients of mu_W / mu_v / mu_U */
+int nmgp_dsvi_prefinal_f64(const nmgp_dsvi_args* a, hipStream_t s);   /* training step: recon + KL sums -> out[8..14] */
 /* fp32 twins (HCP / ECoG-shaped configurations): same arguments, every buffer float */
 int nmgp_dsvi_hyper_f32(const nmgp_dsvi_args* a, hipStream_t s);
 int nmgp_dsvi_trow_f32(const nmgp_dsvi_args* a, hipStream_t s);
@@ -345,6 +347,7 @@ int nmgp_dsvi_tbwd_f32(const nmgp_dsvi_args* a, hipStream_t s);
 int nmgp_dsvi_vbwd_f32(const nmgp_dsvi_args* a, hipStream_t s);
 int nmgp_dsvi_finalize_f32(const nmgp_dsvi_args* a, hipStream_t s);
 int nmgp_dsvi_mugrad_f32(const nmgp_dsvi_args* a, hipStream_t s);
+int nmgp_dsvi_prefinal_f32(const nmgp_dsvi_args* a, hipStream_t s);
 
 /* ------------------------------------------------------------------ optimiser / RNG
  * torch.optim.Adam update (code/nmgp_dsvi.py:777,854) on a flat parameter vector; step is a
