@@ -85,6 +85,12 @@ _SIGS = {
     "nmgp_gemm_grouped_dyn_f32": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
     "nmgp_gemm_grouped_lat_f64": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
     "nmgp_gemm_grouped_lat_f32": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
+    "nmgp_gemm_plan": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp]),
+    "nmgp_gemm_plan_lat": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp]),
+    "nmgp_gemm_grouped_dyn_planned_f64": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
+    "nmgp_gemm_grouped_dyn_planned_f32": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
+    "nmgp_gemm_grouped_lat_planned_f64": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
+    "nmgp_gemm_grouped_lat_planned_f32": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
     "nmgp_gemm_f64": (c_int, [ctypes.POINTER(GemmDesc), c_vp, c_vp]),
     "nmgp_gemm_f32": (c_int, [ctypes.POINTER(GemmDesc), c_vp, c_vp]),
     "nmgp_potrf_batched_f64": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),

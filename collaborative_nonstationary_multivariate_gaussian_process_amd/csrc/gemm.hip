@@ -750,15 +750,17 @@ static int launch_grouped(const nmgp_gemm_desc* d_desc, int nprob, int total_til
 // `grid` workgroups striding over them.  Split-K combines by last arriver (no co-residency waits).
 template <typename T>
 static int launch_grouped_dyn(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles, const int32_t* d_seg,
-                              int32_t* d_plan, int grid, hipStream_t s) {
+                              int32_t* d_plan, int grid, hipStream_t s, bool planned = false) {
   if (d_desc == nullptr) return -1;
   if (nprob <= 0) return -2;
   if (total_tiles < 0) return -3;
   if (d_plan == nullptr) return -5;
   if (total_tiles == 0) return NMGP_OK;
   if (grid <= 0 || grid > total_tiles) grid = total_tiles;
-  hipLaunchKernelGGL(gemm_plan_kernel, dim3(1), dim3(256), 0, s, d_desc, nprob, d_seg, d_plan);
-  NMGP_CHECK_LAUNCH();
+  if (!planned) {
+    hipLaunchKernelGGL(gemm_plan_kernel, dim3(1), dim3(256), 0, s, d_desc, nprob, d_seg, d_plan);
+    NMGP_CHECK_LAUNCH();
+  }
   GemmArgs a;
   a.descs = d_desc;
   a.nprob = nprob;
@@ -820,6 +822,21 @@ int nmgp_gemm_grouped_dyn_f64(const nmgp_gemm_desc* d, int np, int tt, const int
 int nmgp_gemm_grouped_dyn_f32(const nmgp_gemm_desc* d, int np, int tt, const int32_t* seg, int32_t* plan, int grid,
                               hipStream_t s) {
   return nmgp::launch_grouped_dyn<float>(d, np, tt, seg, plan, grid, s);
+}
+int nmgp_gemm_plan(const nmgp_gemm_desc* d, int np, const int32_t* seg, int32_t* plan, hipStream_t s) {
+  if (!d || !plan) return -1;
+  if (np <= 0) return -2;
+  hipLaunchKernelGGL(nmgp::gemm_plan_kernel, dim3(1), dim3(256), 0, s, d, np, seg, plan);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
+int nmgp_gemm_grouped_dyn_planned_f64(const nmgp_gemm_desc* d, int np, int tt, const int32_t* seg, int32_t* plan,
+                                      int grid, hipStream_t s) {
+  return nmgp::launch_grouped_dyn<double>(d, np, tt, seg, plan, grid, s, true);
+}
+int nmgp_gemm_grouped_dyn_planned_f32(const nmgp_gemm_desc* d, int np, int tt, const int32_t* seg, int32_t* plan,
+                                      int grid, hipStream_t s) {
+  return nmgp::launch_grouped_dyn<float>(d, np, tt, seg, plan, grid, s, true);
 }
 int nmgp_gemm_grouped_f32(const nmgp_gemm_desc* d, int np, int tt, const int32_t* seg, hipStream_t s) {
   return nmgp::launch_grouped<float>(d, np, tt, seg, s);

@@ -338,7 +338,7 @@ __global__ __launch_bounds__(256) void lat_plan_kernel(const nmgp_gemm_desc* __r
 
 template <typename T>
 int launch_lat(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles, const int32_t* d_seg, int32_t* d_plan,
-               int grid, hipStream_t s) {
+               int grid, hipStream_t s, bool planned = false) {
   if (d_desc == nullptr) return -1;
   if (nprob <= 0) return -2;
   if (total_tiles < 0) return -3;
@@ -351,8 +351,10 @@ int launch_lat(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles, const i
   a.dyn_start = nullptr;
   int wgs = ((total_tiles + 7) / 8) * 8;
   if (d_plan != nullptr) {
-    hipLaunchKernelGGL(lat_plan_kernel, dim3(1), dim3(256), 0, s, d_desc, nprob, d_seg, d_plan);
-    NMGP_CHECK_LAUNCH();
+    if (!planned) {
+      hipLaunchKernelGGL(lat_plan_kernel, dim3(1), dim3(256), 0, s, d_desc, nprob, d_seg, d_plan);
+      NMGP_CHECK_LAUNCH();
+    }
     a.dyn_start = d_plan;
     if (grid > 0) wgs = min(wgs, ((grid + 7) / 8) * 8);   // a multiple of 8 keeps each workgroup on one XCD chunk
   }
@@ -384,5 +386,22 @@ int nmgp_gemm_grouped_lat_f64(const nmgp_gemm_desc* d, int np, int tt, const int
 int nmgp_gemm_grouped_lat_f32(const nmgp_gemm_desc* d, int np, int tt, const int32_t* seg, int32_t* plan, int grid,
                               hipStream_t s) {
   return nmgp::launch_lat<float>(d, np, tt, seg, plan, grid, s);
+}
+int nmgp_gemm_plan_lat(const nmgp_gemm_desc* d, int np, const int32_t* seg, int32_t* plan, hipStream_t s) {
+  if (!d || !plan) return -1;
+  if (np <= 0) return -2;
+  hipLaunchKernelGGL(nmgp::lat_plan_kernel, dim3(1), dim3(256), 0, s, d, np, seg, plan);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
+int nmgp_gemm_grouped_lat_planned_f64(const nmgp_gemm_desc* d, int np, int tt, const int32_t* seg, int32_t* plan,
+                                      int grid, hipStream_t s) {
+  if (!plan) return -5;
+  return nmgp::launch_lat<double>(d, np, tt, seg, plan, grid, s, true);
+}
+int nmgp_gemm_grouped_lat_planned_f32(const nmgp_gemm_desc* d, int np, int tt, const int32_t* seg, int32_t* plan,
+                                      int grid, hipStream_t s) {
+  if (!plan) return -5;
+  return nmgp::launch_lat<float>(d, np, tt, seg, plan, grid, s, true);
 }
 }

@@ -514,8 +514,21 @@ class DsviEngine:
         def row(fn):
             return lambda s: L.check(fn(ctypes.byref(a), s), fn.__name__)
 
+        # segment-sized groups of the training step whose tile plans are computed ahead, on the side
+        # stream right after the minibatch gather (off the main chain): quad and bwd_w
+        pre_planned = set()
+        if not elbo_mode and os.environ.get("NMGP_PLAN_AHEAD", "1") != "0":
+            pre_planned = {nm for nm in ("quad", "bwd_w")
+                           if isinstance(p.get(nm), H.GemmGroup) and p[nm].plan is not None}
+
         def gemm(name):
+            if name in pre_planned:
+                return lambda s: p[name](s, planned=True)
             return lambda s: p[name](s)
+
+        def plans(s):
+            for nm in sorted(pre_planned):
+                p[nm].plan_now(s)
 
         def pw(name):
             return lambda s: p[name](self.dt, s)
@@ -569,6 +582,8 @@ class DsviEngine:
                           ("syrk_side", "gemm", gemm("syrk_side"), "side")]
             else:
                 steps.append(("syrk_side", "gemm", gemm("syrk_side"), "side"))
+            if pre_planned:
+                steps += [("plans", "gemm_plan", plans, "side"), ("sig", "side", "plans")]
             steps.append(("chol_side", "chol", chol(0, FV), "side"))
             if not elbo_mode:
                 steps.append(("xs_side", "gemm", gemm("xs_side"), "side"))
@@ -631,6 +646,10 @@ class DsviEngine:
             ("kl_abar", "gemm", gemm("kl_abar"), "side"),
             ("bwd_kly", "gemm", gemm("bwd_kly"), "side"),
             ("sig", "side", "kl_done"),
+        ]
+        if pre_planned:
+            steps.append(("wait", "main", "plans"))
+        steps += [
             ("quad", "gemm", gemm("quad"), "main"),
             ("recon", "row", row(getattr(lib, "nmgp_dsvi_recon_" + self.sfx)), "main"),
             ("sig", "main", "recon"),

@@ -245,19 +245,31 @@ class GemmGroup:
     def macs(self, seg=None):
         return sum(desc_macs(d, seg) for d in self.descs)
 
-    def __call__(self, stream=None):
+    def plan_now(self, stream=None):
+        """Enqueue only the device tile plan of a segment-sized group (e.g. right after the minibatch
+        gather, on another stream); later calls with planned=True reuse it.  No-op for static groups."""
+        if self.plan is None or self.n == 0 or self.total == 0:
+            return False
+        s = stream if stream is not None else L.stream_handle()
+        fn = L.lib().nmgp_gemm_plan_lat if self.lat else L.lib().nmgp_gemm_plan
+        L.check(fn(ctypes.c_void_p(self.dev.data_ptr()), self.n, ctypes.c_void_p(self.seg.data_ptr()),
+                   ctypes.c_void_p(self.plan.data_ptr()), s), "gemm_plan")
+        return True
+
+    def __call__(self, stream=None, planned=False):
         if self.n == 0 or self.total == 0:
             return
         s = stream if stream is not None else L.stream_handle()
         segp = ctypes.c_void_p(self.seg.data_ptr()) if self.seg is not None else None
+        pre = "_planned_" if (planned and self.plan is not None) else "_"
         if self.lat:
-            fn = getattr(L.lib(), "nmgp_gemm_grouped_lat_" + _sfx(self.dtype))
+            fn = getattr(L.lib(), "nmgp_gemm_grouped_lat" + pre + _sfx(self.dtype))
             plan = ctypes.c_void_p(self.plan.data_ptr()) if self.plan is not None else None
             L.check(fn(ctypes.c_void_p(self.dev.data_ptr()), self.n, self.total, segp, plan, self.grid, s),
                     "gemm_grouped_lat")
             return
         if self.plan is not None:
-            fn = getattr(L.lib(), "nmgp_gemm_grouped_dyn_" + _sfx(self.dtype))
+            fn = getattr(L.lib(), "nmgp_gemm_grouped_dyn" + pre + _sfx(self.dtype))
             L.check(fn(ctypes.c_void_p(self.dev.data_ptr()), self.n, self.total, segp,
                        ctypes.c_void_p(self.plan.data_ptr()), self.grid, s), "gemm_grouped_dyn")
             return

@@ -117,6 +117,20 @@ int nmgp_gemm_grouped_lat_f64(const nmgp_gemm_desc* d_desc, int nprob, int total
                               int32_t* plan, int grid, hipStream_t stream);
 int nmgp_gemm_grouped_lat_f32(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles, const int32_t* d_seg,
                               int32_t* plan, int grid, hipStream_t stream);
+/* Tile plans computed ahead (e.g. right after the minibatch gather, on another stream): the plan
+ * kernels alone (64-row tiles for the tile kernel, 32-row for the latency kernel), and the grouped
+ * launches that use such a plan as is.                                                         */
+int nmgp_gemm_plan(const nmgp_gemm_desc* d_desc, int nprob, const int32_t* d_seg, int32_t* plan, hipStream_t stream);
+int nmgp_gemm_plan_lat(const nmgp_gemm_desc* d_desc, int nprob, const int32_t* d_seg, int32_t* plan,
+                       hipStream_t stream);
+int nmgp_gemm_grouped_dyn_planned_f64(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles,
+                                      const int32_t* d_seg, int32_t* plan, int grid, hipStream_t stream);
+int nmgp_gemm_grouped_dyn_planned_f32(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles,
+                                      const int32_t* d_seg, int32_t* plan, int grid, hipStream_t stream);
+int nmgp_gemm_grouped_lat_planned_f64(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles,
+                                      const int32_t* d_seg, int32_t* plan, int grid, hipStream_t stream);
+int nmgp_gemm_grouped_lat_planned_f32(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles,
+                                      const int32_t* d_seg, int32_t* plan, int grid, hipStream_t stream);
 /* one problem passed by value (host descriptor; tiles fields are filled internally)          */
 int nmgp_gemm_f64(const nmgp_gemm_desc* h_desc, const int32_t* d_seg, hipStream_t stream);
 int nmgp_gemm_f32(const nmgp_gemm_desc* h_desc, const int32_t* d_seg, hipStream_t stream);
