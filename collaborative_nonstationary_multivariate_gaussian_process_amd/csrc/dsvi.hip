@@ -31,22 +31,31 @@ __device__ inline void pair_ij(int q, int& i, int& j) {
 }
 // Block index of coefficient pair (i, j <= i) in mu_U / sqrt_U / Y_0 / Y_1: the reference's dense
 // D x D layout, or the packed Q-pair layout (engine.param_layout)
+// (pair sharding, SURVEY §8e axis 3: a rank holds only the packed pairs [pair_q0, pair_q0 + Q) -- the
+// pairs (i, j <= i) of its contiguous range of outputs -- and its blocks are numbered from pair_q0)
 __device__ inline int64_t pair_blk(const nmgp_dsvi_args& a, int i, int j) {
-  return a.pair_packed ? (int64_t)i * (i + 1) / 2 + j : (int64_t)i * a.D + j;
+  return a.pair_packed ? (int64_t)i * (i + 1) / 2 + j - a.pair_q0 : (int64_t)i * a.D + j;
+}
+// position of pair (i, j) in the Q x B pair noise (reference call order, local pair window)
+__device__ inline int64_t pair_noise(const nmgp_dsvi_args& a, int i, int j) {
+  return (int64_t)i * (i + 1) / 2 + j - a.pair_q0;
 }
 __device__ inline int64_t pair_cols(const nmgp_dsvi_args& a) {
   return a.pair_packed ? (int64_t)a.Q : (int64_t)a.D * a.D;
 }
 
-// Variational factor order: f < D latent functions W_f | D <= f < D+Q coefficient pairs (i,j) in
-// (i, j<=i) order | f = D+Q (= NF-1) the length-scale process v.  Prior slot of factor f:
+// Variational factor order: f < nW latent functions W_f (nW = n_wfac: D, or 0 on a pair-sharded rank
+// that does not own KL_W) | nW <= f < nW+Q coefficient pairs (i,j) in (i, j<=i) order, packed index
+// pair_q0 + f - nW | f = NF-1 the length-scale process v.  Prior slot of factor f:
 // 0 = t (v), 1 = L0 (off-diagonal pairs), 2 = L1 (diagonal pairs), 3 = G (W).
-__device__ inline int prior_of(int f, int D) {
-  const int Q = D * (D + 1) / 2;
-  if (f < D) return 3;
-  if (f == D + Q) return 0;
+__device__ inline void fac_pair(const nmgp_dsvi_args& a, int f, int& i, int& j) {
+  pair_ij(f - a.n_wfac + a.pair_q0, i, j);
+}
+__device__ inline int prior_of(const nmgp_dsvi_args& a, int f) {
+  if (f < a.n_wfac) return 3;
+  if (f == a.NF - 1) return 0;
   int i, j;
-  pair_ij(f - D, i, j);
+  fac_pair(a, f, i, j);
   return i == j ? 2 : 1;
 }
 
@@ -227,7 +236,7 @@ __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
       const T m = tot(3 + 4 * u), g = (T)1 - qG + tot(4 + 4 * u);
       const T s2p = var_floor((diag ? s21 : s20) - (diag ? q1 : q0) + tot(6 + 4 * u));
       const T sd = dsqrt(s2p + lam);
-      const T zz = noise[M + B + (int64_t)(pi * (pi + 1) / 2 + pj) * B + r];
+      const T zz = noise[M + B + pair_noise(a, pi, pj) * B + r];
       const T smp = tot(5 + 4 * u) + zz * sd;
       const T l = diag ? dexp(smp) : smp;
       lm += l * m;
@@ -252,7 +261,7 @@ __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
           const T m = tot(3 + 4 * u), g = (T)1 - qG + tot(4 + 4 * u);
           const T s2p = var_floor((diag ? s21 : s20) - (diag ? q1 : q0) + tot(6 + 4 * u));
           const T sd = dsqrt(s2p + lam);
-          const T zz = noise[M + B + (int64_t)(o * (o + 1) / 2 + s) * B + r];
+          const T zz = noise[M + B + pair_noise(a, o, s) * B + r];
           const T smp = tot(5 + 4 * u) + zz * sd;
           const T l = diag ? dexp(smp) : smp;
           mbar = Fbar * l;
@@ -331,27 +340,27 @@ __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
 template <typename T> __device__ inline const T* fac_S(const Args& a, int f) {
   const T* th = (const T*)a.theta;
   const int64_t MM = (int64_t)a.M * a.M;
-  if (f < a.D) return th + a.off_sW + f * MM;
+  if (f < a.n_wfac) return th + a.off_sW + f * MM;
   if (f == a.NF - 1) return th + a.off_sv;
   int i, j;
-  pair_ij(f - a.D, i, j);
+  fac_pair(a, f, i, j);
   return th + a.off_sU + pair_blk(a, i, j) * MM;
 }
 template <typename T> __device__ inline const T* fac_mu(const Args& a, int f) {
   const T* th = (const T*)a.theta;
-  if (f < a.D) return th + a.off_muW + (int64_t)f * a.M;
+  if (f < a.n_wfac) return th + a.off_muW + (int64_t)f * a.M;
   if (f == a.NF - 1) return th + a.off_muv;
   int i, j;
-  pair_ij(f - a.D, i, j);
+  fac_pair(a, f, i, j);
   return th + a.off_muU + pair_blk(a, i, j) * a.M;
 }
 template <typename T> __device__ inline const T* fac_y(const Args& a, int f) {
   const T* Y = (const T*)a.Y;
   const int D = a.D, M = a.M;
-  if (f < D) return Y + (int64_t)f * M;
+  if (f < a.n_wfac) return Y + (int64_t)f * M;
   if (f == a.NF - 1) return Y + (int64_t)D * M;
   int i, j;
-  pair_ij(f - D, i, j);
+  fac_pair(a, f, i, j);
   const int64_t base = (int64_t)(D + 1) * M + (i == j ? pair_cols(a) * M : 0);
   return Y + base + pair_blk(a, i, j) * M;
 }
@@ -372,7 +381,7 @@ __global__ __launch_bounds__(256) void dsvi_kl_kernel(Args a) {
   const T lam = (T)a.jitter;
   const T* Af = (const T*)a.Afac;
   T* fb = (T*)a.facbuf;
-  const int f = blockIdx.x, k = prior_of(f, D), slab = blockIdx.y;
+  const int f = blockIdx.x, k = prior_of(a, f), slab = blockIdx.y;
   const int q = threadIdx.x & 15, i = slab * KL_ROWS + (threadIdx.x >> 4);
   const T* S = fac_S<T>(a, f);
   T ld1 = 0, ld2 = 0, t2 = 0, t3 = 0;
@@ -427,7 +436,7 @@ __global__ __launch_bounds__(256) void dsvi_delta_kernel(Args a) {
   const T* ev = fb + NF + 8 * (int64_t)M + 4 * pair_cols(a);
   T dl = 0;
   for (int f = 0; f < NF; ++f)
-    if (prior_of(f, D) == k) dl += ev[(int64_t)f * M + i];
+    if (prior_of(a, f) == k) dl += ev[(int64_t)f * M + i];
   const T c2 = C2[(int64_t)i * M + i];
   fb[NF + (int64_t)k * M + i] = dl;
   fb[NF + 4 * (int64_t)M + (int64_t)k * M + i] = (T)1 / (c2 * c2);
@@ -549,16 +558,16 @@ __global__ __launch_bounds__(256) void dsvi_mugrad_kernel(Args a) {
   const int64_t n = DM + M + DDM, stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     if (i < DM) {
-      gw[a.off_muW + i] = gw[a.off_muW + i] + Y[i];
+      if (a.n_wfac > 0) gw[a.off_muW + i] = gw[a.off_muW + i] + Y[i];
     } else if (i < DM + M) {
       const int64_t c = i - DM;
-      gw[a.off_muv + c] += vbar[c] + Y[DM + c];
+      gw[a.off_muv + c] += a.kl_v ? vbar[c] + Y[DM + c] : vbar[c];
     } else {
       const int64_t idx = i - DM - M;
       const int ij = (int)(idx / M);
       int pi, pj;
       if (a.pair_packed) {
-        pair_ij(ij, pi, pj);
+        pair_ij(ij + a.pair_q0, pi, pj);
       } else {
         pi = ij / D;
         pj = ij - pi * D;
@@ -612,10 +621,11 @@ __device__ inline void sum_recon_kl(const Args& a, T (&acc)[20], T* klstage) {
       T p[4] = {0, 0, 0, 0};
       for (int sl = 0; sl < nslab; ++sl)
         for (int j = 0; j < 4; ++j) p[j] += klstage[((f - fb) * nslab + sl) * 4 + j];
-      const T v = p[1] - p[0] + (T)0.5 * (p[2] + p[3] - (T)M);
+      // (a rank without KL_v never launched the v factor's KL: no -M/2 constant for it either)
+      const T v = (f == NF - 1 && !a.kl_v) ? (T)0 : p[1] - p[0] + (T)0.5 * (p[2] + p[3] - (T)M);
       ((T*)a.facbuf)[f] = v;                   // per-factor KL (kept for inspection)
       // static indices only: a computed index into acc[] put the whole array in scratch memory
-      if (f < D) acc[5] += v;
+      if (f < a.n_wfac) acc[5] += v;
       else if (f == NF - 1) acc[6] += v;
       else acc[7] += v;
     }
@@ -1007,7 +1017,9 @@ template <typename T> static int dsvi_recon(const Args* a, hipStream_t s) {
 }
 template <typename T> static int dsvi_kl(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
-  hipLaunchKernelGGL(dsvi_kl_kernel<T>, dim3(a->NF, (a->M + KL_ROWS - 1) / KL_ROWS), dim3(256), 0, s, *a);
+  const int nf = a->NF - (a->kl_v ? 0 : 1);       // the v factor is last: a rank without KL_v skips it
+  if (nf <= 0) return NMGP_OK;
+  hipLaunchKernelGGL(dsvi_kl_kernel<T>, dim3(nf, (a->M + KL_ROWS - 1) / KL_ROWS), dim3(256), 0, s, *a);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }

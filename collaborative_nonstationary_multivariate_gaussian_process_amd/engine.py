@@ -33,15 +33,28 @@ PARAM_NAMES = ["mu_W", "sqrt_W", "mu_v", "sqrt_v", "mu_U", "sqrt_U",
 HYPER_NAMES = PARAM_NAMES[6:]
 
 
-def param_layout(D, M, packed=False):
+def pair_window(D, pair_range=None):
+    """(q0, Q) of the packed pairs held for outputs [i0, i1): the pairs (i, j <= i) of those outputs are
+    the contiguous packed indices [i0(i0+1)/2, i1(i1+1)/2).  None = all D outputs."""
+    i0, i1 = (0, D) if pair_range is None else (int(pair_range[0]), int(pair_range[1]))
+    if not 0 <= i0 < i1 <= D:
+        raise ValueError(f"pair_range {pair_range} must be a non-empty output range inside [0, {D})")
+    q0 = i0 * (i0 + 1) // 2
+    return q0, i1 * (i1 + 1) // 2 - q0
+
+
+def param_layout(D, M, packed=False, pair_range=None):
     """Offsets (elements) of the 13 parameters inside the flat theta vector, registration order.
 
     packed=False: the reference's dense layout, mu_U (D, D, M) and sqrt_U (D, D, M, M) with all D^2
     coefficient blocks (code/nmgp_dsvi.py:136-143).  packed=True: only the Q = D(D+1)/2 live pairs
     (i, j <= i) in (i, j) order, mu_U (Q, M) and sqrt_U (Q, M, M) -- the dead upper blocks never
     receive a gradient, and at the ECoG shape (D=128, M=1024) the dense layout is
-    69 GB per copy of sqrt_U in fp32 against 35 GB packed."""
-    Q = D * (D + 1) // 2
+    69 GB per copy of sqrt_U in fp32 against 35 GB packed.  pair_range=(i0, i1) (packed only): a
+    pair-sharded rank's vector -- mu_U / sqrt_U hold only the pairs of outputs [i0, i1)."""
+    if pair_range is not None and not packed:
+        raise ValueError("pair_range needs the packed pair layout")
+    Q = pair_window(D, pair_range)[1]
     if packed:
         shapes = [(D, M), (D, M, M), (M,), (M, M), (Q, M), (Q, M, M)] + [()] * 7
     else:
@@ -54,17 +67,26 @@ def param_layout(D, M, packed=False):
     return offs, o
 
 
-def pair_list(D):
-    return [(i, j) for i in range(D) for j in range(i + 1)]
+def pair_list(D, pair_range=None):
+    i0, i1 = (0, D) if pair_range is None else pair_range
+    return [(i, j) for i in range(i0, i1) for j in range(i + 1)]
 
 
 class DsviEngine:
     """Workspace + launch schedule of one DSVI step for fixed (D, M, B)."""
 
-    def __init__(self, D, M, B, z, device="cuda", jitter=JITTER, dtype=F64, packed=False, factor_ws=None):
+    def __init__(self, D, M, B, z, device="cuda", jitter=JITTER, dtype=F64, packed=False, factor_ws=None,
+                 pair_range=None, kl_owner=True):
         """packed: the parameter vector uses the packed pair layout of param_layout.  factor_ws: the
         (Afac, Cinv, Xs) factor workspaces of another engine of the same (D, M, dtype) to share (they
-        hold no state between steps; a model's engines never run concurrently)."""
+        hold no state between steps; a model's engines never run concurrently).
+
+        Pair sharding (SURVEY §8e axis 3, training steps only): pair_range=(i0, i1) makes this the
+        engine of a rank that owns outputs [i0, i1) -- its minibatch holds only rows of those outputs,
+        its parameter vector only their pairs (param_layout(pair_range=...)), and it factors only their
+        Sigma_U blocks; kl_owner=False drops KL_W and KL_v (and the W factors, which only the KL needs)
+        so that exactly one rank adds them.  The loss and the replicated gradients (mu_W, sqrt_W, mu_v,
+        sqrt_v, hyper-parameters) of the ranks then sum to the whole model's (distributed.PairShard)."""
         if not torch.cuda.is_available():
             raise RuntimeError("DsviEngine needs a HIP device; there is no CPU fallback")
         if dtype not in (F64, F32):
@@ -73,12 +95,18 @@ class DsviEngine:
         self.dt = dtype
         self.sfx = _sfx(dtype)
         self.D, self.M, self.B = D, M, B
-        self.Q = D * (D + 1) // 2
-        self.NF = D + 1 + self.Q
+        if pair_range is not None and not packed:
+            raise ValueError("pair sharding needs the packed pair layout")
+        self.pair_range = None if pair_range is None else (int(pair_range[0]), int(pair_range[1]))
+        self.q0, self.Q = pair_window(D, self.pair_range)
+        self.pairs = pair_list(D, self.pair_range)
+        self.kl_owner = bool(kl_owner)
+        self.nW = D if self.kl_owner else 0      # W factors in the factor list (only their KL needs them)
+        self.NF = self.nW + 1 + self.Q
         self.dev = torch.device(device)
         self.jitter = jitter
         self.packed = bool(packed)
-        self.offs, self.nparam = param_layout(D, M, packed=self.packed)
+        self.offs, self.nparam = param_layout(D, M, packed=self.packed, pair_range=self.pair_range)
         Q, NF = self.Q, self.NF
         self.NPC = Q if self.packed else D * D     # pair columns of mu_U / Y_0 / Y_1 / sel
         e = lambda *shape: torch.zeros(*shape, dtype=self.dt, device=self.dev)
@@ -140,9 +168,8 @@ class DsviEngine:
             self.pri_X64 = torch.zeros(4, M, M, dtype=F64, device=self.dev)
         # selection weights for the -1/2 Y diag(sel) Y^T prior adjoint (static)
         sel = np.zeros((4, self.NPC))
-        for i in range(D):
-            for j in range(i + 1):
-                sel[2 if i == j else 1, self.pidx(i, j)] = 1.0
+        for (i, j) in self.pairs:
+            sel[2 if i == j else 1, self.pidx(i, j)] = 1.0
         base = NF + 8 * M
         self.facbuf[base:base + 4 * self.NPC] = torch.from_numpy(sel.reshape(-1)).to(self.dev)
         self._theta = None
@@ -150,7 +177,7 @@ class DsviEngine:
 
     def pidx(self, i, j):
         """Block index of coefficient pair (i, j) in mu_U / sqrt_U (dense i*D + j, or packed)."""
-        return i * (i + 1) // 2 + j if self.packed else i * self.D + j
+        return i * (i + 1) // 2 + j - self.q0 if self.packed else i * self.D + j
 
     def factor_workspace(self):
         return (self.Afac, self.Cinv, self.Xs)
@@ -189,6 +216,7 @@ class DsviEngine:
         a.n_ct, a.n_rt, a.n_rt22, a.nblk_rows = self.n_ct, self.n_rt, self.n_rt22, self.nblk
         for i, v in enumerate(self.scal_off):
             a.scal_off[i] = int(v)
+        a.pair_q0, a.n_wfac, a.kl_v = self.q0, self.nW, 1 if self.kl_owner else 0
         return a
 
     # ------------------------------------------------------------------------------------ plans
@@ -201,12 +229,18 @@ class DsviEngine:
         o = self.offs
         sW, sv, sU = o["sqrt_W"][0], o["sqrt_v"][0], o["sqrt_U"][0]
         muW, muv, muU, hyp = o["mu_W"][0], o["mu_v"][0], o["mu_U"][0], o["sigma2_tildeell_log"][0]
-        pairs = pair_list(D)
-        # factor order: W (D) | pairs (Q) | v  -> v and the 3 static priors are contiguous slots NF-1..NF+2
+        if elbo_mode and self.pair_range is not None:
+            raise NotImplementedError("compute_ELBO gathers a column of L (code/nmgp_dsvi.py:361): rows of output o "
+                                      "need the pairs (s, o) of every s >= o, so it is sharded over samples, not pairs")
+        pairs = self.pairs
+        nW = self.nW
+        i0, i1 = self.pair_range if self.pair_range is not None else (0, D)
+        # factor order: W (nW) | pairs (Q) | v  -> v and the 3 static priors are contiguous slots NF-1..NF+2
         pq = self.pidx
         NPC = self.NPC
-        fac_off = [sW + d * MM for d in range(D)] + [sU + pq(i, j) * MM for (i, j) in pairs] + [sv]
-        prior_of = [3] * D + [2 if i == j else 1 for (i, j) in pairs] + [0]
+        fac_off = [sW + d * MM for d in range(nW)] + [sU + pq(i, j) * MM for (i, j) in pairs] + [sv]
+        prior_of = [3] * nW + [2 if i == j else 1 for (i, j) in pairs] + [0]
+        NFK = NF if self.kl_owner else NF - 1    # factors whose KL this engine adds (v is last)
         FV = NF - 1
         dev, seg = self.dev, self.seg
         G = lambda descs: H.GemmGroup(descs, dev, self.dt, seg=seg)
@@ -297,7 +331,7 @@ class DsviEngine:
         # >= d, so k runs over the (i + 1) latent blocks that are non-zero there, not all D)
         d17 = [g(self.Pbar, self.WG, th, B, M, (i + 1) * M, (M, 1, BM), (1, M, MM), (M, 1), flags=L.B_UPPER,
                  kb=(M, M), beta=1.0, offs=(0, sW, 3 * BM), row_seg=i) for i in range(D)]
-        for i in range(D):
+        for i in range(i0, i1):
             d17.append(g(self.Pbar, self.WP, th, B, M, M, (M, 1, 0), (1, M, 0), (M, 1), flags=L.B_UPPER, beta=1.0,
                          offs=(i * BM, sU + pq(i, i) * MM, 2 * BM), row_seg=i))
             if i > 0:
@@ -341,7 +375,7 @@ class DsviEngine:
             d18.append(g(self.Abar, self.Cinv, self.Cinv, M, M, M, (1, M, 0), (M, 1, 0), (M, 1),
                          flags=L.A_UPPER | L.B_LOWER, kscale=(fb, NF + k * M),
                          offs=((NF + k) * MM, (NF + k) * MM, k * MM)))
-        for f in range(NF):
+        for f in range(NFK):
             k = prior_of[f]
             d18.append(g(gr, self.Cinv, self.Xs, M, M, M, (1, M, 0), (M, 1, 0), (M, 1),
                          flags=L.A_UPPER | L.B_LOWER | L.OUT_TRIL | L.EPI_E_LOWER, alpha=-1.0, beta=1.0,
@@ -356,18 +390,20 @@ class DsviEngine:
         p["kl_lbar"] = G(d18[7:])
         if self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0":
             # KL L-bar of all NF factors: -C_f^-T Xs_f + diag(1/C_ii^2) L_f on the 128x128 kernel
-            slots = [f * MM for f in range(NF)]
-            p["kl_lbar"] = H.BigBatch(self.Cinv, self.Xs, gr, slots, slots, fac_off, M, M, M, lda=M, ldb=M,
+            slots = [f * MM for f in range(NFK)]
+            p["kl_lbar"] = H.BigBatch(self.Cinv, self.Xs, gr, slots, slots, fac_off[:NFK], M, M, M, lda=M, ldb=M,
                                       a_kcontig=False, b_kcontig=False,
                                       flags=L.A_UPPER | L.B_LOWER | L.OUT_TRIL | L.EPI_E_LOWER, alpha=-1.0, beta=1.0,
-                                      epi=(th, fac_off, (M, 1), fb, [NF + 4 * M + prior_of[f] * M for f in range(NF)],
-                                           1.0))
+                                      epi=(th, fac_off[:NFK], (M, 1), fb,
+                                           [NF + 4 * M + prior_of[f] * M for f in range(NFK)], 1.0))
         # B4: Abar_k -= 1/2 Y_k diag(sel_k) Y_k^T
         ybase = [D * M, (D + 1) * M, (D + 1 + NPC) * M, 0]
         ncol = [1, NPC, NPC, D]
         sel_base = NF + 8 * M
         d19 = []
         for k in range(4):
+            if (k == 0 and not self.kl_owner) or (k == 3 and nW == 0):
+                continue                          # KL_v / KL_W belong to another rank
             ks = (fb, sel_base + k * NPC) if k in (1, 2) else None
             d19.append(g(self.Abar, self.Y, self.Y, M, M, ncol[k], (1, M, 0), (M, 1, 0), (M, 1), alpha=-0.5,
                          beta=1.0, kscale=ks, offs=(ybase[k], ybase[k], k * MM)))

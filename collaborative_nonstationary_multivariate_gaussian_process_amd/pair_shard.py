@@ -1,0 +1,212 @@
+"""Pair sharding of the coefficient GPs across ranks (SURVEY.md §8e axis 3; HCP / ECoG shapes).
+
+The reference keeps every coefficient pair (i, j <= i) of the D x D LMC matrix in one process:
+mu_U (D, D, M), sqrt_U (D, D, M, M), the Q Cholesky factors of Sigma_U and their KL terms
+(code/nmgp_dsvi.py:136-155, 227-237, 281-295).  At the ECoG shape (D = 128, M = 1024, Q = 8256)
+those are 35 GB of parameters per copy (fp32, packed) and ~95% of a training step's flops.
+
+Here rank r owns a contiguous range of OUTPUTS [i0, i1) and with it
+
+* the pairs (i, j <= i) of those outputs (a contiguous window of the packed pair layout): their
+  mu_U / sqrt_U rows, Adam moments, Sigma_U factorizations and KL_U terms -- never communicated;
+* the observations of those outputs: row n of output i reads only the pairs (i, j), j <= i
+  (code/nmgp_dsvi.py:238, the row gather of the training step), so a rank's rows need no pair it
+  does not own.
+
+Everything else -- mu_W / sqrt_W (every output's rows read all latent functions j <= i), mu_v /
+sqrt_v (the shared length-scale process) and the 7 hyper-parameters -- is replicated; its gradient
+is the SUM over ranks of the per-rank gradients (one all-reduce per step, two buffers), so every rank
+applies the same Adam update.  KL_W and KL_v are added by rank 0 only (kl_owner), KL_U by the owner
+of each pair, so the summed loss is the whole model's -SELBO.  z_v is drawn from a seed shared by all
+ranks (every rank samples the same v, hence the same Gibbs prior); the row and pair noise from
+rank-distinct streams.
+
+Minibatches are stratified by output: rank r draws b_r = round(b * N_r / N) of its N_r rows and
+scales its reconstruction term by N_r / b_r.  With the full batch (b = N) this is exactly the
+reference's objective; with minibatches it is an unbiased estimator of the same ELBO whose
+row sampling is stratified by output instead of uniform over all rows (documented deviation).
+
+Not sharded this way: compute_ELBO (its column gather reads pairs (s, o) of every s >= o,
+code/nmgp_dsvi.py:361) -- it shards over Monte-Carlo samples (distributed.py).
+"""
+import numpy as np
+import torch
+
+from . import distributed as DD
+from . import hip_ops as H
+from .engine import DsviEngine, param_layout, pair_window, PARAM_NAMES, HYPER_NAMES
+
+
+def pair_shard_ranges(D, world):
+    """Contiguous output ranges [(i0, i1)] for `world` ranks balancing the factor count: output i
+    brings i + 1 pair factors, rank 0 additionally the D + 1 W / v factors whose KL it owns."""
+    if world > D:
+        raise ValueError(f"pair sharding needs at least one output per rank (D={D}, world={world})")
+    cost = np.arange(1, D + 1, dtype=np.float64)
+    cum = np.concatenate([[0.0], np.cumsum(cost)]) + (D + 1)      # load of rank 0 if it ended at i
+    cum[0] = 0.0
+    total = cum[-1]
+    bounds = [0]
+    for r in range(1, world):
+        target = total * r / world
+        i = int(np.searchsorted(cum, target))
+        if i > 0 and abs(cum[i - 1] - target) < abs(cum[i] - target):
+            i -= 1
+        i = max(i, bounds[-1] + 1)                   # at least one output per rank
+        i = min(i, D - (world - r))                  # leave one for each later rank
+        bounds.append(i)
+    bounds.append(D)
+    return [(bounds[r], bounds[r + 1]) for r in range(world)]
+
+
+def _pack(t, D):
+    """(D, D, ...) dense pair blocks -> (Q, ...) packed in (i, j <= i) order."""
+    idx = [i * D + j for i in range(D) for j in range(i + 1)]
+    return t.reshape(D * D, *t.shape[2:])[idx]
+
+
+class PairShard:
+    """One rank's share of a pair-sharded DSVI model: local parameter vector (replicated W / v /
+    hyper-parameters + the owned pairs), its engine, Adam state and the per-step all-reduce.
+
+    params: the 13 parameters (dense reference shapes, or packed mu_U (Q, M) / sqrt_U (Q, M, M)); each
+    rank takes its window.  B_r: this rank's minibatch rows.  N_r: its number of observations (the
+    reconstruction scale is N_r / B_r)."""
+
+    def __init__(self, params, z, B_r, N_r, rank=None, world=None, group=None, dtype=torch.float32,
+                 device="cuda", lr=0.01, betas=(0.9, 0.999), eps=1e-8, frozen=(), seed=22, ranges=None,
+                 pairs_local=False):
+        """pairs_local: params' mu_U / sqrt_U already hold only this rank's pair window (Q_r, ...)."""
+        r_, w_ = DD.world_info(group)
+        self.rank = r_ if rank is None else int(rank)
+        self.world = w_ if world is None else int(world)
+        self.group = group
+        D, M = params["mu_W"].shape
+        self.D, self.M = int(D), int(M)
+        self.ranges = ranges if ranges is not None else pair_shard_ranges(self.D, self.world)
+        self.pair_range = tuple(self.ranges[self.rank])
+        self.q0, self.Q = pair_window(self.D, self.pair_range)
+        self.kl_owner = self.rank == 0
+        self.dt, self.dev = dtype, torch.device(device)
+        self.offs, n = param_layout(self.D, self.M, packed=True, pair_range=self.pair_range)
+        self.theta = torch.zeros(n, dtype=dtype, device=self.dev)
+        self.grad = torch.zeros_like(self.theta)
+        for name in PARAM_NAMES:
+            o, shp = self.offs[name]
+            t = torch.as_tensor(params[name])
+            if name in ("mu_U", "sqrt_U"):
+                if pairs_local:
+                    assert t.shape[0] == self.Q, (name, tuple(t.shape), self.Q)
+                else:
+                    if t.dim() == (3 if name == "mu_U" else 4) and t.shape[0] == self.D and t.shape[1] == self.D:
+                        t = _pack(t, self.D)
+                    t = t[self.q0:self.q0 + self.Q]
+            cnt = int(np.prod(shp)) if shp else 1
+            self.theta[o:o + cnt] = t.reshape(-1).to(device=self.dev, dtype=dtype)
+        self.B, self.N = int(B_r), float(N_r)
+        self.engine = DsviEngine(self.D, self.M, self.B, z, device=self.dev, dtype=dtype, packed=True,
+                                 pair_range=self.pair_range, kl_owner=self.kl_owner)
+        mask = 0
+        for k, name in enumerate(HYPER_NAMES):
+            if name in frozen:
+                mask |= 1 << k
+        self.engine.bind(self.theta, self.grad, frozen_mask=mask, N=self.N)
+        # replicated slices (summed over ranks): mu_W, sqrt_W, mu_v, sqrt_v | the 7 hyper-parameters
+        self._rep = [self.grad[:self.offs["mu_U"][0]], self.grad[self.offs[HYPER_NAMES[0]][0]:]]
+        self.m = torch.zeros_like(self.theta)
+        self.v = torch.zeros_like(self.theta)
+        self.step_count = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.seed = int(seed)
+        self.noise_counter = torch.zeros(1, dtype=torch.int64, device=self.dev)
+
+    # ------------------------------------------------------------------------------------ data
+    def load(self, xs, ys, noise=None):
+        """This rank's minibatch: xs / ys = lists of row arrays of its outputs i0 .. i1-1 (in order).
+        noise: optional injected (M + B_r + Q_r * B_r) vector (z_v | z_t of these rows | the owned pairs'
+        rows, reference call order); otherwise device Philox noise is drawn in grad_step."""
+        i0, i1 = self.pair_range
+        assert len(xs) == len(ys) == i1 - i0, "one row list per owned output"
+        sizes = [len(np.asarray(x).reshape(-1)) for x in xs]
+        x = np.concatenate([np.asarray(a, np.float64).reshape(-1) for a in xs])
+        y = np.concatenate([np.asarray(a, np.float64).reshape(-1) for a in ys])
+        self.engine.load_batch(x, y, sizes, noise=noise, index=list(range(i0, i1)))
+        self._host_noise = noise is not None
+
+    def draw_noise(self):
+        """z_v from the seed every rank shares (one v sample for the whole model), the row / pair noise
+        from a rank-distinct stream; then advance the shared counter."""
+        nz, M = self.engine.noise, self.M
+        H.normal_(nz[:M], self.seed, counter=self.noise_counter)
+        H.normal_(nz[M:], self.seed + 1000003 * (self.rank + 1), counter=self.noise_counter)
+        H.counter_add_(self.noise_counter, 1)
+
+    # ------------------------------------------------------------------------------------ step
+    def grad_step(self, reduce=True):
+        """-SELBO of the whole model (summed over ranks) and this rank's gradient: owned pairs exact,
+        replicated parameters summed over ranks.  reduce=False: this share's own terms only (the
+        caller sums them, e.g. several shares simulated in one process)."""
+        if not getattr(self, "_host_noise", False):
+            self.draw_noise()
+        self.engine.forward_backward()
+        loss = self.engine.out[0:1].clone()
+        if reduce and self.world > 1:
+            import torch.distributed as dist
+            for t in self._rep:
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            dist.all_reduce(loss, op=dist.ReduceOp.SUM, group=self.group)
+        return loss[0]
+
+    def update(self):
+        H.adam_(self.theta, self.grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps)
+
+    def step(self):
+        loss = self.grad_step()
+        self.update()
+        return loss
+
+    def check(self):
+        self.engine.check_info()
+
+    # ------------------------------------------------------------------------------------ state
+    def local(self, name):
+        o, shp = self.offs[name]
+        cnt = int(np.prod(shp)) if shp else 1
+        return self.theta[o:o + cnt].view(shp) if shp else self.theta[o]
+
+    def local_grad(self, name):
+        o, shp = self.offs[name]
+        cnt = int(np.prod(shp)) if shp else 1
+        return self.grad[o:o + cnt].view(shp) if shp else self.grad[o]
+
+    def gather_state_dict(self, dst=0):
+        """The reference's dense state_dict (code/nmgp_dsvi.py:117-155 shapes, dead upper pair blocks 0)
+        assembled on rank `dst` from every rank's pair window (None on the other ranks)."""
+        D, M = self.D, self.M
+        mine = torch.cat([self.local("mu_U").reshape(-1), self.local("sqrt_U").reshape(-1)]).cpu()
+        if self.world > 1:
+            import torch.distributed as dist
+            parts = [None] * self.world
+            dist.all_gather_object(parts, (self.rank, mine), group=self.group)
+        else:
+            parts = [(0, mine)]
+        if self.rank != dst:
+            return None
+        sd = {}
+        for name in PARAM_NAMES:
+            if name in ("mu_U", "sqrt_U"):
+                continue
+            sd[name] = self.local(name).detach().cpu().clone()
+        muU = torch.zeros(D, D, M, dtype=self.dt)
+        sU = torch.zeros(D, D, M, M, dtype=self.dt)
+        for r, flat in sorted(parts, key=lambda t: t[0]):
+            i0, i1 = self.ranges[r]
+            pr = [(i, j) for i in range(i0, i1) for j in range(i + 1)]
+            nq = len(pr)
+            mu = flat[:nq * M].view(nq, M)
+            su = flat[nq * M:].view(nq, M, M)
+            for n, (i, j) in enumerate(pr):
+                muU[i, j] = mu[n]
+                sU[i, j] = su[n]
+        sd["mu_U"], sd["sqrt_U"] = muU, sU
+        return {k: sd[k] for k in PARAM_NAMES}

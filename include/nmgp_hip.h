@@ -339,6 +339,11 @@ typedef struct nmgp_dsvi_args {
   void* T;                    /* (4, B, M) K12 C2^-T per prior (t,0,1,G): the Nystrom variance
                                  rowsum(P o K12) is formed as ||T_row||^2 (no cancellation-prone
                                  explicit-inverse product) and P = T C2^-1                       */
+  /* pair sharding (SURVEY §8e axis 3; 0 / D / 1 = the whole model): the packed pairs this rank holds
+     are [pair_q0, pair_q0 + Q) -- the pairs (i, j <= i) of a contiguous range of outputs, blocks of
+     mu_U / sqrt_U / Y / noise numbered from pair_q0; n_wfac = number of W factors in the factor list
+     (D on the rank that owns KL_W, else 0); kl_v = 1 on the rank that owns KL_v                   */
+  int32_t pair_q0, n_wfac, kl_v, pair_pad;
 } nmgp_dsvi_args;
 
 int nmgp_dsvi_hyper_f64(const nmgp_dsvi_args* a, hipStream_t s);      /* hyper values + v sample   */

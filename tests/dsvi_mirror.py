@@ -42,16 +42,21 @@ def gibbs_bwd(Kbar, K, r2, S, ex, ez):
     return gx, gz
 
 
-def forward_backward(p, x, y, sizes, z, N, noise):
+def forward_backward(p, x, y, sizes, z, N, noise, pair_range=None, kl_owner=True):
     """Return (loss, grads dict, intermediates dict) with the engine's closed-form algorithm.
 
     p: dict of the 13 parameters (float64 tensors); x, y: (B,) concatenated rows grouped by output;
     sizes: rows per output; noise: flat (M + B + Q*B) in reference call order.
+    pair_range=(i0, i1), kl_owner: one rank's share under pair sharding (engine.DsviEngine): rows only
+    of outputs [i0, i1) (sizes of the others 0), only their pairs (noise Q_r x B in their order), and
+    KL_W / KL_v only when kl_owner.  The shares' losses and gradients sum to the whole model's.
     """
     D, M = p["mu_W"].shape
     B = x.shape[0]
-    Q = D * (D + 1) // 2
-    pairs = pair_list(D)
+    i0, i1 = (0, D) if pair_range is None else pair_range
+    pairs = [(i, j) for i in range(i0, i1) for j in range(i + 1)]
+    Q = len(pairs)
+    assert all(sizes[d] == 0 for d in range(D) if not i0 <= d < i1)
     off = np.concatenate([[0], np.cumsum(sizes)]).astype(int)
     I = np.concatenate([np.full(n, i) for i, n in enumerate(sizes)]).astype(int)
     z_v = noise[:M]
@@ -147,6 +152,7 @@ def forward_backward(p, x, y, sizes, z, N, noise):
     # ---------------------------------------------------------------- F12 KL
     prior_of = ["G"] * D + ["t"] + ["1" if i == j else "0" for (i, j) in pairs]
     ycol = list(range(D)) + [None] + [i * D + j for (i, j) in pairs]
+    wkl = [1.0 if kl_owner else 0.0] * (D + 1) + [1.0] * Q        # whose KL this share adds
     KL = []
     evec = []
     for f in range(len(facs)):
@@ -158,7 +164,7 @@ def forward_backward(p, x, y, sizes, z, N, noise):
         term3 = mus[f] @ yf
         KL.append(torch.log(c2d).sum() - torch.log(torch.diagonal(Cf)).sum() + 0.5 * ((a1d / c2d ** 2).sum() + term3 - M))
         evec.append(0.5 - 0.5 * a1d / c2d ** 2)
-    KL = torch.stack(KL)
+    KL = torch.stack(KL) * torch.tensor(wkl, dtype=DT)
     loss = c * R + KL.sum()
     # ================================================================= backward
     grads = {}
@@ -210,7 +216,10 @@ def forward_backward(p, x, y, sizes, z, N, noise):
     # B1: prior adjoints from KL
     Abar = {}
     for k in ["G", "t", "0", "1"]:
-        fs = [f for f in range(len(facs)) if prior_of[f] == k]
+        fs = [f for f in range(len(facs)) if prior_of[f] == k and wkl[f]]
+        if not fs:
+            Abar[k] = torch.zeros(M, M, dtype=DT)
+            continue
         delta = sum(evec[f] for f in fs)
         Ys = torch.stack([(Y[k] if ycol[f] is None else Y[k][:, ycol[f]]) for f in fs], 1)
         Abar[k] = C2inv[k].t() @ torch.diag(delta) @ C2inv[k] - 0.5 * Ys @ Ys.t()
@@ -254,14 +263,14 @@ def forward_backward(p, x, y, sizes, z, N, noise):
         k = prior_of[f]
         Xf = C1inv[f] @ facs[f]
         wv = 1 / torch.diagonal(C2[k]) ** 2
-        Lbar_kl.append(-C1inv[f].t() @ Xf + wv[:, None] * facs[f])
+        Lbar_kl.append(wkl[f] * (-C1inv[f].t() @ Xf + wv[:, None] * facs[f]))
     gsW = gsW + torch.stack(Lbar_kl[:D])
     gsv = Lvbar + Lbar_kl[D]
     for n_, (i, j) in enumerate(pairs):
         gsU[i, j] += Lbar_kl[D + 1 + n_]
         gmU[i, j] += Y["1" if i == j else "0"][:, i * D + j]
-    gmW = gmW + Y["G"].t()
-    gmv = vbar + Y["t"]
+    gmW = gmW + Y["G"].t() if kl_owner else gmW
+    gmv = vbar + Y["t"] if kl_owner else vbar
     grads = {"mu_W": gmW, "sqrt_W": torch.tril(gsW), "mu_v": gmv, "sqrt_v": torch.tril(gsv), "mu_U": gmU,
              "sqrt_U": torch.tril(gsU), "sigma2_tildeell_log": at, "length_scales_tildeell_log": bt,
              "sigma2_L0_log": a0, "length_scales_L0_log": b0, "sigma2_L1_log": a1, "length_scales_L1_log": b1,

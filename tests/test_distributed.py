@@ -176,3 +176,85 @@ def test_sample_sharded_elbo_equals_single_process():
     ref, _ = O.compute_ELBO(p, xs, ys, g["z"], float(g["N"]), O.TapeNoise(tape), n_sample=N_SAMPLE)
     assert outs[0] == outs[1]
     assert outs[0] == pytest.approx(float(ref), rel=1e-12)
+
+
+# ------------------------------------------------------------------------------------ pair sharding
+REP = ["mu_W", "sqrt_W", "mu_v", "sqrt_v", "sigma2_tildeell_log", "length_scales_tildeell_log", "sigma2_L0_log",
+       "length_scales_L0_log", "sigma2_L1_log", "length_scales_L1_log", "sigma2_err_log"]
+
+
+def _pair_problem(name):
+    from tests import _golden as G
+    g = G.load(name)
+    sizes = [int(s) for s in g["sizes"]]
+    D, M = len(sizes), len(g["z"])
+    p = G.params(g, D=D, M=M)
+    B = sum(sizes)
+    Q = D * (D + 1) // 2
+    noise = np.asarray(g["noise"], np.float64)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(int)
+    return g, p, sizes, D, M, B, noise[:M], noise[M:M + B], noise[M + B:].reshape(Q, B), off
+
+
+def _pair_share(name, rank, world, pair_range):
+    """Rank `rank`'s share (mirror): rows and pairs of outputs [i0, i1), KL_W / KL_v on rank 0."""
+    from tests import dsvi_mirror as MR
+    g, p, sizes, D, M, B, z_v, z_t, z_p, off = _pair_problem(name)
+    i0, i1 = pair_range
+    rows = np.arange(off[i0], off[i1])
+    sz = [sizes[d] if i0 <= d < i1 else 0 for d in range(D)]
+    q0, q1 = i0 * (i0 + 1) // 2, i1 * (i1 + 1) // 2
+    noise = np.concatenate([z_v, z_t[rows], z_p[q0:q1][:, rows].reshape(-1)])
+    N_r = float(g["N"]) * len(rows) / B                 # N_r / B_r = N / B: the full-batch objective
+    loss, grads, _ = MR.forward_backward(p, torch.from_numpy(g["x"][rows].copy()), torch.from_numpy(g["y"][rows].copy()),
+                                         sz, torch.from_numpy(g["z"]), N_r, torch.from_numpy(noise),
+                                         pair_range=pair_range, kl_owner=rank == 0)
+    rep = torch.cat([grads[k].reshape(-1) for k in REP])
+    own = {(i, j): (grads["mu_U"][i, j].numpy(), grads["sqrt_U"][i, j].numpy())
+           for i in range(i0, i1) for j in range(i + 1)}
+    return float(loss), rep, own
+
+
+def _pair_rank(rank, name):
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.pair_shard import pair_shard_ranges
+    rank_, world = DD.world_info()
+    g = _pair_problem(name)
+    loss, rep, own = _pair_share(name, rank_, world, pair_shard_ranges(g[3], world)[rank_])
+    DD.allreduce_sum_(rep)
+    lt = DD.allreduce_sum_(torch.tensor([loss], dtype=torch.float64))
+    return rep.numpy(), float(lt[0]), own
+
+
+@pytest.mark.parametrize("name", ["toy_forward", "mid_forward"])
+def test_pair_sharded_objective_equals_whole_model(name):
+    """SURVEY §8e axis 3: ranks owning contiguous output ranges (their rows, their pairs; KL_W / KL_v on
+    rank 0) sum to the whole model's -SELBO and gradient; pair gradients never leave their rank."""
+    from tests import dsvi_mirror as MR
+    outs = _run(_pair_rank, name)
+    g, p, sizes, D, M, B, z_v, z_t, z_p, off = _pair_problem(name)
+    loss, grads, _ = MR.forward_backward(p, torch.from_numpy(g["x"]), torch.from_numpy(g["y"]), sizes,
+                                         torch.from_numpy(g["z"]), float(g["N"]), torch.from_numpy(np.asarray(g["noise"])))
+    ref = torch.cat([grads[k].reshape(-1) for k in REP]).numpy()
+    seen = set()
+    for rep, lsum, own in outs:
+        assert np.array_equal(rep, outs[0][0])                       # identical on every rank
+        # (row sums split over ranks: summation order only)
+        assert np.linalg.norm(rep - ref) <= 1e-11 * np.linalg.norm(ref)
+        assert lsum == pytest.approx(float(loss), rel=1e-12)
+        for (i, j), (gm, gs) in own.items():
+            assert (i, j) not in seen
+            seen.add((i, j))
+            np.testing.assert_allclose(gm, grads["mu_U"][i, j].numpy(), rtol=1e-10, atol=1e-12)
+            np.testing.assert_allclose(gs, grads["sqrt_U"][i, j].numpy(), rtol=1e-10, atol=1e-12)
+    assert seen == {(i, j) for i in range(D) for j in range(i + 1)}
+
+
+@pytest.mark.parametrize("D,world", [(2, 2), (3, 2), (5, 4), (50, 8), (128, 8)])
+def test_pair_shard_ranges_cover_outputs(D, world):
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.pair_shard import pair_shard_ranges
+    rs = pair_shard_ranges(D, world)
+    assert rs[0][0] == 0 and rs[-1][1] == D
+    assert all(a < b for a, b in rs) and all(rs[k][1] == rs[k + 1][0] for k in range(world - 1))
+    loads = [(b * (b + 1) - a * (a + 1)) // 2 + (D + 1 if k == 0 else 0) for k, (a, b) in enumerate(rs)]
+    if D >= 8 * world:
+        assert max(loads) <= 1.25 * (sum(loads) / world)

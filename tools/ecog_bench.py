@@ -10,7 +10,12 @@ modes:
   elbo   compute_ELBO on all N rows, S Monte-Carlo samples (default 8 = one GPU's share of 64 over 8
          GPUs): samples/s; the first sample of the call also builds the sample-independent factors
          (RBF priors, pair quadratic forms), the last one the KL terms (8385 Cholesky factors).
-usage: python tools/ecog_bench.py {train|elbo} [--steps K] [--samples S] [--D 128] [--M 1024] [--rows 391]
+  shard  pair sharding (SURVEY §8e axis 3, pair_shard.PairShard): the training step split over W ranks by
+         output ranges; each rank's share (its rows b_r = B N_r / N, its pairs, KL_W / KL_v on rank 0) is
+         built and timed ALONE on this GPU, one after the other (eager launches; the per-step all-reduce of
+         the replicated gradient is reported as bytes).  The W-GPU step is bounded by the slowest share.
+usage: python tools/ecog_bench.py {train|elbo|shard} [--steps K] [--samples S] [--D 128] [--M 1024] [--rows 391]
+       [--world W] [--ranks r0,r1,..]
 """
 import argparse
 import json
@@ -45,7 +50,9 @@ def model(D, M, N, dev):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["train", "elbo"])
+    ap.add_argument("mode", choices=["train", "elbo", "shard"])
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--ranks", type=str, default="")
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--M", type=int, default=1024)
     ap.add_argument("--rows", type=int, default=391)
@@ -57,6 +64,8 @@ def main():
     D, M = a.D, a.M
     xs, ys = data(D, a.rows)
     N = D * a.rows
+    if a.mode == "shard":
+        return shard(a, xs, ys, N, dev)
     m, t_init = model(D, M, N, dev)
     rec = {"config": f"ECoG-shaped: D={D}, Q={D * (D + 1) // 2}, M={M}, N={N}, fp32, packed pairs",
            "init_s": round(t_init, 2), "param_GB": round(m._theta.numel() * 4 / 1e9, 2)}
@@ -121,6 +130,69 @@ def main():
                     "call_s": round(t_s, 3), "samples_per_s": round(a.samples / t_s, 3), "elbo": float(e),
                     "elbo_1": float(e1), "peak_mem_GB": round(torch.cuda.max_memory_allocated() / 1e9, 1)})
     print(json.dumps(rec), flush=True)
+
+
+def shard(a, xs, ys, N, dev):
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.pair_shard import PairShard, pair_shard_ranges
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.engine import pair_window
+    D, M, W = a.D, a.M, a.world
+    ranges = pair_shard_ranges(D, W)
+    ranks = [int(r) for r in a.ranks.split(",")] if a.ranks else list(range(W))
+    out = {"config": f"ECoG-shaped: D={D}, Q={D * (D + 1) // 2}, M={M}, N={N}, fp32, B={a.B}, pair-sharded over {W} ranks",
+           "ranges": ranges, "ranks": {}}
+    rep_bytes = None
+    for r in ranks:
+        i0, i1 = ranges[r]
+        q0, Q = pair_window(D, (i0, i1))
+        g = torch.Generator(device=dev).manual_seed(100 + r)
+        rn = lambda *s: torch.randn(*s, generator=g, device=dev, dtype=torch.float32)
+        p = {"mu_W": 0.1 * rn(D, M), "sqrt_W": 0.1 * rn(D, M, M), "mu_v": -4 * torch.ones(M, device=dev),
+             "sqrt_v": 0.1 * rn(M, M), "mu_U": 0.1 * rn(Q, M), "sqrt_U": 0.1 * rn(Q, M, M),
+             "sigma2_tildeell_log": torch.tensor(0.), "length_scales_tildeell_log": torch.tensor(float(np.log(3.0 / M))),
+             "sigma2_L0_log": torch.tensor(0.), "length_scales_L0_log": torch.tensor(float(np.log(3.0 / M))),
+             "sigma2_L1_log": torch.tensor(0.), "length_scales_L1_log": torch.tensor(float(np.log(3.0 / M))),
+             "sigma2_err_log": torch.tensor(-2.)}
+        n_r = sum(len(x) for x in xs[i0:i1])
+        b_r = max(1, int(round(a.B * n_r / N)))
+        rng = np.random.default_rng(5 + r)
+        torch.cuda.reset_peak_memory_stats()
+        t0 = time.time()
+        sh = PairShard(p, np.linspace(0, 1, M), B_r=b_r, N_r=n_r, rank=r, world=W, dtype=torch.float32, device=dev,
+                       frozen=("length_scales_tildeell_log", "length_scales_L0_log", "length_scales_L1_log"),
+                       ranges=ranges, pairs_local=True)
+        del p
+        # stratified minibatch: b_r rows of this rank's outputs
+        idx = np.sort(rng.choice(n_r, b_r, replace=False))
+        cuts = np.concatenate([[0], np.cumsum([len(x) for x in xs[i0:i1]])])
+        bx = [xs[i0 + k][idx[(idx >= cuts[k]) & (idx < cuts[k + 1])] - cuts[k]] for k in range(i1 - i0)]
+        by = [ys[i0 + k][idx[(idx >= cuts[k]) & (idx < cuts[k + 1])] - cuts[k]] for k in range(i1 - i0)]
+        sh.load(bx, by)
+        t_init = time.time() - t0
+        sh.grad_step(reduce=False)                  # warm-up (plans, first launches)
+        sh.update()
+        torch.cuda.synchronize()
+        sh.check()
+        t0 = time.time()
+        for _ in range(a.steps):
+            loss = sh.grad_step(reduce=False)
+            sh.update()
+        torch.cuda.synchronize()
+        dt = (time.time() - t0) / a.steps
+        sh.check()
+        rep_bytes = sum(t.numel() for t in sh._rep) * 4
+        out["ranks"][r] = {"outputs": [i0, i1], "pairs": Q, "factors": sh.engine.NF, "rows": b_r,
+                           "s_per_step": round(dt, 4), "loss_share": float(loss), "init_s": round(t_init, 2),
+                           "param_GB": round(sh.theta.numel() * 4 / 1e9, 2),
+                           "peak_mem_GB": round(torch.cuda.max_memory_allocated() / 1e9, 1)}
+        print(json.dumps({"rank": r, **out["ranks"][r]}), flush=True)
+        del sh
+        torch.cuda.empty_cache()
+    ts = [v["s_per_step"] for v in out["ranks"].values()]
+    out["slowest_share_s"] = max(ts)
+    out["replicated_grad_bytes_per_step"] = rep_bytes
+    # ring all-reduce: 2 (W-1)/W of the bytes over each GPU's busiest xGMI link (~150 GB/s spec)
+    out["allreduce_s_at_150GBps"] = round(2 * (W - 1) / W * rep_bytes / 150e9, 4)
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
