@@ -187,6 +187,88 @@ def elbo_sharded(dev, world, rank, dist, D=128, M=1024, rows=391, samples=64):
     return out
 
 
+def pair_sharded_train(dev, world, rank, dist, D=128, M=1024, rows=391, B=512, steps=4):
+    """SURVEY §8e axis 3 at the ECoG-full shape (BASELINE.json configs[3]): the training step with the
+    coefficient pairs sharded over the ranks by output range (pair_shard.PairShard): each rank holds its
+    pairs' parameters / Adam state / factors, draws b_r = B N_r / N rows of its outputs, and the
+    replicated gradient (mu_W, sqrt_W, mu_v, sqrt_v, hyper-parameters) is summed with one RCCL
+    all-reduce per step.  fp32, eager launches; timed over `steps` steps after one warm-up step,
+    barrier + synchronize on both sides, max over ranks.  A rank that fails to build its share makes
+    every rank skip the leg (flag all-reduce) instead of leaving the others in a collective."""
+    import gc
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.pair_shard import PairShard, pair_shard_ranges
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.engine import pair_window
+    ok = torch.ones(1, device=dev)
+    sh, err = None, None
+    try:
+        ranges = pair_shard_ranges(D, world)
+        i0, i1 = ranges[rank]
+        q0, Q = pair_window(D, (i0, i1))
+        g = torch.Generator(device=dev).manual_seed(100 + rank)
+        rn = lambda *s: torch.randn(*s, generator=g, device=dev, dtype=torch.float32)
+        # replicated parameters drawn from one seed on every rank; the pair window from the rank's own
+        gr = torch.Generator(device=dev).manual_seed(99)
+        rr = lambda *s: torch.randn(*s, generator=gr, device=dev, dtype=torch.float32)
+        ls = float(np.log(3.0 / M))
+        p = {"mu_W": 0.1 * rr(D, M), "sqrt_W": 0.1 * rr(D, M, M), "mu_v": -4 * torch.ones(M, device=dev),
+             "sqrt_v": 0.1 * rr(M, M), "mu_U": 0.1 * rn(Q, M), "sqrt_U": 0.1 * rn(Q, M, M),
+             "sigma2_tildeell_log": torch.tensor(0.), "length_scales_tildeell_log": torch.tensor(ls),
+             "sigma2_L0_log": torch.tensor(0.), "length_scales_L0_log": torch.tensor(ls),
+             "sigma2_L1_log": torch.tensor(0.), "length_scales_L1_log": torch.tensor(ls), "sigma2_err_log": torch.tensor(-2.)}
+        rng = np.random.default_rng(7)
+        xs = [np.sort(rng.uniform(0, 1, rows)) for _ in range(D)]
+        ys = [np.sin(6 * x + 0.1 * d) + 0.3 * rng.standard_normal(rows) for d, x in enumerate(xs)]
+        N = D * rows
+        n_r = rows * (i1 - i0)
+        b_r = max(1, int(round(B * n_r / N)))
+        sh = PairShard(p, np.linspace(0, 1, M), B_r=b_r, N_r=n_r, rank=rank, world=world, dtype=torch.float32,
+                       device=dev, frozen=("length_scales_tildeell_log", "length_scales_L0_log", "length_scales_L1_log"),
+                       ranges=ranges, pairs_local=True)
+        del p
+        idx = np.sort(np.random.default_rng(5 + rank).choice(n_r, b_r, replace=False))
+        sh.load([xs[i0 + k][idx[(idx >= k * rows) & (idx < (k + 1) * rows)] - k * rows] for k in range(i1 - i0)],
+                [ys[i0 + k][idx[(idx >= k * rows) & (idx < (k + 1) * rows)] - k * rows] for k in range(i1 - i0)])
+    except Exception as exc:                      # e.g. out of memory on a small world
+        ok.zero_()
+        err = f"{type(exc).__name__}: {exc}"[:300]
+    if world > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if float(ok) == 0:
+        sh = None
+        gc.collect()
+        torch.cuda.empty_cache()
+        return {"error": err or "another rank could not build its share"}
+    sh.step()                                     # warm-up: plans, first launches
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.time()
+    for _ in range(steps):
+        loss = sh.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = (time.time() - t0) / steps
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    sh.check()
+    out = {"workload": f"DSVI training step, ECoG-full shape D={D} (Q={D * (D + 1) // 2} pairs), M={M}, N={D * rows}, "
+                       f"B={B}, fp32, pairs sharded over {world} rank(s) by output range",
+           "ranges": pair_shard_ranges(D, world), "s_per_step": round(el, 4), "it_per_s": round(1.0 / el, 3),
+           "loss": float(loss), "rank0_pairs": sh.Q, "rank0_param_GB": round(sh.theta.numel() * 4 / 1e9, 2),
+           "replicated_allreduce_MB": round(sum(t.numel() for t in sh._rep) * 4 / 1e6, 1),
+           "peak_mem_GB_rank0": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)}
+    if D == 128 and M == 1024:
+        # the same step unsharded on one GPU (packed pairs, 247 GB peak): profiles/r02_ecog_train.json
+        out["single_gpu_unsharded_s_per_step"] = 0.562
+    del sh, loss
+    gc.collect()
+    torch.cuda.empty_cache()
+    return out
+
+
 class PhaseTimer:
     """HIP events around every launch of an eager step (same stream as the kernels)."""
 
@@ -282,6 +364,8 @@ def main():
     ap.add_argument("--no-stress", action="store_true", help="skip the M=4096 stress Cholesky line (configs[4])")
     ap.add_argument("--no-elbo", action="store_true", help="skip the sample-sharded ECoG compute_ELBO leg (configs[3])")
     ap.add_argument("--no-api", action="store_true", help="skip the inference() API-path leg")
+    ap.add_argument("--no-pair", action="store_true", help="skip the pair-sharded ECoG training leg (N > 1 only)")
+    ap.add_argument("--pair-D", type=int, default=128, help="channels of the pair-sharded leg (default: ECoG-full 128)")
     ap.add_argument("--elbo-D", type=int, default=128, help="channels of the ELBO leg (default: ECoG-full 128)")
     args = ap.parse_args()
 
@@ -460,6 +544,11 @@ def main():
         except Exception as exc:                        # reported, never masks the headline line
             elbo = {"error": f"{type(exc).__name__}: {exc}"[:300]}
 
+    pair = None
+    if world > 1 and not args.no_pair:
+        torch.cuda.empty_cache()
+        pair = pair_sharded_train(dev, world, rank, dist, D=args.pair_D)
+
     api = None
     if rank == 0 and world == 1 and not args.no_api:
         torch.cuda.empty_cache()
@@ -487,6 +576,7 @@ def main():
                           "hip_graph": used_graph},
                "roofline": roofline, "cpu_baseline": cpu, "cholesky": chol, "cholesky_stress": stress,
                "elbo_sample_sharded": elbo,
+               "pair_sharded_train": pair,
                "api_path": api,
                "phase_ms": breakdown,
                "final_loss": loss_val}

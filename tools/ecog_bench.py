@@ -185,7 +185,9 @@ def shard(a, xs, ys, N, dev):
                            "param_GB": round(sh.theta.numel() * 4 / 1e9, 2),
                            "peak_mem_GB": round(torch.cuda.max_memory_allocated() / 1e9, 1)}
         print(json.dumps({"rank": r, **out["ranks"][r]}), flush=True)
-        del sh
+        del sh, loss
+        import gc
+        gc.collect()                                # the engine's schedule closures form cycles
         torch.cuda.empty_cache()
     ts = [v["s_per_step"] for v in out["ranks"].values()]
     out["slowest_share_s"] = max(ts)
