@@ -93,7 +93,7 @@ class PairShard:
         self.grad = torch.zeros_like(self.theta)
         for name in PARAM_NAMES:
             o, shp = self.offs[name]
-            t = torch.as_tensor(params[name])
+            t = torch.as_tensor(params[name]).detach()
             if name in ("mu_U", "sqrt_U"):
                 if pairs_local:
                     assert t.shape[0] == self.Q, (name, tuple(t.shape), self.Q)
