@@ -59,6 +59,20 @@ __device__ inline int prior_of(const nmgp_dsvi_args& a, int f) {
   return i == j ? 2 : 1;
 }
 
+// sum_{q < cnt} p[q * stride] in a fixed order with 8 loads in flight: written as a plain loop these
+// partial-sum reductions waited one L2 round trip per element (63 G12 column partials in the v backward)
+template <typename T> __device__ inline T strided_sum(const T* p, int cnt, int64_t stride) {
+  T acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int q = 0; q < cnt; q += 8) {
+    T v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = (q + u < cnt) ? p[(int64_t)(q + u) * stride] : (T)0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] += v[u];
+  }
+  return ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+}
+
 template <typename T> struct RowBuf {
   T* base;
   int64_t B;
@@ -434,9 +448,15 @@ __global__ __launch_bounds__(256) void dsvi_delta_kernel(Args a) {
   T* fb = (T*)a.facbuf;
   const T* C2 = (const T*)a.Afac + (int64_t)(NF + k) * MM;
   const T* ev = fb + NF + 8 * (int64_t)M + 4 * pair_cols(a);
-  T dl = 0;
-  for (int f = 0; f < NF; ++f)
-    if (prior_of(a, f) == k) dl += ev[(int64_t)f * M + i];
+  T acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int f = 0; f < NF; f += 8) {                 // 8 loads in flight (see strided_sum)
+    T v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = (f + u < NF && prior_of(a, f + u) == k) ? ev[(int64_t)(f + u) * M + i] : (T)0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] += v[u];
+  }
+  const T dl = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   const T c2 = C2[(int64_t)i * M + i];
   fb[NF + (int64_t)k * M + i] = dl;
   fb[NF + 4 * (int64_t)M + (int64_t)k * M + i] = (T)1 / (c2 * c2);
@@ -489,10 +509,9 @@ __global__ __launch_bounds__(256) void dsvi_vbwd_kernel(Args a) {
   const T* ellZ = (const T*)a.ellZ;
   T* vbar = (T*)a.vbar;
   for (int c = threadIdx.x; c < M; c += blockDim.x) {
-    T ez = 0;
-    for (int rt = 0; rt < a.n_rt; ++rt) ez += gcol[(int64_t)rt * M + c];                 // G12 columns
-    for (int ct = 0; ct < a.n_ct; ++ct) ez += grow[(int64_t)a.n_ct * B + (int64_t)ct * M + c];   // G22 rows
-    for (int rt = 0; rt < a.n_rt22; ++rt) ez += gcol[(int64_t)a.n_rt * M + (int64_t)rt * M + c];  // G22 cols
+    T ez = strided_sum(gcol + c, a.n_rt, M);                                         // G12 columns
+    ez += strided_sum(grow + (int64_t)a.n_ct * B + c, a.n_ct, M);                     // G22 rows
+    ez += strided_sum(gcol + (int64_t)a.n_rt * M + c, a.n_rt22, M);                   // G22 cols
     const T vb = vbar[c] + ez * ellZ[c];
     vbs[c] = vb;
     if (blockIdx.x == 0) vbar[M + c] = vb;

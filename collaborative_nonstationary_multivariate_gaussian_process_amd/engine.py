@@ -703,6 +703,19 @@ class DsviEngine:
         # G prior: R_G -> the K_G12 builder backward (ell_X adjoints) stays on the main chain; the prior
         # adjoint Abar_G -= P_G^T R_G and the K_G22 builder backward (ell_Z adjoints: the v chain only)
         # run on the second side stream
+        # A/B on the box (tools/ab_env.sh NMGP_SIDE3, 3 x 300 steps each): 0.815-0.818 -> 0.798-0.802 ms
+        side3 = os.environ.get("NMGP_SIDE3", "1") != "0"
+        if side3:
+            # the L0 / L1 prior adjoints (R_0, R_1 -> P^T R -> builder backward: hyper-parameter partials
+            # only) need P-bar_0/1 (bwd_w) and the KL parts of Abar (kl_done): a third side stream starts
+            # them right after bwd_w.  On side2 they queued behind the G-prior adjoint and, in the graph,
+            # shared a hardware queue with the t chain (finalize waited ~50 us for them, r02b timeline).
+            # Like side2 it synchronises with the main stream only.
+            steps += [("wait", "main", "kl_done"), ("sig", "main", "bwd_w_kl"), ("wait", "side3", "bwd_w_kl"),
+                      ("bwd_R_L", "gemm", gemm("bwd_R_L"), "side3"),
+                      ("bwd_pr_L", "gemm", gemm("bwd_pr_L"), "side3"),
+                      ("bwd_build_L", "pairwise_bwd", pw("bwd_build_L"), "side3"),
+                      ("sig", "side3", "L_done")]
         steps += [
             # (the second side stream synchronises with the main stream only: a side <-> side2 event
             # edge made hipGraph instantiation crash on this stack; the KL prior adjoints are long done
@@ -715,15 +728,16 @@ class DsviEngine:
             ("bwd_pr", "gemm", gemm("bwd_pr"), "side2"),
             ("bwd_build22", "pairwise_bwd", pw("bwd_build22"), "side2"),
             ("sig", "side2", "g22"),
+        ]
+        if not side3:
             # the L0 / L1 prior adjoints feed only their hyper-parameter partials (scal_part slots and
             # row-coefficient rows of their own): second side stream after the G prior adjoint (R_G was
             # signalled after bwd_w and the KL parts of Abar), so the v chain on the side stream does not
             # queue behind them
-            ("bwd_R_L", "gemm", gemm("bwd_R_L"), "side2"),
-            ("bwd_pr_L", "gemm", gemm("bwd_pr_L"), "side2"),
-            ("bwd_build_L", "pairwise_bwd", pw("bwd_build_L"), "side2"),
-            ("sig", "side2", "L_done"),
-        ]
+            steps += [("bwd_R_L", "gemm", gemm("bwd_R_L"), "side2"),
+                      ("bwd_pr_L", "gemm", gemm("bwd_pr_L"), "side2"),
+                      ("bwd_build_L", "pairwise_bwd", pw("bwd_build_L"), "side2"),
+                      ("sig", "side2", "L_done")]
         steps += [
             ("tbwd", "row", row(getattr(lib, "nmgp_dsvi_tbwd_" + self.sfx)), "main"),
             # after the t-row backward the t-prior chain (bwd_t1 -> bwd_t2 -> builder backward) and the
@@ -731,6 +745,9 @@ class DsviEngine:
             # Gibbs partials) share no buffer: the v chain runs on the side stream (after bwd_lbar there,
             # which keeps the order of the sqrt_v gradient accumulation fixed: kl_lbar, bwd_lbar,
             # bwd_v2), followed by the KL mean gradients of the mu rows
+            # (starting P_t^T tbar before the K_G22 builder backward is done -- the g22 partials relayed to
+            # the v-backward kernel through the main stream -- measured slower in the graph: 0.84 ms and,
+            # with the third side stream, 0.94 ms per step; more cross-queue edges)
             ("wait", "main", "g22"),
             ("sig", "main", "tb"),
             ("wait", "side", "tb"),
@@ -772,7 +789,8 @@ class DsviEngine:
             if getattr(self, "_side", None) is None:
                 self._side = torch.cuda.Stream(device=self.dev)
                 self._side2 = torch.cuda.Stream(device=self.dev)
-            streams = {"main": main, "side": self._side, "side2": self._side2}
+                self._side3 = torch.cuda.Stream(device=self.dev)
+            streams = {"main": main, "side": self._side, "side2": self._side2, "side3": self._side3}
             handles = {k: ctypes.c_void_p(v.cuda_stream) for k, v in streams.items()}
         events = {}
         for item in steps:
