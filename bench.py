@@ -117,12 +117,34 @@ def stress_cholesky(dev, reps=5):
             "kernel": "nmgp_potrf_blocked_f32 (128-wide fused leaves, panel GEMM, lookahead, side-stream SYRK)",
             "potrf_ms": round(t_fac, 4), "gflops": round(f / (t_fac * 1e-3) / 1e9, 1),
             "residual": resid,
-            "syrk": {"kernel": "gemm_big_kernel (128x128 f32 MFMA, stream-K)", "n": Mst, "k": Mst,
-                     "ms": round(t_syrk, 4), "achieved_tflops": round(syrk_tf, 2), "peak_tflops": 157.3,
-                     "frac": round(syrk_tf / 157.3, 4)},
+            "syrk_in_factorization": _stress_syrk_pmc(),
+            "syrk_isolated_proxy": {"kernel": "gemm_big_kernel (128x128 f32 MFMA, stream-K)", "n": Mst, "k": Mst,
+                                    "ms": round(t_syrk, 4), "achieved_tflops": round(syrk_tf, 2), "peak_tflops": 157.3,
+                                    "frac": round(syrk_tf / 157.3, 4),
+                                    "note": "a fresh n = k = 4096 SYRK, NOT an update the factorization issues"},
             "cpu": {"potrf_ms": round(1e3 * t_cpu, 2), "gflops": round(f / t_cpu / 1e9, 1),
                     "cores": torch.get_num_threads(), "kind": "torch.linalg.cholesky (LAPACK spotrf)"},
             "speedup_vs_cpu": round(t_cpu * 1e3 / t_fac, 1)}
+
+
+def _stress_syrk_pmc():
+    """MFMA-busy of the trailing-update SYRK launches INSIDE the M=4096 factorization (k = 128), time-weighted,
+    from the committed rocprofv3 PMC pass (tools/syrk_inside_pmc.sh: SQ_VALU_MFMA_BUSY_CYCLES /
+    (GRBM_GUI_ACTIVE/8 * 4 * 256), one pass, no tracing domains) and the whole factorization's."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_stress_potrf_mfma_util.json")))
+    if not files:
+        return None
+    rows = json.load(open(files[-1]))["rows"]
+    nm = lambda r: r["kernel"]
+    syrk = [r for r in rows if "gemm_big_kernel" in nm(r)]
+    fac = [r for r in rows if any(k in nm(r) for k in ("gemm_big_kernel", "potrf_step_kernel", "chol_inv_kernel"))]
+    tw = lambda rs: sum(r["mfma_util"] * r["avg_us"] * r["dispatches"] for r in rs) / max(
+        1e-9, sum(r["avg_us"] * r["dispatches"] for r in rs))
+    return {"kernel": "gemm_big_kernel (the factorization's own trailing SYRKs, k = 128)",
+            "launches": sum(r["dispatches"] for r in syrk), "mfma_busy_time_weighted": round(tw(syrk), 4),
+            "factorization_kernels_mfma_busy": round(tw(fac), 4),
+            "source": os.path.relpath(files[-1], ROOT)}
 
 
 def api_path(dev, xs, ys, z, epochs_device=100, epochs_torch=20):
@@ -531,6 +553,21 @@ def main():
                                     "achieved": round(prof_tf, 4), "frac": round(prof_tf / FP64_MFMA_PEAK_TFLOPS, 5)}
             prof(roofline, lambda n: "gemm_lat_kernel<double" in n)
             prof(roofline["tile_kernel"], lambda n: n.startswith("void nmgp::gemm_kernel<double"))
+        # MFMA-busy of the same kernels from the committed PMC pass (tools/pm25_pmc.sh: SQ_VALU_MFMA_BUSY_CYCLES /
+        # (GRBM_GUI_ACTIVE/8 * 4 * 256), dispatches serialised by counter collection), time-weighted per kernel
+        mf = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pm25_mfma.json")))
+        if mf:
+            rows = json.load(open(mf[-1]))["rows"]
+
+            def busy(pred):
+                rs = [r for r in rows if pred(r["kernel"])]
+                w = sum(r["avg_us"] * r["dispatches"] for r in rs)
+                return round(sum(r["mfma_util"] * r["avg_us"] * r["dispatches"] for r in rs) / w, 4) if w else None
+            roofline["mfma_busy"] = busy(lambda n: "gemm_lat_kernel<double" in n)
+            roofline["tile_kernel"]["mfma_busy"] = busy(lambda n: n.startswith("void nmgp::gemm_kernel<double"))
+            roofline["mfma_busy_source"] = os.path.relpath(mf[-1], ROOT)
+            if chol is not None:
+                chol["mfma_busy"] = busy(lambda n: "chol_inv3_kernel" in n)
 
     # free the headline workload before the large ELBO leg
     elbo = None
