@@ -579,18 +579,27 @@ __global__ __launch_bounds__(RW * 64) void chol_inv_kernel(T* A, int n, int64_t 
 // so stale bits in an uninitialised X cannot pass for progress.  Role 1 waits only on its own
 // role 0 (block 2b before 2b+1) and every spin is bounded: a lost peer gives wrong output, not a hang.
 constexpr unsigned long long kFlagTag = 0x7ff8d5a1c0de0000ull;
+// The 64-bit control words live at the end of X's row 0 (strictly upper, zeroed at the end): the
+// progress flag in the last 8 bytes, the three-role consumer count in the 8 bytes before.  f32 needs
+// n even and X 8-byte aligned (checked by the host, chol_ctl_ok).
+template <typename T> constexpr int kCtl = 8 / (int)sizeof(T);     // elements per control word
+template <typename T> __device__ inline unsigned long long* ctl_flag(T* Xm, int n) {
+  return (unsigned long long*)(Xm + (n - kCtl<T>));
+}
+template <typename T> __device__ inline unsigned long long* ctl_done(T* Xm, int n) {
+  return (unsigned long long*)(Xm + (n - 2 * kCtl<T>));
+}
 
-template <int NTPW>
-__device__ __attribute__((always_inline)) inline void chol2_potrf_role(double* Am, double* Xm, int n, int64_t lda, int64_t ldx, int32_t* info, int col_off,
+template <typename T, int NTPW>
+__device__ __attribute__((always_inline)) inline void chol2_potrf_role(T* Am, T* Xm, int n, int64_t lda, int64_t ldx, int32_t* info, int col_off,
                                   int info_first, int mat, unsigned char* smem_raw) {
-  using T = double;
   using acc_t = typename Mfma<T>::acc_t;
   const int nt = (n + 15) >> 4, NR = nt * 16;
   T* colbuf = (T*)smem_raw;   // role 0: NR x CP block column kb before the panel step
   T* Ps = colbuf + NR * CP;   // NR x CP : L[:, kb] (local rows, diagonal block first)
   T* Xrow = Ps + NR * CP;     // role 1: nt tiles x 16 rows x CP : X[kb, jb]
   T* LiT = Xrow + NR * CP;    // 16 x CP : (L_kk^-1)^T
-  unsigned long long* flag = (unsigned long long*)(Xm + (n - 1));
+  unsigned long long* flag = ctl_flag(Xm, n);
   const __amdgpu_buffer_rsrc_t rAm = make_rsrc(Am, ((int64_t)(n - 1) * lda + n) * (int64_t)sizeof(T));
   const __amdgpu_buffer_rsrc_t rXm = make_rsrc(Xm, ((int64_t)(n - 1) * ldx + n) * (int64_t)sizeof(T));
   const int t = threadIdx.x, lane = t & 63;
@@ -627,9 +636,8 @@ __device__ __attribute__((always_inline)) inline void chol2_potrf_role(double* A
     }
   }
   int first_fail = 0;
-  // strictly-upper block tiles of L are zero (the stores drain while the factorization runs)
-  for (int i = w; i < n; i += RW)
-    for (int j = ((i >> 4) + 1) * 16 + lane; j < n; j += 64) Am[(int64_t)i * lda + j] = 0;
+  // (the strictly-upper block tiles of L are zeroed by the inverse workgroups while they wait for the
+  // first block column: here the ~n^2/2 stores sat in front of the first vmcnt wait, 10 us of prologue)
   CHOL_STAMPX(1);
   for (int kb = 0; kb < nt; ++kb) {
     CHOL_STAMP(kb, 0);
@@ -732,17 +740,16 @@ __device__ __attribute__((always_inline)) inline void chol2_potrf_role(double* A
   }
 }
 
-template <int NTPW>
-__device__ __attribute__((always_inline)) inline void chol2_trtri_role(double* Am, double* Xm, int n, int64_t lda, int64_t ldx, int32_t* info, int col_off,
+template <typename T, int NTPW>
+__device__ __attribute__((always_inline)) inline void chol2_trtri_role(T* Am, T* Xm, int n, int64_t lda, int64_t ldx, int32_t* info, int col_off,
                                   int info_first, int mat, unsigned char* smem_raw) {
-  using T = double;
   using acc_t = typename Mfma<T>::acc_t;
   const int nt = (n + 15) >> 4, NR = nt * 16;
   T* colbuf = (T*)smem_raw;   // role 0: NR x CP block column kb before the panel step
   T* Ps = colbuf + NR * CP;   // NR x CP : L[:, kb] (local rows, diagonal block first)
   T* Xrow = Ps + NR * CP;     // role 1: nt tiles x 16 rows x CP : X[kb, jb]
   T* LiT = Xrow + NR * CP;    // 16 x CP : (L_kk^-1)^T
-  unsigned long long* flag = (unsigned long long*)(Xm + (n - 1));
+  unsigned long long* flag = ctl_flag(Xm, n);
   const __amdgpu_buffer_rsrc_t rAm = make_rsrc(Am, ((int64_t)(n - 1) * lda + n) * (int64_t)sizeof(T));
   const __amdgpu_buffer_rsrc_t rXm = make_rsrc(Xm, ((int64_t)(n - 1) * ldx + n) * (int64_t)sizeof(T));
   const int t = threadIdx.x, lane = t & 63;
@@ -765,8 +772,10 @@ __device__ __attribute__((always_inline)) inline void chol2_trtri_role(double* A
     }
   }
   for (int i = w; i < n; i += RW)
-    for (int j = ((i >> 4) + 1) * 16 + lane; j < n; j += 64)
-      if (i != 0 || j != n - 1) Xm[(int64_t)i * ldx + j] = 0;
+    for (int j = ((i >> 4) + 1) * 16 + lane; j < n; j += 64) {
+      if (i != 0 || j < n - kCtl<T>) Xm[(int64_t)i * ldx + j] = 0;
+      Am[(int64_t)i * lda + j] = 0;                // strictly-upper block tiles of L (factor role reads none)
+    }
   for (int kb = 0; kb < nt; ++kb) {
     const int nrow = NR - kb * 16;
     if (t == 0) {
@@ -880,17 +889,16 @@ __device__ inline void tri_decode_par(int tp, int par, int& ib, int& jb) {
   }
 }
 
-template <int NTPW>
-__device__ __attribute__((always_inline)) inline void chol3_trtri_role(double* Am, double* Xm, int n, int64_t lda,
+template <typename T, int NTPW>
+__device__ __attribute__((always_inline)) inline void chol3_trtri_role(T* Am, T* Xm, int n, int64_t lda,
                                                                        int64_t ldx, int par, unsigned char* smem_raw) {
-  using T = double;
   using acc_t = typename Mfma<T>::acc_t;
   const int nt = (n + 15) >> 4, NR = nt * 16;
   T* Ps = (T*)smem_raw + NR * CP;
   T* Xrow = Ps + NR * CP;
   T* LiT = Xrow + NR * CP;
-  unsigned long long* flag = (unsigned long long*)(Xm + (n - 1));
-  unsigned long long* done = (unsigned long long*)(Xm + (n - 2));
+  unsigned long long* flag = ctl_flag(Xm, n);
+  unsigned long long* done = ctl_done(Xm, n);
   const __amdgpu_buffer_rsrc_t rAm = make_rsrc(Am, ((int64_t)(n - 1) * lda + n) * (int64_t)sizeof(T));
   const __amdgpu_buffer_rsrc_t rXm = make_rsrc(Xm, ((int64_t)(n - 1) * ldx + n) * (int64_t)sizeof(T));
   const int t = threadIdx.x, lane = t & 63;
@@ -915,8 +923,10 @@ __device__ __attribute__((always_inline)) inline void chol3_trtri_role(double* A
   }
   // strictly upper part of X is zero (rows of this parity; the two control words stay)
   for (int i = 2 * w + par; i < n; i += 2 * RW)
-    for (int j = ((i >> 4) + 1) * 16 + lane; j < n; j += 64)
-      if (i != 0 || j < n - 2) Xm[(int64_t)i * ldx + j] = 0;
+    for (int j = ((i >> 4) + 1) * 16 + lane; j < n; j += 64) {
+      if (i != 0 || j < n - 2 * kCtl<T>) Xm[(int64_t)i * ldx + j] = 0;
+      Am[(int64_t)i * lda + j] = 0;                // strictly-upper block tiles of L (factor role reads none)
+    }
   for (int kb = 0; kb < nt; ++kb) {
     const int nrow = NR - kb * 16;
     if (t == 0) {
@@ -1014,37 +1024,36 @@ __device__ __attribute__((always_inline)) inline void chol3_trtri_role(double* A
   }
 }
 
-template <int NTPW, int NTPW1>
-__global__ __launch_bounds__(RW * 64) void chol_inv3_kernel(double* A, int n, int64_t lda, int64_t strideA, double* X,
+template <typename T, int NTPW, int NTPW1>
+__global__ __launch_bounds__(RW * 64) void chol_inv3_kernel(T* A, int n, int64_t lda, int64_t strideA, T* X,
                                                             int64_t ldx, int64_t strideX, int32_t* info, int col_off,
                                                             int info_first) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int mat = blockIdx.x / 3, role = blockIdx.x - 3 * mat;
-  double* Am = A + (int64_t)mat * strideA;
-  double* Xm = X + (int64_t)mat * strideX;
+  T* Am = A + (int64_t)mat * strideA;
+  T* Xm = X + (int64_t)mat * strideX;
   if (role == 0) {
-    if (threadIdx.x == 0)
-      __hip_atomic_store((unsigned long long*)(Xm + (n - 2)), kDoneTag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    chol2_potrf_role<NTPW>(Am, Xm, n, lda, ldx, info, col_off, info_first, mat, smem_raw);
+    if (threadIdx.x == 0) __hip_atomic_store(ctl_done(Xm, n), kDoneTag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    chol2_potrf_role<T, NTPW>(Am, Xm, n, lda, ldx, info, col_off, info_first, mat, smem_raw);
   } else {
-    chol3_trtri_role<NTPW1>(Am, Xm, n, lda, ldx, role - 1, smem_raw);
+    chol3_trtri_role<T, NTPW1>(Am, Xm, n, lda, ldx, role - 1, smem_raw);
   }
 }
 
-template <int NTPW>
-__global__ __launch_bounds__(RW * 64) void chol_inv2_kernel(double* A, int n, int64_t lda, int64_t strideA, double* X,
+template <typename T, int NTPW>
+__global__ __launch_bounds__(RW * 64) void chol_inv2_kernel(T* A, int n, int64_t lda, int64_t strideA, T* X,
                                                             int64_t ldx, int64_t strideX, int32_t* info, int col_off,
                                                             int info_first) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int mat = blockIdx.x >> 1;
-  double* Am = A + (int64_t)mat * strideA;
-  double* Xm = X + (int64_t)mat * strideX;
+  T* Am = A + (int64_t)mat * strideA;
+  T* Xm = X + (int64_t)mat * strideX;
   // separate functions: with one shared tile set the two roles' live ranges merged past the
   // register file
   if ((blockIdx.x & 1) == 0)
-    chol2_potrf_role<NTPW>(Am, Xm, n, lda, ldx, info, col_off, info_first, mat, smem_raw);
+    chol2_potrf_role<T, NTPW>(Am, Xm, n, lda, ldx, info, col_off, info_first, mat, smem_raw);
   else
-    chol2_trtri_role<NTPW>(Am, Xm, n, lda, ldx, info, col_off, info_first, mat, smem_raw);
+    chol2_trtri_role<T, NTPW>(Am, Xm, n, lda, ldx, info, col_off, info_first, mat, smem_raw);
 }
 
 template <typename T> static size_t chol_inv_smem(int n) {
@@ -1117,16 +1126,16 @@ static void chol_inv_go(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx,
 }
 
 // one diagonal block (n <= 256) with the fused register-resident kernel
-template <int NTPW>
-static void chol_inv2_go(double* A, int n, int64_t lda, int64_t sA, double* X, int64_t ldx, int64_t sX, int64_t batch,
+template <typename T, int NTPW>
+static void chol_inv2_go(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx, int64_t sX, int64_t batch,
                          int32_t* info, size_t sm, hipStream_t s, int col_off, int info_first) {
   static bool attr_done = false;
   if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)chol_inv2_kernel<NTPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)chol_inv2_kernel<T, NTPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     attr_done = true;
   }
-  hipLaunchKernelGGL((chol_inv2_kernel<NTPW>), dim3((unsigned)(2 * batch)), dim3(RW * 64), sm, s, A, n, lda, sA, X,
+  hipLaunchKernelGGL((chol_inv2_kernel<T, NTPW>), dim3((unsigned)(2 * batch)), dim3(RW * 64), sm, s, A, n, lda, sA, X,
                      ldx, sX, info, col_off, info_first);
 }
 
@@ -1140,17 +1149,25 @@ static bool use_three_role(int n, int64_t batch) {
   return !off && n >= 128 && n <= 256 && batch <= 85;
 }
 
-template <int NTPW, int NTPW1>
-static void chol_inv3_go(double* A, int n, int64_t lda, int64_t sA, double* X, int64_t ldx, int64_t sX, int64_t batch,
+template <typename T, int NTPW, int NTPW1>
+static void chol_inv3_go(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx, int64_t sX, int64_t batch,
                          int32_t* info, size_t sm, hipStream_t s, int col_off, int info_first) {
   static bool attr_done = false;
   if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)chol_inv3_kernel<NTPW, NTPW1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)chol_inv3_kernel<T, NTPW, NTPW1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     attr_done = true;
   }
-  hipLaunchKernelGGL((chol_inv3_kernel<NTPW, NTPW1>), dim3((unsigned)(3 * batch)), dim3(RW * 64), sm, s, A, n, lda, sA,
-                     X, ldx, sX, info, col_off, info_first);
+  hipLaunchKernelGGL((chol_inv3_kernel<T, NTPW, NTPW1>), dim3((unsigned)(3 * batch)), dim3(RW * 64), sm, s, A, n, lda,
+                     sA, X, ldx, sX, info, col_off, info_first);
+}
+
+// the multi-role kernels keep 64-bit control words in X's row 0: f32 needs them 8-byte aligned
+template <typename T> static bool chol_ctl_ok(int n, const T* X, int64_t sX) {
+  if (sizeof(T) == 8) return true;
+  static int off = -1;
+  if (off < 0) off = getenv("NMGP_CHOL_F32_ROLES") && atoi(getenv("NMGP_CHOL_F32_ROLES")) == 0 ? 1 : 0;
+  return !off && n % 2 == 0 && ((uintptr_t)X % 8) == 0 && sX % 2 == 0;
 }
 
 template <typename T>
@@ -1158,24 +1175,27 @@ static int chol_inv_small(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ld
                           int32_t* info, hipStream_t s, int col_off, int info_first, bool two_role = true) {
   const int nt = (n + 15) >> 4, ntiles = nt * (nt + 1) / 2;
   const size_t sm = chol_inv_smem<T>(n);
-  if constexpr (std::is_same<T, double>::value) {
+  // multi-role kernels (f64 always; f32 when the control words can be 8-byte aligned, round 2)
+  if (chol_ctl_ok<T>(n, X, sX)) {
     if (two_role && use_three_role(n, batch) && !getenv("NMGP_CHOL_FUSED1")) {
-      if (ntiles <= RW * 9)
-        chol_inv3_go<9, 5>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+      if (ntiles <= RW * 5)
+        chol_inv3_go<T, 5, 3>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+      else if (ntiles <= RW * 9)
+        chol_inv3_go<T, 9, 5>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
       else
-        chol_inv3_go<17, 9>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+        chol_inv3_go<T, 17, 9>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
       NMGP_CHECK_LAUNCH();
       return NMGP_OK;
     }
     if (two_role && use_two_role(n, batch) && !getenv("NMGP_CHOL_FUSED1")) {
       if (ntiles <= RW * 3)
-        chol_inv2_go<3>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+        chol_inv2_go<T, 3>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
       else if (ntiles <= RW * 5)
-        chol_inv2_go<5>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+        chol_inv2_go<T, 5>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
       else if (ntiles <= RW * 9)
-        chol_inv2_go<9>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+        chol_inv2_go<T, 9>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
       else
-        chol_inv2_go<17>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
+        chol_inv2_go<T, 17>(A, n, lda, sA, X, ldx, sX, batch, info, sm, s, col_off, info_first);
       NMGP_CHECK_LAUNCH();
       return NMGP_OK;
     }
@@ -1398,6 +1418,12 @@ __global__ __launch_bounds__(256) void zero_upper_kernel(T* A, int n, int64_t ld
   for (int j = i + 1 + (int)threadIdx.x; j < n; j += 256) A[(int64_t)i * lda + j] = (T)0;
 }
 
+static bool leaf_roles() {
+  static int v = -1;
+  if (v < 0) v = getenv("NMGP_POTRF_LEAF_ROLES") && atoi(getenv("NMGP_POTRF_LEAF_ROLES")) == 0 ? 0 : 1;
+  return v == 1;
+}
+
 template <typename T>
 static int potrf_blocked(T* A, int n, int64_t lda, int32_t* info, void* ws, hipStream_t s) {
   PotrfSide* ctx = nullptr;
@@ -1422,7 +1448,10 @@ static int potrf_blocked(T* A, int n, int64_t lda, int32_t* info, void* ws, hipS
     const int j0 = jb * PNB, nbj = min(PNB, n - j0), r0 = j0 + nbj, n2 = n - r0;
     T* Ajj = A + (int64_t)j0 * lda + j0;
     T* Xj = Xd + (int64_t)jb * PNB * PNB;
-    if ((rc = chol_inv_small<T>(Ajj, nbj, lda, 0, Xj, PNB, 0, 1, info, s, j0, jb == 0, false)) != NMGP_OK) return rc;
+    // the diagonal leaf on the multi-role kernel (factor + two inverse workgroups; role 0 waits on
+    // nobody, so a side-stream SYRK holding the CUs only delays it) unless NMGP_POTRF_LEAF_ROLES=0
+    if ((rc = chol_inv_small<T>(Ajj, nbj, lda, 0, Xj, PNB, 0, 1, info, s, j0, jb == 0, leaf_roles())) != NMGP_OK)
+      return rc;
     if (n2 == 0) break;
     T* Lj = A + (int64_t)r0 * lda + j0;   // block column j below the diagonal block
     const int c1 = min(PNB, n2), n3 = n2 - c1;
