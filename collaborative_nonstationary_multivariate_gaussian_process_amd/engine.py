@@ -319,6 +319,11 @@ class DsviEngine:
             d14.append(g(self.WP, self.P, th, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), flags=L.B_LOWER,
                          offs=(typ * BM, sU + pq(i, j) * MM, slot * BM), row_seg=rseg))
         p["quad"] = G(d14)
+        if not elbo_mode:
+            # the pair factors W_P = P_{0,1} L_ij need only the L0 / L1 projections (proj3, side2): they run
+            # on side2 beside the Gibbs prior chain; only the latent factors W_G = P_G L_d follow projG
+            p["quad_W"] = G(d14[:D])
+            p["quad_P"] = G(d14[D:])
         if elbo_mode:
             # later Monte-Carlo samples of compute_ELBO: the pair factors W_P = P_{0,1} L_ij do not depend
             # on the sample (the L priors and Sigma_U are fixed within a call) -- only the D latent ones
@@ -554,7 +559,9 @@ class DsviEngine:
         # stream right after the minibatch gather (off the main chain): quad and bwd_w
         pre_planned = set()
         if not elbo_mode and os.environ.get("NMGP_PLAN_AHEAD", "1") != "0":
-            pre_planned = {nm for nm in ("quad", "bwd_w")
+            # (quad_P plans inline on side2: waiting there for the side stream's plans would be a
+            # side <-> side2 edge, which hipGraph instantiation does not survive on this stack)
+            pre_planned = {nm for nm in ("quad", "quad_W", "bwd_w")
                            if isinstance(p.get(nm), H.GemmGroup) and p[nm].plan is not None}
 
         def gemm(name):
@@ -643,6 +650,10 @@ class DsviEngine:
             ("trow", "row", row(getattr(lib, "nmgp_dsvi_trow_" + self.sfx)), "side2"),
             ("build_g12", "pairwise", pw("build_g12"), "side2"),
             ("sig", "side2", "g12"),
+        ]
+        if not elbo_mode and os.environ.get("NMGP_QUAD_SPLIT", "1") != "0":
+            steps += [("quad_P", "gemm", gemm("quad_P"), "side2"), ("sig", "side2", "quadP")]
+        steps += [
             ("chol_G", "chol", chol_g, "main"),
             ("wait", "main", "g12"),
             ("invG", "gemm", gemm("invG"), "main"),
@@ -685,8 +696,12 @@ class DsviEngine:
         ]
         if pre_planned:
             steps.append(("wait", "main", "plans"))
+        quad_split = os.environ.get("NMGP_QUAD_SPLIT", "1") != "0"
+        if quad_split:
+            steps += [("quad_W", "gemm", gemm("quad_W"), "main"), ("wait", "main", "quadP")]
+        else:
+            steps.append(("quad", "gemm", gemm("quad"), "main"))
         steps += [
-            ("quad", "gemm", gemm("quad"), "main"),
             ("recon", "row", row(getattr(lib, "nmgp_dsvi_recon_" + self.sfx)), "main"),
             ("sig", "main", "recon"),
             ("bwd_w", "gemm", gemm("bwd_w"), "main"),
