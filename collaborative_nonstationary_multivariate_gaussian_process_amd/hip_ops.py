@@ -150,7 +150,11 @@ class GemmGroup:
             if kernel == "lat" and not ok:
                 raise ValueError("GemmGroup(kernel='lat'): a descriptor is not addressable by the latency kernel")
             short = ok and _lat_split(descs, seg, target_wgs)[1] <= _LAT_MAX_ROUNDS
-            self.lat = ok and (kernel == "lat" or _LAT_MODE == "force" or (short and dtype == _F64))
+            # f32 too (round 2) where k <= 256: PM2.5-shaped fp32 step 1150 -> 1285 it/s A/B on the box.  At
+            # M = 512 (HCP) it was no faster and its different summation order moved the HCP-like fp32 loss
+            # from 6.1e-4 to 2.7e-3 of the fp64 reference (gate 1e-3): those groups stay on the tile kernel
+            f32_ok = dtype == _F64 or all(d.k <= 256 for d in descs)
+            self.lat = ok and (kernel == "lat" or _LAT_MODE == "force" or (short and f32_ok))
         if self.lat:
             self._init_lat(descs, device, dyn_plan, target_wgs)
             return
