@@ -1424,6 +1424,12 @@ static bool leaf_roles() {
   return v == 1;
 }
 
+static bool syrk_after_leaf() {
+  static int v = -1;
+  if (v < 0) v = getenv("NMGP_POTRF_SYRK_FIRST") && atoi(getenv("NMGP_POTRF_SYRK_FIRST")) == 1 ? 0 : 1;
+  return v == 1;
+}
+
 template <typename T>
 static int potrf_blocked(T* A, int n, int64_t lda, int32_t* info, void* ws, hipStream_t s) {
   PotrfSide* ctx = nullptr;
@@ -1444,6 +1450,21 @@ static int potrf_blocked(T* A, int n, int64_t lda, int32_t* info, void* ws, hipS
     step_flag = (int32_t*)((char*)ws_side + al256(gemm_big_ws_bytes()));
   }
   bool side_used = false;
+  // the trailing SYRK of step j is issued after the leaf of step j+1: both follow the step kernel of
+  // step j, and in a captured graph the first-issued child keeps the parent's queue -- the leaf -> step
+  // hand-off of the serial chain then stays on one queue (the cross-queue wait moves to the SYRK)
+  struct { const T* Lb; T* C; int n3, nbj, jb; bool on; } pend{nullptr, nullptr, 0, 0, -1, false};
+  auto issue_syrk = [&]() -> int {
+    if (!pend.on) return NMGP_OK;
+    pend.on = false;
+    if (hipStreamWaitEvent(ctx->side, ctx->ev_main, 0) != hipSuccess) return NMGP_ERR_LAUNCH;
+    int r = pgemm<T>(pend.Lb, lda, pend.Lb, lda, pend.C, lda, pend.n3, pend.n3, pend.nbj, NMGP_OUT_LOWER, -1.0, 1.0,
+                     ws_side, ctx->side);
+    if (r != NMGP_OK) return r;
+    if (hipEventRecord(ctx->ev_side, ctx->side) != hipSuccess) return NMGP_ERR_LAUNCH;
+    side_used = true;
+    return NMGP_OK;
+  };
   for (int jb = 0; jb < nblk; ++jb) {
     const int j0 = jb * PNB, nbj = min(PNB, n - j0), r0 = j0 + nbj, n2 = n - r0;
     T* Ajj = A + (int64_t)j0 * lda + j0;
@@ -1452,6 +1473,7 @@ static int potrf_blocked(T* A, int n, int64_t lda, int32_t* info, void* ws, hipS
     // nobody, so a side-stream SYRK holding the CUs only delays it) unless NMGP_POTRF_LEAF_ROLES=0
     if ((rc = chol_inv_small<T>(Ajj, nbj, lda, 0, Xj, PNB, 0, 1, info, s, j0, jb == 0, leaf_roles())) != NMGP_OK)
       return rc;
+    if ((rc = issue_syrk()) != NMGP_OK) return rc;
     if (n2 == 0) break;
     T* Lj = A + (int64_t)r0 * lda + j0;   // block column j below the diagonal block
     const int c1 = min(PNB, n2), n3 = n2 - c1;
@@ -1476,16 +1498,11 @@ static int potrf_blocked(T* A, int n, int64_t lda, int32_t* info, void* ws, hipS
     }
     if (n3 > 0) {
       if (hipEventRecord(ctx->ev_main, s) != hipSuccess) return NMGP_ERR_LAUNCH;
-      if (hipStreamWaitEvent(ctx->side, ctx->ev_main, 0) != hipSuccess) return NMGP_ERR_LAUNCH;
-      const T* Lb = Lj + (int64_t)c1 * lda;
-      T* C = A + (int64_t)(r0 + c1) * lda + (r0 + c1);
-      if ((rc = pgemm<T>(Lb, lda, Lb, lda, C, lda, n3, n3, nbj, NMGP_OUT_LOWER, -1.0, 1.0, ws_side, ctx->side)) !=
-          NMGP_OK)
-        return rc;
-      if (hipEventRecord(ctx->ev_side, ctx->side) != hipSuccess) return NMGP_ERR_LAUNCH;
-      side_used = true;
+      pend = {Lj + (int64_t)c1 * lda, A + (int64_t)(r0 + c1) * lda + (r0 + c1), n3, nbj, jb, true};
+      if (!(std::is_same<T, float>::value && syrk_after_leaf()) && (rc = issue_syrk()) != NMGP_OK) return rc;
     }
   }
+  if ((rc = issue_syrk()) != NMGP_OK) return rc;
   if (side_used && hipStreamWaitEvent(s, ctx->ev_side, 0) != hipSuccess) return NMGP_ERR_LAUNCH;
   hipLaunchKernelGGL(zero_upper_kernel<T>, dim3((unsigned)n), dim3(256), 0, s, A, n, lda);
   NMGP_CHECK_LAUNCH();
