@@ -1172,9 +1172,10 @@ template <typename T> static bool chol_ctl_ok(int n, const T* X, int64_t sX) {
 
 template <typename T>
 static int chol_inv_small(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx, int64_t sX, int64_t batch,
-                          int32_t* info, hipStream_t s, int col_off, int info_first, bool two_role = true) {
+                          int32_t* info, hipStream_t s, int col_off, int info_first, bool two_role = true,
+                          size_t sm_min = 0) {
   const int nt = (n + 15) >> 4, ntiles = nt * (nt + 1) / 2;
-  const size_t sm = chol_inv_smem<T>(n);
+  const size_t sm = chol_inv_smem<T>(n) > sm_min ? chol_inv_smem<T>(n) : sm_min;
   // multi-role kernels (f64 always; f32 when the control words can be 8-byte aligned, round 2)
   if (chol_ctl_ok<T>(n, X, sX)) {
     if (two_role && use_three_role(n, batch) && !getenv("NMGP_CHOL_FUSED1")) {
@@ -1253,6 +1254,8 @@ int gemm_big_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int b
 size_t gemm_big_ws_bytes();
 int potrf_step_f32(float* P, float* C, const float* X, int64_t lda, int n2, int nb, int c1, int32_t* flag,
                    hipStream_t s);
+int potrf_strip_f32(const float* L, float* C, int64_t lda, int m, int c1, hipStream_t s);
+bool potrf_step32_active();
 
 // f32 recursion (same algebra as chol_inv_rec below) with the products on the 128x128 MFMA kernel
 // of gemm_big.hip, split-K into `ws` where the tile grid would not fill the chip.
@@ -1370,7 +1373,7 @@ constexpr int PNB = 128;
 
 struct PotrfSide {
   hipStream_t side = nullptr;
-  hipEvent_t ev_main = nullptr, ev_side = nullptr;
+  hipEvent_t ev_main = nullptr, ev_side = nullptr, ev_tail = nullptr;
 };
 
 static int potrf_side_ctx(PotrfSide*& out) {
@@ -1384,6 +1387,7 @@ static int potrf_side_ctx(PotrfSide*& out) {
     if (hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking) != hipSuccess) return NMGP_ERR_LAUNCH;
     if (hipEventCreateWithFlags(&c.ev_main, hipEventDisableTiming) != hipSuccess) return NMGP_ERR_LAUNCH;
     if (hipEventCreateWithFlags(&c.ev_side, hipEventDisableTiming) != hipSuccess) return NMGP_ERR_LAUNCH;
+    if (hipEventCreateWithFlags(&c.ev_tail, hipEventDisableTiming) != hipSuccess) return NMGP_ERR_LAUNCH;
   }
   out = &c;
   return NMGP_OK;
@@ -1424,6 +1428,20 @@ static bool leaf_roles() {
   return v == 1;
 }
 
+static bool potrf_strip() {
+  static int v = -1;
+  if (v < 0) v = getenv("NMGP_POTRF_STRIP") && atoi(getenv("NMGP_POTRF_STRIP")) == 0 ? 0 : 1;
+  return v == 1;
+}
+
+// f32 leaves reserve enough LDS that no trailing-SYRK workgroup (2 x 36 KB stages) shares their CUs: the
+// rest of the previous step's SYRK runs beside the leaf (NMGP_POTRF_LEAF_LDS bytes, 0 = the leaf's own size)
+static size_t leaf_lds_reserve() {
+  static long v = -1;
+  if (v < 0) v = getenv("NMGP_POTRF_LEAF_LDS") ? atol(getenv("NMGP_POTRF_LEAF_LDS")) : 88 * 1024;
+  return (size_t)v;
+}
+
 static bool syrk_after_leaf() {
   static int v = -1;
   if (v < 0) v = getenv("NMGP_POTRF_SYRK_FIRST") && atoi(getenv("NMGP_POTRF_SYRK_FIRST")) == 1 ? 0 : 1;
@@ -1450,6 +1468,7 @@ static int potrf_blocked(T* A, int n, int64_t lda, int32_t* info, void* ws, hipS
     step_flag = (int32_t*)((char*)ws_side + al256(gemm_big_ws_bytes()));
   }
   bool side_used = false;
+  const bool strip = std::is_same<T, float>::value && potrf_step32_active() && potrf_strip();
   // the trailing SYRK of step j is issued after the leaf of step j+1: both follow the step kernel of
   // step j, and in a captured graph the first-issued child keeps the parent's queue -- the leaf -> step
   // hand-off of the serial chain then stays on one queue (the cross-queue wait moves to the SYRK)
@@ -1458,10 +1477,26 @@ static int potrf_blocked(T* A, int n, int64_t lda, int32_t* info, void* ws, hipS
     if (!pend.on) return NMGP_OK;
     pend.on = false;
     if (hipStreamWaitEvent(ctx->side, ctx->ev_main, 0) != hipSuccess) return NMGP_ERR_LAUNCH;
-    int r = pgemm<T>(pend.Lb, lda, pend.Lb, lda, pend.C, lda, pend.n3, pend.n3, pend.nbj, NMGP_OUT_LOWER, -1.0, 1.0,
-                     ws_side, ctx->side);
-    if (r != NMGP_OK) return r;
-    if (hipEventRecord(ctx->ev_side, ctx->side) != hipSuccess) return NMGP_ERR_LAUNCH;
+    int r;
+    if (std::is_same<T, float>::value && strip) {
+      // block column j+2 first (the next step kernel's lookahead writes it: it waits for this strip only),
+      // then the rest of the trailing SYRK (columns >= j+3), which the step after next waits for
+      const int cs = min(PNB, pend.n3), n4 = pend.n3 - cs;
+      if ((r = potrf_strip_f32((const float*)pend.Lb, (float*)pend.C, lda, pend.n3, cs, ctx->side)) != NMGP_OK) return r;
+      if (hipEventRecord(ctx->ev_side, ctx->side) != hipSuccess) return NMGP_ERR_LAUNCH;
+      if (n4 > 0) {
+        const T* Lb2 = pend.Lb + (int64_t)cs * lda;
+        if ((r = pgemm<T>(Lb2, lda, Lb2, lda, pend.C + (int64_t)cs * lda + cs, lda, n4, n4, pend.nbj, NMGP_OUT_LOWER,
+                          -1.0, 1.0, ws_side, ctx->side)) != NMGP_OK)
+          return r;
+      }
+    } else {
+      r = pgemm<T>(pend.Lb, lda, pend.Lb, lda, pend.C, lda, pend.n3, pend.n3, pend.nbj, NMGP_OUT_LOWER, -1.0, 1.0,
+                   ws_side, ctx->side);
+      if (r != NMGP_OK) return r;
+      if (hipEventRecord(ctx->ev_side, ctx->side) != hipSuccess) return NMGP_ERR_LAUNCH;
+    }
+    if (hipEventRecord(ctx->ev_tail, ctx->side) != hipSuccess) return NMGP_ERR_LAUNCH;
     side_used = true;
     return NMGP_OK;
   };
@@ -1471,7 +1506,8 @@ static int potrf_blocked(T* A, int n, int64_t lda, int32_t* info, void* ws, hipS
     T* Xj = Xd + (int64_t)jb * PNB * PNB;
     // the diagonal leaf on the multi-role kernel (factor + two inverse workgroups; role 0 waits on
     // nobody, so a side-stream SYRK holding the CUs only delays it) unless NMGP_POTRF_LEAF_ROLES=0
-    if ((rc = chol_inv_small<T>(Ajj, nbj, lda, 0, Xj, PNB, 0, 1, info, s, j0, jb == 0, leaf_roles())) != NMGP_OK)
+    if ((rc = chol_inv_small<T>(Ajj, nbj, lda, 0, Xj, PNB, 0, 1, info, s, j0, jb == 0, leaf_roles(),
+                                std::is_same<T, float>::value ? leaf_lds_reserve() : 0)) != NMGP_OK)
       return rc;
     if ((rc = issue_syrk()) != NMGP_OK) return rc;
     if (n2 == 0) break;
@@ -1503,7 +1539,7 @@ static int potrf_blocked(T* A, int n, int64_t lda, int32_t* info, void* ws, hipS
     }
   }
   if ((rc = issue_syrk()) != NMGP_OK) return rc;
-  if (side_used && hipStreamWaitEvent(s, ctx->ev_side, 0) != hipSuccess) return NMGP_ERR_LAUNCH;
+  if (side_used && hipStreamWaitEvent(s, ctx->ev_tail, 0) != hipSuccess) return NMGP_ERR_LAUNCH;
   hipLaunchKernelGGL(zero_upper_kernel<T>, dim3((unsigned)n), dim3(256), 0, s, A, n, lda);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;

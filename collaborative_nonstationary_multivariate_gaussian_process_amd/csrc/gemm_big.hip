@@ -667,7 +667,50 @@ __global__ __launch_bounds__(256) void potrf_step32_kernel(PotrfStepArgs pa) {
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cv[q][r] - acc[q >> 1][q & 1][r]), rC, coff[q][r], 0, 0);
 }
 
-static bool potrf_step32_active() {
+static // The first block column of a trailing update on the 32-row scheme: C(i, j) -= sum_k L[i][k] L[j][k] for
+// i < m, j < c1 (k = 128; the B rows are L's rows 0..c1-1).  The blocked potrf runs the column next to the
+// lookahead (block column j+2 at step j) as this separate strip launch ahead of the rest of the trailing
+// SYRK, so the next step kernel -- which writes that column too -- waits only for the strip.
+__global__ __launch_bounds__(256) void potrf_strip32_kernel(const float* L, float* C, int64_t lda, int m, int c1) {
+  const int t = threadIdx.x, lane = t & 63, li = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int i0 = blockIdx.x * PS_ROWS;
+  const __amdgpu_buffer_rsrc_t rL = make_rsrc(L, ((int64_t)(m - 1) * lda + 128) * 4);
+  const __amdgpu_buffer_rsrc_t rC = make_rsrc(C, ((int64_t)(m - 1) * lda + c1) * 4);
+  float a[2][PS_NV], b[2][PS_NV];
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q >> 1][q & 1] = f32x4{0, 0, 0, 0};
+  ps_load_rows(a, rL, i0, lda, m, false);
+  ps_load_rows(b, rL, 32 * w, lda, c1, false);
+  f32x4 cv[4];
+  uint32_t coff[4][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + 16 * (q >> 1) + 4 * g + r, j = 32 * w + 16 * (q & 1) + li;
+      coff[q][r] = (i < m && j < c1) ? (uint32_t)(((int64_t)i * lda + j) * 4) : 0x80000000u;
+      cv[q][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rC, coff[q][r], 0, 0));
+    }
+  ps_mma(a, b, acc);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (coff[q][r] != 0x80000000u)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cv[q][r] - acc[q >> 1][q & 1][r]), rC, coff[q][r], 0, 0);
+}
+
+int potrf_strip_f32(const float* L, float* C, int64_t lda, int m, int c1, hipStream_t s) {
+  if (m <= 0 || c1 <= 0) return NMGP_OK;
+  hipLaunchKernelGGL(potrf_strip32_kernel, dim3((unsigned)((m + PS_ROWS - 1) / PS_ROWS)), dim3(256), 0, s, L, C, lda,
+                     m, c1);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
+
+bool potrf_step32_active() {
   static int v = -1;
   if (v < 0) v = getenv("NMGP_POTRF_STEP128") && atoi(getenv("NMGP_POTRF_STEP128")) == 1 ? 1 : 0;
   return v == 0;
