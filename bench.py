@@ -114,7 +114,8 @@ def stress_cholesky(dev, reps=5):
     t_cpu = time.time() - t0
     f = Mst ** 3 / 3.0
     return {"workload": "stress: one SPD M=4096 fp32 matrix (BASELINE.json configs[4])",
-            "kernel": "nmgp_potrf_blocked_f32 (128-wide fused leaves, panel GEMM, lookahead, side-stream SYRK)",
+            "kernel": "nmgp_potrf_blocked_f32 (128-wide fused leaves; 32-row panel + lookahead step kernel; "
+                      "side stream: 32-row strip of block column j+2, then the trailing SYRK)",
             "potrf_ms": round(t_fac, 4), "gflops": round(f / (t_fac * 1e-3) / 1e9, 1),
             "residual": resid,
             "syrk_in_factorization": _stress_syrk_pmc(),
@@ -138,7 +139,7 @@ def _stress_syrk_pmc():
     rows = json.load(open(files[-1]))["rows"]
     nm = lambda r: r["kernel"]
     syrk = [r for r in rows if "gemm_big_kernel" in nm(r)]
-    fac = [r for r in rows if any(k in nm(r) for k in ("gemm_big_kernel", "potrf_step_kernel", "chol_inv_kernel"))]
+    fac = [r for r in rows if any(k in nm(r) for k in ("gemm_big_kernel", "potrf_step", "potrf_strip", "chol_inv"))]
     tw = lambda rs: sum(r["mfma_util"] * r["avg_us"] * r["dispatches"] for r in rs) / max(
         1e-9, sum(r["avg_us"] * r["dispatches"] for r in rs))
     return {"kernel": "gemm_big_kernel (the factorization's own trailing SYRKs, k = 128)",
