@@ -536,22 +536,24 @@ __global__ __launch_bounds__(256, 2) void potrf_step_kernel(PotrfStepArgs pa) {
   big_epilogue<0>(g2, 0, i0, 0, acc);
 }
 
-// 32-row variant (the default): the step kernel above runs two dependent 128x128x128 products on each of
-// n2/128 workgroups (<= 31 CUs busy, ~30 us per block step on the serial chain of the factorization).
-// Here workgroup b owns panel rows [32b, 32b + 32): 4x the workgroups, a quarter of the serial MFMA work
-// each.  Wave w owns output columns [32w, 32w + 32) as 2x2 16x16 f32 MFMA blocks; k = nb = 128 in one
-// register-resident panel: lane (li, g) loads k = 32g .. 32g + 31 of its rows (eight 16-byte loads per
-// row block) and MFMA step s consumes k-slot g <-> k = 32g + s for both operands (a sum over k does not
-// care about the order).  Workgroups 0..3 (the rows of block column j+1, L_0) publish by counting on
-// flag[0]; every workgroup then reads them back (sc1) for A(rows, block column j+1) -= L_i L_0^T.
-// In place: the four waves read all of their rows before the barrier that precedes the stores.
-constexpr int PS_ROWS = 32, PS_NV = 32;
+// Row-panel variant (the default): the step kernel above runs two dependent 128x128x128 products on each
+// of n2/128 workgroups (<= 31 CUs busy, ~30 us per block step on the serial chain of the factorization).
+// Here workgroup b owns 16 RB panel rows: 8x (RB = 1) or 4x (RB = 2) the workgroups, 1/8 or 1/4 of the
+// serial MFMA work each.  Wave w owns output columns [32w, 32w + 32) as RB x 2 16x16 f32 MFMA blocks;
+// k = nb = 128 in one register-resident panel: lane (li, g) loads k = 32g .. 32g + 31 of its rows (eight
+// 16-byte loads per row block) and MFMA step s consumes k-slot g <-> k = 32g + s for both operands (a sum
+// over k does not care about the order).  The workgroups holding the rows of block column j+1 (L_0)
+// publish by counting on flag[0]; every workgroup then reads them back (sc1) for
+// A(rows, block column j+1) -= L_i L_0^T.  In place: the four waves read all of their rows before the
+// barrier that precedes the stores.
+constexpr int PS_NV = 32;
 
-__device__ __forceinline__ void ps_load_rows(float (&v)[2][PS_NV], __amdgpu_buffer_rsrc_t r, int64_t row0, int64_t ld,
-                                             int nrows, bool sc1) {
+template <int RB>
+__device__ __forceinline__ void ps_load_rows(float (&v)[RB][PS_NV], __amdgpu_buffer_rsrc_t r, int64_t row0,
+                                             int64_t ld, int nrows, bool sc1) {
   const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
 #pragma unroll
-  for (int bi = 0; bi < 2; ++bi) {
+  for (int bi = 0; bi < RB; ++bi) {
     const int64_t row = row0 + 16 * bi + li;
     const uint32_t off = row < nrows ? (uint32_t)((row * ld + PS_NV * g) * 4) : 0x80000000u;
 #pragma unroll
@@ -564,51 +566,75 @@ __device__ __forceinline__ void ps_load_rows(float (&v)[2][PS_NV], __amdgpu_buff
   }
 }
 
-__device__ __forceinline__ void ps_mma(const float (&a)[2][PS_NV], const float (&b)[2][PS_NV], f32x4 (&acc)[2][2]) {
+template <int RA>
+__device__ __forceinline__ void ps_mma(const float (&a)[RA][PS_NV], const float (&b)[2][PS_NV],
+                                       f32x4 (&acc)[RA][2]) {
 #pragma unroll
   for (int s = 0; s < PS_NV; ++s)
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < 2 * RA; ++q)
       acc[q >> 1][q & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q >> 1][s], b[q & 1][s], acc[q >> 1][q & 1], 0, 0, 0);
 }
 
-__global__ __launch_bounds__(256) void potrf_step32_kernel(PotrfStepArgs pa) {
-  constexpr int LP = 128 + 4;                                   // LDS pitch of the L_i rows (floats)
-  __shared__ __attribute__((aligned(16))) float Ls[PS_ROWS * LP];
-  const int t = threadIdx.x, lane = t & 63, li = lane & 15, g = lane >> 4;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int i0 = blockIdx.x * PS_ROWS;
-  const int npub = (pa.c1 + PS_ROWS - 1) / PS_ROWS;          // workgroups holding L_0 (<= 4)
-  const __amdgpu_buffer_rsrc_t rP = make_rsrc(pa.P, ((int64_t)(pa.n2 - 1) * pa.lda + pa.nb) * 4);
-  const __amdgpu_buffer_rsrc_t rX = make_rsrc(pa.X, (int64_t)128 * 128 * 4);
-  const __amdgpu_buffer_rsrc_t rC = make_rsrc(pa.C, ((int64_t)(pa.n2 - 1) * pa.lda + pa.c1) * 4);
-  float a[2][PS_NV], b[2][PS_NV];
-  f32x4 acc[2][2];
+// lookahead target of this workgroup's rows (prefetched: its other writers finished before the launch)
+template <int RB>
+__device__ __forceinline__ void ps_load_c(__amdgpu_buffer_rsrc_t rC, int i0, int64_t lda, int m, int c1,
+                                          f32x4 (&cv)[RB][2], uint32_t (&coff)[RB][2][4]) {
+  const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) acc[q >> 1][q & 1] = f32x4{0, 0, 0, 0};
-  // 1. L_i = A_i X^T: op(B)(k, j) = X[j][k], zero above the diagonal (X lower triangular)
-  ps_load_rows(a, rP, i0, pa.lda, pa.n2, false);
-  ps_load_rows(b, rX, 32 * w, 128, pa.nb, false);
-  // the lookahead target (block column j+1; its other writers finished before this launch) comes in
-  // behind the operands, so its round trip overlaps the panel product
-  f32x4 cv[4];
-  uint32_t coff[4][4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < 2 * RB; ++q)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = i0 + 16 * (q >> 1) + 4 * g + r, j = 32 * w + 16 * (q & 1) + li;
-      coff[q][r] = (i < pa.n2 && j < pa.c1) ? (uint32_t)(((int64_t)i * pa.lda + j) * 4) : 0x80000000u;
-      cv[q][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rC, coff[q][r], 0, 0));
+      coff[q >> 1][q & 1][r] = (i < m && j < c1) ? (uint32_t)(((int64_t)i * lda + j) * 4) : 0x80000000u;
+      cv[q >> 1][q & 1][r] =
+          __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rC, coff[q >> 1][q & 1][r], 0, 0));
     }
+}
+
+template <int RB>
+__device__ __forceinline__ void ps_store_c(__amdgpu_buffer_rsrc_t rC, const f32x4 (&cv)[RB][2],
+                                           const uint32_t (&coff)[RB][2][4], const f32x4 (&acc)[RB][2]) {
+#pragma unroll
+  for (int q = 0; q < 2 * RB; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (coff[q >> 1][q & 1][r] != 0x80000000u)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cv[q >> 1][q & 1][r] - acc[q >> 1][q & 1][r]), rC,
+                                              coff[q >> 1][q & 1][r], 0, 0);
+}
+
+template <int RB>
+__global__ __launch_bounds__(256) void potrf_step32_kernel(PotrfStepArgs pa) {
+  constexpr int ROWS = 16 * RB;
+  constexpr int LP = 128 + 4;                                   // LDS pitch of the L_i rows (floats)
+  __shared__ __attribute__((aligned(16))) float Ls[ROWS * LP];
+  const int t = threadIdx.x, lane = t & 63, li = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int i0 = blockIdx.x * ROWS;
+  const int npub = (pa.c1 + ROWS - 1) / ROWS;                   // workgroups holding L_0
+  const __amdgpu_buffer_rsrc_t rP = make_rsrc(pa.P, ((int64_t)(pa.n2 - 1) * pa.lda + pa.nb) * 4);
+  const __amdgpu_buffer_rsrc_t rX = make_rsrc(pa.X, (int64_t)128 * 128 * 4);
+  const __amdgpu_buffer_rsrc_t rC = make_rsrc(pa.C, ((int64_t)(pa.n2 - 1) * pa.lda + pa.c1) * 4);
+  float a[RB][PS_NV], b[2][PS_NV];
+  f32x4 acc[RB][2];
+#pragma unroll
+  for (int q = 0; q < 2 * RB; ++q) acc[q >> 1][q & 1] = f32x4{0, 0, 0, 0};
+  // 1. L_i = A_i X^T: op(B)(k, j) = X[j][k], zero above the diagonal (X lower triangular)
+  ps_load_rows<RB>(a, rP, i0, pa.lda, pa.n2, false);
+  ps_load_rows<2>(b, rX, 32 * w, 128, pa.nb, false);
+  f32x4 cv[RB][2];
+  uint32_t coff[RB][2][4];
+  ps_load_c<RB>(rC, i0, pa.lda, pa.n2, pa.c1, cv, coff);   // behind the operands: overlaps the panel product
 #pragma unroll
   for (int bj = 0; bj < 2; ++bj)
 #pragma unroll
     for (int s = 0; s < PS_NV; ++s) b[bj][s] = keep_if(b[bj][s], PS_NV * g + s <= 32 * w + 16 * bj + li);
-  ps_mma(a, b, acc);
+  ps_mma<RB>(a, b, acc);
   __syncthreads();   // every wave has read its rows of A_i: the in-place stores may start
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < 2 * RB; ++q)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int il = 16 * (q >> 1) + 4 * g + r, j = 32 * w + 16 * (q & 1) + li;
@@ -639,10 +665,10 @@ __global__ __launch_bounds__(256) void potrf_step32_kernel(PotrfStepArgs pa) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   // 2. lookahead: A(rows i, block column j+1) -= L_i L_0^T; L_i from LDS, L_0 read back write-through
 #pragma unroll
-  for (int q = 0; q < 4; ++q) acc[q >> 1][q & 1] = f32x4{0, 0, 0, 0};
-  ps_load_rows(b, rP, 32 * w, pa.lda, pa.c1, true);
+  for (int q = 0; q < 2 * RB; ++q) acc[q >> 1][q & 1] = f32x4{0, 0, 0, 0};
+  ps_load_rows<2>(b, rP, 32 * w, pa.lda, pa.c1, true);
 #pragma unroll
-  for (int bi = 0; bi < 2; ++bi)
+  for (int bi = 0; bi < RB; ++bi)
 #pragma unroll
     for (int q = 0; q < PS_NV / 4; ++q) {
       const float4 v = *(const float4*)&Ls[(16 * bi + li) * LP + PS_NV * g + 4 * q];
@@ -651,7 +677,7 @@ __global__ __launch_bounds__(256) void potrf_step32_kernel(PotrfStepArgs pa) {
       a[bi][4 * q + 2] = v.z;
       a[bi][4 * q + 3] = v.w;
     }
-  ps_mma(a, b, acc);
+  ps_mma<RB>(a, b, acc);
   if (t == 0) {
     const int old = __hip_atomic_fetch_add(pa.flag + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old == (int)gridDim.x - 1) {   // every reader is past its loads of L_0: re-arm for the next launch
@@ -659,53 +685,48 @@ __global__ __launch_bounds__(256) void potrf_step32_kernel(PotrfStepArgs pa) {
       __hip_atomic_store(pa.flag + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (coff[q][r] != 0x80000000u)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cv[q][r] - acc[q >> 1][q & 1][r]), rC, coff[q][r], 0, 0);
+  ps_store_c<RB>(rC, cv, coff, acc);
 }
 
-static // The first block column of a trailing update on the 32-row scheme: C(i, j) -= sum_k L[i][k] L[j][k] for
+// The first block column of a trailing update on the row-panel scheme: C(i, j) -= sum_k L[i][k] L[j][k] for
 // i < m, j < c1 (k = 128; the B rows are L's rows 0..c1-1).  The blocked potrf runs the column next to the
 // lookahead (block column j+2 at step j) as this separate strip launch ahead of the rest of the trailing
 // SYRK, so the next step kernel -- which writes that column too -- waits only for the strip.
+template <int RB>
 __global__ __launch_bounds__(256) void potrf_strip32_kernel(const float* L, float* C, int64_t lda, int m, int c1) {
-  const int t = threadIdx.x, lane = t & 63, li = lane & 15, g = lane >> 4;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int i0 = blockIdx.x * PS_ROWS;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int i0 = blockIdx.x * 16 * RB;
   const __amdgpu_buffer_rsrc_t rL = make_rsrc(L, ((int64_t)(m - 1) * lda + 128) * 4);
   const __amdgpu_buffer_rsrc_t rC = make_rsrc(C, ((int64_t)(m - 1) * lda + c1) * 4);
-  float a[2][PS_NV], b[2][PS_NV];
-  f32x4 acc[2][2];
+  float a[RB][PS_NV], b[2][PS_NV];
+  f32x4 acc[RB][2];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) acc[q >> 1][q & 1] = f32x4{0, 0, 0, 0};
-  ps_load_rows(a, rL, i0, lda, m, false);
-  ps_load_rows(b, rL, 32 * w, lda, c1, false);
-  f32x4 cv[4];
-  uint32_t coff[4][4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = i0 + 16 * (q >> 1) + 4 * g + r, j = 32 * w + 16 * (q & 1) + li;
-      coff[q][r] = (i < m && j < c1) ? (uint32_t)(((int64_t)i * lda + j) * 4) : 0x80000000u;
-      cv[q][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rC, coff[q][r], 0, 0));
-    }
-  ps_mma(a, b, acc);
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (coff[q][r] != 0x80000000u)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cv[q][r] - acc[q >> 1][q & 1][r]), rC, coff[q][r], 0, 0);
+  for (int q = 0; q < 2 * RB; ++q) acc[q >> 1][q & 1] = f32x4{0, 0, 0, 0};
+  ps_load_rows<RB>(a, rL, i0, lda, m, false);
+  ps_load_rows<2>(b, rL, 32 * w, lda, c1, false);
+  f32x4 cv[RB][2];
+  uint32_t coff[RB][2][4];
+  ps_load_c<RB>(rC, i0, lda, m, c1, cv, coff);
+  ps_mma<RB>(a, b, acc);
+  ps_store_c<RB>(rC, cv, coff, acc);
+}
+
+// rows per workgroup of the step / strip kernels (NMGP_POTRF_ROWS=16 or 32; 16 halves the MFMA work per
+// workgroup and measured the same 1.52-1.54 ms at M = 4096: the kernels are bound by their memory round
+// trips and the L_0 hand-off, not by the products)
+static int ps_rows() {
+  static int v = -1;
+  if (v < 0) v = getenv("NMGP_POTRF_ROWS") && atoi(getenv("NMGP_POTRF_ROWS")) == 16 ? 16 : 32;
+  return v;
 }
 
 int potrf_strip_f32(const float* L, float* C, int64_t lda, int m, int c1, hipStream_t s) {
   if (m <= 0 || c1 <= 0) return NMGP_OK;
-  hipLaunchKernelGGL(potrf_strip32_kernel, dim3((unsigned)((m + PS_ROWS - 1) / PS_ROWS)), dim3(256), 0, s, L, C, lda,
-                     m, c1);
+  const int R = ps_rows();
+  if (R == 16)
+    hipLaunchKernelGGL(potrf_strip32_kernel<1>, dim3((unsigned)((m + 15) / 16)), dim3(256), 0, s, L, C, lda, m, c1);
+  else
+    hipLaunchKernelGGL(potrf_strip32_kernel<2>, dim3((unsigned)((m + 31) / 32)), dim3(256), 0, s, L, C, lda, m, c1);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
@@ -721,7 +742,10 @@ int potrf_step_f32(float* P, float* C, const float* X, int64_t lda, int n2, int 
   if (n2 <= 0) return NMGP_OK;
   PotrfStepArgs pa{P, C, X, lda, n2, nb, c1, flag};
   if (potrf_step32_active() && nb == 128) {
-    hipLaunchKernelGGL(potrf_step32_kernel, dim3((unsigned)((n2 + PS_ROWS - 1) / PS_ROWS)), dim3(256), 0, s, pa);
+    if (ps_rows() == 16)
+      hipLaunchKernelGGL(potrf_step32_kernel<1>, dim3((unsigned)((n2 + 15) / 16)), dim3(256), 0, s, pa);
+    else
+      hipLaunchKernelGGL(potrf_step32_kernel<2>, dim3((unsigned)((n2 + 31) / 32)), dim3(256), 0, s, pa);
     NMGP_CHECK_LAUNCH();
     return NMGP_OK;
   }
