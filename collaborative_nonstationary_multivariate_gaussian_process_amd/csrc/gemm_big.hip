@@ -380,7 +380,15 @@ __global__ __launch_bounds__(256, 2) void gemm_big_kernel(BigGemmArgs g) {
   // XCD-aware block order: hardware places block b on XCD b % 8; give each XCD a contiguous run
   int bid = blockIdx.x;
   const int nb = gridDim.x;
-  if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);
+  if (gridDim.y == 1) {
+    if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);
+  } else {
+    // batched (one problem per blockIdx.y): workgroup x runs on XCD x % 8, so the contiguous-run map above
+    // gave each XCD the same tile row of EVERY problem -- with triangular operands (the ECoG / HCP factor
+    // products) the row with the longest k ranges landed on one XCD (144 of 480 k-tiles per problem at
+    // M = 1024).  Rotating the tile index by 9 per problem walks each XCD over all tile columns instead.
+    bid = (int)(((int64_t)bid + 9LL * blockIdx.y) % nb);
+  }
   const int64_t bat = blockIdx.y;
   f32x16 acc[2][2];
   if constexpr (MODE != 0) {
