@@ -284,8 +284,8 @@ def pair_sharded_train(dev, world, rank, dist, D=128, M=1024, rows=391, B=512, s
            "replicated_allreduce_MB": round(sum(t.numel() for t in sh._rep) * 4 / 1e6, 1),
            "peak_mem_GB_rank0": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)}
     if D == 128 and M == 1024:
-        # the same step unsharded on one GPU (packed pairs, 247 GB peak): profiles/r02_ecog_train.json
-        out["single_gpu_unsharded_s_per_step"] = 0.562
+        # the same step unsharded on one GPU (packed pairs, 247 GB peak): profiles/r02d_ecog_train.json
+        out["single_gpu_unsharded_s_per_step"] = 0.442
     del sh, loss
     gc.collect()
     torch.cuda.empty_cache()
