@@ -16,8 +16,9 @@
 //   * Deterministic split-K when the grid would not fill the chip: partials are published
 //     write-through (sc1) into caller workspace, the last-arriving chunk of a tile sums them in
 //     chunk order (its own from registers) and applies the epilogue.
-//   * blockIdx -> tile mapping is XCD-aware: the 8 XCDs each get a contiguous run of tiles (shared
-//     A rows stay in one L2).
+//   * blockIdx -> tile mapping is XCD-aware: single problems give each of the 8 XCDs a contiguous run of
+//     tiles (shared A rows stay in one L2); batched problems rotate the tile index per problem so no XCD
+//     gets the same (for triangular operands: the longest-k) tile row of every problem.
 #include "common.hpp"
 
 namespace nmgp {
@@ -380,8 +381,11 @@ __global__ __launch_bounds__(256, 2) void gemm_big_kernel(BigGemmArgs g) {
   // XCD-aware block order: hardware places block b on XCD b % 8; give each XCD a contiguous run
   int bid = blockIdx.x;
   const int nb = gridDim.x;
-  if (gridDim.y == 1) {
-    if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);
+  if ((nb & 7) != 0) {
+    // (tile counts that are not a multiple of 8 -- e.g. the 36 lower tiles of a batched SYRK -- already
+    // spread each problem's tiles over the XCDs through the flattened workgroup index)
+  } else if (gridDim.y == 1) {
+    bid = (bid & 7) * (nb >> 3) + (bid >> 3);
   } else {
     // batched (one problem per blockIdx.y): workgroup x runs on XCD x % 8, so the contiguous-run map above
     // gave each XCD the same tile row of EVERY problem -- with triangular operands (the ECoG / HCP factor
