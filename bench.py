@@ -119,6 +119,7 @@ def stress_cholesky(dev, reps=5):
             "potrf_ms": round(t_fac, 4), "gflops": round(f / (t_fac * 1e-3) / 1e9, 1),
             "residual": resid,
             "syrk_in_factorization": _stress_syrk_pmc(),
+            "syrk_in_ecog_factorization": _ecog_syrk_pmc(),
             "syrk_isolated_proxy": {"kernel": "gemm_big_kernel (128x128 f32 MFMA, stream-K)", "n": Mst, "k": Mst,
                                     "ms": round(t_syrk, 4), "achieved_tflops": round(syrk_tf, 2), "peak_tflops": 157.3,
                                     "frac": round(syrk_tf / 157.3, 4),
@@ -146,6 +147,25 @@ def _stress_syrk_pmc():
             "launches": sum(r["dispatches"] for r in syrk), "mfma_busy_time_weighted": round(tw(syrk), 4),
             "factorization_kernels_mfma_busy": round(tw(fac), 4),
             "source": os.path.relpath(files[-1], ROOT)}
+
+
+def _ecog_syrk_pmc():
+    """MFMA-busy of the trailing-update SYRK inside the batched recursive Cholesky of the ECoG-shaped step
+    (BASELINE.json configs[3]: 8384 variational factors of M = 1024; top recursion level A22 -= L21 L21^T,
+    k = 512, 10 lower 128x128 tiles per factor = grid 21463040 threads), from the committed PMC pass of one
+    training step (tools/syrk_inside_pmc.sh -> profiles/r*_ecog_step_mfma_util.json)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_ecog_step_mfma_util.json")))
+    if not files:
+        return None
+    rows = [r for r in json.load(open(files[-1]))["rows"]
+            if r["kernel"].startswith("void nmgp::gemm_big_kernel<true, true, 0>") and r["grid_threads"] == 21463040]
+    if not rows:
+        return None
+    w = sum(r["avg_us"] * r["dispatches"] for r in rows)
+    return {"kernel": "gemm_big_kernel (batched trailing SYRK A22 -= L21 L21^T of 8384 M=1024 factors, k = 512)",
+            "mfma_busy_time_weighted": round(sum(r["mfma_util"] * r["avg_us"] * r["dispatches"] for r in rows) / w, 4),
+            "avg_us": round(w / sum(r["dispatches"] for r in rows), 1), "source": os.path.relpath(files[-1], ROOT)}
 
 
 def api_path(dev, xs, ys, z, epochs_device=100, epochs_torch=20):
