@@ -55,3 +55,8 @@ run("kl_lbar form (A, B not k-contig, A_UPPER B_LOWER, OUT_TRIL)", False, False,
 run("dense, both k-contig", True, True, 0, dense)
 run("dense, B not k-contig", True, False, 0, dense)
 run("dense, A and B not k-contig", False, False, 0, dense)
+if len(sys.argv) > 3 and sys.argv[3] == "kl":
+    run("kl form, A k-contig (same k ranges)", True, False, L.A_UPPER | L.B_LOWER | L.OUT_TRIL, tri_work)
+    run("kl form, B k-contig (same k ranges)", False, True, L.A_UPPER | L.B_LOWER | L.OUT_TRIL, tri_work)
+    run("kl form, no OUT_TRIL", False, False, L.A_UPPER | L.B_LOWER, tri_work)
+    run("kl form, no triangular flags (dense k, OUT_TRIL)", False, False, L.OUT_TRIL, dense / 2)
