@@ -60,3 +60,26 @@ if len(sys.argv) > 3 and sys.argv[3] == "kl":
     run("kl form, B k-contig (same k ranges)", False, True, L.A_UPPER | L.B_LOWER | L.OUT_TRIL, tri_work)
     run("kl form, no OUT_TRIL", False, False, L.A_UPPER | L.B_LOWER, tri_work)
     run("kl form, no triangular flags (dense k, OUT_TRIL)", False, False, L.OUT_TRIL, dense / 2)
+if len(sys.argv) > 3 and sys.argv[3] == "rank":
+    # the ECoG pair L-bar form: C += P^T W-hat over the ~4 rows of one output (k = 4), OUT_TRIL, beta = 1
+    for kk in (4, 16, 64):
+        bb = H.BigBatch(A, B, C, offs, offs, offs, M, M, kk, lda=M, ldb=M, a_kcontig=False, b_kcontig=False,
+                        flags=L.OUT_TRIL, beta=1.0)
+        bb()
+        torch.cuda.synchronize()
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            for _ in range(3):
+                bb()
+        gr.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        gr.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 3
+        # HBM floor: read + write C (lower tiles), write C (upper tiles) ~ 3/2 x 4 MB per problem
+        print(json.dumps({"case": f"rank-{kk} update C += A^T B (OUT_TRIL, beta 1)", "nb": nb, "ms": round(ms, 3),
+                          "GB_per_s_C_traffic": round(nb * 1.5 * M * M * 4 * 2 / 2 / (ms * 1e-3) / 1e9, 1)}),
+              flush=True)
