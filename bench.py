@@ -305,7 +305,7 @@ def pair_sharded_train(dev, world, rank, dist, D=128, M=1024, rows=391, B=512, s
            "peak_mem_GB_rank0": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)}
     if D == 128 and M == 1024:
         # the same step unsharded on one GPU (packed pairs, 247 GB peak): profiles/r02d_ecog_train.json
-        out["single_gpu_unsharded_s_per_step"] = 0.409
+        out["single_gpu_unsharded_s_per_step"] = 0.405
     del sh, loss
     gc.collect()
     torch.cuda.empty_cache()
