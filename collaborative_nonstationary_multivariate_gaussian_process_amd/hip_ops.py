@@ -62,7 +62,9 @@ def gemm_desc(C, A, B, m, n, k, sA, sB, sC, *, flags=0, alpha=1.0, beta=0.0, kb=
 
 
 GEMM_BK = 32   # k-tile of gemm_kernel (csrc/gemm.hip GBK)
-_KSPLIT_FACTOR = float(os.environ.get("NMGP_KSPLIT_FACTOR", "2.0"))   # tuning knob (tools/gemm_probe.py)
+# tuning knob (tools/gemm_probe.py; tools/ab_env.sh on the PM2.5 bench, round 2: 2.0 -> 1283-1291 it/s,
+# 4.0 -> 1300-1302, 8.0 -> 1298-1329, no large-k split 1315-1322, 3 x 300 steps each; HCP unchanged)
+_KSPLIT_FACTOR = float(os.environ.get("NMGP_KSPLIT_FACTOR", "8.0"))
 
 
 def _auto_ksplit(k_eff, group_tiles, work_per_wg):
