@@ -136,17 +136,25 @@ __global__ __launch_bounds__(256) void dsvi_trow_kernel(Args a) {
   if (r >= B) return;
   const T* Pt = (const T*)a.P + (int64_t)r * M;       // slot 0 = t
   const T* Tt = (const T*)a.T + (int64_t)r * M;       // K_t12 C_t^-T: rowsum(P o K12) = ||T_row||^2
+  const double* Tt64 = a.T64 ? (const double*)a.T64 + (int64_t)r * M : nullptr;
   const T* v = (const T*)a.v;
-  T mean = 0, q = 0;
+  T mean = 0;
+  double q = 0;                                       // (fp64 sum of fp64 T rows in fp32 engines)
   for (int c = lane; c < M; c += 64) {
-    const T tt = Tt[c];
     mean += Pt[c] * v[c];
-    q += tt * tt;
+    if (Tt64) {
+      const double tt = Tt64[c];
+      q += tt * tt;
+    } else {
+      const T tt = Tt[c];
+      q += (double)(tt * tt);
+    }
   }
   mean = wave_sum(mean);
   q = wave_sum(q);
   if (lane == 0) {
-    const T var = var_floor(hyp<T>(a, 0) - q);
+    // k11 - ||T||^2 cancels to ~ the jitter on smooth priors: formed in fp64 when T64 is given
+    const T var = var_floor((T)((double)hyp<T>(a, 0) - q));
     const T zt = ((const T*)a.noise)[M + r];
     const T tl = mean + zt * dsqrt(var + (T)a.jitter);
     ((T*)a.ellX)[r] = dexp(tl);
@@ -200,7 +208,24 @@ __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
   const T* noise = (const T*)a.noise;
 
   // ---- phase 1: column-parallel dot products
-  {
+  // (fp32 engines with T64: the three Nystrom sums in fp64 -- the variances k11 - ||T_row||^2 cancel to
+  //  ~ the jitter on smooth priors -- kept as fp64 partials in qd[] and summed by wave 0 below)
+  __shared__ double qd[4][3];
+  if (a.T64) {
+    const double* T64 = (const double*)a.T64 + (int64_t)r * M;
+    double q[3] = {0, 0, 0};
+    for (int c = t; c < M; c += 256) {
+      const double g = T64[3 * BM + c], u0 = T64[1 * BM + c], u1 = T64[2 * BM + c];
+      q[0] += g * g;
+      q[1] += u0 * u0;
+      q[2] += u1 * u1;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double v = wave_sum(q[k]);
+      if (lane == 0) qd[w][k] = v;
+    }
+  } else {
     T q[3] = {0, 0, 0};
     for (int c = t; c < M; c += 256) {
       q[0] += TG[c] * TG[c];
@@ -241,14 +266,25 @@ __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
   T Rrow = 0, epart = 0, c0p = 0, c1p = 0;
   if (w == 0) {
     auto tot = [&](int k) { return part[k] + part[K + k] + part[2 * K + k] + part[3 * K + k]; };
-    const T qG = tot(0), q0 = tot(1), q1 = tot(2);
+    // residual prior variances k11 - ||T_row||^2 (G: k11 = 1); fp64 when T64 is given
+    T rG, r0, r1;
+    if (a.T64) {
+      auto totd = [&](int k) { return qd[0][k] + qd[1][k] + qd[2][k] + qd[3][k]; };
+      rG = (T)(1.0 - totd(0));
+      r0 = (T)((double)s20 - totd(1));
+      r1 = (T)((double)s21 - totd(2));
+    } else {
+      rG = (T)1 - tot(0);
+      r0 = s20 - tot(1);
+      r1 = s21 - tot(2);
+    }
     T lm = 0, lg = 0;
     for (int u = lane; u < ns; u += 64) {
       const int s = slo + u;
       const int pi = elbo ? s : o, pj = elbo ? o : s;
       const bool diag = (s == o);
-      const T m = tot(3 + 4 * u), g = (T)1 - qG + tot(4 + 4 * u);
-      const T s2p = var_floor((diag ? s21 : s20) - (diag ? q1 : q0) + tot(6 + 4 * u));
+      const T m = tot(3 + 4 * u), g = rG + tot(4 + 4 * u);
+      const T s2p = var_floor((diag ? r1 : r0) + tot(6 + 4 * u));
       const T sd = dsqrt(s2p + lam);
       const T zz = noise[M + B + pair_noise(a, pi, pj) * B + r];
       const T smp = tot(5 + 4 * u) + zz * sd;
@@ -272,8 +308,8 @@ __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
         if (s <= o) {
           const int u = s;                      // training: slo = 0
           const bool diag = (s == o);
-          const T m = tot(3 + 4 * u), g = (T)1 - qG + tot(4 + 4 * u);
-          const T s2p = var_floor((diag ? s21 : s20) - (diag ? q1 : q0) + tot(6 + 4 * u));
+          const T m = tot(3 + 4 * u), g = rG + tot(4 + 4 * u);
+          const T s2p = var_floor((diag ? r1 : r0) + tot(6 + 4 * u));
           const T sd = dsqrt(s2p + lam);
           const T zz = noise[M + B + pair_noise(a, o, s) * B + r];
           const T smp = tot(5 + 4 * u) + zz * sd;

@@ -4,6 +4,8 @@ import pickle
 
 import numpy as np
 
+from ._dataload import load_data_pickle
+
 
 class DriverData:
     """The module-level arrays the reference drivers derive from their data pickle
@@ -23,10 +25,10 @@ class DriverData:
 
 
 def read_pickle(path):
-    """A data file in the reference layout: pickle of [X_list, Y_list, Xt_list, Yt_list] (numpy arrays).
-    Only for files the user supplies; the reference ships none."""
-    with open(path, "rb") as fh:
-        X_list, Y_list, Xt_list, Yt_list = pickle.load(fh)
+    """A data file in the reference layout: pickle of [X_list, Y_list, Xt_list, Yt_list] (numpy arrays),
+    read with the data-only loader (_dataload: the pickle is interpreted, never unpickled; anything but
+    numpy array data is refused).  Only for files the user supplies; the reference ships none."""
+    X_list, Y_list, Xt_list, Yt_list = load_data_pickle(path)
     return DriverData(X_list, Y_list, Xt_list, Yt_list)
 
 
@@ -82,5 +84,8 @@ def vtvlcm(cfg, data, M, batchsize, lr, itnum, do_inference, do_test, res_dir, i
         return tuple(out)
     if path is None:
         raise ValueError("do_inference=False reloads an earlier run's result pickle: res_dir must be given")
-    with open(path, "rb") as res:          # do_inference=False: reload the results of an earlier run
+    # do_inference=False: reload the results of an earlier run OF THIS DRIVER (it wrote the file above: whole
+    # NMGP objects and lists, as the reference's result pickles, code/NMGP_PM25.py:101-113) -- the driver's
+    # own output, not a user data file; user data goes through read_pickle's data-only loader
+    with open(path, "rb") as res:
         return tuple(pickle.load(res))

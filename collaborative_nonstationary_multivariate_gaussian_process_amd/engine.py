@@ -166,6 +166,19 @@ class DsviEngine:
         if self.prior64:
             self.pri_A64 = torch.zeros(4, M, M, dtype=F64, device=self.dev)
             self.pri_X64 = torch.zeros(4, M, M, dtype=F64, device=self.dev)
+        # fp32 engines also form the prior kernel matrices K22 / K12, the Nystrom factors T = K12 C2^-T,
+        # the projections P = T C2^-1 and the prior inverses in fp64 (rounded to fp32 only for the fp32
+        # consumers), and take the Nystrom variances k11 - ||T_row||^2 from the fp64 T: built in fp32, the
+        # entries' rounding is amplified by A^-1 (cond ~1e5-1e6 at length scales 3/M) -- the ECoG-like
+        # fixture's loss was 1.6e-3 off with fp32 projections (tests/analysis/ecog_fp32_diag.py).
+        # NMGP_PROJ_FP64=0: the round-2 fp32 projections (A/B only).
+        self.p64 = self.prior64 and os.environ.get("NMGP_PROJ_FP64", "0") != "0"
+        if self.p64:
+            z64 = lambda *s: torch.zeros(*s, dtype=F64, device=self.dev)
+            self.x64, self.hyp64, self.ellX64, self.ellZ64 = z64(B), z64(8), z64(B), z64(M)
+            self.Z64 = torch.as_tensor(np.asarray(z, np.float64).reshape(-1, 1), device=self.dev).contiguous()
+            self.K12_64, self.T64, self.P64 = z64(4, B, M), z64(4, B, M), z64(4, B, M)
+            self.Ainv64 = z64(4, M, M)
         # selection weights for the -1/2 Y diag(sel) Y^T prior adjoint (static)
         sel = np.zeros((4, self.NPC))
         for (i, j) in self.pairs:
@@ -217,6 +230,7 @@ class DsviEngine:
         for i, v in enumerate(self.scal_off):
             a.scal_off[i] = int(v)
         a.pair_q0, a.n_wfac, a.kl_v = self.q0, self.nW, 1 if self.kl_owner else 0
+        a.T64 = self.T64.data_ptr() if self.p64 else 0
         return a
 
     # ------------------------------------------------------------------------------------ plans
@@ -252,9 +266,33 @@ class DsviEngine:
         for k, hoff in [(0, hyp + 0), (1, hyp + 2), (2, hyp + 4)]:
             K12v = self.K12[k]
             bl.append(H.pairwise_desc(K12v, self.x, self.Z, mode=L.RBF, hyp=th, hyp_off=hoff, hyp_log=True))
-            bl.append(H.pairwise_desc(self.Afac[NF + k], self.Z, self.Z, mode=L.RBF, hyp=th, hyp_off=hoff,
-                                      hyp_log=True, diag_add=self.jitter))
+            if not self.p64:
+                bl.append(H.pairwise_desc(self.Afac[NF + k], self.Z, self.Z, mode=L.RBF, hyp=th, hyp_off=hoff,
+                                          hyp_log=True, diag_add=self.jitter))
         p["build_rbf"] = H.PairwiseGroup(bl, dev)
+        p64 = self.p64
+        if p64:
+            # the fp64 path of fp32 engines: K12 / K22 + lam I of the RBF priors in fp64 (K22 straight into
+            # the fp64 factor slots), from fp64 copies of x and the hyper-parameters (conv_in)
+            bl64 = []
+            for k, hoff in [(0, 0), (1, 2), (2, 4)]:
+                bl64.append(H.pairwise_desc(self.K12_64[k], self.x64, self.Z64, mode=L.RBF, hyp=self.hyp64,
+                                            hyp_off=hoff, hyp_log=True))
+                bl64.append(H.pairwise_desc(self.pri_A64[k], self.Z64, self.Z64, mode=L.RBF, hyp=self.hyp64,
+                                            hyp_off=hoff, hyp_log=True, diag_add=self.jitter))
+            p["build_rbf64"] = H.PairwiseGroup(bl64, dev)
+            G64 = lambda descs: H.GemmGroup(descs, dev, F64, seg=seg)
+            X64 = self.pri_X64
+            ainv64 = lambda k: g(self.Ainv64, X64, X64, M, M, M, (1, M, 0), (M, 1, 0), (M, 1),
+                                 flags=L.A_UPPER | L.B_LOWER, offs=(k * MM, k * MM, k * MM))
+            tproj64 = lambda k: g(self.T64, self.K12_64, X64, B, M, M, (M, 1, 0), (1, M, 0), (M, 1), flags=L.B_UPPER,
+                                  offs=(k * BM, k * MM, k * BM), **rows_all)
+            pproj64 = lambda k: g(self.P64, self.T64, X64, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), flags=L.B_LOWER,
+                                  offs=(k * BM, k * MM, k * BM), **rows_all)
+            p["inv3_64"] = G64([ainv64(k) for k in range(3)] + [tproj64(k) for k in range(3)])
+            p["proj3_64"] = G64([pproj64(k) for k in range(3)])
+            p["invG_64"] = G64([ainv64(3), tproj64(3)])
+            p["projG_64"] = G64([pproj64(3)])
         # F2: A1_f = tril(S_f) tril(S_f)^T + lam I (lower part); v on the main path, the rest on the side stream
         syrk = lambda f: g(self.Afac, th, th, M, M, M, (M, 1, 0), (1, M, 0), (M, 1),
                            flags=L.A_LOWER | L.B_UPPER | L.OUT_LOWER, diag_add=self.jitter,
@@ -274,10 +312,12 @@ class DsviEngine:
         pproj = lambda k: g(self.P, self.T, self.Cinv, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), flags=L.B_LOWER,
                             offs=(k * BM, (NF + k) * MM, k * BM), **rows_all)
         d5 += [tproj(k) for k in range(3)]
+        if p64:
+            d5 = []                       # prior inverses and T in fp64 (inv3_64)
         if not elbo_mode:
             d5.append(xs(FV))
             p["xs_side"] = G([xs(f) for f in range(FV)])
-        p["inv3"] = G(d5)
+        p["inv3"] = G(d5) if d5 else None
         if self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0":
             # HCP / ECoG shapes: the D+Q factor products are 1000s of M x M triangular products --
             # the 128x128 f32 MFMA kernel at per-factor parameter offsets instead of 64x64 grouped tiles
@@ -289,7 +329,7 @@ class DsviEngine:
                 p["xs_side"] = H.BigBatch(self.Cinv, th, self.Xs, slots, offs_f, slots, M, M, M, lda=M, ldb=M,
                                           b_kcontig=False, flags=L.A_LOWER | L.B_LOWER | L.OUT_TRIL)
         # F6: P_k = K12_k Ainv_k (k = t,0,1) ; Y_t, Y_0, Y_1
-        d6 = [pproj(k) for k in range(3)]
+        d6 = [pproj(k) for k in range(3)] if not p64 else []
         d6 += [g(self.Y, self.Ainv, th, M, 1, M, (M, 1, 0), (1, M, 0), (1, M), offs=(0, muv, D * M)),
                g(self.Y, self.Ainv, th, M, NPC, M, (M, 1, 0), (1, M, 0), (1, M), offs=(MM, muU, (D + 1) * M)),
                g(self.Y, self.Ainv, th, M, NPC, M, (M, 1, 0), (1, M, 0), (1, M),
@@ -298,15 +338,26 @@ class DsviEngine:
         # F9: Gibbs builders (K_G22 + lam I into the G prior slot, K_G12)
         # K_G22 + lam I needs only ell_Z (the v sample) and feeds chol_G on the main chain; K_G12 also needs
         # ell_X (the t-row) and is built on the second side stream beside chol_G
-        p["build_g22"] = H.PairwiseGroup([
-            H.pairwise_desc(self.Afac[NF + 3], self.Z, self.Z, mode=L.GIBBS, ellX=self.ellZ, ellZ=self.ellZ,
-                            diag_add=self.jitter)], dev)
-        p["build_g12"] = H.PairwiseGroup([
-            H.pairwise_desc(self.K12[3], self.x, self.Z, mode=L.GIBBS, ellX=self.ellX, ellZ=self.ellZ)], dev)
+        if not p64:
+            p["build_g22"] = H.PairwiseGroup([
+                H.pairwise_desc(self.Afac[NF + 3], self.Z, self.Z, mode=L.GIBBS, ellX=self.ellZ, ellZ=self.ellZ,
+                                diag_add=self.jitter)], dev)
+        else:
+            # K_G22 + lam I in fp64 from ell_Z (fp32 sample, widened), straight into the fp64 factor slot
+            p["build_g22"] = H.PairwiseGroup([
+                H.pairwise_desc(self.pri_A64[3], self.Z64, self.Z64, mode=L.GIBBS, ellX=self.ellZ64,
+                                ellZ=self.ellZ64, diag_add=self.jitter)], dev)
+        bg12 = [H.pairwise_desc(self.K12[3], self.x, self.Z, mode=L.GIBBS, ellX=self.ellX, ellZ=self.ellZ)]
+        p["build_g12"] = H.PairwiseGroup(bg12, dev)
+        if p64:
+            p["build_g12_64"] = H.PairwiseGroup([
+                H.pairwise_desc(self.K12_64[3], self.x64, self.Z64, mode=L.GIBBS, ellX=self.ellX64,
+                                ellZ=self.ellZ64)], dev)
         p["invG"] = G([g(self.Ainv, self.Cinv, self.Cinv, M, M, M, (1, M, 0), (M, 1, 0), (M, 1),
-                         flags=L.A_UPPER | L.B_LOWER, offs=((NF + 3) * MM, (NF + 3) * MM, 3 * MM)), tproj(3)])
-        p["projG"] = G([pproj(3),
-                        g(self.Y, self.Ainv, th, M, D, M, (M, 1, 0), (1, M, 0), (1, M), offs=(3 * MM, muW, 0))])
+                         flags=L.A_UPPER | L.B_LOWER, offs=((NF + 3) * MM, (NF + 3) * MM, 3 * MM)), tproj(3)]) \
+            if not p64 else None
+        p["projG"] = G(([pproj(3)] if not p64 else []) +
+                       [g(self.Y, self.Ainv, th, M, D, M, (M, 1, 0), (1, M, 0), (1, M), offs=(3 * MM, muW, 0))])
         # F14: quadratic-form factors W = P L on the rows that use them
         d14 = []
         for d in range(D):
@@ -484,13 +535,24 @@ class DsviEngine:
         self.y.copy_(torch.as_tensor(yv[order] if perm else yv).to(self.dt))
         self.seg.copy_(torch.from_numpy(seg))
         self.row_out.copy_(torch.from_numpy(row_out))
+        # kept for load_noise: later noise draws for the same batch (compute_ELBO's further samples)
+        # must be regrouped exactly like the rows
+        self._row_order = torch.from_numpy(order) if perm else None
         if noise is not None:
-            nz = torch.as_tensor(noise, dtype=F64).reshape(-1)
-            if perm:
-                M, Q = self.M, self.Q
-                o = torch.from_numpy(order)
-                nz = torch.cat([nz[:M], nz[M:M + B][o], nz[M + B:].reshape(Q, B)[:, o].reshape(-1)])
-            self.noise.copy_(nz.to(self.dt))
+            self.load_noise(noise)
+
+    def load_noise(self, noise):
+        """Copy one step's host noise (z_v (M), z_t (B), then Q x (B) pair rows, the reference's draw
+        order) into the engine, its per-row parts permuted like the rows of the batch last loaded by
+        load_batch (rows regrouped by output when `index` was not in output order)."""
+        M, B, Q = self.M, self.B, self.Q
+        nz = torch.as_tensor(noise, dtype=F64).reshape(-1)
+        if nz.numel() != M + B + Q * B:
+            raise ValueError(f"noise has {nz.numel()} values, the step draws M + B + Q*B = {M + B + Q * B}")
+        o = getattr(self, "_row_order", None)
+        if o is not None:
+            nz = torch.cat([nz[:M], nz[M:M + B][o], nz[M + B:].reshape(Q, B)[:, o].reshape(-1)])
+        self.noise.copy_(nz.to(self.dt))
 
     def bind_dataset(self, Xb, Yb, Ib, Sb, counter=None):
         """Keep an epoch of pre-split minibatches resident in HBM (Xb, Yb (nb, B) engine dtype; Ib (nb, B) int32
@@ -576,6 +638,29 @@ class DsviEngine:
         def pw(name):
             return lambda s: p[name](self.dt, s)
 
+        def pw64(name):
+            return lambda s: p[name](F64, s)
+
+        conv_up32, conv_dn64 = lib.nmgp_convert_f32_to_f64, lib.nmgp_convert_f64_to_f32
+
+        def widen(src, dst, n, src_off=0):
+            # fp32 -> fp64 copy of n elements (the fp64 path's inputs)
+            return lambda s: L.check(conv_up32(vp(src.data_ptr() + 4 * src_off), vp(dst.data_ptr()), n, s), "convert")
+
+        def conv_in(s):
+            widen(self.x, self.x64, self.B)(s)
+            widen(self._theta, self.hyp64, 7, self.offs["sigma2_tildeell_log"][0])(s)
+
+        def round_back(k0, cnt):
+            # fp64 P / prior inverses of priors k0 .. k0+cnt-1 -> the fp32 buffers the fp32 kernels read
+            def run(s):
+                BM_, MM_ = self.B * self.M, self.M * self.M
+                L.check(conv_dn64(vp(self.P64.data_ptr() + 8 * k0 * BM_), vp(self.P.data_ptr() + 4 * k0 * BM_),
+                                  cnt * BM_, s), "convert")
+                L.check(conv_dn64(vp(self.Ainv64.data_ptr() + 8 * k0 * MM_), vp(self.Ainv.data_ptr() + 4 * k0 * MM_),
+                                  cnt * MM_, s), "convert")
+            return run
+
         chol_fn = getattr(lib, "nmgp_chol_inv_batched_" + self.sfx)
 
         def chol(first, count):
@@ -592,8 +677,9 @@ class DsviEngine:
             es = self.Afac.element_size()
 
             def chol_prior(k0, cnt, v_too=False):
-                # slots NF + k0 .. NF + k0 + cnt - 1: up-convert K22 + lam I, fp64 factor + inverse, round
-                # L and L^-1 back into the fp32 slots (info as the fp32 kernel reports it)
+                # slots NF + k0 .. NF + k0 + cnt - 1: up-convert K22 + lam I (built in fp64 already with the
+                # fp64 projections), fp64 factor + inverse, round L and L^-1 back into the fp32 slots (info as
+                # the fp32 kernel reports it)
                 f32 = chol(FV, 1) if v_too else None
                 n = cnt * MM
 
@@ -601,7 +687,8 @@ class DsviEngine:
                     if f32 is not None:
                         f32(s)
                     src = vp(Af + (NF + k0) * MM * es)
-                    L.check(conv_up(src, vp(A64 + k0 * MM * 8), n, s), "convert")
+                    if not self.p64:
+                        L.check(conv_up(src, vp(A64 + k0 * MM * 8), n, s), "convert")
                     L.check(chol64(vp(A64 + k0 * MM * 8), M, M, MM, vp(X64 + k0 * MM * 8), M, MM, cnt,
                                    vp(info + (NF + k0) * 4), s), "chol_inv f64 prior")
                     L.check(conv_dn(vp(A64 + k0 * MM * 8), src, n, s), "convert")
@@ -630,6 +717,9 @@ class DsviEngine:
             steps.append(("chol_side", "chol", chol(0, FV), "side"))
             if not elbo_mode:
                 steps.append(("xs_side", "gemm", gemm("xs_side"), "side"))
+        if self.p64:
+            steps += [("conv_in", "convert", conv_in, "main"),
+                      ("build_rbf64", "pairwise", pw64("build_rbf64"), "main")]
         steps.append(("build_rbf", "pairwise", pw("build_rbf"), "main"))
         if v_on_side:
             steps.append(("wait", "main", "syrk"))
@@ -641,24 +731,44 @@ class DsviEngine:
         steps += [
             ("chol", "chol", chol_main, "main"),
             ("sig", "main", "chol"), ("wait", "side2", "chol"),
-            ("inv3", "gemm", gemm("inv3"), "side2"),
+        ]
+        if self.p64:
+            steps += [("inv3_64", "gemm", gemm("inv3_64"), "side2"),
+                      ("proj3_64", "gemm", gemm("proj3_64"), "side2"),
+                      ("conv3", "convert", round_back(0, 3), "side2")]
+        if p["inv3"] is not None:
+            steps.append(("inv3", "gemm", gemm("inv3"), "side2"))
+        steps += [
             ("proj3", "gemm", gemm("proj3"), "side2"),
             ("v", "row", row(getattr(lib, "nmgp_dsvi_hyper_" + self.sfx)), "main"),
             ("sig", "main", "v"),
-            ("build_g22", "pairwise", pw("build_g22"), "main"),
+        ]
+        if self.p64:
+            steps.append(("conv_ellZ", "convert", widen(self.ellZ, self.ellZ64, self.M), "main"))
+        steps += [
+            ("build_g22", "pairwise", (pw64 if self.p64 else pw)("build_g22"), "main"),
             ("wait", "side2", "v"),
             ("trow", "row", row(getattr(lib, "nmgp_dsvi_trow_" + self.sfx)), "side2"),
-            ("build_g12", "pairwise", pw("build_g12"), "side2"),
-            ("sig", "side2", "g12"),
         ]
+        if self.p64:
+            steps.append(("conv_ellX", "convert", widen(self.ellX, self.ellX64, self.B), "side2"))
+        steps.append(("build_g12", "pairwise", pw("build_g12"), "side2"))
+        if self.p64:
+            steps.append(("build_g12_64", "pairwise", pw64("build_g12_64"), "side2"))
+        steps.append(("sig", "side2", "g12"))
         if not elbo_mode and os.environ.get("NMGP_QUAD_SPLIT", "1") != "0":
             steps += [("quad_P", "gemm", gemm("quad_P"), "side2"), ("sig", "side2", "quadP")]
         steps += [
             ("chol_G", "chol", chol_g, "main"),
             ("wait", "main", "g12"),
-            ("invG", "gemm", gemm("invG"), "main"),
-            ("projG", "gemm", gemm("projG"), "main"),
         ]
+        if self.p64:
+            steps += [("invG_64", "gemm", gemm("invG_64"), "main"),
+                      ("projG_64", "gemm", gemm("projG_64"), "main"),
+                      ("convG", "convert", round_back(3, 1), "main")]
+        else:
+            steps.append(("invG", "gemm", gemm("invG"), "main"))
+        steps.append(("projG", "gemm", gemm("projG"), "main"))
         if os.environ.get("NMGP_SIDE2_FWD", "1") == "0":
             steps = self._remap(steps, 0, len(steps), "side2", "main")
         n_fwd = len(steps)
@@ -675,7 +785,8 @@ class DsviEngine:
                 # the RBF priors t, L0, L1 (builds, factors, inverses, projections P / T / Y), chol(Sigma_v)
                 # and the pair quadratic-form factors W_P; per sample only v, ell_X, the Gibbs prior and
                 # the latent-function factors W_G are recomputed (code/nmgp_dsvi.py:330-376)
-                skip = {"build_rbf", "syrk", "chol", "inv3", "proj3"}
+                skip = {"build_rbf", "syrk", "chol", "inv3", "proj3",
+                        "conv_in", "build_rbf64", "inv3_64", "proj3_64", "conv3"}
                 steps = [it for it in steps if not (len(it) == 4 and it[0] in skip)]
                 steps = [("quad_W",) + it[1:] if len(it) == 4 and it[0] == "quad" else it for it in steps]
                 steps = [(it[0], it[1], gemm("quad_W"), it[3]) if it[0] == "quad_W" else it for it in steps]
@@ -798,9 +909,14 @@ class DsviEngine:
         return out
 
     def _run(self, steps, stream, timer):
+        """Enqueue `steps`.  timer=None: on the four streams.  A timer with concurrent=False: serially on
+        one stream, every launch bracketed by events (isolated launch times).  concurrent=True: on the four
+        streams as in the graph, each launch bracketed by events on ITS stream (recorded after its
+        cross-stream waits), so the durations include the contention with the other streams' kernels."""
         main = stream if stream is not None else torch.cuda.current_stream(self.dev)
         s_main = ctypes.c_void_p(main.cuda_stream)
-        if timer is None:
+        conc = timer is not None and getattr(timer, "concurrent", False)
+        if timer is None or conc:
             if getattr(self, "_side", None) is None:
                 self._side = torch.cuda.Stream(device=self.dev)
                 self._side2 = torch.cuda.Stream(device=self.dev)
@@ -810,7 +926,7 @@ class DsviEngine:
         events = {}
         for item in steps:
             if item[0] in ("sig", "wait"):
-                if timer is not None:
+                if timer is not None and not conc:
                     continue                       # timed runs are serial on one stream
                 _, who, tag = item
                 st = streams[who]
@@ -825,7 +941,11 @@ class DsviEngine:
                     st.wait_event(events[tag])
                 continue
             name, kind, fn, where = item
-            if timer is not None:
+            if conc:
+                timer.start(name, kind, streams[where])
+                fn(handles[where])
+                timer.stop(name, kind, streams[where])
+            elif timer is not None:
                 timer.start(name, kind)
                 fn(s_main)
                 timer.stop(name, kind)

@@ -215,12 +215,16 @@ class NMGP(Model):
         return self.sqrt_U[i * (i + 1) // 2 + j] if self.packed else self.sqrt_U[i, j]
 
     def state_dict(self, *args, **kwargs):
-        """The reference's 13 keys with its dense shapes (code/nmgp_dsvi.py:117-155, model.pt)."""
+        """The reference's 13 keys with its dense shapes (code/nmgp_dsvi.py:117-155, model.pt).
+
+        Packed models export mu_U / sqrt_U as dense HOST tensors, unpacked output by output straight
+        from the device vector: the dense sqrt_U is 69 GB in fp32 at the ECoG shape, which must not be
+        materialised in HBM next to the model (the other keys stay device views as usual)."""
         sd = super().state_dict(*args, **kwargs)
         if self.packed:
             prefix = kwargs.get("prefix", args[1] if len(args) > 1 else "")
             for k in ("mu_U", "sqrt_U"):
-                sd[prefix + k] = _unpack_pairs(sd[prefix + k].detach(), self.D)
+                sd[prefix + k] = _unpack_pairs_host(sd[prefix + k].detach(), self.D)
         return sd
 
     def load_state_dict(self, state_dict, strict=True, assign=False):
@@ -317,7 +321,7 @@ class NMGP(Model):
             if first:
                 eng.load_batch(x, y, sizes, noise=noise, index=index)
             elif noise is not None:
-                eng.noise.copy_(noise.to(eng.dt))
+                eng.load_noise(noise)               # regrouped like the rows of the first load_batch
             if noise is None:
                 eng.device_noise(self._noise_seed, self._noise_counter)
                 H.counter_add_(self._noise_counter, 1)
@@ -351,6 +355,17 @@ def _unpack_pairs(packed, D):
     out = torch.zeros((D, D) + tuple(packed.shape[1:]), dtype=packed.dtype, device=packed.device)
     ii, jj = np.tril_indices(D)
     out[torch.from_numpy(ii).to(packed.device), torch.from_numpy(jj).to(packed.device)] = packed
+    return out
+
+
+def _unpack_pairs_host(packed, D):
+    """(Q, ...) device tensor -> (D, D, ...) host tensor with zero dead (upper) pairs, copied one output
+    row at a time (the pairs (i, 0..i) are contiguous in the packed layout), so no dense or temporary
+    copy is ever allocated on the device."""
+    out = torch.zeros((D, D) + tuple(packed.shape[1:]), dtype=packed.dtype)
+    for i in range(D):
+        q0 = i * (i + 1) // 2
+        out[i, :i + 1].copy_(packed[q0:q0 + i + 1])
     return out
 
 
@@ -876,8 +891,8 @@ def _adam_state_dict(model, trainer):
         o, shp = model._offs[name]
         n = int(np.prod(shp)) if shp else 1
         ea, eq = trainer.m[o:o + n].reshape(shp), trainer.v[o:o + n].reshape(shp)
-        if model.packed and name in ("mu_U", "sqrt_U"):      # the reference's dense shapes
-            ea, eq = _unpack_pairs(ea, model.D), _unpack_pairs(eq, model.D)
+        if model.packed and name in ("mu_U", "sqrt_U"):      # the reference's dense shapes, built on the host
+            ea, eq = _unpack_pairs_host(ea, model.D), _unpack_pairs_host(eq, model.D)
         state[idx] = {"step": torch.tensor(step), "exp_avg": ea.cpu(), "exp_avg_sq": eq.cpu()}
     return {"state": state, "param_groups": [{"lr": trainer.lr, "betas": tuple(trainer.betas), "eps": trainer.eps,
                                               "weight_decay": 0,

@@ -198,30 +198,54 @@ class PairShard:
         """The reference's dense state_dict (code/nmgp_dsvi.py:117-155 shapes, dead upper pair blocks 0)
         assembled on rank `dst` from every rank's pair window (None on the other ranks)."""
         D, M = self.D, self.M
-        mine = torch.cat([self.local("mu_U").reshape(-1), self.local("sqrt_U").reshape(-1)]).cpu()
-        if self.world > 1:
-            import torch.distributed as dist
-            parts = [None] * self.world
-            dist.all_gather_object(parts, (self.rank, mine), group=self.group)
-        else:
-            parts = [(0, mine)]
-        if self.rank != dst:
-            return None
-        sd = {}
-        for name in PARAM_NAMES:
-            if name in ("mu_U", "sqrt_U"):
+        is_dst = self.rank == dst
+        if is_dst:
+            muU = torch.zeros(D, D, M, dtype=self.dt)
+            sU = torch.zeros(D, D, M, M, dtype=self.dt)
+        for r in range(self.world):
+            if not (is_dst or self.rank == r):
                 continue
-            sd[name] = self.local(name).detach().cpu().clone()
-        muU = torch.zeros(D, D, M, dtype=self.dt)
-        sU = torch.zeros(D, D, M, M, dtype=self.dt)
-        for r, flat in sorted(parts, key=lambda t: t[0]):
             i0, i1 = self.ranges[r]
-            pr = [(i, j) for i in range(i0, i1) for j in range(i + 1)]
-            nq = len(pr)
-            mu = flat[:nq * M].view(nq, M)
-            su = flat[nq * M:].view(nq, M, M)
-            for n, (i, j) in enumerate(pr):
-                muU[i, j] = mu[n]
-                sU[i, j] = su[n]
+            if r == self.rank:
+                mu, su = self.local("mu_U").detach(), self.local("sqrt_U").detach()
+            if self.world > 1 and r != dst:
+                # point to point, only between rank r and dst, in bounded chunks (NCCL: device buffers)
+                nq = i1 * (i1 + 1) // 2 - i0 * (i0 + 1) // 2
+                if is_dst:
+                    mu, su = torch.empty(nq, M, dtype=self.dt), torch.empty(nq, M, M, dtype=self.dt)
+                for t in (mu, su):
+                    self._p2p_chunks(t.reshape(-1), r, dst)
+            if is_dst:
+                q = 0
+                for i in range(i0, i1):                  # pairs (i, 0..i) are contiguous in the window
+                    muU[i, :i + 1].copy_(mu[q:q + i + 1])
+                    sU[i, :i + 1].copy_(su[q:q + i + 1])
+                    q += i + 1
+        if not is_dst:
+            return None
+        sd = {name: self.local(name).detach().cpu().clone() for name in PARAM_NAMES if name not in ("mu_U", "sqrt_U")}
         sd["mu_U"], sd["sqrt_U"] = muU, sU
         return {k: sd[k] for k in PARAM_NAMES}
+
+    def _p2p_chunks(self, flat, src, dst, chunk=1 << 26):
+        """Send `flat` (on src: this rank's device window) to dst's host tensor `flat` in chunks of at most
+        `chunk` elements (256 MB fp32): NCCL moves device buffers, gloo host ones."""
+        import torch.distributed as dist
+        dev_comm = dist.get_backend(self.group) == "nccl"
+        # send / recv take ranks of the default group
+        g_src, g_dst = (src, dst) if self.group is None else (dist.get_global_rank(self.group, src),
+                                                               dist.get_global_rank(self.group, dst))
+        stage = None
+        for c0 in range(0, flat.numel(), chunk):
+            c1 = min(flat.numel(), c0 + chunk)
+            if self.rank == src:
+                part = flat[c0:c1]
+                dist.send(part.contiguous() if dev_comm else part.cpu(), g_dst, group=self.group)
+            else:
+                if not dev_comm:
+                    dist.recv(flat[c0:c1], g_src, group=self.group)
+                    continue
+                if stage is None:
+                    stage = torch.empty(min(chunk, flat.numel()), dtype=flat.dtype, device=self.dev)
+                dist.recv(stage[:c1 - c0], g_src, group=self.group)
+                flat[c0:c1].copy_(stage[:c1 - c0])

@@ -344,6 +344,10 @@ typedef struct nmgp_dsvi_args {
      mu_U / sqrt_U / Y / noise numbered from pair_q0; n_wfac = number of W factors in the factor list
      (D on the rank that owns KL_W, else 0); kl_v = 1 on the rank that owns KL_v                   */
   int32_t pair_q0, n_wfac, kl_v, pair_pad;
+  /* fp32 engines (round 3): (4, B, M) fp64 K12 C2^-T per prior, formed from fp64 kernel matrices and fp64
+     prior factors; when set, the Nystrom variances k11 - ||T_row||^2 are taken from it in fp64 (the fp32
+     T is not read).  NULL: use T */
+  const void* T64;
 } nmgp_dsvi_args;
 
 int nmgp_dsvi_hyper_f64(const nmgp_dsvi_args* a, hipStream_t s);      /* hyper values + v sample   */

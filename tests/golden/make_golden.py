@@ -390,6 +390,46 @@ def case_driver_hyper():
     save("driver_hyper_forward", {**pack_inputs({"N": 6000}, X_list, Y_list, z, params, noise), **out})
 
 
+def case_ecog_like():
+    """ECoG-full-shaped at a size the reference finishes on the CPU: M = 1024
+    inducing points with the ECoG configuration's length scales 3/M (code/NMGP_ECoG_full.py trains at
+    M = 1024), D = 4 outputs, B = N = 2000 rows (500 per output), NMGP(seed=22) initialisation.
+    Records (1) one forward + backward with injected noise (gradient digest) and (2) compute_ELBO over
+    the same data with 2 injected-noise samples (per-sample reconstruction terms + ELBO).  At M = 1024
+    the fp32 engine takes its large-M path: recursive chol_inv_rec, the 128x128 offsets products and
+    (with pair_layout="packed") the packed pair layout -- this fixture pins that path."""
+    D, M, sizes = 4, 1024, [500] * 4
+    N = sum(sizes)
+    rng = np.random.default_rng(41)
+    X_list = [np.sort(rng.uniform(0, 1, n))[:, None] for n in sizes]
+    Y_list = [(np.sin(6 * x + 0.7 * d) + 0.3 * rng.standard_normal(x.shape)) for d, x in enumerate(X_list)]
+    z = np.linspace(0, 1, M)
+    m = build_model(N, D, z, seed=22)
+    ls = float(np.log(3.0 / M))
+    for k in ["length_scales_tildeell_log", "length_scales_L0_log", "length_scales_L1_log"]:
+        getattr(m, k).data.fill_(ls)
+    params = model_params(m)
+    noise = forward_noise(rng, D, M, N)
+    out = run_forward(m, X_list, Y_list, noise, full=False)
+    keep = {k: v for k, v in params.items() if k not in ("sqrt_W", "sqrt_U", "sqrt_v")}
+    d = pack_inputs({"N": N}, X_list, Y_list, z, keep, noise)
+    S = 2
+    enoise = []
+    for _ in range(S):
+        enoise += forward_noise(rng, D, M, N)
+    Xt = [torch.from_numpy(x).type(DT) for x in X_list]
+    Yt = [torch.from_numpy(y).type(DT) for y in Y_list]
+    TAPE.inject(enoise)
+    with Spy() as spy, torch.no_grad():
+        elbo = m.compute_ELBO(Xt, Yt, n_sample=S)
+    TAPE.off()
+    lp = np64(spy.get("Normal_logprob"))
+    d.update({"elbo_n_sample": S, "elbo_noise": np.concatenate([np.asarray(a, np.float64).reshape(-1) for a in enoise]),
+              "elbo": np64(elbo), "elbo_logprob_per_sample": np.array(lp)})
+    print("ecog_like loss", float(out["loss"]), "elbo", float(elbo))
+    save("ecog_like_forward", {**d, **_grad_digest(out)})
+
+
 def case_elbo():
     X_list, Y_list, _, _ = toy_data("low")
     M, D, N, S = 20, 2, 200, 8

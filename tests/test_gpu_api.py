@@ -81,6 +81,27 @@ def test_compute_elbo_through_api():
     assert float(elbo) == pytest.approx(float(g["elbo"]), rel=1e-10)
 
 
+def test_compute_elbo_unsorted_index_matches_oracle():
+    """compute_ELBO(..., index=[2, 0, 1]) with 3 reference-RNG samples: the engine regroups rows by output,
+    and every sample's per-row noise (the first AND the cached later ones, engine.load_noise) must be
+    regrouped the same way; equals the oracle run with the same lists, index and noise."""
+    g = G.load("mid_forward")
+    xs, ys = G.split_lists(g)
+    order = [2, 0, 1]
+    xl, yl = [xs[k] for k in order], [ys[k] for k in order]
+    N = sum(len(x) for x in xl)
+    S, M, Q = 3, 64, 6
+    rng = np.random.default_rng(23)
+    noise = rng.standard_normal(S * (M + N + Q * N)).astype(np.float32).astype(np.float64)
+    m = _model_from(g, 3, M, N)
+    tape = O.TapeNoise(noise)
+    m._torch_noise = lambda B, n_pairs: tape(M + B + n_pairs * B)
+    elbo = m.compute_ELBO([torch.from_numpy(x) for x in xl], [torch.from_numpy(y) for y in yl], index=order,
+                          n_sample=S)
+    ref, _ = O.compute_ELBO(G.params(g), xl, yl, g["z"], N, O.TapeNoise(noise), n_sample=S, index=order)
+    assert float(elbo) == pytest.approx(float(ref), rel=1e-10)
+
+
 def test_predict_Y_matches_oracle():
     from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import predict_Y
     g = G.load("mid_forward")

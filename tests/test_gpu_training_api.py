@@ -313,6 +313,33 @@ def test_packed_pair_layout_matches_dense():
     # the packed model's dense export holds the live pairs; a dense state_dict loads into it
     ii, jj = np.tril_indices(3)
     for k in ("mu_U", "sqrt_U"):
-        assert torch.equal(mp.state_dict()[k][ii, jj], md.state_dict()[k][ii, jj])
+        assert torch.equal(mp.state_dict()[k][ii, jj].cpu(), md.state_dict()[k][ii, jj].cpu())
     mp.load_state_dict(md.state_dict())
     assert torch.equal(mp.sqrt_U.detach(), md.sqrt_U.detach()[ii, jj])
+
+
+def test_packed_export_allocates_no_device_memory():
+    """state_dict() and the Adam state export of a packed model build the reference's dense mu_U / sqrt_U
+    on the host (at the ECoG shape one dense fp32 sqrt_U is 69 GB): device memory in use is unchanged
+    across the exports, and the exported pairs equal the device's packed pairs."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import (
+        NMGP, DsviTrainer, _adam_state_dict)
+    D, M = 6, 96
+    m = NMGP(1000, D, np.linspace(0, 1, M), device="cuda:0", noise="device", pair_layout="packed",
+             dtype=torch.float32)
+    tr = DsviTrainer(m, lr=0.01)
+    tr.m.normal_()
+    torch.cuda.synchronize()
+    before = torch.cuda.memory_allocated()
+    sd = m.state_dict()
+    opt = _adam_state_dict(m, tr)
+    torch.cuda.synchronize()
+    assert torch.cuda.memory_allocated() == before
+    assert sd["sqrt_U"].device.type == "cpu" and tuple(sd["sqrt_U"].shape) == (D, D, M, M)
+    ii, jj = np.tril_indices(D)
+    assert torch.equal(sd["sqrt_U"][ii, jj], m.sqrt_U.detach().cpu())
+    assert float(sd["sqrt_U"][0, 1].abs().sum()) == 0.0
+    o, _ = m._offs["sqrt_U"]
+    ea = opt["state"][5]["exp_avg"]
+    assert tuple(ea.shape) == (D, D, M, M)
+    assert torch.equal(ea[ii, jj].reshape(-1), tr.m[o:o + ea[ii, jj].numel()].cpu())

@@ -105,3 +105,55 @@ def test_modelpt_fixture_matches_the_shipped_checkpoint():
         assert torch.equal(st["exp_avg"], sf["state"][pid]["exp_avg"])
         assert torch.equal(st["exp_avg_sq"], sf["state"][pid]["exp_avg_sq"])
         assert int(st["step"]) == int(float(sf["state"][pid]["step"]))
+
+
+# ------------------------------------------------------------------------------ driver data loader
+@pytest.mark.parametrize("protocol", [2, 3, 4, 5])
+def test_driver_data_pickle_loader_reads_numpy_lists(tmp_path, protocol):
+    """drivers._dataload reads the reference drivers' data layout ([X_list, Y_list, Xt_list, Yt_list] of
+    numpy arrays, code/NMGP_PM25.py:26-28) from pickles of every protocol without unpickling them."""
+    import pickle
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.drivers._dataload import load_data_pickle
+    rng = np.random.default_rng(protocol)
+    obj = [[rng.standard_normal((7, 1)), rng.standard_normal((5, 1)).astype(np.float32)],
+           [np.arange(6, dtype=np.int64).reshape(3, 2), np.asfortranarray(rng.standard_normal((3, 4)))],
+           [rng.standard_normal(0)], [np.array(2.5)], {"t_max": 1.5, "name": "pm25", "b": b"xy"}, (1, None, True)]
+    p = tmp_path / "d.pickle"
+    p.write_bytes(pickle.dumps(obj, protocol=protocol))
+    got = load_data_pickle(str(p))
+    for a, b in zip(got[:4], obj[:4]):
+        for x, y in zip(a, b):
+            assert x.dtype == y.dtype and x.shape == y.shape and np.array_equal(x, y)
+    assert got[4] == obj[4] and tuple(got[5]) == obj[5]
+
+
+class _Evil:
+    def __reduce__(self):
+        import os
+        return (os.system, ("echo pwned > /dev/null",))
+
+
+def test_driver_data_pickle_loader_refuses_code(tmp_path):
+    import pickle
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.drivers._dataload import load_data_pickle
+    for bad in ([np.zeros(3), _Evil()], [np.array([object()], dtype=object)]):
+        p = tmp_path / "bad.pickle"
+        p.write_bytes(pickle.dumps(bad, protocol=3))
+        with pytest.raises(ValueError):
+            load_data_pickle(str(p))
+
+
+def test_driver_data_pickle_loader_reads_reference_toy_pickle():
+    """The reference's shipped simulation pickle (build container only: skipped where the tree is absent)."""
+    import os
+    path = "/root/reference/data/simulation/sim_illustration_low_freq.pickle"
+    if not os.path.exists(path):
+        pytest.skip("reference tree not present")
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.drivers._dataload import load_data_pickle
+    obj = load_data_pickle(path)
+    assert len(obj) == 4 and all(len(l) == 2 for l in obj)
+    arrs = [a for l in obj for a in l]
+    assert all(isinstance(a, np.ndarray) and a.dtype == np.float64 and a.shape == (100, 1) for a in arrs)
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "toy_forward.npz"))
+    assert np.array_equal(np.concatenate([a.reshape(-1) for a in obj[0]]), g["x"])
+    assert np.array_equal(np.concatenate([a.reshape(-1) for a in obj[1]]), g["y"])

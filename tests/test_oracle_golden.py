@@ -46,7 +46,8 @@ def test_modelpt_known_answer_with_reference_rng():
     assert float(loss) == pytest.approx(float(g["loss"]), rel=1e-13)
 
 
-@pytest.mark.parametrize("case,D,M", [("pm25_forward", 5, 256), ("hcp_like_forward", 8, 512)])
+@pytest.mark.parametrize("case,D,M", [("pm25_forward", 5, 256), ("hcp_like_forward", 8, 512),
+                                      ("ecog_like_forward", 4, 1024)])
 def test_big_shape_digests(case, D, M):
     """Loss, per-parameter gradient norms and strided gradient samples of the PM2.5-shaped and the
     HCP-like (D=8, M=512, B=5000) reference runs."""
@@ -61,6 +62,18 @@ def test_big_shape_digests(case, D, M):
         assert np.linalg.norm(gr) == pytest.approx(float(g["gnorm_" + k]), rel=1e-8, abs=1e-300), k
         samp = gr[:: max(1, gr.size // 997)]
         assert _rel(samp, g["gsample_" + k]) <= 1e-8 or np.linalg.norm(g["gsample_" + k]) == 0, k
+
+
+def test_compute_elbo_ecog_like():
+    """The M = 1024 (ECoG length scales) fixture's 2-sample compute_ELBO."""
+    g = G.load("ecog_like_forward")
+    xs, ys = G.split_lists(g)
+    p = G.params(g, D=4, M=1024)
+    tape = O.TapeNoise(g["elbo_noise"])
+    elbo, lps = O.compute_ELBO(p, xs, ys, g["z"], float(g["N"]), tape, n_sample=int(g["elbo_n_sample"]))
+    assert tape.done()
+    assert float(elbo) == pytest.approx(float(g["elbo"]), rel=1e-11)
+    np.testing.assert_allclose(lps.numpy(), g["elbo_logprob_per_sample"], rtol=1e-11)
 
 
 def test_compute_elbo():
