@@ -190,6 +190,21 @@ def api_path(dev, xs, ys, z, epochs_device=100, epochs_torch=20):
         span = tl[-1] - tl[per_epoch - 1]
         out[noise] = {"epochs": epochs, "steps": len(tl), "it_per_s": round((len(tl) - per_epoch) / span, 2),
                       "final_loss": float(losses[-1])}
+    # the reference's published PM2.5 workload (RMSE-vs-time charts): training with predict_Y on held-out
+    # test inputs after EVERY iteration (code/nmgp_dsvi.py:865-868), 200 test points per output
+    rng = np.random.default_rng(77)
+    xt = [np.sort(rng.uniform(0, 1, 200)) for _ in range(D)]
+    yt = [rng.standard_normal(200) for _ in range(D)]
+    epochs = epochs_device // 2
+    with contextlib.redirect_stdout(io.StringIO()):
+        _, losses, rmse, tl = nmgp_dsvi.inference(xs, ys, z, B, D, hyperpars=hyper, itnum=epochs, show_ELBO=False,
+                                                  noise="device", device=dev, seed=22,
+                                                  X_test_list=[x[:, None] for x in xt], Y_test_list=[y[:, None] for y in yt])
+    per_epoch = len(tl) // epochs
+    span = tl[-1] - tl[per_epoch - 1]
+    out["device_with_predict_Y"] = {"epochs": epochs, "steps": len(tl), "test_points": D * 200,
+                                    "it_per_s": round((len(tl) - per_epoch) / span, 2),
+                                    "final_loss": float(losses[-1]), "final_test_rmse": float(rmse[-1])}
     return out
 
 

@@ -63,7 +63,9 @@ class DsviArgs(ctypes.Structure):
                 ("gib_row", c_vp), ("gib_col", c_vp), ("scal_part", c_vp), ("phi", c_vp),
                 ("info", c_vp), ("n_ct", c_int), ("n_rt", c_int), ("n_rt22", c_int), ("nblk_rows", c_int),
                 ("scal_off", c_i64 * 8), ("T", c_vp),
-                ("pair_q0", c_int), ("n_wfac", c_int), ("kl_v", c_int), ("pair_pad", c_int), ("T64", c_vp)]
+                ("pair_q0", c_int), ("n_wfac", c_int), ("kl_v", c_int), ("pair_pad", c_int), ("T64", c_vp),
+                ("kl_f0", c_int), ("kl_f1", c_int), ("v64", c_vp), ("ellZ64", c_vp), ("K12_64", c_vp),
+                ("t64", c_vp), ("scal64", c_vp)]
 
 
 # flags (include/nmgp_hip.h)

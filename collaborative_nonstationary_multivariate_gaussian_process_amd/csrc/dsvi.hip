@@ -116,8 +116,25 @@ __global__ __launch_bounds__(256) void dsvi_v_kernel(Args a) {
   const int M = a.M, lane = threadIdx.x & 63;
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= M) return;
-  const T* Cv = (const T*)a.Afac + (int64_t)(a.NF - 1) * M * M;   // C1 of the v factor (Sigma_v)
   const T* zv = (const T*)a.noise;
+  if (a.v64) {
+    // fp32 engines: the sample from the fp64 factor, in fp64 (an fp32 factor of Sigma_v + 1e-4 I left the
+    // ECoG-like fixture's compute_ELBO samples ~1e-3 off: exp(v) turns v's absolute error into relative
+    // error of every Gibbs length scale)
+    const double* Cv = (const double*)a.v64;
+    double s = 0;
+    for (int k = lane; k <= c; k += 64) s += Cv[(int64_t)c * M + k] * (double)zv[k];
+    s = wave_sum(s);
+    if (lane == 0) {
+      const double v = (double)((const T*)a.theta)[a.off_muv + c] + s;
+      const double ez = exp(v);
+      ((T*)a.v)[c] = (T)v;
+      ((T*)a.ellZ)[c] = (T)ez;
+      ((double*)a.ellZ64)[c] = ez;
+    }
+    return;
+  }
+  const T* Cv = (const T*)a.Afac + (int64_t)(a.NF - 1) * M * M;   // C1 of the v factor (Sigma_v)
   T s = 0;
   for (int k = lane; k <= c; k += 64) s += Cv[(int64_t)c * M + k] * zv[k];
   s = wave_sum(s);
@@ -431,7 +448,9 @@ __global__ __launch_bounds__(256) void dsvi_kl_kernel(Args a) {
   const T lam = (T)a.jitter;
   const T* Af = (const T*)a.Afac;
   T* fb = (T*)a.facbuf;
-  const int f = blockIdx.x, k = prior_of(a, f), slab = blockIdx.y;
+  // blocks 0 .. kl_f1 - kl_f0 - 1: the factors of the KL range; the one after them: the v factor
+  const int f = blockIdx.x < a.kl_f1 - a.kl_f0 ? a.kl_f0 + (int)blockIdx.x : NF - 1;
+  const int k = prior_of(a, f), slab = blockIdx.y;
   const int q = threadIdx.x & 15, i = slab * KL_ROWS + (threadIdx.x >> 4);
   const T* S = fac_S<T>(a, f);
   T ld1 = 0, ld2 = 0, t2 = 0, t3 = 0;
@@ -514,15 +533,30 @@ __global__ __launch_bounds__(256) void dsvi_tbwd_kernel(Args a) {
     const T zt = ((const T*)a.noise)[M + r];
     const T varbar = tbar * zt / ((T)2 * sd);
     const T* v = (const T*)a.v;
-    const T* Kt = (const T*)a.K12 + (int64_t)r * M;
-    T* Pb = (T*)a.Pbar + (int64_t)r * M;
-    for (int c = lane; c < M; c += 64) Pb[c] = tbar * v[c] - varbar * Kt[c];
+    if (a.t64) {
+      // fp32 engines: P-bar_t and varbar in fp64 from the fp64 K_t12 (the t-prior adjoints are formed
+      // in fp64 from here on); the per-4-row varbar partials below go to the fp64 workspace as well
+      const double* Kt = (const double*)a.K12_64 + (int64_t)r * M;
+      double* Pb = (double*)a.t64 + (int64_t)r * M;
+      const double tb = tbar, vb64 = varbar;
+      for (int c = lane; c < M; c += 64) Pb[c] = tb * (double)v[c] - vb64 * Kt[c];
+      if (lane == 0) ((double*)a.t64)[(int64_t)B * M + r] = vb64;
+    } else {
+      const T* Kt = (const T*)a.K12 + (int64_t)r * M;
+      T* Pb = (T*)a.Pbar + (int64_t)r * M;
+      for (int c = lane; c < M; c += 64) Pb[c] = tbar * v[c] - varbar * Kt[c];
+    }
     if (lane == 0) {
       RowBuf<T> rb{(T*)a.rowbuf, B, a.D};
       rb.tbar()[r] = tbar;
       rb.varbar()[r] = varbar;
     }
     vb = (lane == 0) ? varbar : (T)0;
+  }
+  if (a.t64) {
+    __shared__ double red64[16];
+    const double v64 = block_sum((double)vb, red64);
+    if (threadIdx.x == 0) ((double*)a.t64)[(int64_t)B * M + B + blockIdx.x] = v64;
   }
   vb = block_sum(vb, red);
   if (threadIdx.x == 0) ((T*)a.red)[(int64_t)a.nblk_rows * 4 + blockIdx.x] = vb;
@@ -676,8 +710,10 @@ __device__ inline void sum_recon_kl(const Args& a, T (&acc)[20], T* klstage) {
       T p[4] = {0, 0, 0, 0};
       for (int sl = 0; sl < nslab; ++sl)
         for (int j = 0; j < 4; ++j) p[j] += klstage[((f - fb) * nslab + sl) * 4 + j];
-      // (a rank without KL_v never launched the v factor's KL: no -M/2 constant for it either)
-      const T v = (f == NF - 1 && !a.kl_v) ? (T)0 : p[1] - p[0] + (T)0.5 * (p[2] + p[3] - (T)M);
+      // (factors outside the KL range -- and the v factor on a rank without KL_v -- were never launched:
+      //  no -M/2 constant for them either)
+      const bool on = f == NF - 1 ? a.kl_v != 0 : (f >= a.kl_f0 && f < a.kl_f1);
+      const T v = on ? p[1] - p[0] + (T)0.5 * (p[2] + p[3] - (T)M) : (T)0;
       ((T*)a.facbuf)[f] = v;                   // per-factor KL (kept for inspection)
       // static indices only: a computed index into acc[] put the whole array in scratch memory
       if (f < a.n_wfac) acc[5] += v;
@@ -784,6 +820,22 @@ __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
     }
     return;
   }
+  // fp32 engines with the fp64 t-prior adjoints (a.scal64): the t12 + t22 hyper-parameter partials and
+  // the varbar partials summed in fp64 -- their sum cancels to ~1e-7 of its terms at ECoG length scales
+  double t64s[3] = {0, 0, 0};
+  if (a.scal64) {
+    __shared__ double red64[16];
+    const double* s64 = (const double*)a.scal64;
+    const int64_t n64 = a.scal_off[6] - a.scal_off[4];
+    for (int64_t i = t; i < n64; i += blockDim.x) {
+      t64s[0] += s64[2 * i];
+      t64s[1] += s64[2 * i + 1];
+    }
+    const double* vpart = (const double*)a.t64 + (int64_t)a.B * a.M + a.B;
+    for (int64_t i = t; i < ntb; i += blockDim.x) t64s[2] += vpart[i];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) t64s[k] = block_sum(t64s[k], red64);
+  }
   // L0_12 + L0_22, L1_12 + L1_22, t12 + t22 (sigma2 / length-scale partials)
   if (threadIdx.x == 0) {
     sc[0] = acc[8] + acc[10];
@@ -805,6 +857,10 @@ __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
     T gs[7];
     gs[0] = sc[4] + hyp<T>(a, 0) * vs;   // sigma2_tildeell_log
     gs[1] = sc[5];                        // length_scales_tildeell_log
+    if (a.scal64) {
+      gs[0] = (T)(t64s[0] + exp((double)((const T*)a.theta)[a.off_hyp]) * t64s[2]);
+      gs[1] = (T)t64s[1];
+    }
     gs[2] = sc[0] + hyp<T>(a, 2) * c0;   // sigma2_L0_log
     gs[3] = sc[1];                        // length_scales_L0_log
     gs[4] = sc[2] + hyp<T>(a, 4) * c1;   // sigma2_L1_log
@@ -1072,7 +1128,9 @@ template <typename T> static int dsvi_recon(const Args* a, hipStream_t s) {
 }
 template <typename T> static int dsvi_kl(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
-  const int nf = a->NF - (a->kl_v ? 0 : 1);       // the v factor is last: a rank without KL_v skips it
+  // the factors of the KL range, then the v factor (last in the factor list) unless this rank has no KL_v
+  if (a->kl_f0 < 0 || a->kl_f1 > a->NF - 1 || a->kl_f0 > a->kl_f1) return -1;
+  const int nf = a->kl_f1 - a->kl_f0 + (a->kl_v ? 1 : 0);
   if (nf <= 0) return NMGP_OK;
   hipLaunchKernelGGL(dsvi_kl_kernel<T>, dim3(nf, (a->M + KL_ROWS - 1) / KL_ROWS), dim3(256), 0, s, *a);
   NMGP_CHECK_LAUNCH();

@@ -9,8 +9,9 @@ Two independent axes:
   -(N/(W b)) sum_r R_r + KL: the gradient of the global-batch objective (bit-for-bit up to the
   reduction order when the ranks share z_v and the row noise of the global batch).
 * **Monte-Carlo samples** (`compute_ELBO`, code/nmgp_dsvi.py:330-380): rank r evaluates samples
-  r, r+W, ...; one all-reduce of [sum_s R_s, KL] where only the rank owning the LAST sample
-  contributes the KL terms (the reference evaluates KL with the last sample's K_G22, :385).
+  r, r+W, ...; the KL terms are split over the ranks too (kl_shares: the pairs' KL_U by factor range,
+  KL_W and KL_v on the rank owning the LAST sample -- the reference evaluates KL with the last sample's
+  K_G22, :385); one all-reduce of [sum_s R_s, KL share].
 
 Backend-neutral (`nccl` = RCCL on the GPU box, `gloo` in the CPU tests); uses SUM + divide
 rather than ReduceOp.AVG, which gloo does not implement.
@@ -67,12 +68,35 @@ def last_sample_owner(n_sample, world):
     return (int(n_sample) - 1) % int(world)
 
 
+def kl_shares(n_w, n_pairs, world, owner):
+    """compute_ELBO's KL terms split over the ranks: the variational factors are W_0..W_{n_w-1} then the
+    n_pairs coefficient pairs (the engine's factor list, Sigma_v separate).  Returns, per rank, the
+    factor range [f0, f1) and whether it adds KL_v.  The W factors need the LAST sample's K_G22
+    (the reference evaluates KL_W with it, code/nmgp_dsvi.py:385), so they -- and KL_v -- go to the
+    rank that owns the last sample (`owner`); the pairs (KL_U: sample-independent, ~all the work at
+    the ECoG shape) are split so that every rank carries about (n_w + n_pairs + 1) / world factors.
+    The ranges tile [0, n_w + n_pairs) exactly once."""
+    n = n_w + n_pairs
+    shares = [None] * world
+    # chunk c of a near-even split of the n + 1 factors (v counted as the owner's) goes to rank owner + c
+    tot = n + 1
+    bounds = [min(n, (c * tot) // world) for c in range(world + 1)]
+    bounds[0], bounds[world] = 0, n
+    # the owner's chunk must cover the W factors
+    bounds[1] = max(bounds[1], min(n, n_w))
+    for c in range(2, world + 1):
+        bounds[c] = max(bounds[c], bounds[c - 1])
+    for c in range(world):
+        shares[(owner + c) % world] = (bounds[c], bounds[c + 1], c == 0)
+    return shares
+
+
 def combine_elbo(r_sum, kl, n_sample, group=None, device=None, dtype=torch.float64):
     """ELBO = (1/n) sum_s R_s - KL from per-rank partials.
 
     r_sum: this rank's sum of reconstruction terms over its samples (0-d tensor or float);
-    kl:    KL_W + KL_v + KL_U evaluated with the last sample's K_G22 on its owner rank, None on
-           the other ranks.  Returns a 0-d tensor on `device` (identical on every rank).
+    kl:    this rank's share of KL_W + KL_v + KL_U (kl_shares; KL_W with the last sample's K_G22, on its
+           owner), or None.  Returns a 0-d tensor on `device` (identical on every rank).
     """
     rank, world = world_info(group)
     dev = device if device is not None else (r_sum.device if torch.is_tensor(r_sum) else "cpu")

@@ -163,22 +163,35 @@ class DsviEngine:
         # ~cond(K22) * eps32 (HCP-like fixture: P_G off by 40% with an fp32 factorization, 5e-4 with
         # an fp64 one -- DESIGN.md §5).  NMGP_PRIOR_FP64=0 turns it off (A/B only).
         self.prior64 = dtype == F32 and os.environ.get("NMGP_PRIOR_FP64", "1") != "0"
+        self.p64 = self.prior64 and os.environ.get("NMGP_PROJ_FP64", "0") != "0"
         if self.prior64:
-            self.pri_A64 = torch.zeros(4, M, M, dtype=F64, device=self.dev)
-            self.pri_X64 = torch.zeros(4, M, M, dtype=F64, device=self.dev)
+            # with p64 a fifth fp64 slot in front holds Sigma_v + 1e-4 I: [v | t | L0 | L1 | G] is then
+            # one contiguous batch whose first four slots factor in one launch, like the fp32 slots
+            # FV .. FV + 3 (v, t, L0, L1) they are rounded back into
+            nsl = 5 if self.p64 else 4
+            rawA = torch.zeros(nsl, M, M, dtype=F64, device=self.dev)
+            rawX = torch.zeros(nsl, M, M, dtype=F64, device=self.dev)
+            self.pri_A64, self.pri_X64 = rawA[nsl - 4:], rawX[nsl - 4:]
+            self.v_A64, self.v_X64 = (rawA[0], rawX[0]) if self.p64 else (None, None)
         # fp32 engines also form the prior kernel matrices K22 / K12, the Nystrom factors T = K12 C2^-T,
         # the projections P = T C2^-1 and the prior inverses in fp64 (rounded to fp32 only for the fp32
         # consumers), and take the Nystrom variances k11 - ||T_row||^2 from the fp64 T: built in fp32, the
         # entries' rounding is amplified by A^-1 (cond ~1e5-1e6 at length scales 3/M) -- the ECoG-like
         # fixture's loss was 1.6e-3 off with fp32 projections (tests/analysis/ecog_fp32_diag.py).
         # NMGP_PROJ_FP64=0: the round-2 fp32 projections (A/B only).
-        self.p64 = self.prior64 and os.environ.get("NMGP_PROJ_FP64", "0") != "0"
         if self.p64:
             z64 = lambda *s: torch.zeros(*s, dtype=F64, device=self.dev)
             self.x64, self.hyp64, self.ellX64, self.ellZ64 = z64(B), z64(8), z64(B), z64(M)
             self.Z64 = torch.as_tensor(np.asarray(z, np.float64).reshape(-1, 1), device=self.dev).contiguous()
             self.K12_64, self.T64, self.P64 = z64(4, B, M), z64(4, B, M), z64(4, B, M)
             self.Ainv64 = z64(4, M, M)
+            # the v sample in fp64: sqrt_v / mu_v widened, Sigma_v + 1e-4 I formed and factored in fp64
+            self.sv64, self.muv64 = z64(M * M), z64(M)
+            # the t-prior adjoints in fp64: P-bar_t | varbar | varbar partials (t-row
+            # backward), R_t, A-bar_t, the KL_v parts' delta_t | Y_t, and the t12 / t22 builder partials
+            self.t64 = z64(B * M + B + (B + 3) // 4)
+            self.Rt64, self.Abt64, self.dY64 = z64(B, M), z64(M, M), z64(2 * M)
+            self.scal64 = z64(2 * int(self.scal_off[6] - self.scal_off[4]))
         # selection weights for the -1/2 Y diag(sel) Y^T prior adjoint (static)
         sel = np.zeros((4, self.NPC))
         for (i, j) in self.pairs:
@@ -187,6 +200,7 @@ class DsviEngine:
         self.facbuf[base:base + 4 * self.NPC] = torch.from_numpy(sel.reshape(-1)).to(self.dev)
         self._theta = None
         self._plans = {}
+        self._elbo_kl = None      # (f0, f1, with_v): compute_ELBO KL share (None: the whole model's)
 
     def pidx(self, i, j):
         """Block index of coefficient pair (i, j) in mu_U / sqrt_U (dense i*D + j, or packed)."""
@@ -231,12 +245,21 @@ class DsviEngine:
             a.scal_off[i] = int(v)
         a.pair_q0, a.n_wfac, a.kl_v = self.q0, self.nW, 1 if self.kl_owner else 0
         a.T64 = self.T64.data_ptr() if self.p64 else 0
+        if self.p64:
+            a.v64, a.ellZ64, a.K12_64 = self.v_A64.data_ptr(), self.ellZ64.data_ptr(), self.K12_64.data_ptr()
+            a.t64, a.scal64 = self.t64.data_ptr(), self.scal64.data_ptr()
+        a.kl_f0, a.kl_f1 = 0, self.NF - 1
+        kp = self._elbo_kl if elbo_mode else None
+        if kp is not None:                       # this rank's share of compute_ELBO's KL terms
+            a.kl_f0, a.kl_f1 = kp[0], kp[1]
+            a.kl_v = 1 if (kp[2] and self.kl_owner) else 0
         return a
 
     # ------------------------------------------------------------------------------------ plans
     def _plan(self, elbo_mode):
-        if elbo_mode in self._plans:
-            return self._plans[elbo_mode]
+        key = (elbo_mode, self._elbo_kl if elbo_mode else None)
+        if key in self._plans:
+            return self._plans[key]
         D, M, B, NF, Q = self.D, self.M, self.B, self.NF, self.Q
         MM, BM = M * M, B * M
         th, gr = self._theta, self._grad
@@ -300,7 +323,14 @@ class DsviEngine:
         xs = lambda f: g(self.Xs, self.Cinv, th, M, M, M, (M, 1, 0), (M, 1, 0), (M, 1),
                          flags=L.A_LOWER | L.B_LOWER | L.OUT_TRIL, offs=(f * MM, fac_off[f], f * MM))
         p["syrk"] = G([syrk(FV)])
-        p["syrk_side"] = G([syrk(f) for f in range(FV)])
+        if self.p64:
+            p["syrk"] = H.GemmGroup([g(self.v_A64, self.sv64, self.sv64, M, M, M, (M, 1, 0), (1, M, 0), (M, 1),
+                                       flags=L.A_LOWER | L.B_UPPER | L.OUT_LOWER, diag_add=self.jitter,
+                                       offs=(0, 0, 0))], dev, F64, seg=seg)
+        # the side factors: all W / pair factors, or in compute_ELBO this rank's KL share of them
+        kf0, kf1 = (self._elbo_kl[0], self._elbo_kl[1]) if (elbo_mode and self._elbo_kl is not None) else (0, FV)
+        p["kl_range"] = (kf0, kf1)
+        p["syrk_side"] = G([syrk(f) for f in range(kf0, kf1)]) if kf1 > kf0 else None
         p["syrk_all"] = G([syrk(f) for f in range(FV + 1)])   # training step: Sigma_v with the others
         # F5: prior inverses t,0,1 and Xs_f = Cinv_f L_f (KL gradient)
         d5 = [g(self.Ainv, self.Cinv, self.Cinv, M, M, M, (1, M, 0), (M, 1, 0), (M, 1), flags=L.A_UPPER | L.B_LOWER,
@@ -322,9 +352,10 @@ class DsviEngine:
             # HCP / ECoG shapes: the D+Q factor products are 1000s of M x M triangular products --
             # the 128x128 f32 MFMA kernel at per-factor parameter offsets instead of 64x64 grouped tiles
             offs_f, slots = fac_off[:FV], [f * MM for f in range(FV)]
-            p["syrk_side"] = H.BigBatch(th, th, self.Afac, offs_f, offs_f, slots, M, M, M, lda=M, ldb=M,
-                                        b_kcontig=True, flags=L.A_LOWER | L.B_UPPER | L.OUT_LOWER,
-                                        diag_add=self.jitter)
+            if kf1 > kf0:
+                p["syrk_side"] = H.BigBatch(th, th, self.Afac, offs_f[kf0:kf1], offs_f[kf0:kf1], slots[kf0:kf1], M, M,
+                                            M, lda=M, ldb=M, b_kcontig=True, flags=L.A_LOWER | L.B_UPPER | L.OUT_LOWER,
+                                            diag_add=self.jitter)
             if not elbo_mode:
                 p["xs_side"] = H.BigBatch(self.Cinv, th, self.Xs, slots, offs_f, slots, M, M, M, lda=M, ldb=M,
                                           b_kcontig=False, flags=L.A_LOWER | L.B_LOWER | L.OUT_TRIL)
@@ -380,7 +411,7 @@ class DsviEngine:
             # on the sample (the L priors and Sigma_U are fixed within a call) -- only the D latent ones
             p["quad_W"] = G(d14[:D])
         if elbo_mode:
-            self._plans[elbo_mode] = p
+            self._plans[key] = p
             return p
         # B2: P-bar += W-hat L^T ; L-bar = P^T W-hat ; mu-bar = P^T adjoints
         # rows of output i: P-bar_G += sum_{d <= i} W-hat_d L_d^T (W-hat_d holds only the rows of outputs
@@ -442,8 +473,18 @@ class DsviEngine:
         # quad / recon (see _schedule)
         p["bwd_R"] = G(d18[:1])          # R_G: the main chain (Gibbs builder backward -> t chain)
         p["bwd_R_L"] = G(d18[1:3])       # R_0, R_1: only the L0/L1 hyper-parameter gradients need them
-        p["kl_abar"] = G(d18[3:7])
+        p["kl_abar"] = G(d18[4:7] if p64 else d18[3:7])      # (p64: the t prior's below, in fp64)
         p["kl_lbar"] = G(d18[7:])
+        if p64:
+            X64 = self.pri_X64
+            G64 = lambda descs: H.GemmGroup(descs, dev, F64, seg=seg)
+            # A-bar_t = C_t^-T diag(delta_t) C_t^-1 and Y_t = A_t^-1 mu_v in fp64, then -1/2 Y_t Y_t^T
+            p["kl_t64a"] = G64([g(self.Abt64, X64, X64, M, M, M, (1, M, 0), (M, 1, 0), (M, 1),
+                                  flags=L.A_UPPER | L.B_LOWER, kscale=(self.dY64, 0), offs=(0, 0, 0)),
+                                g(self.dY64, self.Ainv64, self.muv64, M, 1, M, (M, 1, 0), (1, M, 0), (1, M),
+                                  offs=(0, 0, M))])
+            p["kl_t64b"] = G64([g(self.Abt64, self.dY64, self.dY64, M, M, 1, (1, M, 0), (M, 1, 0), (M, 1),
+                                  alpha=-0.5, beta=1.0, offs=(M, M, 0))]) if self.kl_owner else None
         if self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0":
             # KL L-bar of all NF factors: -C_f^-T Xs_f + diag(1/C_ii^2) L_f on the 128x128 kernel
             slots = [f * MM for f in range(NFK)]
@@ -458,8 +499,8 @@ class DsviEngine:
         sel_base = NF + 8 * M
         d19 = []
         for k in range(4):
-            if (k == 0 and not self.kl_owner) or (k == 3 and nW == 0):
-                continue                          # KL_v / KL_W belong to another rank
+            if (k == 0 and (not self.kl_owner or p64)) or (k == 3 and nW == 0):
+                continue                          # KL_v / KL_W belong to another rank (p64: KL_v's in fp64)
             ks = (fb, sel_base + k * NPC) if k in (1, 2) else None
             d19.append(g(self.Abar, self.Y, self.Y, M, M, ncol[k], (1, M, 0), (M, 1, 0), (M, 1), alpha=-0.5,
                          beta=1.0, kscale=ks, offs=(ybase[k], ybase[k], k * MM)))
@@ -504,12 +545,29 @@ class DsviEngine:
                                 scal_part=self.scal_part, offs=(0, 0, 0, 0, 0, 2 * int(so[4]))),
             H.pairwise_bwd_desc(self.Z, self.Z, None, self.Abar, mode=L.RBF, ld=M, hyp=th, hyp_off=hyp,
                                 hyp_log=True, scal_part=self.scal_part, offs=(0, 0, 0, 0, 0, 2 * int(so[5])))], dev)
+        if p64:
+            # the t-prior chain in fp64 from the t-row backward's fp64 P-bar_t / varbar: R_t = P-bar_t A_t^-1,
+            # A-bar_t -= P_t^T R_t, builder backward (K_t12 - P_t K_t22 cancels to ~1e-4 P_t: the
+            # sigma2 / length-scale partials of the t prior lost all digits in fp32 at ECoG length scales)
+            G64 = lambda descs: H.GemmGroup(descs, dev, F64, seg=seg)
+            p["bwd_t1"] = G64([g(self.Rt64, self.t64, self.Ainv64, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1),
+                                 offs=(0, 0, 0), **rows_all)])
+            p["bwd_t2"] = G64([g(self.Abt64, self.P64, self.Rt64, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), alpha=-1.0,
+                                 beta=1.0, offs=(0, 0, 0), k_seg=0, seg_span=D)])
+            ntb12 = int(so[5] - so[4])
+            p["bwd_tbuild"] = H.PairwiseBwdGroup([
+                H.pairwise_bwd_desc(self.x64, self.Z64, self.K12_64, self.Rt64, mode=L.RBF, ld=M, Pm=self.P64,
+                                    rowcoef=(self.t64, B * M), hyp=self.hyp64, hyp_off=0, hyp_log=True,
+                                    scal_part=self.scal64, offs=(0, 0, 0, 0, 0, 0)),
+                H.pairwise_bwd_desc(self.Z64, self.Z64, None, self.Abt64, mode=L.RBF, ld=M, hyp=self.hyp64,
+                                    hyp_off=0, hyp_log=True, scal_part=self.scal64,
+                                    offs=(0, 0, 0, 0, 0, 2 * ntb12))], dev)
         # B9: v Cholesky backward: grad_sv += Cinv_v^T (Psi Xs_v)
         p["bwd_v1"] = G([g(self.T2, self.phi, self.Xs, M, M, M, (M, 1, 0), (M, 1, 0), (M, 1), flags=L.B_LOWER,
                            offs=(0, FV * MM, 0))])
         p["bwd_v2"] = G([g(gr, self.Cinv, self.T2, M, M, M, (1, M, 0), (M, 1, 0), (M, 1),
                            flags=L.A_UPPER | L.OUT_TRIL, beta=1.0, offs=(FV * MM, 0, sv))])
-        self._plans[elbo_mode] = p
+        self._plans[key] = p
         return p
 
     # ------------------------------------------------------------------------------------ data
@@ -650,6 +708,8 @@ class DsviEngine:
         def conv_in(s):
             widen(self.x, self.x64, self.B)(s)
             widen(self._theta, self.hyp64, 7, self.offs["sigma2_tildeell_log"][0])(s)
+            widen(self._theta, self.sv64, MM, self.offs["sqrt_v"][0])(s)
+            widen(self._theta, self.muv64, M, self.offs["mu_v"][0])(s)
 
         def round_back(k0, cnt):
             # fp64 P / prior inverses of priors k0 .. k0+cnt-1 -> the fp32 buffers the fp32 kernels read
@@ -680,6 +740,16 @@ class DsviEngine:
                 # slots NF + k0 .. NF + k0 + cnt - 1: up-convert K22 + lam I (built in fp64 already with the
                 # fp64 projections), fp64 factor + inverse, round L and L^-1 back into the fp32 slots (info as
                 # the fp32 kernel reports it)
+                if v_too and self.p64:
+                    # Sigma_v + lam I (fp64 syrk) and the three RBF priors: one fp64 batch of 4 from slot FV
+                    VA, VX, n4 = self.v_A64.data_ptr(), self.v_X64.data_ptr(), 4 * MM
+
+                    def run4(s):
+                        L.check(chol64(vp(VA), M, M, MM, vp(VX), M, MM, 4, vp(info + FV * 4), s),
+                                "chol_inv f64 prior")
+                        L.check(conv_dn(vp(VA), vp(Af + FV * MM * es), n4, s), "convert")
+                        L.check(conv_dn(vp(VX), vp(Ci + FV * MM * es), n4, s), "convert")
+                    return run4
                 f32 = chol(FV, 1) if v_too else None
                 n = cnt * MM
 
@@ -698,7 +768,8 @@ class DsviEngine:
         else:
             chol_main, chol_g = chol(FV, 4), chol(NF + 3, 1)
 
-        need_side = (not elbo_mode) or with_kl
+        kf0, kf1 = p["kl_range"]
+        need_side = (not elbo_mode) or (with_kl and kf1 > kf0)
         steps = []
         # (fp64 engines only: in fp32 Sigma_v's summation order shows through ell_Z = exp(v), so fp32
         # engines keep forming it exactly as the reference-checked grouped single launch does)
@@ -714,7 +785,7 @@ class DsviEngine:
                 steps.append(("syrk_side", "gemm", gemm("syrk_side"), "side"))
             if pre_planned:
                 steps += [("plans", "gemm_plan", plans, "side"), ("sig", "side", "plans")]
-            steps.append(("chol_side", "chol", chol(0, FV), "side"))
+            steps.append(("chol_side", "chol", chol(kf0, kf1 - kf0), "side"))
             if not elbo_mode:
                 steps.append(("xs_side", "gemm", gemm("xs_side"), "side"))
         if self.p64:
@@ -743,8 +814,6 @@ class DsviEngine:
             ("v", "row", row(getattr(lib, "nmgp_dsvi_hyper_" + self.sfx)), "main"),
             ("sig", "main", "v"),
         ]
-        if self.p64:
-            steps.append(("conv_ellZ", "convert", widen(self.ellZ, self.ellZ64, self.M), "main"))
         steps += [
             ("build_g22", "pairwise", (pw64 if self.p64 else pw)("build_g22"), "main"),
             ("wait", "side2", "v"),
@@ -799,6 +868,13 @@ class DsviEngine:
             ("sig", "main", "kl_in"), ("wait", "side", "kl_in"),
             ("kl", "row", row(getattr(lib, "nmgp_dsvi_kl_" + self.sfx)), "side"),
             ("delta", "row", row(getattr(lib, "nmgp_dsvi_delta_" + self.sfx)), "side"),
+        ]
+        if self.p64:
+            steps += [("conv_d64", "convert", widen(self.facbuf, self.dY64, M, NF), "side"),
+                      ("kl_t64a", "gemm", gemm("kl_t64a"), "side")]
+            if p["kl_t64b"] is not None:
+                steps.append(("kl_t64b", "gemm", gemm("kl_t64b"), "side"))
+        steps += [
             ("kl_lbar", "gemm", gemm("kl_lbar"), "side"),
             ("sig", "side", "kl_lbar"),
             ("kl_abar", "gemm", gemm("kl_abar"), "side"),
@@ -885,7 +961,7 @@ class DsviEngine:
             ("sig", "side", "v_done"),
             ("bwd_t1", "gemm", gemm("bwd_t1"), "main"),
             ("bwd_t2", "gemm", gemm("bwd_t2"), "main"),
-            ("bwd_tbuild", "pairwise_bwd", pw("bwd_tbuild"), "main"),
+            ("bwd_tbuild", "pairwise_bwd", (pw64 if self.p64 else pw)("bwd_tbuild"), "main"),
             ("wait", "main", "v_done"),
             ("wait", "main", "lbar_done"),
             ("wait", "main", "L_done"),
@@ -963,12 +1039,16 @@ class DsviEngine:
         self._run(self._sched, stream, timer)
         return self.out
 
-    def elbo_sample(self, stream=None, with_kl=False, cached=False):
+    def elbo_sample(self, stream=None, with_kl=False, cached=False, kl_part=None):
         """Enqueue one Monte-Carlo sample of compute_ELBO's reconstruction term (self.out[1]);
         with_kl also evaluates the KL terms from THIS sample's K_G22 (out[2..4]).  cached: reuse the
         sample-independent factors of the previous (uncached) sample of the same call -- parameters,
-        data and the factor workspace must be unchanged since then."""
-        key = ("elbo", with_kl, cached, self._theta.data_ptr(), self.frozen_mask, self.N)
+        data and the factor workspace must be unchanged since then.  kl_part=(f0, f1, with_v): only
+        the KL terms of the variational factors f0 .. f1-1 of the W | pairs list (and of Sigma_v when
+        with_v) -- a rank's share of the KL when compute_ELBO is sharded (W factors need THIS sample's
+        K_G22: only the owner of the last sample may include them)."""
+        self._elbo_kl = None if kl_part is None else (int(kl_part[0]), int(kl_part[1]), bool(kl_part[2]))
+        key = ("elbo", with_kl, cached, self._theta.data_ptr(), self.frozen_mask, self.N, self._elbo_kl)
         cache = getattr(self, "_elbo_sched", {})
         if key not in cache:
             cache[key] = self._schedule(1, with_kl, cached)

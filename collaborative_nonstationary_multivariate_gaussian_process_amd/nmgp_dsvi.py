@@ -174,6 +174,7 @@ class NMGP(Model):
             setattr(self, k, Parameter(view))
             self._grad_views.append(self._grad[o:o + cnt].view(shp))
         self._engines = {}
+        self._pending_info = []
         self._batch = None
         self._noise_seed = seed
         self._noise_counter = torch.zeros(1, dtype=torch.int64, device=self.device_)
@@ -245,6 +246,9 @@ class NMGP(Model):
         Lb.check_device_status()
         for eng in (engines if engines is not None else self._engines.values()):
             eng.check_info()
+        pend, self._pending_info = getattr(self, "_pending_info", []), []
+        if pend and int(torch.cat(pend).abs().max().cpu()) != 0:   # deferred predict_Y Cholesky checks
+            raise torch.linalg.LinAlgError("cholesky: K22 + 1e-4 I is not positive-definite (predict_Y)")
 
     def engine(self, B, N=None):
         eng = self._engines.get(B)
@@ -310,6 +314,12 @@ class NMGP(Model):
         rank, world = DD.world_info(group) if distributed else (0, 1)
         out, kl = None, None
         first = True
+        # the KL terms: on one process with the last sample; sharded, every rank adds a factor range
+        # with its own last sample (KL_W / KL_v on the owner of the global last sample, DD.kl_shares)
+        my_last = max([s for s in range(n_sample) if s % world == rank], default=-1)
+        kl_part = None
+        if world > 1 and n_sample >= world:
+            kl_part = DD.kl_shares(eng.nW, eng.Q, world, DD.last_sample_owner(n_sample, world))[rank]
         for s in range(n_sample):
             if verbose:
                 print("Monte Carlo index:", s)
@@ -327,10 +337,11 @@ class NMGP(Model):
                 H.counter_add_(self._noise_counter, 1)
             # the first sample of this rank computes everything; later ones reuse the sample-independent
             # RBF-prior factors and pair quadratic forms (engine.elbo_sample(cached=True))
-            out = eng.elbo_sample(with_kl=(s == n_sample - 1), cached=not first)
+            with_kl = (s == my_last) if kl_part is not None else (s == n_sample - 1)
+            out = eng.elbo_sample(with_kl=with_kl, cached=not first, kl_part=kl_part if with_kl else None)
             first = False
             acc += out[1]
-            if s == n_sample - 1:
+            if with_kl:
                 kl = out[2] + out[3] + out[4]
         if out is not None:
             self.check_numerics([eng])
@@ -758,8 +769,18 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
         gen.manual_seed(int(seed) + 0x5eed)
     N_train = X_train_vec.shape[0]
     if X_test_list is not None:
-        rmse_test_list = []
+        # per-iteration predict_Y (code/nmgp_dsvi.py:865-868) on the device: test inputs uploaded once, the
+        # RMSE kept on the device (the reference's broadcast est[:, None] - Y_test_vec included) and read
+        # back after the loop, the predictions' Cholesky checks deferred to the loop's check points
+        from . import predict as _pred
+        rmse_dev = []
         Y_test_vec = np.concatenate(Y_test_list)
+        test_prep = _pred.prepare_inputs(model, [np.asarray(x, np.float64) for x in X_test_list])
+        Y_test_dev = torch.as_tensor(np.asarray(Y_test_vec, np.float64)).to(model.device_)
+
+        def _test_rmse():
+            est = _pred.predict_mean(model, None, prepared=test_prep, defer_check=True)
+            rmse_dev.append(torch.sqrt(torch.mean((est[:, None] - Y_test_dev) ** 2)))
     Q = dim_outputs * (dim_outputs + 1) // 2
     pipe = None
     if noise == "device":
@@ -805,8 +826,7 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
                 if check_every and nstep % check_every == 0:
                     _sync_check()
                 if X_test_list is not None:
-                    est = predict_Y(model, X_test_list)
-                    rmse_test_list.append(np.sqrt(np.mean((est[:, None] - Y_test_vec) ** 2)))
+                    _test_rmse()
                 if verbose:
                     print("epoch: {}/{}, batch: {}/{}, loss: {}".format(epoch, itnum, batch, N_train / batch_size,
                                                                        float(losses_dev[-1])))
@@ -837,8 +857,7 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
                 time_list.append(time.time() - ts)
                 nstep += 1
                 if X_test_list is not None:
-                    est = predict_Y(model, X_test_list)
-                    rmse_test_list.append(np.sqrt(np.mean((est[:, None] - Y_test_vec) ** 2)))
+                    _test_rmse()
                 if verbose:
                     print("epoch: {}/{}, batch: {}/{}, loss: {}".format(epoch, itnum, batch, N_train / batch_size,
                                                                        float(loss)))
@@ -873,6 +892,7 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
         print("epoch: {}, ELBO: {}".format(epoch + 1, float(elbo)))
         print(print_mem(epoch + 1))
     if X_test_list is not None:
+        rmse_test_list = [np.float64(v) for v in torch.stack(rmse_dev).cpu().numpy()] if rmse_dev else []
         return model, loss_list, rmse_test_list, time_list
     return model, loss_list, time_list
 

@@ -15,52 +15,73 @@ F64 = torch.float64
 JIT = 1e-4
 
 
-def _solve_rows(K12, K22, rhs):
-    """K12 (K22 + 1e-4 I)^{-1} rhs  for rhs (M, k): Cholesky -> inverse -> two GEMMs."""
+def _solve_rows(K12, K22, rhs, infos):
+    """K12 (K22 + 1e-4 I)^{-1} rhs  for rhs (M, k): Cholesky -> inverse -> two GEMMs.  The Cholesky
+    info word is appended to `infos` (checked by the caller: no host synchronisation here)."""
     A = K22.clone()
     A.diagonal().add_(JIT)
     Ci, info = H.chol_inv_(A)
-    if int(info.cpu()[0]) != 0:
-        raise torch.linalg.LinAlgError("cholesky: K22 + 1e-4 I is not positive-definite")
+    infos.append(info)
     Ainv = H.matmul(Ci, Ci, transA=True, maskA=L.A_UPPER, maskB=L.B_LOWER)
     return H.matmul(K12, H.matmul(Ainv, rhs))
 
 
-def predict_mean(model, inputs_list, index=None):
+def prepare_inputs(model, inputs_list, index=None):
+    """Device copies of the prediction inputs (x as a column, the output id of every row): made once
+    when the same test inputs are predicted every iteration (inference(X_test_list=...))."""
     dev = model.device_
-    D, M = model.D, model.M
     xs = [torch.as_tensor(x).reshape(-1).to(F64) for x in inputs_list]
     ids = list(range(len(xs))) if index is None else list(index)
     I = torch.cat([torch.full((x.shape[0],), int(j), dtype=torch.long) for x, j in zip(xs, ids)]).to(dev)
-    x = torch.cat(xs).to(dev).reshape(-1, 1).contiguous()
+    x = torch.cat([t.to(dev) for t in xs]).reshape(-1, 1).contiguous()
+    return x, I
+
+
+def _rbf(model, hyp64, a, b, k):
+    """RBF kernel of prior k (0: tilde-ell, 1: L0, 2: L1) with its hyper-parameters read ON THE DEVICE
+    (log scale, from the fp64 copy of theta's 7 hyper-parameters): no host round trip."""
+    out = torch.empty(a.shape[0], b.shape[0], dtype=F64, device=a.device)
+    H.PairwiseGroup([H.pairwise_desc(out, a, b, mode=L.RBF, hyp=hyp64, hyp_off=2 * k, hyp_log=True)],
+                    a.device)(F64)
+    return out
+
+
+def predict_mean(model, inputs_list, index=None, prepared=None, defer_check=False):
+    """NMGP.predict_Y (code/nmgp_dsvi.py:666-722) -> (N,) device tensor, computed in fp64.
+
+    Sync-free: hyper-parameters are read on the device and the four Cholesky info words are checked
+    at the end -- or, with defer_check=True, left to the model's next check_numerics() (the caller's
+    existing synchronisation point; inference() predicts every iteration this way).  `prepared`: the
+    (x, I) of prepare_inputs for repeated predictions on the same inputs."""
+    dev = model.device_
+    D, M = model.D, model.M
+    x, I = prepared if prepared is not None else prepare_inputs(model, inputs_list, index)
     Z = model.Z
     th = {k: getattr(model, k).detach().to(F64) for k in ["mu_W", "mu_v", "mu_U"]}   # predicts in fp64
-    hyp = {k: float(torch.exp(getattr(model, k).detach())) for k in
-           ["sigma2_tildeell_log", "length_scales_tildeell_log", "sigma2_L0_log", "length_scales_L0_log",
-            "sigma2_L1_log", "length_scales_L1_log"]}
-
-    def rbf(a, b, s2, ls):
-        return H.pairwise(a, b, mode=L.RBF, scale2=s2, length_scale=ls)
-
-    Kt12 = rbf(x, Z, hyp["sigma2_tildeell_log"], hyp["length_scales_tildeell_log"])
-    Kt22 = rbf(Z, Z, hyp["sigma2_tildeell_log"], hyp["length_scales_tildeell_log"])
+    o = model._offs["sigma2_tildeell_log"][0]
+    hyp64 = model._theta.detach()[o:o + 7].to(F64)
+    infos = []
+    Kt12, Kt22 = _rbf(model, hyp64, x, Z, 0), _rbf(model, hyp64, Z, Z, 0)
     v = th["mu_v"].reshape(-1, 1).contiguous()
-    t_ell = _solve_rows(Kt12, Kt22, v).reshape(-1)
+    t_ell = _solve_rows(Kt12, Kt22, v, infos).reshape(-1)
     ellZ, ellX = torch.exp(v.reshape(-1)), torch.exp(t_ell)
-    K012 = rbf(x, Z, hyp["sigma2_L0_log"], hyp["length_scales_L0_log"])
-    K022 = rbf(Z, Z, hyp["sigma2_L0_log"], hyp["length_scales_L0_log"])
-    K112 = rbf(x, Z, hyp["sigma2_L1_log"], hyp["length_scales_L1_log"])
-    K122 = rbf(Z, Z, hyp["sigma2_L1_log"], hyp["length_scales_L1_log"])
+    K012, K022 = _rbf(model, hyp64, x, Z, 1), _rbf(model, hyp64, Z, Z, 1)
+    K112, K122 = _rbf(model, hyp64, x, Z, 2), _rbf(model, hyp64, Z, Z, 2)
     muU = model.mu_U_dense().to(F64).reshape(D * D, M).t().contiguous()   # (M, D*D)
-    L0 = _solve_rows(K012, K022, muU)                                   # (B, D*D)
-    L1 = _solve_rows(K112, K122, muU)
+    L0 = _solve_rows(K012, K022, muU, infos)                            # (B, D*D)
+    L1 = _solve_rows(K112, K122, muU, infos)
     KG12 = H.pairwise(x, Z, mode=L.GIBBS, ellX=ellX, ellZ=ellZ)
     KG22 = H.pairwise(Z, Z, mode=L.GIBBS, ellX=ellZ, ellZ=ellZ)
-    Gm = _solve_rows(KG12, KG22, th["mu_W"].t().contiguous())          # (B, D)
+    Gm = _solve_rows(KG12, KG22, th["mu_W"].t().contiguous(), infos)   # (B, D)
     Bn = x.shape[0]
     Lr = torch.where(torch.eye(D, dtype=torch.bool, device=dev).reshape(-1), torch.exp(L1), L0).reshape(Bn, D, D)
     Lr = torch.tril(Lr)                                                 # est_L[i, j] for j <= i
     rowsL = Lr[torch.arange(Bn, device=dev), I]                          # (B, D): row I_n of L at n
+    info = torch.cat(infos)
+    if defer_check:
+        model._pending_info.append(info)
+    elif int(info.abs().max().cpu()) != 0:
+        raise torch.linalg.LinAlgError("cholesky: K22 + 1e-4 I is not positive-definite")
     return (rowsL * Gm).sum(1)
 
 

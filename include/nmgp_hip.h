@@ -348,6 +348,25 @@ typedef struct nmgp_dsvi_args {
      prior factors; when set, the Nystrom variances k11 - ||T_row||^2 are taken from it in fp64 (the fp32
      T is not read).  NULL: use T */
   const void* T64;
+  /* KL factor range (round 3, compute_ELBO with the KL sharded over ranks): only the variational factors
+     f in [kl_f0, kl_f1) of the W | pairs list (and the v factor when kl_v) are given a KL term; the whole
+     model is [0, NF - 1) */
+  int32_t kl_f0, kl_f1;
+  /* fp64 sample / hyper-gradient path of fp32 engines (round 3; all NULL otherwise):
+     v64     (M, M) fp64 lower Cholesky factor of Sigma_v + 1e-4 I: the v sample mu_v + C z is formed in
+             fp64 (ell_Z = exp(v) amplifies its absolute error), written to v / ellZ (fp32) and ellZ64;
+     ellZ64  (M) fp64 ell_Z;
+     K12_64  (4, B, M) fp64 K12 of the priors (slot 0 = t);
+     t64     fp64 t-prior adjoint workspace: [P-bar_t (B x M) | varbar (B) | per-4-row varbar partials]
+             written by the t-row backward (the t-prior builder backward and hyper-parameter partials then
+             run in fp64 from it: K12 - P K22 cancels to ~1e-4 P, cond ~1e7 at the ECoG length scales);
+     scal64  fp64 hyper-parameter partials of the t-prior builders (t12 tiles, then t22 tiles), summed
+             by the finalize kernel in fp64 (sigma2_tildeell_log / length_scales_tildeell_log)          */
+  const void* v64;
+  void* ellZ64;
+  const void* K12_64;
+  void* t64;
+  void* scal64;
 } nmgp_dsvi_args;
 
 int nmgp_dsvi_hyper_f64(const nmgp_dsvi_args* a, hipStream_t s);      /* hyper values + v sample   */

@@ -178,6 +178,82 @@ def test_sample_sharded_elbo_equals_single_process():
     assert outs[0] == pytest.approx(float(ref), rel=1e-12)
 
 
+@pytest.mark.parametrize("D,world,owner", [(2, 2, 1), (2, 3, 0), (4, 8, 3), (5, 2, 0), (128, 8, 7), (50, 4, 2)])
+def test_kl_shares_tile_the_factors(D, world, owner):
+    """DD.kl_shares: the W | pairs factor ranges of the ranks tile [0, D + Q) exactly once, the owner of the
+    last sample holds every W factor and KL_v, and the loads (v counted) differ by at most D + 1."""
+    Q = D * (D + 1) // 2
+    sh = DD.kl_shares(D, Q, world, owner)
+    cover = sorted(f for (f0, f1, _) in sh for f in range(f0, f1))
+    assert cover == list(range(D + Q))
+    assert sh[owner][0] == 0 and sh[owner][1] >= D and sh[owner][2]
+    assert sum(1 for s in sh if s[2]) == 1
+    loads = [f1 - f0 + (1 if v else 0) for (f0, f1, v) in sh]
+    assert max(loads) - min(loads) <= D + 1
+
+
+def _factor_kls(p, c, K_G22, D, M):
+    """Per-factor KL terms in the engine's factor order (W_0..W_{D-1}, pairs (i, j <= i), then v), the
+    oracle's KL_Gaussian against the priors of sample core `c` (KL_W with this sample's K_G22)."""
+    from oracle import nmgp_oracle as O
+    Sigma_W, Sigma_v, Sigma_U = O._covs(p)
+    zero = torch.zeros(M, dtype=torch.float64)
+    kls = [float(v) for v in O.KL_Gaussian(p["mu_W"], Sigma_W, zero, K_G22)]
+    for i in range(D):
+        for j in range(i + 1):
+            K22 = c["K_L1_22"] if i == j else c["K_L0_22"]
+            kls.append(float(O.KL_Gaussian(p["mu_U"][i, j][None], Sigma_U[i, j][None], zero, K22)[0]))
+    kls.append(float(O.KL_Gaussian(p["mu_v"], Sigma_v, zero, c["K_t22"])))
+    return kls
+
+
+def _elbo_kl_sharded_rank(rank):
+    """compute_ELBO with the samples AND the KL terms sharded (nmgp_dsvi.compute_ELBO(distributed=True)'s
+    decomposition): each rank adds the KL of its kl_shares factor range, evaluated with its own last
+    sample (the W factors -- on the owner of the global last sample -- with that sample's K_G22)."""
+    from oracle import nmgp_oracle as O
+    from tests import _golden as G
+    g = _elbo_tape()
+    xs, ys = G.split_lists(g)
+    D, M = 2, 20
+    p = G.params(g, D=D, M=M)
+    B, Q = int(np.sum(g["sizes"])), 3
+    per = M + B + Q * B
+    tape = np.asarray(g["noise"], np.float64)
+    rank_, world = DD.world_info()
+    owner = DD.last_sample_owner(N_SAMPLE, world)
+    f0, f1, with_v = DD.kl_shares(D, Q, world, owner)[rank_]
+    mine = DD.sample_ids(N_SAMPLE, rank_, world)
+    r_sum, kl = 0.0, None
+    Z = torch.as_tensor(np.asarray(g["z"], np.float64)).reshape(-1, 1)
+    inputs = torch.cat([torch.as_tensor(x) for x in xs]).reshape(-1, 1)
+    for s in mine:
+        nz = tape[s * per:(s + 1) * per]
+        _, lps = O.compute_ELBO(p, xs, ys, g["z"], float(g["N"]), O.TapeNoise(nz), n_sample=1)
+        r_sum += float(lps[0])
+        if s == mine[-1]:
+            Sigma_W, Sigma_v, Sigma_U = O._covs(p)
+            c = O._sample_core(p, Sigma_v, Sigma_U, O._hyper(p), Z, inputs, D, O.TapeNoise(nz), float(g["N"]))
+            K_G22 = O.create_Gibbs(Z, Z, c["ell_Z"], c["ell_Z"])
+            kls = _factor_kls(p, c, K_G22, D, M)
+            kl = sum(kls[f] for f in range(f0, f1)) + (kls[-1] if with_v else 0.0)
+    return float(DD.combine_elbo(torch.tensor(r_sum, dtype=torch.float64), kl, N_SAMPLE))
+
+
+def test_kl_sharded_elbo_equals_single_process():
+    from oracle import nmgp_oracle as O
+    from tests import _golden as G
+    outs = _run(_elbo_kl_sharded_rank)
+    g = _elbo_tape()
+    xs, ys = G.split_lists(g)
+    p = G.params(g, D=2, M=20)
+    M, B, Q = 20, int(np.sum(g["sizes"])), 3
+    tape = np.asarray(g["noise"], np.float64)[:N_SAMPLE * (M + B + Q * B)]
+    ref, _ = O.compute_ELBO(p, xs, ys, g["z"], float(g["N"]), O.TapeNoise(tape), n_sample=N_SAMPLE)
+    assert outs[0] == outs[1]
+    assert outs[0] == pytest.approx(float(ref), rel=1e-12)
+
+
 # ------------------------------------------------------------------------------------ pair sharding
 REP = ["mu_W", "sqrt_W", "mu_v", "sqrt_v", "sigma2_tildeell_log", "length_scales_tildeell_log", "sigma2_L0_log",
        "length_scales_L0_log", "sigma2_L1_log", "length_scales_L1_log", "sigma2_err_log"]

