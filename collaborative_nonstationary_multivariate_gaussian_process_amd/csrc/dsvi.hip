@@ -820,21 +820,30 @@ __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
     }
     return;
   }
-  // fp32 engines with the fp64 t-prior adjoints (a.scal64): the t12 + t22 hyper-parameter partials and
-  // the varbar partials summed in fp64 -- their sum cancels to ~1e-7 of its terms at ECoG length scales
-  double t64s[3] = {0, 0, 0};
+  // fp32 engines with the fp64 prior adjoints (a.scal64): the six builder partial sets (L0_12, L0_22,
+  // L1_12, L1_22, t12, t22), the varbar partials and the row coefficients c0 / c1 summed in fp64 --
+  // each hyper-parameter gradient cancels to ~1e-7 of its terms at ECoG length scales
+  double h64[15];
+#pragma unroll
+  for (int k = 0; k < 15; ++k) h64[k] = 0;
   if (a.scal64) {
     __shared__ double red64[16];
     const double* s64 = (const double*)a.scal64;
-    const int64_t n64 = a.scal_off[6] - a.scal_off[4];
-    for (int64_t i = t; i < n64; i += blockDim.x) {
-      t64s[0] += s64[2 * i];
-      t64s[1] += s64[2 * i + 1];
-    }
-    const double* vpart = (const double*)a.t64 + (int64_t)a.B * a.M + a.B;
-    for (int64_t i = t; i < ntb; i += blockDim.x) t64s[2] += vpart[i];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) t64s[k] = block_sum(t64s[k], red64);
+    for (int q = 0; q < 6; ++q)
+      for (int64_t i = a.scal_off[q] + t; i < a.scal_off[q + 1]; i += blockDim.x) {
+        h64[2 * q] += s64[2 * i];
+        h64[2 * q + 1] += s64[2 * i + 1];
+      }
+    const double* vpart = (const double*)a.t64 + (int64_t)a.B * a.M + a.B;
+    for (int64_t i = t; i < ntb; i += blockDim.x) h64[12] += vpart[i];
+    const T* rcrow = (const T*)a.rowbuf + (int64_t)(2 * a.D + 1) * a.B;     // c0 | c1 rows
+    for (int64_t i = t; i < a.B; i += blockDim.x) {
+      h64[13] += (double)rcrow[i];
+      h64[14] += (double)rcrow[a.B + i];
+    }
+#pragma unroll
+    for (int k = 0; k < 15; ++k) h64[k] = block_sum(h64[k], red64);
   }
   // L0_12 + L0_22, L1_12 + L1_22, t12 + t22 (sigma2 / length-scale partials)
   if (threadIdx.x == 0) {
@@ -857,15 +866,20 @@ __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
     T gs[7];
     gs[0] = sc[4] + hyp<T>(a, 0) * vs;   // sigma2_tildeell_log
     gs[1] = sc[5];                        // length_scales_tildeell_log
-    if (a.scal64) {
-      gs[0] = (T)(t64s[0] + exp((double)((const T*)a.theta)[a.off_hyp]) * t64s[2]);
-      gs[1] = (T)t64s[1];
-    }
     gs[2] = sc[0] + hyp<T>(a, 2) * c0;   // sigma2_L0_log
     gs[3] = sc[1];                        // length_scales_L0_log
     gs[4] = sc[2] + hyp<T>(a, 4) * c1;   // sigma2_L1_log
     gs[5] = sc[3];                        // length_scales_L1_log
     gs[6] = e;                            // sigma2_err_log
+    if (a.scal64) {
+      const T* hy = (const T*)a.theta + a.off_hyp;
+      gs[0] = (T)((h64[8] + h64[10]) + exp((double)hy[0]) * h64[12]);
+      gs[1] = (T)(h64[9] + h64[11]);
+      gs[2] = (T)((h64[0] + h64[2]) + exp((double)hy[2]) * h64[13]);
+      gs[3] = (T)(h64[1] + h64[3]);
+      gs[4] = (T)((h64[4] + h64[6]) + exp((double)hy[4]) * h64[14]);
+      gs[5] = (T)(h64[5] + h64[7]);
+    }
     for (int k = 0; k < 7; ++k) g[a.off_hyp + k] = (a.frozen_mask >> k & 1) ? (T)0 : gs[k];
   }
   // (the KL mean gradients A2^{-1} mu and mu_v += vbar are added by dsvi_mugrad_kernel on the side stream)

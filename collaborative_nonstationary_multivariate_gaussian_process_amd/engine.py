@@ -163,7 +163,7 @@ class DsviEngine:
         # ~cond(K22) * eps32 (HCP-like fixture: P_G off by 40% with an fp32 factorization, 5e-4 with
         # an fp64 one -- DESIGN.md §5).  NMGP_PRIOR_FP64=0 turns it off (A/B only).
         self.prior64 = dtype == F32 and os.environ.get("NMGP_PRIOR_FP64", "1") != "0"
-        self.p64 = self.prior64 and os.environ.get("NMGP_PROJ_FP64", "0") != "0"
+        self.p64 = self.prior64 and os.environ.get("NMGP_PROJ_FP64", "1") != "0"
         if self.prior64:
             # with p64 a fifth fp64 slot in front holds Sigma_v + 1e-4 I: [v | t | L0 | L1 | G] is then
             # one contiguous batch whose first four slots factor in one launch, like the fp32 slots
@@ -177,8 +177,11 @@ class DsviEngine:
         # the projections P = T C2^-1 and the prior inverses in fp64 (rounded to fp32 only for the fp32
         # consumers), and take the Nystrom variances k11 - ||T_row||^2 from the fp64 T: built in fp32, the
         # entries' rounding is amplified by A^-1 (cond ~1e5-1e6 at length scales 3/M) -- the ECoG-like
-        # fixture's loss was 1.6e-3 off with fp32 projections (tests/analysis/ecog_fp32_diag.py).
-        # NMGP_PROJ_FP64=0: the round-2 fp32 projections (A/B only).
+        # fixture's loss was 1.6e-3 off with fp32 projections (tests/analysis/ecog_fp32_diag.py).  With it
+        # the v sample (fp64 factor of Sigma_v) and the prior adjoint chains (R, A-bar, builder backward,
+        # hyper-parameter partial sums) are fp64 as well (tests/analysis/ecog_hyper_sensitivity.py: the
+        # hyper-parameter gradients cancel to ~1e-7 of their terms; fp32 adjoints left them 14-30% off).
+        # NMGP_PROJ_FP64=0: the round-2 all-fp32 projections and adjoints (A/B only).
         if self.p64:
             z64 = lambda *s: torch.zeros(*s, dtype=F64, device=self.dev)
             self.x64, self.hyp64, self.ellX64, self.ellZ64 = z64(B), z64(8), z64(B), z64(M)
@@ -191,7 +194,11 @@ class DsviEngine:
             # backward), R_t, A-bar_t, the KL_v parts' delta_t | Y_t, and the t12 / t22 builder partials
             self.t64 = z64(B * M + B + (B + 3) // 4)
             self.Rt64, self.Abt64, self.dY64 = z64(B, M), z64(M, M), z64(2 * M)
-            self.scal64 = z64(2 * int(self.scal_off[6] - self.scal_off[4]))
+            # the L0 / L1 prior adjoints likewise: P-bar_0/1 and their KL A-bar parts widened, the
+            # row coefficients c0 / c1, R and A-bar in fp64; all six builder partial sets in fp64
+            # (same tile offsets as scal_part)
+            self.PbL64, self.RL64, self.AbL64, self.rcL64 = z64(2, B, M), z64(2, B, M), z64(2, M, M), z64(2, B)
+            self.scal64 = z64(2 * int(self.scal_off[6]))
         # selection weights for the -1/2 Y diag(sel) Y^T prior adjoint (static)
         sel = np.zeros((4, self.NPC))
         for (i, j) in self.pairs:
@@ -554,14 +561,29 @@ class DsviEngine:
                                  offs=(0, 0, 0), **rows_all)])
             p["bwd_t2"] = G64([g(self.Abt64, self.P64, self.Rt64, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), alpha=-1.0,
                                  beta=1.0, offs=(0, 0, 0), k_seg=0, seg_span=D)])
-            ntb12 = int(so[5] - so[4])
             p["bwd_tbuild"] = H.PairwiseBwdGroup([
                 H.pairwise_bwd_desc(self.x64, self.Z64, self.K12_64, self.Rt64, mode=L.RBF, ld=M, Pm=self.P64,
                                     rowcoef=(self.t64, B * M), hyp=self.hyp64, hyp_off=0, hyp_log=True,
-                                    scal_part=self.scal64, offs=(0, 0, 0, 0, 0, 0)),
+                                    scal_part=self.scal64, offs=(0, 0, 0, 0, 0, 2 * int(so[4]))),
                 H.pairwise_bwd_desc(self.Z64, self.Z64, None, self.Abt64, mode=L.RBF, ld=M, hyp=self.hyp64,
                                     hyp_off=0, hyp_log=True, scal_part=self.scal64,
-                                    offs=(0, 0, 0, 0, 0, 2 * ntb12))], dev)
+                                    offs=(0, 0, 0, 0, 0, 2 * int(so[5])))], dev)
+            # L0 / L1: R_k = P-bar_k A_k^-1, A-bar_k -= P_k^T R_k, builder backward, all fp64 (k = 1, 2)
+            p["bwd_R_L"] = G64([g(self.RL64, self.PbL64, self.Ainv64, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1),
+                                  offs=(q * BM, (q + 1) * MM, q * BM), **rows_all) for q in range(2)])
+            p["bwd_pr_L"] = G64([g(self.AbL64, self.P64, self.RL64, M, M, B, (1, M, 0), (M, 1, 0), (M, 1),
+                                   alpha=-1.0, beta=1.0, offs=((q + 1) * BM, q * BM, q * MM), k_seg=0, seg_span=D)
+                                 for q in range(2)])
+            bwL = []
+            for q, hoff in ((0, 2), (1, 4)):
+                bwL.append(H.pairwise_bwd_desc(self.x64, self.Z64, self.K12_64, self.RL64, mode=L.RBF, ld=M,
+                                               Pm=self.P64, rowcoef=(self.rcL64, q * B), hyp=self.hyp64,
+                                               hyp_off=hoff, hyp_log=True, scal_part=self.scal64,
+                                               offs=((q + 1) * BM, q * BM, (q + 1) * BM, 0, 0, 2 * int(so[2 * q]))))
+                bwL.append(H.pairwise_bwd_desc(self.Z64, self.Z64, None, self.AbL64, mode=L.RBF, ld=M,
+                                               hyp=self.hyp64, hyp_off=hoff, hyp_log=True, scal_part=self.scal64,
+                                               offs=(0, q * MM, 0, 0, 0, 2 * int(so[2 * q + 1]))))
+            p["bwd_build_L"] = H.PairwiseBwdGroup(bwL, dev)
         # B9: v Cholesky backward: grad_sv += Cinv_v^T (Psi Xs_v)
         p["bwd_v1"] = G([g(self.T2, self.phi, self.Xs, M, M, M, (M, 1, 0), (M, 1, 0), (M, 1), flags=L.B_LOWER,
                            offs=(0, FV * MM, 0))])
@@ -907,17 +929,26 @@ class DsviEngine:
         # run on the second side stream
         # A/B on the box (tools/ab_env.sh NMGP_SIDE3, 3 x 300 steps each): 0.815-0.818 -> 0.798-0.802 ms
         side3 = os.environ.get("NMGP_SIDE3", "1") != "0"
+        BM = self.B * M
+
+        def lchain(where):
+            # (p64: P-bar_0/1, the KL parts of A-bar_0/1 and the row coefficients c0 / c1 widened first)
+            pre = [("wPbL", "convert", widen(self.Pbar, self.PbL64, 2 * BM, BM), where),
+                   ("wAbL", "convert", widen(self.Abar, self.AbL64, 2 * MM, MM), where),
+                   ("wrcL", "convert", widen(self.rowbuf, self.rcL64, 2 * self.B, (2 * D + 1) * self.B), where)] \
+                if self.p64 else []
+            return pre + [("bwd_R_L", "gemm", gemm("bwd_R_L"), where),
+                          ("bwd_pr_L", "gemm", gemm("bwd_pr_L"), where),
+                          ("bwd_build_L", "pairwise_bwd", (pw64 if self.p64 else pw)("bwd_build_L"), where),
+                          ("sig", where, "L_done")]
         if side3:
             # the L0 / L1 prior adjoints (R_0, R_1 -> P^T R -> builder backward: hyper-parameter partials
             # only) need P-bar_0/1 (bwd_w) and the KL parts of Abar (kl_done): a third side stream starts
             # them right after bwd_w.  On side2 they queued behind the G-prior adjoint and, in the graph,
             # shared a hardware queue with the t chain (finalize waited ~50 us for them, r02b timeline).
             # Like side2 it synchronises with the main stream only.
-            steps += [("wait", "main", "kl_done"), ("sig", "main", "bwd_w_kl"), ("wait", "side3", "bwd_w_kl"),
-                      ("bwd_R_L", "gemm", gemm("bwd_R_L"), "side3"),
-                      ("bwd_pr_L", "gemm", gemm("bwd_pr_L"), "side3"),
-                      ("bwd_build_L", "pairwise_bwd", pw("bwd_build_L"), "side3"),
-                      ("sig", "side3", "L_done")]
+            steps += [("wait", "main", "kl_done"), ("sig", "main", "bwd_w_kl"), ("wait", "side3", "bwd_w_kl")]
+            steps += lchain("side3")
         steps += [
             # (the second side stream synchronises with the main stream only: a side <-> side2 event
             # edge made hipGraph instantiation crash on this stack; the KL prior adjoints are long done
@@ -936,10 +967,7 @@ class DsviEngine:
             # row-coefficient rows of their own): second side stream after the G prior adjoint (R_G was
             # signalled after bwd_w and the KL parts of Abar), so the v chain on the side stream does not
             # queue behind them
-            steps += [("bwd_R_L", "gemm", gemm("bwd_R_L"), "side2"),
-                      ("bwd_pr_L", "gemm", gemm("bwd_pr_L"), "side2"),
-                      ("bwd_build_L", "pairwise_bwd", pw("bwd_build_L"), "side2"),
-                      ("sig", "side2", "L_done")]
+            steps += lchain("side2")
         steps += [
             ("tbwd", "row", row(getattr(lib, "nmgp_dsvi_tbwd_" + self.sfx)), "main"),
             # after the t-row backward the t-prior chain (bwd_t1 -> bwd_t2 -> builder backward) and the

@@ -106,7 +106,8 @@ def test_ecog_like_fp32_packed_engine_within_fp32_gates():
     vec = {k: e for k, e in errs.items() if k != "loss" and not any(h in k for h in HYPER)}
     bad = {k: e for k, e in vec.items() if e > 2e-2}
     assert not bad, f"fp32 gradient digest mismatch {bad} (all {errs})"
-    assert max(e for k, e in errs.items() if any(h in k for h in HYPER)) < 0.2, errs
+    # (hyper-parameter gradients: fp64 prior adjoint chains; 0.26-0.30 with fp32 ones)
+    assert max(e for k, e in errs.items() if any(h in k for h in HYPER)) < 2e-2, errs
     samp = torch.cat([gd[k].reshape(-1)[:: max(1, gd[k].numel() // 997)] for k in O.PARAM_NAMES])
     ref = torch.cat([torch.as_tensor(g["gsample_" + k]).reshape(-1) for k in O.PARAM_NAMES])
     assert _rel(samp, ref) < 2e-2

@@ -170,15 +170,16 @@ def test_fp32_engine_within_fp32_gates(case):
     loss, _ = O.forward(q, xs, ys, g["z"], float(g["N"]), O.TapeNoise(g["noise"]))
     loss.backward()
     assert float(out[0]) == pytest.approx(float(loss), rel=1e-3)
-    # SURVEY §8c fp32 gate on the whole gradient vector (rel-norm 2e-2); per parameter only a sanity
-    # bound (1e-1): small scalar gradients (sigma2 logs) come from cancelling sums, and the toy
-    # fixture's smooth prior has cond(K22 + 1e-4 I) ~ 2e5, which fp32 explicit inverses feel
+    # SURVEY §8c fp32 gate on the whole gradient vector (rel-norm 2e-2), and per parameter too: the small
+    # scalar gradients (sigma2 logs) come from cancelling sums (cond(K22 + 1e-4 I) ~ 2e5 on the toy
+    # fixture's smooth prior), which the fp32 engine forms in fp64 (fp64 projections and prior adjoints)
     gd = _unflatten(eng, grad)
     full_g = torch.cat([gd[k].reshape(-1).double() for k in O.PARAM_NAMES])
     full_r = torch.cat([q[k].grad.reshape(-1) for k in O.PARAM_NAMES])
     assert _rel(full_g, full_r) < 2e-2, _rel(full_g, full_r)
     errs = {k: _rel(gd[k], q[k].grad) for k in O.PARAM_NAMES if float(q[k].grad.norm()) > 0}
-    bad = {k: e for k, e in errs.items() if e > 1e-1}
+    print(f"PARITY {case} fp32 per-parameter:", {k: f"{e:.2e}" for k, e in errs.items()})
+    bad = {k: e for k, e in errs.items() if e > 2e-2}
     assert not bad, f"fp32 gradient mismatch {bad} (all: {errs})"
 
 
@@ -313,9 +314,11 @@ def test_hcp_like_fp32_engine_within_fp32_gates():
     vec = {k: e for k, e in errs.items() if k != "loss" and not any(h in k for h in HYPER)}
     bad = {k: e for k, e in vec.items() if e > 2e-2}
     assert not bad, f"fp32 gradient digest mismatch {bad} (all {errs})"
-    # scalar hyper-parameter gradients are sums of cancelling terms: sanity bound only (as the toy /
-    # mid fp32 tests; d/d sigma2_tildeell_log: 0.13 measured)
-    assert max(e for k, e in errs.items() if any(h in k for h in HYPER)) < 0.2, errs
+    # scalar hyper-parameter gradients are sums whose terms cancel to ~1e-7 of their size (K12 - P K22 ~
+    # 1e-4 P at these length scales): with fp32 adjoints d/d sigma2_tildeell_log was 0.13 off (round 2);
+    # the fp32 engine forms the prior adjoint chains and these sums in fp64, so they meet the
+    # vector parameters' 2e-2
+    assert max(e for k, e in errs.items() if any(h in k for h in HYPER)) < 2e-2, errs
     gd = _unflatten(eng, grad)
     samp = torch.cat([gd[k].reshape(-1).double()[:: max(1, gd[k].numel() // 997)] for k in O.PARAM_NAMES])
     ref = torch.cat([torch.as_tensor(g["gsample_" + k]).reshape(-1) for k in O.PARAM_NAMES])

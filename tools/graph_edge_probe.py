@@ -1,0 +1,96 @@
+"""Which cross-stream event patterns does hipGraph capture + instantiate survive?  
+
+Round 2 saw hipGraphInstantiate segfault once the DSVI step schedule had event edges between its two
+side streams (side <-> side2); the schedule was rerouted through the main stream.  This probe isolates
+the trigger with plain torch ops (no nmgp kernels): each pattern is captured, instantiated and replayed
+in a CHILD process (a segfault ends only that child), and the probe stops at the first pattern that
+fails (no GPU work after a crash).  Output: one JSON line per pattern.
+
+  python tools/graph_edge_probe.py [pattern ...]
+"""
+import json
+import os
+import subprocess
+import sys
+
+PATTERNS = {
+    # fork main -> side, side2; ops; join both back to main (no side <-> side2 edge): the baseline
+    "fork_join": "",
+    # side2 waits an event recorded on side
+    "side_to_side2": "s->s2",
+    # side waits an event recorded on side2
+    "side2_to_side": "s2->s",
+    # both directions at different points (round 2's schedule: side2 waits kl_done, side waits g22)
+    "ping_pong": "s->s2,s2->s",
+    # the same side event waited by main AND side2 (two paths to one node)
+    "shared_wait": "s->m,s->s2",
+    # the same event waited twice by one stream
+    "double_wait": "s->s2,s->s2",
+    # side2 waits a side event, then main waits side2 only (side joined to main only through side2)
+    "transitive_join": "s->s2,nojoin_s",
+}
+
+
+def child(spec):
+    import torch
+    dev = torch.device("cuda:0")
+    main = torch.cuda.Stream(device=dev)
+    side, side2 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    S = {"m": main, "s": side, "s2": side2}
+    x = {k: torch.ones(1 << 16, device=dev) for k in S}
+    edges = [e for e in spec.split(",") if e and "->" in e]
+    nojoin = {e.split("_", 1)[1] for e in spec.split(",") if e.startswith("nojoin_")}
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(main):
+        torch.cuda.synchronize()
+        g.capture_begin()
+        fork = torch.cuda.Event()
+        fork.record(main)
+        for k in ("s", "s2"):
+            S[k].wait_event(fork)
+        for k in S:                                  # one op per stream before the edges
+            with torch.cuda.stream(S[k]):
+                x[k].mul_(1.5)
+        for e in edges:                              # record on the source, wait on the destination, op after
+            a, b = e.split("->")
+            ev = torch.cuda.Event()
+            ev.record(S[a])
+            S[b].wait_event(ev)
+            with torch.cuda.stream(S[b]):
+                x[b].add_(1.0)
+        for k in ("s", "s2"):                        # join the side streams back to main
+            if k in nojoin:
+                continue
+            ev = torch.cuda.Event()
+            ev.record(S[k])
+            main.wait_event(ev)
+        if nojoin:                                   # joined only transitively (through side2)
+            ev = torch.cuda.Event()
+            ev.record(side2)
+            main.wait_event(ev)
+        g.capture_end()
+    g.replay()
+    torch.cuda.synchronize()
+    print("ok", float(x["m"][0]), float(x["s"][0]), float(x["s2"][0]))
+
+
+def main(names):
+    if len(sys.argv) > 2 and sys.argv[1] == "--child":
+        child(sys.argv[2])
+        return
+    for name in names:
+        env = dict(os.environ)
+        p = subprocess.run([sys.executable, __file__, "--child", PATTERNS[name]], env=env, capture_output=True,
+                           text=True, timeout=120)
+        rec = {"pattern": name, "spec": PATTERNS[name], "rc": p.returncode,
+               "out": p.stdout.strip()[-200:], "err": p.stderr.strip()[-400:]}
+        print(json.dumps(rec), flush=True)
+        if p.returncode != 0:
+            break                                    # nothing more on the GPU after a crash
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "--child":
+        child(sys.argv[2])
+    else:
+        main(sys.argv[1:] or list(PATTERNS))
