@@ -1228,10 +1228,10 @@ __device__ inline bool lds_wait_ge(int* p, int target) {
 }
 __device__ inline int tab_off(int j) { return j * 16 - j * (j - 1) / 2; }   // start of column j's entries
 
-template <typename T, int R>
+template <typename T, int R, int J0 = 0, int J1 = 16>
 __device__ __attribute__((always_inline)) inline void rows_apply(T (&a)[kRowSlots][16], const T* tab) {
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
+  for (int j = J0; j < J1; ++j) {
     const T inv = tab[tab_off(j)];
 #pragma unroll
     for (int s = 0; s < R; ++s) a[s][j] = a[s][j] * inv;
@@ -1254,18 +1254,30 @@ __device__ __attribute__((always_inline)) inline void chol6_potrf_role(T* Am, T*
   T* Ps0 = colbuf0 + 2 * NR * CP;      // 2 x NR x CP: L[:, k] (local rows, diagonal block first)
   T* LiT0 = Ps0 + 2 * NR * CP;         // 2 x 16 x CP: L_kk^-T rows by parity
   T* Tab0 = LiT0 + 32 * CP;            // 2 x 136: the diagonal wave's table by parity
-  int* ctl = (int*)(Tab0 + 2 * kTab);  // [0], [1] colcnt by parity, [2] diag, [3] rows, [4] pub
+  // [0], [1] colcnt by parity, [2] diag, [3] rows, [4] pub, [5] table column groups published (4 columns
+  // each, k * 4 + g + 1), [6] diagonal tiles spilled ahead (k + 1: tile (k+1, k+1) with step k applied),
+  // [7] update-wave steps finished (their last reads of Ps / LiT of that step done)
+  int* ctl = (int*)(Tab0 + 2 * kTab);
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  if (t < 8) ctl[t] = 0;
+  if (t < 16) ctl[t] = 0;
   __syncthreads();
   const __amdgpu_buffer_rsrc_t rAm = make_rsrc(Am, ((int64_t)(n - 1) * lda + n) * (int64_t)sizeof(T));
   if (w == 0) {
     // ------------------------------------------------------------------ diagonal wave
+    // the pivot chain is the kernel's critical path: it wins issue arbitration over the update waves'
+    // MFMAs on its SIMD (without it the chain ran ~2x slower while the trailing update was in flight)
+    __builtin_amdgcn_s_setprio(3);
     int first_fail = 0;
     bool ok = true;
     for (int k = 0; k < nt; ++k) {
-      ok &= lds_wait_ge(&ctl[k & 1], kUpdW * ((k >> 1) + 1));
+      if (k == 0) {
+        ok &= lds_wait_ge(&ctl[0], kUpdW);                    // the prologue spill of block column 0
+      } else {
+        ok &= lds_wait_ge(&ctl[6], k);                        // tile (k, k), spilled ahead by its owner
+        // Ps / LiT / Tab of this parity were last read by the update waves in step k - 2
+        if (k >= 2) ok &= lds_wait_ge(&ctl[7], kUpdW * (k - 1));
+      }
       CHOL4_STAMP(0, k, 0);
       const T* cb = colbuf0 + (k & 1) * NR * CP;
       T a[16];
@@ -1295,6 +1307,12 @@ __device__ __attribute__((always_inline)) inline void chol6_potrf_role(T* Am, T*
         if (lane == 0) tab[tab_off(j)] = inv;
         a[j] = (lane == j) ? sj : a[j] * inv;
         if (lane > j && lane < 16) tab[tab_off(j) + lane - j] = a[j];     // L_{lane, j}
+        if ((j & 3) == 3 && j < 15) {
+          // columns j-3..j of the table are complete: the row waves start on them now instead of after
+          // the whole 16-column chain
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0) __hip_atomic_store(&ctl[5], k * 4 + (j >> 2) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
 #pragma unroll
         for (int c = j + 1; c < 16; ++c) a[c] = fma(-a[j], readlane(a[j], c), a[c]);
       }
@@ -1327,6 +1345,7 @@ __device__ __attribute__((always_inline)) inline void chol6_potrf_role(T* Am, T*
   }
   if (w <= kRowW) {
     // ------------------------------------------------------------------ row waves
+    __builtin_amdgcn_s_setprio(2);
     const int rw = w - 1;
     bool ok = true;
     for (int k = 0; k < nt; ++k) {
@@ -1344,11 +1363,21 @@ __device__ __attribute__((always_inline)) inline void chol6_potrf_role(T* Am, T*
 #pragma unroll
         for (int c = 0; c < 16; ++c) a[s][c] = (s < nslot) ? src[c] : (T)0;
       }
-      ok &= lds_wait_ge(&ctl[2], k + 1);                     // the diagonal wave's table of column k
-      if (w == 1) CHOL4_STAMP(1, k, 0);
+      // the diagonal wave's table of column k, four table columns at a time as they are published
       const T* tab = Tab0 + (k & 1) * kTab;
-      if (nslot == 2) rows_apply<T, 2>(a, tab);
-      else if (nslot == 1) rows_apply<T, 1>(a, tab);
+      ok &= lds_wait_ge(&ctl[5], k * 4 + 1);
+      if (w == 1) CHOL4_STAMP(1, k, 0);
+      if (nslot == 2) rows_apply<T, 2, 0, 4>(a, tab);
+      else if (nslot == 1) rows_apply<T, 1, 0, 4>(a, tab);
+      ok &= lds_wait_ge(&ctl[5], k * 4 + 2);
+      if (nslot == 2) rows_apply<T, 2, 4, 8>(a, tab);
+      else if (nslot == 1) rows_apply<T, 1, 4, 8>(a, tab);
+      ok &= lds_wait_ge(&ctl[5], k * 4 + 3);
+      if (nslot == 2) rows_apply<T, 2, 8, 12>(a, tab);
+      else if (nslot == 1) rows_apply<T, 1, 8, 12>(a, tab);
+      ok &= lds_wait_ge(&ctl[2], k + 1);
+      if (nslot == 2) rows_apply<T, 2, 12, 16>(a, tab);
+      else if (nslot == 1) rows_apply<T, 1, 12, 16>(a, tab);
       T* ps = Ps0 + (k & 1) * NR * CP;
 #pragma unroll
       for (int s = 0; s < kRowSlots; ++s) {
@@ -1443,10 +1472,26 @@ __device__ __attribute__((always_inline)) inline void chol6_potrf_role(T* Am, T*
     if (sw == 0) CHOL4_STAMP(2, k, 0);
     const T* ps = Ps0 + (k & 1) * NR * CP;
     T* cb = colbuf0 + ((k + 1) & 1) * NR * CP;
-    // 1. block column k+1 first: the next panel's input
+    // 1. block column k+1 first: the next panel's input.  Its diagonal tile before the others: the
+    // diagonal wave starts step k+1 on it alone (ctl[6])
 #pragma unroll
     for (int u = 0; u < NTPW; ++u) {
-      if (JB(u) == k + 1) {
+      if (JB(u) == k + 1 && IB(u) == k + 1) {
+        const int ra = 16 + (lane & 15);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int kr = Mfma<T>::row(lane, s);
+          acc[u] = Mfma<T>::mma(-ps[ra * CP + kr], ps[ra * CP + kr], acc[u]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cb[Mfma<T>::row(lane, r) * CP + (lane & 15)] = acc[u][r];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&ctl[6], k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NTPW; ++u) {
+      if (JB(u) == k + 1 && IB(u) > k + 1) {
         const int ra = __builtin_amdgcn_readfirstlane(IB(u) - k) * 16 + (lane & 15);
         const int rb = 16 + (lane & 15);
 #pragma unroll
@@ -1477,7 +1522,9 @@ __device__ __attribute__((always_inline)) inline void chol6_potrf_role(T* Am, T*
       }
     }
     if (sw == 0) CHOL4_STAMP(2, k, 2);
-    publish(k);        // (Ps / LiT of this parity are rewritten only after this wave spills column k+2)
+    publish(k);        // (Ps / LiT of this parity are rewritten only after every update wave counted step k)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_fetch_add(&ctl[7], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   ok &= lds_wait_ge(&ctl[3], kRowW * nt);                   // the last panel
   if (nt > 1) drained(nt - 1);

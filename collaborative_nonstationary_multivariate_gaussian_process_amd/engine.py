@@ -433,7 +433,11 @@ class DsviEngine:
                              kb=(M, M), beta=1.0, offs=(0, sU + pq(i, 0) * MM, 1 * BM), row_seg=i))
         # the P-bar products feed R (main chain); the L-bar / mu-bar products below only accumulate
         # gradient rows, so they run on the side stream beside bwd_R .. bwd_v2
-        p["bwd_w"] = G(d17)
+        # A/B knob NMGP_BWD_LAT_WGS=<n>: run P-bar on the latency kernel with split-K sized for ~n workgroups
+        # (its k runs over up to D latent blocks: 5 rounds of panels per workgroup unsplit at PM2.5)
+        bwd_lat = int(os.environ.get("NMGP_BWD_LAT_WGS", "0"))
+        p["bwd_w"] = G(d17) if not bwd_lat else H.GemmGroup(d17, dev, self.dt, seg=seg, target_wgs=bwd_lat,
+                                                             kernel="lat")
         d17 = []
         for d in range(D):
             d17.append(g(gr, self.P, self.WG, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_TRIL, beta=1.0,
@@ -821,21 +825,28 @@ class DsviEngine:
         # forward chain: chol -> v -> K_G22 -> chol_G -> invG -> projG.  The t-prior projections, the
         # t-row (ell_X) and K_G12 run on the second side stream beside v / K_G22 / chol_G: they are
         # needed only from invG on (T_G = K_G12 C_G^-T)
+        # In a replayed graph a node's FIRST-created child stays on the node's hardware queue and every other
+        # child starts on another queue behind a cross-queue barrier (≈ 10-20 us per hop in the r03 kernel
+        # traces).  crit: the critical-path child of each fork is created first (v after chol, quad_W after
+        # projG, bwd_R after bwd_w, bwd_t1 after the t-row backward); stream order and every event edge are
+        # unchanged, only the capture order of independent launches moves.  NMGP_CRIT_FIRST=0: the old order.
+        crit = os.environ.get("NMGP_CRIT_FIRST", "1") != "0"
         steps += [
             ("chol", "chol", chol_main, "main"),
-            ("sig", "main", "chol"), ("wait", "side2", "chol"),
+            ("sig", "main", "chol"),
         ]
+        if crit:
+            steps += [("v", "row", row(getattr(lib, "nmgp_dsvi_hyper_" + self.sfx)), "main"), ("sig", "main", "v")]
+        steps.append(("wait", "side2", "chol"))
         if self.p64:
             steps += [("inv3_64", "gemm", gemm("inv3_64"), "side2"),
                       ("proj3_64", "gemm", gemm("proj3_64"), "side2"),
                       ("conv3", "convert", round_back(0, 3), "side2")]
         if p["inv3"] is not None:
             steps.append(("inv3", "gemm", gemm("inv3"), "side2"))
-        steps += [
-            ("proj3", "gemm", gemm("proj3"), "side2"),
-            ("v", "row", row(getattr(lib, "nmgp_dsvi_hyper_" + self.sfx)), "main"),
-            ("sig", "main", "v"),
-        ]
+        steps.append(("proj3", "gemm", gemm("proj3"), "side2"))
+        if not crit:
+            steps += [("v", "row", row(getattr(lib, "nmgp_dsvi_hyper_" + self.sfx)), "main"), ("sig", "main", "v")]
         steps += [
             ("build_g22", "pairwise", (pw64 if self.p64 else pw)("build_g22"), "main"),
             ("wait", "side2", "v"),
@@ -886,8 +897,15 @@ class DsviEngine:
         # KL terms, prior-diagonal adjoints, the variational factors' KL L-bar (first writer of those
         # gradient rows -- bwd_lbar follows it on the same stream, so the accumulation order is fixed) and the KL part of
         # the prior adjoints Abar (bwd_pr waits for it)
+        quad_split = os.environ.get("NMGP_QUAD_SPLIT", "1") != "0"
+        steps.append(("sig", "main", "kl_in"))
+        quad_first = crit and quad_split
+        if quad_first:
+            if pre_planned:
+                steps.append(("wait", "main", "plans"))
+            steps.append(("quad_W", "gemm", gemm("quad_W"), "main"))
         steps += [
-            ("sig", "main", "kl_in"), ("wait", "side", "kl_in"),
+            ("wait", "side", "kl_in"),
             ("kl", "row", row(getattr(lib, "nmgp_dsvi_kl_" + self.sfx)), "side"),
             ("delta", "row", row(getattr(lib, "nmgp_dsvi_delta_" + self.sfx)), "side"),
         ]
@@ -903,10 +921,11 @@ class DsviEngine:
             ("bwd_kly", "gemm", gemm("bwd_kly"), "side"),
             ("sig", "side", "kl_done"),
         ]
-        if pre_planned:
+        if pre_planned and not quad_first:
             steps.append(("wait", "main", "plans"))
-        quad_split = os.environ.get("NMGP_QUAD_SPLIT", "1") != "0"
-        if quad_split:
+        if quad_first:
+            steps.append(("wait", "main", "quadP"))
+        elif quad_split:
             steps += [("quad_W", "gemm", gemm("quad_W"), "main"), ("wait", "main", "quadP")]
         else:
             steps.append(("quad", "gemm", gemm("quad"), "main"))
@@ -947,13 +966,17 @@ class DsviEngine:
             # them right after bwd_w.  On side2 they queued behind the G-prior adjoint and, in the graph,
             # shared a hardware queue with the t chain (finalize waited ~50 us for them, r02b timeline).
             # Like side2 it synchronises with the main stream only.
-            steps += [("wait", "main", "kl_done"), ("sig", "main", "bwd_w_kl"), ("wait", "side3", "bwd_w_kl")]
+            steps += [("wait", "main", "kl_done"), ("sig", "main", "bwd_w_kl")]
+            if crit:
+                steps.append(("bwd_R", "gemm", gemm("bwd_R"), "main"))
+            steps.append(("wait", "side3", "bwd_w_kl"))
             steps += lchain("side3")
+        if not (side3 and crit):
+            steps.append(("bwd_R", "gemm", gemm("bwd_R"), "main"))
         steps += [
             # (the second side stream synchronises with the main stream only: a side <-> side2 event
             # edge made hipGraph instantiation crash on this stack; the KL prior adjoints are long done
             # when bwd_R finishes, so the main stream's wait on them costs nothing)
-            ("bwd_R", "gemm", gemm("bwd_R"), "main"),
             ("wait", "main", "kl_done"),
             ("sig", "main", "R_G"),
             ("bwd_build12", "pairwise_bwd", pw("bwd_build12"), "main"),
@@ -980,6 +1003,10 @@ class DsviEngine:
             # with the third side stream, 0.94 ms per step; more cross-queue edges)
             ("wait", "main", "g22"),
             ("sig", "main", "tb"),
+        ]
+        if crit:
+            steps.append(("bwd_t1", "gemm", gemm("bwd_t1"), "main"))
+        steps += [
             ("wait", "side", "tb"),
             ("bwd_vt", "gemm", gemm("bwd_vt"), "side"),
             ("vbwd", "row", row(getattr(lib, "nmgp_dsvi_vbwd_" + self.sfx)), "side"),
@@ -987,7 +1014,10 @@ class DsviEngine:
             ("bwd_v2", "gemm", gemm("bwd_v2"), "side"),
             ("mugrad", "row", row(getattr(lib, "nmgp_dsvi_mugrad_" + self.sfx)), "side"),
             ("sig", "side", "v_done"),
-            ("bwd_t1", "gemm", gemm("bwd_t1"), "main"),
+        ]
+        if not crit:
+            steps.append(("bwd_t1", "gemm", gemm("bwd_t1"), "main"))
+        steps += [
             ("bwd_t2", "gemm", gemm("bwd_t2"), "main"),
             ("bwd_tbuild", "pairwise_bwd", (pw64 if self.p64 else pw)("bwd_tbuild"), "main"),
             ("wait", "main", "v_done"),

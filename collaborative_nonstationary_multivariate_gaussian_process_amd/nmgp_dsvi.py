@@ -777,9 +777,15 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
         Y_test_vec = np.concatenate(Y_test_list)
         test_prep = _pred.prepare_inputs(model, [np.asarray(x, np.float64) for x in X_test_list])
         Y_test_dev = torch.as_tensor(np.asarray(Y_test_vec, np.float64)).to(model.device_)
+        # one prediction plan for the whole run (buffers, descriptors; with the device pipeline a HIP graph
+        # replayed after every iteration), its Cholesky info words checked at the loop's check points
+        test_plan = _pred.PredictPlan(model, test_prep, graph=(noise == "device"))
+        model._pending_info.append(test_plan.info_acc)
 
         def _test_rmse():
-            est = _pred.predict_mean(model, None, prepared=test_prep, defer_check=True)
+            est = test_plan()
+            if not any(t is test_plan.info_acc for t in model._pending_info):
+                model._pending_info.append(test_plan.info_acc)
             rmse_dev.append(torch.sqrt(torch.mean((est[:, None] - Y_test_dev) ** 2)))
     Q = dim_outputs * (dim_outputs + 1) // 2
     pipe = None

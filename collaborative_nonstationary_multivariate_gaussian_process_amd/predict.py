@@ -15,17 +15,6 @@ F64 = torch.float64
 JIT = 1e-4
 
 
-def _solve_rows(K12, K22, rhs, infos):
-    """K12 (K22 + 1e-4 I)^{-1} rhs  for rhs (M, k): Cholesky -> inverse -> two GEMMs.  The Cholesky
-    info word is appended to `infos` (checked by the caller: no host synchronisation here)."""
-    A = K22.clone()
-    A.diagonal().add_(JIT)
-    Ci, info = H.chol_inv_(A)
-    infos.append(info)
-    Ainv = H.matmul(Ci, Ci, transA=True, maskA=L.A_UPPER, maskB=L.B_LOWER)
-    return H.matmul(K12, H.matmul(Ainv, rhs))
-
-
 def prepare_inputs(model, inputs_list, index=None):
     """Device copies of the prediction inputs (x as a column, the output id of every row): made once
     when the same test inputs are predicted every iteration (inference(X_test_list=...))."""
@@ -37,52 +26,111 @@ def prepare_inputs(model, inputs_list, index=None):
     return x, I
 
 
-def _rbf(model, hyp64, a, b, k):
-    """RBF kernel of prior k (0: tilde-ell, 1: L0, 2: L1) with its hyper-parameters read ON THE DEVICE
-    (log scale, from the fp64 copy of theta's 7 hyper-parameters): no host round trip."""
-    out = torch.empty(a.shape[0], b.shape[0], dtype=F64, device=a.device)
-    H.PairwiseGroup([H.pairwise_desc(out, a, b, mode=L.RBF, hyp=hyp64, hyp_off=2 * k, hyp_log=True)],
-                    a.device)(F64)
-    return out
+class PredictPlan:
+    """NMGP.predict_Y (code/nmgp_dsvi.py:666-722) for one fixed set of prediction inputs, in fp64.
+
+    The four GP systems of the prediction -- the three RBF priors (tilde-ell, L0, L1) and the Gibbs prior,
+    whose K22 needs only ell_Z = exp(mu_v) -- are built by ONE pairwise launch (K22 + 1e-4 I and the three
+    RBF cross kernels) and factored by ONE batched fused Cholesky + inverse launch; each solve
+    K12 (K22 + 1e-4 I)^{-1} rhs is K12 (C^-T (C^-1 rhs)).  Buffers and kernel descriptors are made once, the
+    hyper-parameters and means are read from theta on the device when the plan runs, so with graph=True the
+    whole prediction is one HIP graph replay (inference(X_test_list=...) predicts after every iteration,
+    code/nmgp_dsvi.py:865-868).  `info_acc` keeps the largest Cholesky info word of every run since the
+    plan was made (0: all factorizations succeeded)."""
+
+    def __init__(self, model, prepared, graph=False):
+        self.model = model
+        self.x, self.I = prepared
+        dev, D, M = model.device_, model.D, model.M
+        Bn = self.x.shape[0]
+        Z = model.Z.to(F64)
+        self.Z = Z
+        e = lambda *shape: torch.empty(*shape, dtype=F64, device=dev)
+        self.K22, self.Ci, self.K12 = e(4, M, M), e(4, M, M), e(3, Bn, M)
+        self.KG12, self.ellZ, self.ellX, self.hyp64 = e(Bn, M), e(M), e(Bn), e(7)
+        self.info = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.info_acc = torch.zeros(4, dtype=torch.int32, device=dev)
+        descs = [H.pairwise_desc(self.K22[k], Z, Z, mode=L.RBF, hyp=self.hyp64, hyp_off=2 * k, hyp_log=True,
+                                 diag_add=JIT) for k in range(3)]
+        descs.append(H.pairwise_desc(self.K22[3], Z, Z, mode=L.GIBBS, ellX=self.ellZ, ellZ=self.ellZ, diag_add=JIT))
+        descs += [H.pairwise_desc(self.K12[k], self.x, Z, mode=L.RBF, hyp=self.hyp64, hyp_off=2 * k, hyp_log=True)
+                  for k in range(3)]
+        self.build = H.PairwiseGroup(descs, dev)
+        self.build_g12 = H.PairwiseGroup([H.pairwise_desc(self.KG12, self.x, Z, mode=L.GIBBS, ellX=self.ellX,
+                                                          ellZ=self.ellZ)], dev)
+        self.rows = torch.arange(Bn, device=dev)
+        self.diag = torch.eye(D, dtype=torch.bool, device=dev).reshape(-1)
+        if model.packed:
+            ii, jj = np.tril_indices(D)
+            self.pair_ij = (torch.from_numpy(ii).to(dev), torch.from_numpy(jj).to(dev))
+        self.graph, self.est = None, None
+        if graph:
+            cur = torch.cuda.current_stream(dev)
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(cur)
+            with torch.cuda.stream(s):
+                self._body()                    # warm-up: library load, GEMM paths, allocator pool
+            cur.wait_stream(s)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.est = self._body()
+
+    def _solve(self, k, K12, rhs):
+        """K12 (K22_k + 1e-4 I)^{-1} rhs = K12 C_k^-T (C_k^-1 rhs), C_k^-1 lower triangular."""
+        Ck = self.Ci[k]
+        y = H.matmul(Ck, rhs, maskA=L.A_LOWER)
+        y = H.matmul(Ck, y, transA=True, maskA=L.A_UPPER)
+        return H.matmul(K12, y)
+
+    def _body(self):
+        m = self.model
+        D, M = m.D, m.M
+        o = m._offs["sigma2_tildeell_log"][0]
+        self.hyp64.copy_(m._theta.detach()[o:o + 7])
+        mu_v = m.mu_v.detach().to(F64).reshape(-1)
+        torch.exp(mu_v, out=self.ellZ)
+        self.build(F64)                                                   # K22 + 1e-4 I (x4), K12 (x3)
+        H.chol_inv_(self.K22, out=self.Ci, info=self.info)                 # one batched launch
+        torch.maximum(self.info_acc, self.info, out=self.info_acc)
+        t_ell = self._solve(0, self.K12[0], mu_v.reshape(-1, 1).contiguous()).reshape(-1)
+        torch.exp(t_ell, out=self.ellX)
+        if m.packed:
+            muU = torch.zeros(D, D, M, dtype=F64, device=m.device_)
+            muU[self.pair_ij] = m.mu_U.detach().to(F64)
+        else:
+            muU = m.mu_U.detach().to(F64)
+        muU = muU.reshape(D * D, M).t().contiguous()                      # (M, D*D)
+        L0 = self._solve(1, self.K12[1], muU)                             # (B, D*D)
+        L1 = self._solve(2, self.K12[2], muU)
+        self.build_g12(F64)                                               # K_G12 from ell_X, ell_Z
+        Gm = self._solve(3, self.KG12, m.mu_W.detach().to(F64).t().contiguous())   # (B, D)
+        Bn = self.x.shape[0]
+        Lr = torch.where(self.diag, torch.exp(L1), L0).reshape(Bn, D, D)
+        Lr = torch.tril(Lr)                                               # est_L[i, j] for j <= i
+        rowsL = Lr[self.rows, self.I]                                     # (B, D): row I_n of L at n
+        return (rowsL * Gm).sum(1)
+
+    def __call__(self):
+        """The posterior means (N,) of the current parameters (no host synchronisation)."""
+        if self.graph is not None:
+            self.graph.replay()
+            return self.est
+        return self._body()
 
 
 def predict_mean(model, inputs_list, index=None, prepared=None, defer_check=False):
-    """NMGP.predict_Y (code/nmgp_dsvi.py:666-722) -> (N,) device tensor, computed in fp64.
+    """NMGP.predict_Y (code/nmgp_dsvi.py:666-722) -> (N,) device tensor, computed in fp64 (PredictPlan).
 
-    Sync-free: hyper-parameters are read on the device and the four Cholesky info words are checked
-    at the end -- or, with defer_check=True, left to the model's next check_numerics() (the caller's
-    existing synchronisation point; inference() predicts every iteration this way).  `prepared`: the
-    (x, I) of prepare_inputs for repeated predictions on the same inputs."""
-    dev = model.device_
-    D, M = model.D, model.M
-    x, I = prepared if prepared is not None else prepare_inputs(model, inputs_list, index)
-    Z = model.Z
-    th = {k: getattr(model, k).detach().to(F64) for k in ["mu_W", "mu_v", "mu_U"]}   # predicts in fp64
-    o = model._offs["sigma2_tildeell_log"][0]
-    hyp64 = model._theta.detach()[o:o + 7].to(F64)
-    infos = []
-    Kt12, Kt22 = _rbf(model, hyp64, x, Z, 0), _rbf(model, hyp64, Z, Z, 0)
-    v = th["mu_v"].reshape(-1, 1).contiguous()
-    t_ell = _solve_rows(Kt12, Kt22, v, infos).reshape(-1)
-    ellZ, ellX = torch.exp(v.reshape(-1)), torch.exp(t_ell)
-    K012, K022 = _rbf(model, hyp64, x, Z, 1), _rbf(model, hyp64, Z, Z, 1)
-    K112, K122 = _rbf(model, hyp64, x, Z, 2), _rbf(model, hyp64, Z, Z, 2)
-    muU = model.mu_U_dense().to(F64).reshape(D * D, M).t().contiguous()   # (M, D*D)
-    L0 = _solve_rows(K012, K022, muU, infos)                            # (B, D*D)
-    L1 = _solve_rows(K112, K122, muU, infos)
-    KG12 = H.pairwise(x, Z, mode=L.GIBBS, ellX=ellX, ellZ=ellZ)
-    KG22 = H.pairwise(Z, Z, mode=L.GIBBS, ellX=ellZ, ellZ=ellZ)
-    Gm = _solve_rows(KG12, KG22, th["mu_W"].t().contiguous(), infos)   # (B, D)
-    Bn = x.shape[0]
-    Lr = torch.where(torch.eye(D, dtype=torch.bool, device=dev).reshape(-1), torch.exp(L1), L0).reshape(Bn, D, D)
-    Lr = torch.tril(Lr)                                                 # est_L[i, j] for j <= i
-    rowsL = Lr[torch.arange(Bn, device=dev), I]                          # (B, D): row I_n of L at n
-    info = torch.cat(infos)
+    The four Cholesky info words are checked at the end -- or, with defer_check=True, left to the model's
+    next check_numerics() (the caller's existing synchronisation point).  `prepared`: the (x, I) of
+    prepare_inputs."""
+    plan = PredictPlan(model, prepared if prepared is not None else prepare_inputs(model, inputs_list, index))
+    est = plan()
     if defer_check:
-        model._pending_info.append(info)
-    elif int(info.abs().max().cpu()) != 0:
+        model._pending_info.append(plan.info_acc)
+    elif int(plan.info_acc.max().cpu()) != 0:
         raise torch.linalg.LinAlgError("cholesky: K22 + 1e-4 I is not positive-definite")
-    return (rowsL * Gm).sum(1)
+    return est
 
 
 # ==================================================================================== sampling (§8f f1)

@@ -38,26 +38,45 @@ def child(spec):
     side, side2 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
     S = {"m": main, "s": side, "s2": side2}
     x = {k: torch.ones(1 << 16, device=dev) for k in S}
+    # PROBE_OP=hip: the per-stream op is the library's own counter kernel launched through ctypes on the
+    # current stream (no torch op, no allocator query) instead of an in-place torch op
+    hip_op = os.environ.get("PROBE_OP") == "hip"
+    if hip_op:
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from collaborative_nonstationary_multivariate_gaussian_process_amd import hip_ops as H
+        ctr = {k: torch.zeros(1, dtype=torch.int64, device=dev) for k in S}
+
+    def op(k, kind):
+        if hip_op:
+            H.counter_add_(ctr[k], 1)
+        elif kind == "mul":
+            x[k].mul_(1.5)
+        else:
+            x[k].add_(1.0)
     edges = [e for e in spec.split(",") if e and "->" in e]
     nojoin = {e.split("_", 1)[1] for e in spec.split(",") if e.startswith("nojoin_")}
     g = torch.cuda.CUDAGraph()
     with torch.cuda.stream(main):
         torch.cuda.synchronize()
-        g.capture_begin()
+        print("stage capture_begin", flush=True)
+        g.capture_begin(capture_error_mode=os.environ.get("PROBE_CAPTURE_MODE", "global"))
         fork = torch.cuda.Event()
         fork.record(main)
         for k in ("s", "s2"):
             S[k].wait_event(fork)
         for k in S:                                  # one op per stream before the edges
             with torch.cuda.stream(S[k]):
-                x[k].mul_(1.5)
+                op(k, "mul")
+        keep = []                                    # PROBE_KEEP_EVENTS=1: no event is freed before capture_end
         for e in edges:                              # record on the source, wait on the destination, op after
             a, b = e.split("->")
             ev = torch.cuda.Event()
+            if os.environ.get("PROBE_KEEP_EVENTS") == "1":
+                keep.append(ev)
             ev.record(S[a])
             S[b].wait_event(ev)
             with torch.cuda.stream(S[b]):
-                x[b].add_(1.0)
+                op(b, "add")
         for k in ("s", "s2"):                        # join the side streams back to main
             if k in nojoin:
                 continue
@@ -68,7 +87,9 @@ def child(spec):
             ev = torch.cuda.Event()
             ev.record(side2)
             main.wait_event(ev)
+        print("stage capture_end", flush=True)
         g.capture_end()
+    print("stage replay", flush=True)
     g.replay()
     torch.cuda.synchronize()
     print("ok", float(x["m"][0]), float(x["s"][0]), float(x["s2"][0]))

@@ -6,7 +6,12 @@
 // ("ping_pong") segfaulting through torch; this takes torch out of the picture.
 //
 //   hipcc --offload-arch=gfx950 -O2 tools/graph_edge_repro.hip -o tools/bin/graph_edge_repro
-//   tools/bin/graph_edge_repro <pattern>   pattern: ping_pong | one_way | relay
+//   tools/bin/graph_edge_repro <pattern> [global] [autofree]   pattern: ping_pong | one_way | relay
+//   global: hipStreamCaptureModeGlobal (torch's default) instead of ThreadLocal; autofree: instantiate with
+//   hipGraphInstantiateFlagAutoFreeOnLaunch through hipGraphInstantiateWithFlags (what torch's CUDAGraph uses);
+//   destroy: hipEventDestroy on each edge's event right after the wait, while the capture is still open
+//   (what Python's garbage collection of a torch.cuda.Event does mid-capture); query: hipStreamGetCaptureInfo(_v2)
+//   on the launching stream before every launch (what torch's caching allocator does for its ops)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -33,11 +38,27 @@ static void stage(const char* s) {
   std::fflush(stdout);
 }
 
+static bool g_destroy = false;   // destroy each edge's event right after the wait (still capturing)
+static bool g_query = false;     // query the capture info of the launching stream before every launch
+
+static void query(hipStream_t s) {
+  if (!g_query) return;
+  hipStreamCaptureStatus st;
+  unsigned long long id = 0;
+  hipGraph_t gr = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t nd = 0;
+  (void)hipStreamGetCaptureInfo(s, &st, &id);
+  (void)hipStreamGetCaptureInfo_v2(s, &st, &id, &gr, &deps, &nd);
+}
+
 static int edge(hipStream_t from, hipStream_t to, float* buf, float v) {
   hipEvent_t ev;
   CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   CK(hipEventRecord(ev, from));
   CK(hipStreamWaitEvent(to, ev, 0));
+  if (g_destroy) CK(hipEventDestroy(ev));
+  query(to);
   hipLaunchKernelGGL(bump, dim3(4), dim3(256), 0, to, buf, v);
   CK(hipGetLastError());
   return 0;
@@ -45,6 +66,14 @@ static int edge(hipStream_t from, hipStream_t to, float* buf, float v) {
 
 int main(int argc, char** argv) {
   const char* pat = argc > 1 ? argv[1] : "ping_pong";
+  bool global = false, autofree = false;
+  for (int i = 2; i < argc; ++i) {
+    if (!std::strcmp(argv[i], "global")) global = true;
+    if (!std::strcmp(argv[i], "autofree")) autofree = true;
+    if (!std::strcmp(argv[i], "destroy")) g_destroy = true;
+    if (!std::strcmp(argv[i], "query")) g_query = true;
+  }
+  std::printf("mode=%s instantiate=%s\n", global ? "global" : "thread_local", autofree ? "with_flags(autofree)" : "plain");
   hipStream_t m, s, s2;
   CK(hipStreamCreateWithFlags(&m, hipStreamNonBlocking));
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -59,14 +88,17 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
 
   stage("begin_capture");
-  CK(hipStreamBeginCapture(m, hipStreamCaptureModeThreadLocal));
+  CK(hipStreamBeginCapture(m, global ? hipStreamCaptureModeGlobal : hipStreamCaptureModeThreadLocal));
   hipEvent_t fork;
   CK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
   CK(hipEventRecord(fork, m));
   CK(hipStreamWaitEvent(s, fork, 0));
   CK(hipStreamWaitEvent(s2, fork, 0));
+  query(m);
   hipLaunchKernelGGL(bump, dim3(4), dim3(256), 0, m, a, 1.f);
+  query(s);
   hipLaunchKernelGGL(bump, dim3(4), dim3(256), 0, s, b, 1.f);
+  query(s2);
   hipLaunchKernelGGL(bump, dim3(4), dim3(256), 0, s2, c, 1.f);
   if (!std::strcmp(pat, "ping_pong")) {            // s -> s2, then s2 -> s
     if (edge(s, s2, c, 1.f) || edge(s2, s, b, 1.f)) return 1;
@@ -90,7 +122,10 @@ int main(int argc, char** argv) {
   std::printf("graph nodes %zu\n", nn);
   stage("instantiate");
   hipGraphExec_t ge;
-  CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  if (autofree)
+    CK(hipGraphInstantiateWithFlags(&ge, g, hipGraphInstantiateFlagAutoFreeOnLaunch));
+  else
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
   stage("launch");
   CK(hipGraphLaunch(ge, m));
   CK(hipStreamSynchronize(m));
