@@ -892,7 +892,7 @@ __device__ inline void tri_decode_par(int tp, int par, int& ib, int& jb) {
   }
 }
 
-template <typename T, int NTPW>
+template <typename T, int NTPW, int NCTL = 2>
 __device__ __attribute__((always_inline)) inline void chol3_trtri_role(T* Am, T* Xm, int n, int64_t lda,
                                                                        int64_t ldx, int par, unsigned char* smem_raw) {
   using acc_t = typename Mfma<T>::acc_t;
@@ -927,7 +927,7 @@ __device__ __attribute__((always_inline)) inline void chol3_trtri_role(T* Am, T*
   // strictly upper part of X is zero (rows of this parity; the two control words stay)
   for (int i = 2 * w + par; i < n; i += 2 * RW)
     for (int j = ((i >> 4) + 1) * 16 + lane; j < n; j += 64) {
-      if (i != 0 || j < n - 2 * kCtl<T>) Xm[(int64_t)i * ldx + j] = 0;
+      if (i != 0 || j < n - NCTL * kCtl<T>) Xm[(int64_t)i * ldx + j] = 0;
       Am[(int64_t)i * lda + j] = 0;                // strictly-upper block tiles of L (factor role reads none)
     }
   for (int kb = 0; kb < nt; ++kb) {
@@ -1189,6 +1189,330 @@ __global__ __launch_bounds__(RW * 64) void chol_inv3_kernel(T* A, int n, int64_t
     chol2_potrf_role<T, NTPW>(Am, Xm, n, lda, ldx, info, col_off, info_first, mat, smem_raw);
   } else {
     chol3_trtri_role<T, NTPW1>(Am, Xm, n, lda, ldx, role - 1, smem_raw);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Four workgroups per matrix (chol_inv7_kernel, round 3): the three-role kernel's factor workgroup spent
+// ~1.9 of its ~5.5 us per block step on the trailing SYRK of its register-resident tiles.  Here that
+// update runs on a fourth workgroup on another CU:
+//   role 0 (factor): per block step k takes block column k (the update workgroup has applied steps
+//     <= k-4 to it), applies steps k-3 .. k-1 itself from the L[:, k-3 .. k-1] it still holds in LDS
+//     (three buffers), then the panel exactly as chol2_potrf_role (lanes 0..15 the diagonal
+//     rows of every panel wave, identity rows for L_kk^-T), publishes L[:, k] and L_kk^-1 write-through.
+//     Column k+1's loads are issued right after column k's spill, so they are in flight during the panel.
+//   role 1 (update): owns the tiles of block columns >= 4 in MFMA accumulators.  Per step j it reads the
+//     published L[:, j], applies it to block column j+4 first and publishes that column (progress word
+//     hflag = j+1), then to the columns beyond.  The three-step lookahead gives its memory round trips
+//     (read L[:, j], publish column j+4) about two factor steps of slack, so the factor drains its own
+//     stores where that is free (after the next panel) and never waits on a round trip.
+//   roles 2, 3 (inverse): chol3_trtri_role, unchanged.
+// Every tile receives the same MFMA updates in the same order as in chol2_potrf_role (steps <= k-3 on the
+// update workgroup, steps k-3 .. k-1 on the factor; the accumulators round-trip through memory exactly), so L and
+// L^-1 are bit-identical to the three-role kernel's.
+template <typename T> __device__ inline unsigned long long* ctl_hflag(T* Xm, int n) {
+  return (unsigned long long*)(Xm + (n - 3 * kCtl<T>));
+}
+
+template <typename T>
+__device__ __attribute__((always_inline)) inline bool poll_word(unsigned long long* word, int need, int nt) {
+  for (int spin = 0; spin < (1 << 26); ++spin) {
+    const unsigned long long f = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (f >= kFlagTag + (unsigned long long)need && f <= kFlagTag + (unsigned long long)nt) return true;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return false;
+}
+
+template <typename T>
+__device__ __attribute__((always_inline)) inline void chol7_factor_role(T* Am, T* Xm, int n, int64_t lda,
+                                                                        int64_t ldx, int32_t* info, int col_off,
+                                                                        int info_first, int mat,
+                                                                        unsigned char* smem_raw) {
+  using acc_t = typename Mfma<T>::acc_t;
+  const int nt = (n + 15) >> 4, NR = nt * 16;
+  T* colbuf = (T*)smem_raw;            // NR x CP: block column k before its panel (local rows)
+  T* Ps0 = colbuf + NR * CP;           // 3 x NR x CP: L[:, k] in buffer k % 3 (local rows, diagonal block first)
+  T* LiT = Ps0 + 3 * NR * CP;          // 16 x CP: (L_kk^-1)^T
+  unsigned long long* flag = ctl_flag(Xm, n);
+  unsigned long long* hflag = ctl_hflag(Xm, n);
+  const __amdgpu_buffer_rsrc_t rAm = make_rsrc(Am, ((int64_t)(n - 1) * lda + n) * (int64_t)sizeof(T));
+  const __amdgpu_buffer_rsrc_t rXm = make_rsrc(Xm, ((int64_t)(n - 1) * ldx + n) * (int64_t)sizeof(T));
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  if (t == 0) __hip_atomic_store(hflag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  bool ok = true;
+  acc_t acc[2];
+  // block column k's tiles (kb + w + RW u, kb): issue their loads (out-of-range ones read 0)
+  auto load_col = [&](int kb) {
+    const int ntc = nt - kb;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int tl = w + RW * u;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gr = (kb + tl) * 16 + Mfma<T>::row(lane, r), gc = kb * 16 + (lane & 15);
+        const bool in = tl < ntc && gr < n && gc < n;
+        acc[u][r] = bload_sc1<T>(rAm, in ? (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)) : 0x80000000u);
+      }
+    }
+  };
+  lds_barrier();
+  load_col(0);
+  int first_fail = 0;
+  for (int kb = 0; kb < nt; ++kb) {
+    const int nrow = NR - kb * 16, ntc = nt - kb;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int tl = w + RW * u;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gr = (kb + tl) * 16 + Mfma<T>::row(lane, r), gc = kb * 16 + (lane & 15);
+        if (tl < ntc && !(gr < n && gc < n)) acc[u][r] = gr == gc ? (T)1 : (T)0;   // padding past n
+      }
+    }
+    // steps kb-3 .. kb-1 on this column, from L[:, kb-3 .. kb-1] in LDS (chol2_potrf_role's MFMA order)
+#pragma unroll
+    for (int back = 3; back >= 1; --back) {
+      if (kb >= back) {
+        const T* Pb = Ps0 + ((kb - back) % 3) * NR * CP;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int tl = w + RW * u;
+          if (tl < ntc) {
+            const int ra = (tl + back) * 16 + (lane & 15), rb = back * 16 + (lane & 15);
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+              const int kr = Mfma<T>::row(lane, s2);
+              acc[u] = Mfma<T>::mma(-Pb[ra * CP + kr], Pb[rb * CP + kr], acc[u]);
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int tl = w + RW * u;
+      if (tl < ntc) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) colbuf[(tl * 16 + Mfma<T>::row(lane, r)) * CP + (lane & 15)] = acc[u][r];
+      }
+    }
+    CHOL_STAMP(kb, 0);
+    // block column kb+1 (from column 4 on: the update workgroup's steps <= kb-3 applied): its loads go out
+    // now and land during the panel
+    if (kb + 1 < nt) {
+      if (kb + 1 >= 4) {
+        bool seen = true;
+        if (lane == 0) seen = poll_word<T>(hflag, kb - 2, nt);
+        ok &= seen;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      load_col(kb + 1);
+    }
+    lds_barrier();
+    CHOL_STAMP(kb, 1);
+    T* Ps = Ps0 + (kb % 3) * NR * CP;
+    if (w < (nrow + 47) / 48) {
+      int lr;
+      bool ident = false;
+      if (lane < 16) {
+        lr = lane;
+      } else {
+        const int slot = w * 48 + lane - 16;
+        ident = slot >= nrow - 16 && slot < nrow;
+        lr = ident ? slot - (nrow - 16) : 16 + slot;
+      }
+      const bool active = ident || lr < nrow;
+      T a[16];
+      {
+        const T keep = (active && !ident) ? (T)1 : (T)0;
+        const T* src = colbuf + min(lr, NR - 1) * CP;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) a[c] = fma(src[c], keep, (ident && c == lr) ? (T)1 : (T)0);
+      }
+      unsigned int bad = 0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const T d = readlane(a[j], j);
+        bad |= (d > (T)0) ? 0u : (1u << j);
+        T sj, inv;
+        sqrt_recip(d, sj, inv);
+        a[j] = (lane == j) ? sj : a[j] * inv;
+#pragma unroll
+        for (int c = j + 1; c < 16; ++c) a[c] = fma(-a[j], readlane(a[j], c), a[c]);
+      }
+      if (bad && first_fail == 0) {
+        const int j0 = __builtin_ctz(bad);
+        if (kb * 16 + j0 < n) first_fail = kb * 16 + j0 + 1;
+      }
+#pragma unroll
+      for (int c = 0; c < 16; ++c) a[c] = (lane < 16 && c > lane) ? (T)0 : a[c];
+      if (ident || (active && (lane >= 16 || w == 0))) {
+        T* dst = (ident ? LiT : Ps) + lr * CP;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) dst[c] = a[c];
+      }
+    }
+    // the stores of L[:, kb-1] had the whole panel to drain (and column kb+1's loads have landed): wait
+    // for them here, where it is free, and raise the progress word
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    if (t == 0 && kb > 0)
+      __hip_atomic_store(flag, kFlagTag + (unsigned long long)kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    CHOL_STAMP(kb, 2);
+    // publish L[:, kb] (final output) and L_kk^-1 (= the final X[kb, kb]) write-through
+    for (int idx = t; idx < nrow * 16; idx += RW * 64) {
+      const int lr = idx >> 4, c = idx & 15;
+      const int gr = kb * 16 + lr, gc = kb * 16 + c;
+      if (gr < n && gc < n) bstore_sc1<T>(rAm, (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)), Ps[lr * CP + c]);
+    }
+    if (t < 256) {
+      const int r = t >> 4, c = t & 15;
+      const int gr = kb * 16 + r, gc = kb * 16 + c;
+      if (gr < n && gc < n) bstore_sc1<T>(rXm, (uint32_t)(((int64_t)gr * ldx + gc) * sizeof(T)), LiT[c * CP + r]);
+    }
+    CHOL_STAMP(kb, 3);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+  if (t == 0) {
+    __hip_atomic_store(flag, kFlagTag + (unsigned long long)nt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(hflag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // no reader left
+    if (info) {
+      if (info_first) info[mat] = first_fail ? first_fail + col_off : 0;
+      else if (first_fail && info[mat] == 0) info[mat] = first_fail + col_off;
+    }
+  }
+  if (lane == 0 && !ok) spin_gave_up(NMGP_STATUS_CHOL_SPIN);
+}
+
+template <typename T, int NTPW>
+__device__ __attribute__((always_inline)) inline void chol7_update_role(T* Am, T* Xm, int n, int64_t lda,
+                                                                        unsigned char* smem_raw) {
+  using acc_t = typename Mfma<T>::acc_t;
+  const int nt = (n + 15) >> 4, NR = nt * 16;
+  T* Ps = (T*)smem_raw;                // NR x CP: L[:, j] (local rows)
+  unsigned long long* flag = ctl_flag(Xm, n);
+  unsigned long long* hflag = ctl_hflag(Xm, n);
+  const __amdgpu_buffer_rsrc_t rAm = make_rsrc(Am, ((int64_t)(n - 1) * lda + n) * (int64_t)sizeof(T));
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  // the lower tiles of block columns >= 4 (ib >= jb >= 4), distributed over the waves
+  const int nt4 = nt - 4, ntiles = nt4 > 0 ? nt4 * (nt4 + 1) / 2 : 0;
+  int tij[NTPW];
+  acc_t acc[NTPW];
+#pragma unroll
+  for (int u = 0; u < NTPW; ++u) {
+    const int tt = w + RW * u;
+    int i_ = -1, j_ = -1;
+    if (tt < ntiles) {
+      tri_decode(tt, i_, j_);
+      i_ += 4;
+      j_ += 4;
+    }
+    tij[u] = tt < ntiles ? (i_ << 8) | j_ : -1;
+  }
+#define IB7(u) (tij[u] < 0 ? -1 : (tij[u] >> 8))
+#define JB7(u) (tij[u] < 0 ? -1 : (tij[u] & 255))
+#pragma unroll
+  for (int u = 0; u < NTPW; ++u) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gr = IB7(u) * 16 + Mfma<T>::row(lane, r), gc = JB7(u) * 16 + (lane & 15);
+      const bool in = IB7(u) >= 0 && gr < n && gc < n;
+      acc[u][r] = bload<T>(rAm, in ? (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)) : 0x80000000u);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NTPW; ++u) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gr = IB7(u) * 16 + Mfma<T>::row(lane, r), gc = JB7(u) * 16 + (lane & 15);
+      if (IB7(u) >= 0 && !(gr < n && gc < n)) acc[u][r] = gr == gc ? (T)1 : (T)0;   // padding past n
+    }
+  }
+  bool ok = true;
+  constexpr int PER = 256 * 16 / (RW * 64);
+  for (int j = 0; j + 4 < nt; ++j) {
+    const int nrow = NR - j * 16;
+    if (t == 0) ok &= poll_word<T>(flag, j + 1, nt);              // L[:, j] published and drained
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    {
+      T v[PER];
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int idx = t + q * RW * 64, lr = idx >> 4, c = idx & 15;
+        const int gr = j * 16 + lr, gc = j * 16 + c;
+        const uint32_t off =
+            (idx < nrow * 16 && gr < n && gc < n) ? (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)) : 0x80000000u;
+        v[q] = bload_sc1<T>(rAm, off);
+      }
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int idx = t + q * RW * 64;
+        if (idx < nrow * 16) Ps[(idx >> 4) * CP + (idx & 15)] = v[q];
+      }
+    }
+    lds_barrier();
+    // 1. block column j+4 first, then out to the factor workgroup
+#pragma unroll
+    for (int u = 0; u < NTPW; ++u) {
+      if (JB7(u) == j + 4) {
+        const int ra = __builtin_amdgcn_readfirstlane(IB7(u) - j) * 16 + (lane & 15);
+        const int rb = 64 + (lane & 15);
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const int kr = Mfma<T>::row(lane, s2);
+          acc[u] = Mfma<T>::mma(-Ps[ra * CP + kr], Ps[rb * CP + kr], acc[u]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gr = IB7(u) * 16 + Mfma<T>::row(lane, r), gc = JB7(u) * 16 + (lane & 15);
+          if (gr < n && gc < n) bstore_sc1<T>(rAm, (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)), acc[u][r]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(hflag, kFlagTag + (unsigned long long)(j + 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    // 2. the columns beyond
+#pragma unroll
+    for (int u = 0; u < NTPW; ++u) {
+      if (JB7(u) > j + 4) {
+        const int ra = __builtin_amdgcn_readfirstlane(IB7(u) - j) * 16 + (lane & 15);
+        const int rb = __builtin_amdgcn_readfirstlane(JB7(u) - j) * 16 + (lane & 15);
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const int kr = Mfma<T>::row(lane, s2);
+          acc[u] = Mfma<T>::mma(-Ps[ra * CP + kr], Ps[rb * CP + kr], acc[u]);
+        }
+      }
+    }
+    lds_barrier();                     // Ps is rewritten by the next step
+  }
+  if (!ok && t == 0) spin_gave_up(NMGP_STATUS_CHOL_SPIN);
+#undef IB7
+#undef JB7
+}
+
+template <typename T, int NTPW, int NTPW1, int NTPWU>
+__global__ __launch_bounds__(RW * 64) void chol_inv7_kernel(T* A, int n, int64_t lda, int64_t strideA, T* X,
+                                                            int64_t ldx, int64_t strideX, int32_t* info, int col_off,
+                                                            int info_first) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int mat = blockIdx.x / 4, role = blockIdx.x - 4 * mat;
+  T* Am = A + (int64_t)mat * strideA;
+  T* Xm = X + (int64_t)mat * strideX;
+  if (role == 0) {
+    if (threadIdx.x == 0) __hip_atomic_store(ctl_done(Xm, n), kDoneTag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    chol7_factor_role<T>(Am, Xm, n, lda, ldx, info, col_off, info_first, mat, smem_raw);
+  } else if (role == 1) {
+    chol7_update_role<T, NTPWU>(Am, Xm, n, lda, smem_raw);
+  } else {
+    chol3_trtri_role<T, NTPW1, 3>(Am, Xm, n, lda, ldx, role - 2, smem_raw);
   }
 }
 
@@ -1694,6 +2018,31 @@ static void chol_inv4_go(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx
                      lda, sA, X, ldx, sX, info, col_off, info_first);
 }
 
+template <typename T, int NTPW1, int NTPWU>
+static void chol_inv7_go(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx, int64_t sX, int64_t batch,
+                         int32_t* info, size_t sm, hipStream_t s, int col_off, int info_first) {
+  static bool attr_done = false;
+  if (!attr_done) {
+    (void)hipFuncSetAttribute((const void*)chol_inv7_kernel<T, 1, NTPW1, NTPWU>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_done = true;
+  }
+  hipLaunchKernelGGL((chol_inv7_kernel<T, 1, NTPW1, NTPWU>), dim3((unsigned)(4 * batch)), dim3(RW * 64), sm, s, A, n,
+                     lda, sA, X, ldx, sX, info, col_off, info_first);
+}
+
+// Four-role kernel (separate update workgroup): the default from n = 192 (at n = 256 f64: 85-88 us against
+// the three-role kernel's 95-97 us per launch, PM2.5 step 1317-1320 -> 1339-1381 it/s in an A/B on the box;
+// at n = 128 f32 it is slower, 31 against 27 us: the update workgroup has too few columns to run ahead).
+// NMGP_CHOL_4ROLE=0 / 1 forces it off / on for 128 <= n <= 256 (read per launch: tests switch it
+// in-process).  Its four workgroups per matrix must be co-resident: at most 64 matrices per launch.
+static bool use_four_role(int n, int64_t batch) {
+  if (n < 128 || n > 256 || batch > 64) return false;
+  const char* e = getenv("NMGP_CHOL_4ROLE");
+  if (e) return atoi(e) != 0;
+  return n >= 192;
+}
+
 // The lookahead factor role (chol_inv4_kernel) is the default wherever the three-role kernel runs;
 // NMGP_CHOL_LA=0 restores chol_inv3_kernel (A/B).
 static bool use_lookahead() {
@@ -1717,6 +2066,18 @@ static int chol_inv_small(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ld
   const size_t sm = chol_inv_smem<T>(n) > sm_min ? chol_inv_smem<T>(n) : sm_min;
   // multi-role kernels (f64 always; f32 when the control words can be 8-byte aligned, round 2)
   if (chol_ctl_ok<T>(n, X, sX)) {
+    if (two_role && use_four_role(n, batch) && !getenv("NMGP_CHOL_FUSED1")) {
+      const size_t sm7 = sm + (size_t)(((n + 15) >> 4) * 16 * CP) * sizeof(T);   // + the third L buffer
+      // inverse-role tiles as the three-role kernel's thresholds; update-role tiles: (nt-4)(nt-3)/2 <= RW*10
+      if (ntiles <= RW * 5)
+        chol_inv7_go<T, 3, 2>(A, n, lda, sA, X, ldx, sX, batch, info, sm7, s, col_off, info_first);
+      else if (ntiles <= RW * 9)
+        chol_inv7_go<T, 5, 4>(A, n, lda, sA, X, ldx, sX, batch, info, sm7, s, col_off, info_first);
+      else
+        chol_inv7_go<T, 9, 10>(A, n, lda, sA, X, ldx, sX, batch, info, sm7, s, col_off, info_first);
+      NMGP_CHECK_LAUNCH();
+      return NMGP_OK;
+    }
     if (two_role && use_three_role(n, batch) && !getenv("NMGP_CHOL_FUSED1") && use_lookahead()) {
       const size_t sm4 = chol_inv4_smem<T>(n) > sm_min ? chol_inv4_smem<T>(n) : sm_min;
       // update-wave tiles ceil(ntiles / kUpdW); inverse-role tiles as the three-role kernel's thresholds

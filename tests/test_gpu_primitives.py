@@ -304,10 +304,40 @@ def test_chol_inv_lookahead_matches_three_role(ops, n, batch, dt, monkeypatch):
     if batch > 2:
         A[1, n // 2, n // 2] = -5.0                    # not PD from column n // 2 on
     res = []
+    monkeypatch.setenv("NMGP_CHOL_4ROLE", "0")         # (the four-role kernel would run in both)
     for la in ("1", "0"):
         monkeypatch.setenv("NMGP_CHOL_LA", la)
         Ad = A.clone().to(DEV)
         X, info = ops.chol_inv_(Ad)
+        torch.cuda.synchronize()
+        res.append((Ad.cpu(), X.cpu(), info.cpu()))
+    (L1, X1, i1), (L0, X0, i0) = res
+    assert torch.equal(i1, i0)
+    if batch > 2:
+        assert int(i1[1]) == n // 2 + 1 and int(i1[0]) == 0
+    ok = [b for b in range(batch) if int(i1[b]) == 0]
+    assert torch.equal(L1[ok], L0[ok]) and torch.equal(X1[ok], X0[ok])
+    ref = torch.linalg.cholesky(A[ok].double())
+    tl, tx = (1e-13, 1e-11) if dt == F64 else (1e-5, 1e-4)
+    assert rel(L1[ok], ref) < tl and rel(X1[ok], torch.linalg.inv(ref)) < tx
+    assert float(torch.triu(L1[ok], 1).abs().max()) == 0.0 and float(torch.triu(X1[ok], 1).abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("n,batch", [(128, 1), (176, 3), (192, 2), (250, 1), (256, 1), (256, 4), (256, 25)])
+@pytest.mark.parametrize("dt", [F64, torch.float32])
+def test_chol_inv_four_role_matches_three_role(ops, n, batch, dt, monkeypatch):
+    """The four-role kernel (chol_inv7_kernel: the trailing update on its own workgroup, the factor applies
+    only the last step to each block column) gives every tile the three-role kernel's MFMA updates in the
+    same order: L and L^-1 bit-identical, the same info for a non-PD matrix, control words cleared."""
+    A = _spd(n, batch, 13 * n + batch).to(dt)
+    if batch > 2:
+        A[1, n // 2, n // 2] = -5.0                    # not PD from column n // 2 on
+    res = []
+    for four in ("1", "0"):
+        monkeypatch.setenv("NMGP_CHOL_4ROLE", four)
+        Ad = A.clone().to(DEV)
+        X = torch.full_like(Ad, float("nan"))          # stale control words must not pass for progress
+        X, info = ops.chol_inv_(Ad, out=X)
         torch.cuda.synchronize()
         res.append((Ad.cpu(), X.cpu(), info.cpu()))
     (L1, X1, i1), (L0, X0, i0) = res

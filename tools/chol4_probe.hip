@@ -70,6 +70,19 @@ int main(int argc, char** argv) {
   std::vector<unsigned long long> tr(4096);
   HC(hipMemcpy(tr.data(), dtr, 4096 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   printf("n=%d batch=%d  launch %.2f us (event, avg of %d)  info0=%d\n", n, batch, 1000.0 * tot / reps, reps, info[0]);
+  if (getenv("NMGP_CHOL_4ROLE")) {
+    // four-role kernel: the factor workgroup's CHOL_STAMP(kb, p): 1 column spilled, 2 panel done, 3 publish
+    // issued + next column's loads issued (relative to the first stamp)
+    unsigned long long b0 = ~0ull;
+    for (int i = 0; i < 256; ++i)
+      if (tr[i] && tr[i] < b0) b0 = tr[i];
+    printf("  k | factor: mfma+spill  polled+barrier  panel  publish\n");
+    for (int k = 0; k < (n + 15) / 16; ++k) {
+      auto r = [&](int p) { return tr[k * 4 + p] ? (double)(long long)(tr[k * 4 + p] - b0) / 100.0 : -1.0; };
+      printf("%3d | %8.2f %8.2f %6.2f %6.2f\n", k, r(0), r(1), r(2), r(3));
+    }
+    return 0;
+  }
   const int nt = (n + 15) / 16;
   auto T = [&](int role, int k, int ph) { return tr[2048 + role * 512 + k * 8 + ph]; };
   // every workgroup runs on its own XCD, whose wall clock is not synchronised with the others': each

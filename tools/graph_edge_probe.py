@@ -55,7 +55,8 @@ def child(spec):
             x[k].add_(1.0)
     edges = [e for e in spec.split(",") if e and "->" in e]
     nojoin = {e.split("_", 1)[1] for e in spec.split(",") if e.startswith("nojoin_")}
-    g = torch.cuda.CUDAGraph()
+    keep_graph = os.environ.get("PROBE_KEEP_GRAPH") == "1"
+    g = torch.cuda.CUDAGraph(keep_graph=True) if keep_graph else torch.cuda.CUDAGraph()
     with torch.cuda.stream(main):
         torch.cuda.synchronize()
         print("stage capture_begin", flush=True)
@@ -89,6 +90,23 @@ def child(spec):
             main.wait_event(ev)
         print("stage capture_end", flush=True)
         g.capture_end()
+    if keep_graph:
+        # PROBE_KEEP_GRAPH=1: capture_end leaves the hipGraph_t uninstantiated; dump its topology (nodes and
+        # edges as a dot file through hipGraphDebugDotPrint), then instantiate it as a separate stage
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        raw = ctypes.c_void_p(g.raw_cuda_graph())
+        n = ctypes.c_size_t(0)
+        print("stage got_graph rc", hip.hipGraphGetNodes(raw, None, ctypes.byref(n)), "nodes", n.value, flush=True)
+        path = f"/tmp/graph_probe_{os.getpid()}.dot"
+        rc = hip.hipGraphDebugDotPrint(raw, path.encode(), 0)
+        print("stage dot rc", rc, flush=True)
+        if os.path.exists(path):
+            for line in open(path):
+                if "->" in line or "label" in line:
+                    print("DOT", line.strip()[:160], flush=True)
+        print("stage instantiate", flush=True)
+        g.instantiate()
     print("stage replay", flush=True)
     g.replay()
     torch.cuda.synchronize()
@@ -104,7 +122,7 @@ def main(names):
         p = subprocess.run([sys.executable, __file__, "--child", PATTERNS[name]], env=env, capture_output=True,
                            text=True, timeout=120)
         rec = {"pattern": name, "spec": PATTERNS[name], "rc": p.returncode,
-               "out": p.stdout.strip()[-200:], "err": p.stderr.strip()[-400:]}
+               "out": p.stdout.strip()[-int(os.environ.get("PROBE_OUT_CHARS", "200")):], "err": p.stderr.strip()[-400:]}
         print(json.dumps(rec), flush=True)
         if p.returncode != 0:
             break                                    # nothing more on the GPU after a crash
