@@ -74,10 +74,24 @@ int main(int argc, char** argv) {
     if (!std::strcmp(argv[i], "query")) g_query = true;
   }
   std::printf("mode=%s instantiate=%s\n", global ? "global" : "thread_local", autofree ? "with_flags(autofree)" : "plain");
+  std::fflush(stdout);
   hipStream_t m, s, s2;
-  CK(hipStreamCreateWithFlags(&m, hipStreamNonBlocking));
-  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+  int prio = 0;
+  bool use_prio = false;
+  for (int i = 2; i < argc; ++i)
+    if (!std::strncmp(argv[i], "prio=", 5)) {
+      use_prio = true;
+      prio = atoi(argv[i] + 5);
+    }
+  if (use_prio) {   // what torch's stream pool does (cudaStreamCreateWithPriority, non-blocking)
+    CK(hipStreamCreateWithPriority(&m, hipStreamNonBlocking, prio));
+    CK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio));
+    CK(hipStreamCreateWithPriority(&s2, hipStreamNonBlocking, prio));
+  } else {
+    CK(hipStreamCreateWithFlags(&m, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+  }
   float *a, *b, *c;
   CK(hipMalloc(&a, 4096));
   CK(hipMalloc(&b, 4096));
