@@ -71,6 +71,7 @@ class DsviArgs(ctypes.Structure):
 # flags (include/nmgp_hip.h)
 A_LOWER, A_UPPER, B_LOWER, B_UPPER = 1, 2, 4, 8
 OUT_LOWER, OUT_TRIL, KSCALE, EPI, EPI_E_LOWER, DIAG_ADD, EPI_RS_NEG = 16, 32, 64, 128, 256, 512, 1024
+LAT_COLPACK = 2048
 RBF, GIBBS = 0, 1
 DIST_DIFF, DIST_EXPAND = 0, 1
 HYP_LOG = 1

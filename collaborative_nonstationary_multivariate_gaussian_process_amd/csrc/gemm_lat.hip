@@ -91,30 +91,65 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
     k0 = args.seg[d.k_seg];
     K = args.seg[d.k_seg + span] - (int)k0;
   }
-  const int n = d.n, i0 = tm * LTM, j0 = tn * LTN;
+  const int n = d.n, i0 = tm * LTM;
   if (i0 >= m) return;
   const int flags = d.flags;
-  const bool above = j0 > i0 + LTM - 1;
-  if (above && (flags & NMGP_OUT_LOWER)) return;
-  const bool zero_tile = above && (flags & NMGP_OUT_TRIL);
+  // The output tiles of this workgroup: one, or with NMGP_LAT_COLPACK (a B-triangular problem whose column
+  // tiles have k ranges of 1..T panels) a group of up to two column tiles whose panels add up to <= LW:
+  // group 0 = {0}, g = 1..h = {g, T-g}, and for even T the middle tile alone (B_UPPER mirrored).  Wave w takes
+  // panel w of the group's concatenated panel list, so no wave idles on a short-k tile.
+  int jt[2] = {tn, -1};
+  const bool pack = (flags & NMGP_LAT_COLPACK) != 0;
+  if (pack) {
+    const int Tn = (n + LTN - 1) / LTN, h = (Tn - 1) / 2;
+    int a, b = -1;
+    if (tn == 0) a = 0;
+    else if (tn <= h) { a = tn; b = Tn - tn; }
+    else a = Tn / 2;
+    if (flags & NMGP_B_UPPER) {
+      a = Tn - 1 - a;
+      if (b >= 0) b = Tn - 1 - b;
+    }
+    jt[0] = a;
+    jt[1] = b;
+  }
   const bool blkA = d.kbA > 0 && d.kbA < K, blkB = d.kbB > 0 && d.kbB < K;
   const int kbA = blkA ? d.kbA : 0x40000000, kbB = blkB ? d.kbB : 0x40000000;
-  int kbeg = 0, kend = K;
-  if (d.k_seg < 0) {
-    if ((flags & NMGP_A_LOWER) && !blkA) kend = min(kend, i0 + LTM);
-    if ((flags & NMGP_A_UPPER) && !blkA) kbeg = max(kbeg, i0);
-    if ((flags & NMGP_B_LOWER) && !blkB) kbeg = max(kbeg, j0);
-    if ((flags & NMGP_B_UPPER) && !blkB) kend = min(kend, j0 + LTN);
+  int tkbeg[2], tkend[2], tnp[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    tkbeg[q] = 0;
+    tkend[q] = 0;
+    tnp[q] = 0;
+    if (jt[q] < 0) continue;
+    const int j0 = jt[q] * LTN;
+    const bool above = j0 > i0 + LTM - 1;
+    if (above && (flags & NMGP_OUT_LOWER)) {
+      jt[q] = -1;                        // (never with COLPACK: the host packs only unmasked outputs)
+      continue;
+    }
+    const bool zero_tile = above && (flags & NMGP_OUT_TRIL);
+    int kbeg = 0, kend = K;
+    if (d.k_seg < 0) {
+      if ((flags & NMGP_A_LOWER) && !blkA) kend = min(kend, i0 + LTM);
+      if ((flags & NMGP_A_UPPER) && !blkA) kbeg = max(kbeg, i0);
+      if ((flags & NMGP_B_LOWER) && !blkB) kbeg = max(kbeg, j0);
+      if ((flags & NMGP_B_UPPER) && !blkB) kend = min(kend, j0 + LTN);
+    }
+    kbeg = (kbeg / LKP) * LKP;
+    if (zero_tile || K <= 0) kend = kbeg;
+    if (ksplit > 1) {               // this workgroup's k chunk (whole panels)
+      const int npan_all = kend > kbeg ? (kend - kbeg + LKP - 1) / LKP : 0;
+      const int per = (npan_all + ksplit - 1) / ksplit;
+      const int cb = kbeg + ks * per * LKP;
+      kend = max(cb, min(kend, cb + per * LKP));
+      kbeg = cb;
+    }
+    tkbeg[q] = kbeg;
+    tkend[q] = kend;
+    tnp[q] = kend > kbeg ? (kend - kbeg + LKP - 1) / LKP : 0;
   }
-  kbeg = (kbeg / LKP) * LKP;
-  if (zero_tile || K <= 0) kend = kbeg;
-  if (ksplit > 1) {               // this workgroup's k chunk (whole panels)
-    const int npan_all = kend > kbeg ? (kend - kbeg + LKP - 1) / LKP : 0;
-    const int per = (npan_all + ksplit - 1) / ksplit;
-    const int cb = kbeg + ks * per * LKP;
-    kend = max(cb, min(kend, cb + per * LKP));
-    kbeg = cb;
-  }
+  if (jt[0] < 0 && jt[1] < 0) return;
 
   const int t = threadIdx.x, lane = t & 63, li = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -123,8 +158,14 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q >> 1][q & 1] = acc_t{0, 0, 0, 0};
 
-  const int npan = kend > kbeg ? (kend - kbeg + LKP - 1) / LKP : 0;
-  if (w < npan) {
+  // this wave's tile (packed: the tile whose panel range holds panel w; otherwise tile 0, panels w, w+LW, ..)
+  const int myq = (pack && w >= tnp[0]) ? 1 : 0;
+  const int pfirst = pack ? (myq ? w - tnp[0] : w) : w;
+  const int pstep = pack ? 0x40000000 : LW;
+  const int npan = (pack && myq == 1 && jt[1] < 0) ? 0 : tnp[myq];
+  const int j0 = jt[myq] < 0 ? 0 : jt[myq] * LTN;
+  const int kbeg = tkbeg[myq], kend = tkend[myq];
+  if (pfirst < npan) {
     constexpr int64_t sz = sizeof(T);
     const int nkbA = blkA ? (K + kbA - 1) / kbA : 1, kinA = blkA ? kbA : K;
     const int nkbB = blkB ? (K + kbB - 1) / kbB : 1, kinB = blkB ? kbB : K;
@@ -139,7 +180,7 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
     const uint32_t stA = (uint32_t)(d.sA_k * sz), stB = (uint32_t)(d.sB_k * sz);
     const bool aLo = flags & NMGP_A_LOWER, aUp = flags & NMGP_A_UPPER;
     const bool bLo = flags & NMGP_B_LOWER, bUp = flags & NMGP_B_UPPER;
-    for (int p = w; p < npan; p += LW) {
+    for (int p = pfirst; p < npan; p += pstep) {
       const int kp = kbeg + p * LKP;
       const int ba = kp / kbA, bb = kp / kbB;        // k-block of the panel (panels never straddle one)
       const int kkA0 = kp - ba * (blkA ? kbA : 0), kkB0 = kp - bb * (blkB ? kbB : 0);   // block-local k
@@ -201,7 +242,7 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
       }
     }
   }
-  // partial tiles of the waves -> LDS, summed in wave order
+  // partial tiles of the waves -> LDS, summed in wave order per output tile
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
 #pragma unroll
@@ -209,79 +250,86 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
       red[w * (LTM * LTN) + (16 * (q >> 1) + Mfma<T>::row(lane, r)) * LTN + 16 * (q & 1) + li] = acc[q >> 1][q & 1][r];
   }
   lds_barrier();
-  constexpr int NE = (LTM * LTN) / (64 * LW);   // output values per thread
-  T vals[NE];
-#pragma unroll
-  for (int q = 0; q < NE; ++q) {
-    const int e = t + 64 * LW * q;
-    T sum = red[e];
-#pragma unroll
-    for (int v = 1; v < LW; ++v) sum += red[v * LTM * LTN + e];
-    vals[q] = sum;
-  }
-  if (ksplit > 1) {
-    // Deterministic split-K: every chunk publishes its partial tile write-through (sc1) and, once its
-    // stores drained, bumps the tile's counter; the last arriver sums all partials in chunk order from
-    // memory (sc1 loads bypass the stale L1) and runs the epilogue.  No waiting, so no co-residency
-    // assumption; the last arriver re-arms the counter for the next launch.
-    const int tid = tm * d.tiles_n + tn;
-    T* wsb = (T*)d.ws + (int64_t)tid * ksplit * (LTM * LTN);
-    const __amdgpu_buffer_rsrc_t rws = make_rsrc(wsb, (int64_t)ksplit * (LTM * LTN) * (int64_t)sizeof(T));
-#pragma unroll
-    for (int q = 0; q < NE; ++q)
-      bstore_sc1<T>(rws, (uint32_t)(((int64_t)ks * (LTM * LTN) + t + 64 * LW * q) * (int64_t)sizeof(T)), vals[q]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* s_last = (int*)red;          // the partial tiles in LDS are consumed (vals) -- reuse a word
-    if (t == 0) {
-      int32_t* ctr = d.counters + tid;
-      const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = old == ksplit - 1;
-      if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *s_last = last;
-    }
-    __syncthreads();
-    const bool last = *s_last != 0;
-    if (!last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the loads below the counter
+  constexpr int NE = (LTM * LTN) / (64 * LW);   // output values per thread and tile
+  const int ntl = (jt[1] >= 0) ? 2 : 1;
+  for (int qt = 0; qt < ntl; ++qt) {
+    if (jt[qt] < 0) continue;
+    // waves holding this tile's partials: all (unpacked) or the tile's panel range (packed)
+    const int wb = pack ? (qt ? tnp[0] : 0) : 0;
+    const int we = pack ? (qt ? tnp[0] + tnp[1] : tnp[0]) : LW;
+    const int tj0 = jt[qt] * LTN;
+    T vals[NE];
 #pragma unroll
     for (int q = 0; q < NE; ++q) {
       const int e = t + 64 * LW * q;
-      T sum = 0;
-      for (int c = 0; c < ksplit; ++c)
-        sum += bload_sc1<T>(rws, (uint32_t)(((int64_t)c * (LTM * LTN) + e) * (int64_t)sizeof(T)));
+      T sum = we > wb ? red[wb * LTM * LTN + e] : (T)0;
+      for (int v = wb + 1; v < we; ++v) sum += red[v * LTM * LTN + e];
       vals[q] = sum;
     }
-  }
-  const GPtr<T> C = (GPtr<T>)d.C;
-  const GPtr<const T> E = (GPtr<const T>)d.epi_E;
-  const GPtr<const T> rsp = (GPtr<const T>)d.epi_rs;
-  const T alpha = (T)d.alpha, beta = (T)d.beta, gamma = (T)d.gamma, dadd = (T)d.diag_add;
+    if (ksplit > 1) {
+      // Deterministic split-K: every chunk publishes its partial tile write-through (sc1) and, once its
+      // stores drained, bumps the tile's counter; the last arriver sums all partials in chunk order from
+      // memory (sc1 loads bypass the stale L1) and runs the epilogue.  No waiting, so no co-residency
+      // assumption; the last arriver re-arms the counter for the next launch.  (Never packed.)
+      const int tid = tm * d.tiles_n + tn;
+      T* wsb = (T*)d.ws + (int64_t)tid * ksplit * (LTM * LTN);
+      const __amdgpu_buffer_rsrc_t rws = make_rsrc(wsb, (int64_t)ksplit * (LTM * LTN) * (int64_t)sizeof(T));
 #pragma unroll
-  for (int q = 0; q < NE; ++q) {
-    const int e = t + 64 * LW * q;
-    const int gi = i0 + (e / LTN), gj = j0 + (e % LTN);
-    const T sum = vals[q];
-    if (gi >= m || gj >= n) continue;
-    const bool upper = gj > gi;
-    if (upper && (flags & NMGP_OUT_LOWER)) continue;
-    const int64_t ci = (r0 + gi) * d.sC_i + (int64_t)gj * d.sC_j;
-    T val;
-    if (upper && (flags & NMGP_OUT_TRIL)) {
-      val = 0;
-    } else {
-      val = alpha * sum;
-      if (beta != (T)0) val += beta * C[ci];
-      if (flags & NMGP_EPI) {
-        T ev = 0;
-        if (!((flags & NMGP_EPI_E_LOWER) && upper)) ev = E[(r0 + gi) * d.sE_i + (int64_t)gj * d.sE_j];
-        T rs = rsp ? rsp[r0 + gi] : (T)1;
-        if (flags & NMGP_EPI_RS_NEG) rs = -rs;
-        val += gamma * rs * ev;
+      for (int q = 0; q < NE; ++q)
+        bstore_sc1<T>(rws, (uint32_t)(((int64_t)ks * (LTM * LTN) + t + 64 * LW * q) * (int64_t)sizeof(T)), vals[q]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      int* s_last = (int*)red;          // the partial tiles in LDS are consumed (vals) -- reuse a word
+      if (t == 0) {
+        int32_t* ctr = d.counters + tid;
+        const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == ksplit - 1;
+        if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_last = last;
       }
-      if ((flags & NMGP_DIAG_ADD) && gi == gj) val += dadd;
+      __syncthreads();
+      const bool last = *s_last != 0;
+      if (!last) return;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the loads below the counter
+#pragma unroll
+      for (int q = 0; q < NE; ++q) {
+        const int e = t + 64 * LW * q;
+        T sum = 0;
+        for (int c = 0; c < ksplit; ++c)
+          sum += bload_sc1<T>(rws, (uint32_t)(((int64_t)c * (LTM * LTN) + e) * (int64_t)sizeof(T)));
+        vals[q] = sum;
+      }
     }
-    C[ci] = val;
+    const GPtr<T> C = (GPtr<T>)d.C;
+    const GPtr<const T> E = (GPtr<const T>)d.epi_E;
+    const GPtr<const T> rsp = (GPtr<const T>)d.epi_rs;
+    const T alpha = (T)d.alpha, beta = (T)d.beta, gamma = (T)d.gamma, dadd = (T)d.diag_add;
+#pragma unroll
+    for (int q = 0; q < NE; ++q) {
+      const int e = t + 64 * LW * q;
+      const int gi = i0 + (e / LTN), gj = tj0 + (e % LTN);
+      const T sum = vals[q];
+      if (gi >= m || gj >= n) continue;
+      const bool upper = gj > gi;
+      if (upper && (flags & NMGP_OUT_LOWER)) continue;
+      const int64_t ci = (r0 + gi) * d.sC_i + (int64_t)gj * d.sC_j;
+      T val;
+      if (upper && (flags & NMGP_OUT_TRIL)) {
+        val = 0;
+      } else {
+        val = alpha * sum;
+        if (beta != (T)0) val += beta * C[ci];
+        if (flags & NMGP_EPI) {
+          T ev = 0;
+          if (!((flags & NMGP_EPI_E_LOWER) && upper)) ev = E[(r0 + gi) * d.sE_i + (int64_t)gj * d.sE_j];
+          T rs = rsp ? rsp[r0 + gi] : (T)1;
+          if (flags & NMGP_EPI_RS_NEG) rs = -rs;
+          val += gamma * rs * ev;
+        }
+        if ((flags & NMGP_DIAG_ADD) && gi == gj) val += dadd;
+      }
+      C[ci] = val;
+    }
   }
 }
 

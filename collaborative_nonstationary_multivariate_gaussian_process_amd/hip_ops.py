@@ -109,6 +109,28 @@ def _lat_split(descs, seg, target_wgs):
     return ks, worst
 
 
+_LAT_COLPACK = os.environ.get("NMGP_LAT_COLPACK", "1") != "0"
+
+
+def _lat_colpack_groups(d):
+    """Column-tile groups of a B-triangular latency-kernel problem (csrc/gemm_lat.hip, NMGP_LAT_COLPACK): with
+    B_LOWER the column tile j of an n == k == 32 T problem has T - j k panels (B_UPPER: j + 1), so {0}, {g, T - g}
+    and, for even T, {T / 2} each fill at most the 8 waves of a workgroup.  0 when the problem does not qualify."""
+    f = d.flags
+    bmask = f & (L.B_LOWER | L.B_UPPER)
+    if not _LAT_COLPACK or bmask not in (L.B_LOWER, L.B_UPPER):
+        return 0
+    if f & (L.A_LOWER | L.A_UPPER | L.OUT_LOWER | L.OUT_TRIL) or d.k_seg >= 0 or d.ksplit > 1:
+        return 0
+    K = d.k
+    if K <= 0 or K % LAT_TILE or d.n != K or (0 < d.kbB < K) or (0 < d.kbA < K):
+        return 0
+    T = K // LAT_TILE
+    if T < 3 or T > LAT_WAVES:
+        return 0
+    return 1 + (T - 1) // 2 + (1 if T % 2 == 0 else 0)
+
+
 def _lat_eligible(d, esz):
     """Can gemm_lat.hip run this descriptor?  Non-negative strides, k-blocks that panels never
     straddle, and operand extents (incl. the rows / k a tile may touch past the problem) addressable
@@ -227,6 +249,10 @@ class GemmGroup:
             d.tiles_m = -(-d.m // LAT_TILE) if d.m > 0 else 0
             d.tiles_n = -(-d.n // LAT_TILE) if d.n > 0 else 0
             d.ksplit = ksplits[i]
+            groups = _lat_colpack_groups(d)
+            if groups:
+                d.flags |= L.LAT_COLPACK          # tiles_n = column-tile groups (5 instead of 8 at M = 256)
+                d.tiles_n = groups
             nt = d.tiles_m * d.tiles_n
             if d.ksplit > 1:
                 ws = torch.empty(nt * d.ksplit * LAT_TILE * LAT_TILE, dtype=self.dtype, device=device)

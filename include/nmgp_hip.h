@@ -64,7 +64,11 @@ enum {
   NMGP_EPI = 128,        /* + gamma * rs(i) * E(i,j)     */
   NMGP_EPI_E_LOWER = 256,/* E(i,j) = 0 for j > i         */
   NMGP_DIAG_ADD = 512,   /* + diag_add on i == j         */
-  NMGP_EPI_RS_NEG = 1024 /* rs(i) taken with a minus sign */
+  NMGP_EPI_RS_NEG = 1024,/* rs(i) taken with a minus sign */
+  NMGP_LAT_COLPACK = 2048/* latency kernel only (set by the host): a B_LOWER / B_UPPER problem with n == k ==
+                          * 32 T, T <= 8, no other mask: tiles_n counts column-tile GROUPS -- {0}, {g, T-g}
+                          * for g = 1..(T-1)/2 and {T/2} for even T (B_UPPER mirrored) -- whose k panels add up
+                          * to <= 8, one group per workgroup                                                  */
 };
 
 typedef struct nmgp_gemm_desc {
