@@ -438,6 +438,10 @@ class DsviEngine:
         bwd_lat = int(os.environ.get("NMGP_BWD_LAT_WGS", "0"))
         p["bwd_w"] = G(d17) if not bwd_lat else H.GemmGroup(d17, dev, self.dt, seg=seg, target_wgs=bwd_lat,
                                                              kernel="lat")
+        # split (round 3, NMGP_BWD_SPLIT): the latent P-bar_G products feed R_G on the main chain; the pair
+        # P-bar_0/1 products feed only the L0 / L1 prior adjoints and run on the third side stream
+        p["bwd_wG"] = G(d17[:D])
+        p["bwd_wP"] = G(d17[D:]) if len(d17) > D else None
         d17 = []
         for d in range(D):
             d17.append(g(gr, self.P, self.WG, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_TRIL, beta=1.0,
@@ -707,7 +711,8 @@ class DsviEngine:
         if not elbo_mode and os.environ.get("NMGP_PLAN_AHEAD", "1") != "0":
             # (quad_P plans inline on side2: waiting there for the side stream's plans would be a
             # side <-> side2 edge, which hipGraph instantiation does not survive on this stack)
-            pre_planned = {nm for nm in ("quad", "quad_W", "bwd_w")
+            split_bw = os.environ.get("NMGP_SIDE3", "1") != "0" and os.environ.get("NMGP_BWD_SPLIT", "1") != "0"
+            pre_planned = {nm for nm in (("quad", "quad_W", "bwd_wG", "bwd_wP") if split_bw else ("quad", "quad_W", "bwd_w"))
                            if isinstance(p.get(nm), H.GemmGroup) and p[nm].plan is not None}
 
         def gemm(name):
@@ -929,10 +934,16 @@ class DsviEngine:
             steps += [("quad_W", "gemm", gemm("quad_W"), "main"), ("wait", "main", "quadP")]
         else:
             steps.append(("quad", "gemm", gemm("quad"), "main"))
+        side3 = os.environ.get("NMGP_SIDE3", "1") != "0"
+        bwd_split = side3 and os.environ.get("NMGP_BWD_SPLIT", "1") != "0"
         steps += [
             ("recon", "row", row(getattr(lib, "nmgp_dsvi_recon_" + self.sfx)), "main"),
             ("sig", "main", "recon"),
-            ("bwd_w", "gemm", gemm("bwd_w"), "main"),
+            ("bwd_wG", "gemm", gemm("bwd_wG"), "main") if bwd_split else ("bwd_w", "gemm", gemm("bwd_w"), "main"),
+        ]
+        if bwd_split:
+            steps.append(("bwd_R", "gemm", gemm("bwd_R"), "main"))
+        steps += [
             # L-bar / mu-bar gradient rows: after the KL L-bar (their first writer, same stream) and recon.
             # (Deferring them until after bwd_w, to leave it the whole chip, measured 2% slower: the
             # main chain after bwd_w is latency-bound either way.)
@@ -947,7 +958,6 @@ class DsviEngine:
         # adjoint Abar_G -= P_G^T R_G and the K_G22 builder backward (ell_Z adjoints: the v chain only)
         # run on the second side stream
         # A/B on the box (tools/ab_env.sh NMGP_SIDE3, 3 x 300 steps each): 0.815-0.818 -> 0.798-0.802 ms
-        side3 = os.environ.get("NMGP_SIDE3", "1") != "0"
         BM = self.B * M
 
         def lchain(where):
@@ -960,7 +970,16 @@ class DsviEngine:
                           ("bwd_pr_L", "gemm", gemm("bwd_pr_L"), where),
                           ("bwd_build_L", "pairwise_bwd", (pw64 if self.p64 else pw)("bwd_build_L"), where),
                           ("sig", where, "L_done")]
-        if side3:
+        if bwd_split:
+            # the pair P-bar_0/1 products start on the third side stream right after recon (beside bwd_wG),
+            # then -- with the KL parts of A-bar_0/1 (kl_done, a one-way side -> side3 edge) -- the L0 / L1
+            # prior adjoints
+            steps += [("wait", "side3", "recon")]
+            if p["bwd_wP"] is not None:
+                steps.append(("bwd_wP", "gemm", gemm("bwd_wP"), "side3"))
+            steps += [("wait", "side3", "kl_done")]
+            steps += lchain("side3")
+        elif side3:
             # the L0 / L1 prior adjoints (R_0, R_1 -> P^T R -> builder backward: hyper-parameter partials
             # only) need P-bar_0/1 (bwd_w) and the KL parts of Abar (kl_done): a third side stream starts
             # them right after bwd_w.  On side2 they queued behind the G-prior adjoint and, in the graph,
@@ -971,7 +990,7 @@ class DsviEngine:
                 steps.append(("bwd_R", "gemm", gemm("bwd_R"), "main"))
             steps.append(("wait", "side3", "bwd_w_kl"))
             steps += lchain("side3")
-        if not (side3 and crit):
+        if not (side3 and crit) and not bwd_split:
             steps.append(("bwd_R", "gemm", gemm("bwd_R"), "main"))
         steps += [
             # (the second side stream synchronises with the main stream only: a side <-> side2 event
