@@ -1020,13 +1020,20 @@ class DsviEngine:
             # (starting P_t^T tbar before the K_G22 builder backward is done -- the g22 partials relayed to
             # the v-backward kernel through the main stream -- measured slower in the graph: 0.84 ms and,
             # with the third side stream, 0.94 ms per step; more cross-queue edges)
-            ("wait", "main", "g22"),
-            ("sig", "main", "tb"),
         ]
+        # round 3 (NMGP_G22_SIDE, default on): the v chain waits for the K_G22 builder backward itself (a
+        # one-way side2 -> side edge; only the side <-> side2 ping-pong breaks torch's capture), so the main
+        # stream's t-prior chain no longer waits for the G-prior adjoint relayed through it
+        g22_side = os.environ.get("NMGP_G22_SIDE", "1") != "0"
+        if not g22_side:
+            steps.append(("wait", "main", "g22"))
+        steps.append(("sig", "main", "tb"))
         if crit:
             steps.append(("bwd_t1", "gemm", gemm("bwd_t1"), "main"))
+        steps.append(("wait", "side", "tb"))
+        if g22_side:
+            steps.append(("wait", "side", "g22"))
         steps += [
-            ("wait", "side", "tb"),
             ("bwd_vt", "gemm", gemm("bwd_vt"), "side"),
             ("vbwd", "row", row(getattr(lib, "nmgp_dsvi_vbwd_" + self.sfx)), "side"),
             ("bwd_v1", "gemm", gemm("bwd_v1"), "side"),
@@ -1042,6 +1049,10 @@ class DsviEngine:
             ("wait", "main", "v_done"),
             ("wait", "main", "lbar_done"),
             ("wait", "main", "L_done"),
+        ]
+        if g22_side:
+            steps.append(("wait", "main", "g22"))          # (explicit join of side2; long done)
+        steps += [
             ("finalize", "row", row(getattr(lib, "nmgp_dsvi_finalize_" + self.sfx)), "main"),
         ]
         if os.environ.get("NMGP_SIDE2_BWD", "1") == "0":
