@@ -16,4 +16,8 @@ bash tools/profile_bench.sh r03y_pm25_bench > gpurun_out/r03y_prof.log 2>&1 || {
 bash tools/pm25_pmc.sh > gpurun_out/r03y_pmc.log 2>&1 || { tail -20 gpurun_out/r03y_pmc.log; exit 6; }
 python tools/step_timeline.py $(find gpurun_out/prof/trace -name "*kernel_trace.csv") > gpurun_out/r03y_step_timeline.txt 2>&1
 head -3 gpurun_out/r03y_step_timeline.txt
+# bench.py's N = 2 path rehearsed with gloo ranks sharing cuda:0 (DP step with the all-reduce, KL-sharded ELBO
+# and pair-sharded legs at D = 32 so that two ranks fit one GPU); never the measured configuration
+NMGP_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --no-breakdown --pair-D 32 --elbo-D 32 > gpurun_out/r03y_bench_n2_rehearsal.json 2> gpurun_out/r03y_bench_n2_rehearsal.err
+rc3=$?; tail -1 gpurun_out/r03y_bench_n2_rehearsal.json | cut -c1-800; [ $rc3 -ne 0 ] && tail -20 gpurun_out/r03y_bench_n2_rehearsal.err
 exit $rc
