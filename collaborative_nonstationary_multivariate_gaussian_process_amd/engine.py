@@ -135,6 +135,15 @@ class DsviEngine:
         self.Abar = e(4, M, M)
         self.WG = e(D, B, M)
         self.WP = e(D, B, M)
+        # W-hat fold (round 3): recon writes the per-(factor, row) scales 2 g-bar / 2 s2p-bar into wsc and
+        # the backward GEMMs apply them to the W operand (NMGP_ASCALE for P-bar, NMGP_KSCALE for L-bar)
+        # instead of recon rewriting W / W_P as W-hat in place (46 MB of stores per PM2.5 step).  Not on the
+        # 128x128 L-bar kernel of the large fp32 engines (no operand scale there) nor with the latency-kernel
+        # P-bar knob; NMGP_WHAT_FOLD=0 restores the in-place W-hat.
+        big_side = self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0"
+        self.what_fold = (not big_side and os.environ.get("NMGP_WHAT_FOLD", "0") == "1"
+                          and int(os.environ.get("NMGP_BWD_LAT_WGS", "0")) == 0)
+        self.wsc = e(2 * D, B) if self.what_fold else None
         self.Y = e(D + 1 + 2 * self.NPC, M)
         self.T2 = e(M, M)
         self.v, self.ellZ = e(M), e(M)
@@ -256,6 +265,7 @@ class DsviEngine:
             a.v64, a.ellZ64, a.K12_64 = self.v_A64.data_ptr(), self.ellZ64.data_ptr(), self.K12_64.data_ptr()
             a.t64, a.scal64 = self.t64.data_ptr(), self.scal64.data_ptr()
         a.kl_f0, a.kl_f1 = 0, self.NF - 1
+        a.wscale = self.wsc.data_ptr() if self.wsc is not None else 0
         kp = self._elbo_kl if elbo_mode else None
         if kp is not None:                       # this rank's share of compute_ELBO's KL terms
             a.kl_f0, a.kl_f1 = kp[0], kp[1]
@@ -423,14 +433,23 @@ class DsviEngine:
         # B2: P-bar += W-hat L^T ; L-bar = P^T W-hat ; mu-bar = P^T adjoints
         # rows of output i: P-bar_G += sum_{d <= i} W-hat_d L_d^T (W-hat_d holds only the rows of outputs
         # >= d, so k runs over the (i + 1) latent blocks that are non-zero there, not all D)
-        d17 = [g(self.Pbar, self.WG, th, B, M, (i + 1) * M, (M, 1, BM), (1, M, MM), (M, 1), flags=L.B_UPPER,
-                 kb=(M, M), beta=1.0, offs=(0, sW, 3 * BM), row_seg=i) for i in range(D)]
+        wsc = self.wsc
+
+        def ascaled(d, off):             # W-hat fold: A = W rows scaled by wsc[off + k-block * B + row]
+            if wsc is not None:
+                d.kscale, d.sAS_kb = H._addr(wsc, off), B
+                d.flags |= L.ASCALE
+            return d
+        ksc = (lambda off: (wsc, off)) if wsc is not None else (lambda off: None)
+        d17 = [ascaled(g(self.Pbar, self.WG, th, B, M, (i + 1) * M, (M, 1, BM), (1, M, MM), (M, 1), flags=L.B_UPPER,
+                         kb=(M, M), beta=1.0, offs=(0, sW, 3 * BM), row_seg=i), 0) for i in range(D)]
         for i in range(i0, i1):
-            d17.append(g(self.Pbar, self.WP, th, B, M, M, (M, 1, 0), (1, M, 0), (M, 1), flags=L.B_UPPER, beta=1.0,
-                         offs=(i * BM, sU + pq(i, i) * MM, 2 * BM), row_seg=i))
+            d17.append(ascaled(g(self.Pbar, self.WP, th, B, M, M, (M, 1, 0), (1, M, 0), (M, 1), flags=L.B_UPPER,
+                                 beta=1.0, offs=(i * BM, sU + pq(i, i) * MM, 2 * BM), row_seg=i), (D + i) * B))
             if i > 0:
-                d17.append(g(self.Pbar, self.WP, th, B, M, i * M, (M, 1, BM), (1, M, MM), (M, 1), flags=L.B_UPPER,
-                             kb=(M, M), beta=1.0, offs=(0, sU + pq(i, 0) * MM, 1 * BM), row_seg=i))
+                d17.append(ascaled(g(self.Pbar, self.WP, th, B, M, i * M, (M, 1, BM), (1, M, MM), (M, 1),
+                                     flags=L.B_UPPER, kb=(M, M), beta=1.0, offs=(0, sU + pq(i, 0) * MM, 1 * BM),
+                                     row_seg=i), D * B))
         # the P-bar products feed R (main chain); the L-bar / mu-bar products below only accumulate
         # gradient rows, so they run on the side stream beside bwd_R .. bwd_v2
         # A/B knob NMGP_BWD_LAT_WGS=<n>: run P-bar on the latency kernel with split-K sized for ~n workgroups
@@ -440,22 +459,32 @@ class DsviEngine:
                                                              kernel="lat")
         # split (round 3, NMGP_BWD_SPLIT): the latent P-bar_G products feed R_G on the main chain; the pair
         # P-bar_0/1 products feed only the L0 / L1 prior adjoints and run on the third side stream
-        p["bwd_wG"] = G(d17[:D])
-        p["bwd_wP"] = G(d17[D:]) if len(d17) > D else None
+        # k-tile caps (split-K so no workgroup runs a longer k loop; 0 = the balanced automatic split): P-bar_G
+        # is on the main chain, its output-(D-1) tiles otherwise run all D latent blocks (40 k-tiles at PM2.5).
+        # fp64 default 20 (PM2.5 A/B on the box, 3 x 300 steps interleaved, two boxes: 1370-1379 -> 1386-1400 it/s;
+        # 8 / 12 / 16 / 24 / 32 and caps on the side-stream P-bar_0/1 and L-bar groups no better:
+        # profiles/r03za_kt_cap_ab.txt).  fp32 engines keep the automatic split (their gates were measured with it).
+        capG = int(os.environ.get("NMGP_KT_CAP_WG", "20" if self.dt == torch.float64 else "0"))
+        capP = int(os.environ.get("NMGP_KT_CAP_WP", "0"))
+        capL = int(os.environ.get("NMGP_KT_CAP_LBAR", "0"))
+        p["bwd_wG"] = H.GemmGroup(d17[:D], dev, self.dt, seg=seg, kt_cap=capG)
+        p["bwd_wP"] = H.GemmGroup(d17[D:], dev, self.dt, seg=seg, kt_cap=capP) if len(d17) > D else None
         d17 = []
         for d in range(D):
             d17.append(g(gr, self.P, self.WG, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_TRIL, beta=1.0,
-                         offs=(3 * BM, d * BM, sW + d * MM), k_seg=d, seg_span=D - d))
+                         offs=(3 * BM, d * BM, sW + d * MM), k_seg=d, seg_span=D - d, kscale=ksc(d * B)))
             d17.append(g(gr, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1), beta=1.0,
                          offs=(3 * BM, d * B, muW + d * M), k_seg=d, seg_span=D - d))
         for (i, j) in pairs:
             typ = 2 if i == j else 1
             d17.append(g(gr, self.P, self.WP, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_TRIL, beta=1.0,
-                         offs=(typ * BM, j * BM, sU + pq(i, j) * MM), k_seg=i))
+                         offs=(typ * BM, j * BM, sU + pq(i, j) * MM), k_seg=i, kscale=ksc((D + j) * B)))
             d17.append(g(gr, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1), beta=1.0,
                          offs=(typ * BM, (D + j) * B, muU + pq(i, j) * M), k_seg=i))
         if not (self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0"):
-            p["bwd_lbar"] = G(d17)
+            p["bwd_lbar"] = H.GemmGroup(d17, dev, self.dt, seg=seg, kt_cap=capL)
+        elif wsc is not None:
+            raise RuntimeError("W-hat fold: the 128x128 L-bar products take no operand scale")
         else:
             # the D + Q L-bar products P^T W (k over each factor's row segment) on the 128x128 kernel,
             # the M x 1 mu-bar products stay one grouped launch

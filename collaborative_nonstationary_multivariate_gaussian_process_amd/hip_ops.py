@@ -43,6 +43,7 @@ def gemm_desc(C, A, B, m, n, k, sA, sB, sC, *, flags=0, alpha=1.0, beta=0.0, kb=
     d.m, d.n, d.k = int(m), int(n), int(k)
     d.kbA, d.kbB = kb
     d.flags = flags | (L.KSCALE if kscale is not None else 0)
+    assert not (d.flags & L.KSCALE and d.flags & L.ASCALE), "KSCALE and ASCALE share the kscale table"
     d.row_seg, d.k_seg, d.seg_span = row_seg, k_seg, seg_span
     d.alpha, d.beta, d.diag_add = alpha, beta, diag_add
     if epi is not None:
@@ -135,7 +136,7 @@ def _lat_eligible(d, esz):
     """Can gemm_lat.hip run this descriptor?  Non-negative strides, k-blocks that panels never
     straddle, and operand extents (incl. the rows / k a tile may touch past the problem) addressable
     by a 32-bit buffer offset."""
-    if d.batch > 1:
+    if d.batch > 1 or d.flags & L.ASCALE:      # (no A operand scale in the latency kernel)
         return False
     st = (d.sA_i, d.sA_k, d.sA_kb, d.sB_k, d.sB_j, d.sB_kb)
     if min(st) < 0:
@@ -162,9 +163,12 @@ class GemmGroup:
     B x M x M and M x M x M products of the DSVI step.  `kernel`: "auto" (latency kernel when every
     problem is eligible and k <= NMGP_GEMM_LAT_KMAX), "tile", "lat"."""
 
-    def __init__(self, descs, device, dtype, seg=None, target_wgs=512, dyn_plan=True, kernel="auto"):
+    def __init__(self, descs, device, dtype, seg=None, target_wgs=512, dyn_plan=True, kernel="auto", kt_cap=0):
         """Split-K is chosen per problem so that the launch has ~target_wgs workgroups when the
-        outputs alone are too few tiles (the M x B x M products P^T R with K = B)."""
+        outputs alone are too few tiles (the M x B x M products P^T R with K = B).  kt_cap > 0 (tile
+        kernel): split every problem so that no workgroup runs more than ~kt_cap k-tiles -- for groups
+        on the step's critical path, where the longest tile's k loop, not the chip's fill, sets the
+        launch time."""
         self.dtype = dtype
         self.seg = seg
         self.lat = False
@@ -196,6 +200,8 @@ class GemmGroup:
         for i, d in enumerate(descs):
             if d.ksplit <= 1:
                 d.ksplit = _auto_ksplit(eff[i][1], group_tiles, work_per_wg)
+            if kt_cap > 0:
+                d.ksplit = max(d.ksplit, min(16, -(-(-(-eff[i][1] // GEMM_BK)) // kt_cap)))
         # longest k-loop per workgroup first: those workgroups are dispatched first instead of
         # forming the launch's tail (problems of one group write disjoint outputs, so their order in
         # the launch is free)
