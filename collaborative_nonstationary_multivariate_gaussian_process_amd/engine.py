@@ -948,13 +948,29 @@ class DsviEngine:
                       ("kl_t64a", "gemm", gemm("kl_t64a"), "side")]
             if p["kl_t64b"] is not None:
                 steps.append(("kl_t64b", "gemm", gemm("kl_t64b"), "side"))
-        steps += [
-            ("kl_lbar", "gemm", gemm("kl_lbar"), "side"),
-            ("sig", "side", "kl_lbar"),
-            ("kl_abar", "gemm", gemm("kl_abar"), "side"),
-            ("bwd_kly", "gemm", gemm("bwd_kly"), "side"),
-            ("sig", "side", "kl_done"),
-        ]
+        # round 3 (NMGP_LBAR_EARLY): the KL parts of A-bar (kl_abar, bwd_kly: they need delta and Y, not the KL
+        # L-bar) on the third side stream, so the side stream reaches bwd_lbar -- the step's longest
+        # backward GEMM, ahead of the v chain -- right after recon
+        lbar_early = os.environ.get("NMGP_LBAR_EARLY", "0") == "1" and os.environ.get("NMGP_SIDE3", "1") != "0" \
+            and os.environ.get("NMGP_BWD_SPLIT", "1") != "0"
+        if lbar_early:
+            steps += [
+                ("sig", "side", "delta_done"),
+                ("kl_lbar", "gemm", gemm("kl_lbar"), "side"),
+                ("sig", "side", "kl_lbar"),
+                ("wait", "side3", "delta_done"),
+                ("kl_abar", "gemm", gemm("kl_abar"), "side3"),
+                ("bwd_kly", "gemm", gemm("bwd_kly"), "side3"),
+                ("sig", "side3", "kl_done"),
+            ]
+        else:
+            steps += [
+                ("kl_lbar", "gemm", gemm("kl_lbar"), "side"),
+                ("sig", "side", "kl_lbar"),
+                ("kl_abar", "gemm", gemm("kl_abar"), "side"),
+                ("bwd_kly", "gemm", gemm("bwd_kly"), "side"),
+                ("sig", "side", "kl_done"),
+            ]
         if pre_planned and not quad_first:
             steps.append(("wait", "main", "plans"))
         if quad_first:
@@ -989,16 +1005,19 @@ class DsviEngine:
         # A/B on the box (tools/ab_env.sh NMGP_SIDE3, 3 x 300 steps each): 0.815-0.818 -> 0.798-0.802 ms
         BM = self.B * M
 
-        def lchain(where):
+        def lchain(where, kl_wait=None):
             # (p64: P-bar_0/1, the KL parts of A-bar_0/1 and the row coefficients c0 / c1 widened first)
-            pre = [("wPbL", "convert", widen(self.Pbar, self.PbL64, 2 * BM, BM), where),
-                   ("wAbL", "convert", widen(self.Abar, self.AbL64, 2 * MM, MM), where),
-                   ("wrcL", "convert", widen(self.rowbuf, self.rcL64, 2 * self.B, (2 * D + 1) * self.B), where)] \
+            # kl_wait: the stream waits for the KL parts of A-bar_0/1 (event kl_done) only after R_0/1 = P-bar Ainv,
+            # which does not read them
+            wP = [("wPbL", "convert", widen(self.Pbar, self.PbL64, 2 * BM, BM), where),
+                  ("wrcL", "convert", widen(self.rowbuf, self.rcL64, 2 * self.B, (2 * D + 1) * self.B), where)] \
                 if self.p64 else []
-            return pre + [("bwd_R_L", "gemm", gemm("bwd_R_L"), where),
-                          ("bwd_pr_L", "gemm", gemm("bwd_pr_L"), where),
-                          ("bwd_build_L", "pairwise_bwd", (pw64 if self.p64 else pw)("bwd_build_L"), where),
-                          ("sig", where, "L_done")]
+            wA = [("wAbL", "convert", widen(self.Abar, self.AbL64, 2 * MM, MM), where)] if self.p64 else []
+            kw = [("wait", where, kl_wait)] if kl_wait else []
+            return wP + [("bwd_R_L", "gemm", gemm("bwd_R_L"), where)] + kw + wA + \
+                [("bwd_pr_L", "gemm", gemm("bwd_pr_L"), where),
+                 ("bwd_build_L", "pairwise_bwd", (pw64 if self.p64 else pw)("bwd_build_L"), where),
+                 ("sig", where, "L_done")]
         if bwd_split:
             # the pair P-bar_0/1 products start on the third side stream right after recon (beside bwd_wG),
             # then -- with the KL parts of A-bar_0/1 (kl_done, a one-way side -> side3 edge) -- the L0 / L1
@@ -1006,8 +1025,16 @@ class DsviEngine:
             steps += [("wait", "side3", "recon")]
             if p["bwd_wP"] is not None:
                 steps.append(("bwd_wP", "gemm", gemm("bwd_wP"), "side3"))
-            steps += [("wait", "side3", "kl_done")]
-            steps += lchain("side3")
+            # round 3 (NMGP_RL_EARLY=1): R_0/1 follow bwd_wP with no other dependency (waiting for kl_done before
+            # them gives the node two parents and the graph puts it on bwd_R's hardware queue, behind the main
+            # chain); it then overlaps bwd_R and the step measured 1389 -> 1373 it/s, so off by default
+            if lbar_early:
+                steps += lchain("side3")                     # (kl_done is this stream's own)
+            elif os.environ.get("NMGP_RL_EARLY", "0") == "1":
+                steps += lchain("side3", kl_wait="kl_done")
+            else:
+                steps += [("wait", "side3", "kl_done")]
+                steps += lchain("side3")
         elif side3:
             # the L0 / L1 prior adjoints (R_0, R_1 -> P^T R -> builder backward: hyper-parameter partials
             # only) need P-bar_0/1 (bwd_w) and the KL parts of Abar (kl_done): a third side stream starts
