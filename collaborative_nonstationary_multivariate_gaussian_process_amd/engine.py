@@ -468,7 +468,10 @@ class DsviEngine:
         capP = int(os.environ.get("NMGP_KT_CAP_WP", "0"))
         capL = int(os.environ.get("NMGP_KT_CAP_LBAR", "0"))
         p["bwd_wG"] = H.GemmGroup(d17[:D], dev, self.dt, seg=seg, kt_cap=capG)
-        p["bwd_wP"] = H.GemmGroup(d17[D:], dev, self.dt, seg=seg, kt_cap=capP) if len(d17) > D else None
+        # grid caps (A/B knobs): at most that many workgroups for the side-stream P-bar_0/1 and L-bar groups
+        gP = int(os.environ.get("NMGP_WP_GRID", "0"))
+        gL = int(os.environ.get("NMGP_LBAR_GRID", "0"))
+        p["bwd_wP"] = H.GemmGroup(d17[D:], dev, self.dt, seg=seg, kt_cap=capP, max_grid=gP) if len(d17) > D else None
         d17 = []
         for d in range(D):
             d17.append(g(gr, self.P, self.WG, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_TRIL, beta=1.0,
@@ -482,7 +485,7 @@ class DsviEngine:
             d17.append(g(gr, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1), beta=1.0,
                          offs=(typ * BM, (D + j) * B, muU + pq(i, j) * M), k_seg=i))
         if not (self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0"):
-            p["bwd_lbar"] = H.GemmGroup(d17, dev, self.dt, seg=seg, kt_cap=capL)
+            p["bwd_lbar"] = H.GemmGroup(d17, dev, self.dt, seg=seg, kt_cap=capL, max_grid=gL)
         elif wsc is not None:
             raise RuntimeError("W-hat fold: the 128x128 L-bar products take no operand scale")
         else:
@@ -1054,19 +1057,36 @@ class DsviEngine:
             # when bwd_R finishes, so the main stream's wait on them costs nothing)
             ("wait", "main", "kl_done"),
             ("sig", "main", "R_G"),
-            ("bwd_build12", "pairwise_bwd", pw("bwd_build12"), "main"),
-            ("wait", "side2", "R_G"),
-            ("bwd_pr", "gemm", gemm("bwd_pr"), "side2"),
-            ("bwd_build22", "pairwise_bwd", pw("bwd_build22"), "side2"),
-            ("sig", "side2", "g22"),
         ]
+        # round 3 (NMGP_PR_MAIN=1): the G-prior adjoint (bwd_pr -> K_G22 builder backward, the longer of the two
+        # chains after R_G, ahead of the v chain) stays on the main stream with no cross-queue hop; the K_G12
+        # builder backward and the t-row backward move to side2 (tb signalled there)
+        pr_main = os.environ.get("NMGP_PR_MAIN", "0") == "1"
+        if pr_main:
+            steps += [
+                ("bwd_pr", "gemm", gemm("bwd_pr"), "main"),
+                ("bwd_build22", "pairwise_bwd", pw("bwd_build22"), "main"),
+                ("sig", "main", "g22"),
+                ("wait", "side2", "R_G"),
+                ("bwd_build12", "pairwise_bwd", pw("bwd_build12"), "side2"),
+                ("tbwd", "row", row(getattr(lib, "nmgp_dsvi_tbwd_" + self.sfx)), "side2"),
+                ("sig", "side2", "tb"),
+            ]
+        else:
+            steps += [
+                ("bwd_build12", "pairwise_bwd", pw("bwd_build12"), "main"),
+                ("wait", "side2", "R_G"),
+                ("bwd_pr", "gemm", gemm("bwd_pr"), "side2"),
+                ("bwd_build22", "pairwise_bwd", pw("bwd_build22"), "side2"),
+                ("sig", "side2", "g22"),
+            ]
         if not side3:
             # the L0 / L1 prior adjoints feed only their hyper-parameter partials (scal_part slots and
             # row-coefficient rows of their own): second side stream after the G prior adjoint (R_G was
             # signalled after bwd_w and the KL parts of Abar), so the v chain on the side stream does not
             # queue behind them
             steps += lchain("side2")
-        steps += [
+        steps += [] if pr_main else [
             ("tbwd", "row", row(getattr(lib, "nmgp_dsvi_tbwd_" + self.sfx)), "main"),
             # after the t-row backward the t-prior chain (bwd_t1 -> bwd_t2 -> builder backward) and the
             # v-factor Cholesky backward (P_t^T tbar -> vbwd -> bwd_v1 -> bwd_v2, reading vbar and the
@@ -1081,9 +1101,10 @@ class DsviEngine:
         # one-way side2 -> side edge; only the side <-> side2 ping-pong breaks torch's capture), so the main
         # stream's t-prior chain no longer waits for the G-prior adjoint relayed through it
         g22_side = os.environ.get("NMGP_G22_SIDE", "1") != "0"
-        if not g22_side:
+        if not g22_side and not pr_main:
             steps.append(("wait", "main", "g22"))
-        steps.append(("sig", "main", "tb"))
+        if not pr_main:
+            steps.append(("sig", "main", "tb"))
         if crit:
             steps.append(("bwd_t1", "gemm", gemm("bwd_t1"), "main"))
         steps.append(("wait", "side", "tb"))
@@ -1106,11 +1127,23 @@ class DsviEngine:
             ("wait", "main", "lbar_done"),
             ("wait", "main", "L_done"),
         ]
-        if g22_side:
+        if g22_side and not pr_main:
             steps.append(("wait", "main", "g22"))          # (explicit join of side2; long done)
         steps += [
             ("finalize", "row", row(getattr(lib, "nmgp_dsvi_finalize_" + self.sfx)), "main"),
         ]
+        if pr_main:
+            # the t-prior chain (bwd_t1 -> bwd_t2 -> builder backward) follows the t-row backward on side2
+            out = []
+            for it in steps:
+                if it[0] == "finalize":
+                    out.append(("wait", "main", "t_done"))
+                if len(it) == 4 and it[0] in ("bwd_t1", "bwd_t2", "bwd_tbuild"):
+                    it = (it[0], it[1], it[2], "side2")
+                out.append(it)
+                if it[0] == "bwd_tbuild":
+                    out.append(("sig", "side2", "t_done"))
+            steps = out
         if os.environ.get("NMGP_SIDE2_BWD", "1") == "0":
             steps = self._remap(steps, n_fwd, len(steps), "side2", "main")
         return steps

@@ -163,15 +163,19 @@ class GemmGroup:
     B x M x M and M x M x M products of the DSVI step.  `kernel`: "auto" (latency kernel when every
     problem is eligible and k <= NMGP_GEMM_LAT_KMAX), "tile", "lat"."""
 
-    def __init__(self, descs, device, dtype, seg=None, target_wgs=512, dyn_plan=True, kernel="auto", kt_cap=0):
+    def __init__(self, descs, device, dtype, seg=None, target_wgs=512, dyn_plan=True, kernel="auto", kt_cap=0,
+                 max_grid=0):
         """Split-K is chosen per problem so that the launch has ~target_wgs workgroups when the
         outputs alone are too few tiles (the M x B x M products P^T R with K = B).  kt_cap > 0 (tile
         kernel): split every problem so that no workgroup runs more than ~kt_cap k-tiles -- for groups
         on the step's critical path, where the longest tile's k loop, not the chip's fill, sets the
-        launch time."""
+        launch time.  max_grid > 0 (tile kernel): at most that many workgroups, striding over the tiles
+        (longest k loops first) -- for off-critical-path groups whose long-lived workgroups would otherwise
+        hold every CU slot while the critical chain's launches wait for them."""
         self.dtype = dtype
         self.seg = seg
         self.lat = False
+        self._static_plan = False
         esz = 8 if dtype == _F64 else 4
         if kernel != "tile" and _LAT_MODE != "0" and descs:
             ok = all(_lat_eligible(d, esz) for d in descs)
@@ -232,7 +236,14 @@ class GemmGroup:
         # (only where the static grid is mostly idle workgroups: the plan launch costs more than it
         # saves on small grids; PM2.5 quad / bwd_w: +2-3% it/s; HCP, D=50: ~95% of the quad-form workgroups removed)
         self.plan, self.grid = None, 0
-        if seg is not None and dyn_plan and any(d.row_seg >= 0 for d in descs):
+        if max_grid > 0 and t > max_grid:
+            if any(d.row_seg >= 0 for d in descs):
+                self.plan = torch.zeros(len(descs) + 1, dtype=torch.int32, device=device)
+            else:                                  # the plan is the static tile layout: uploaded once
+                self.plan = torch.tensor([d.tile_start for d in descs] + [t], dtype=torch.int32, device=device)
+                self._static_plan = True
+            self.grid = int(max_grid)
+        elif seg is not None and dyn_plan and any(d.row_seg >= 0 for d in descs):
             ksp = {id(d): max(d.ksplit, 1) for d in descs}
             expect = sum(eff[order[i]][0] * ksp[id(d)] for i, d in enumerate(descs))
             if dyn_plan == "force" or (t >= int(os.environ.get("NMGP_DYN_MIN_TILES", 1024)) and expect < 0.5 * t):
@@ -286,7 +297,7 @@ class GemmGroup:
     def plan_now(self, stream=None):
         """Enqueue only the device tile plan of a segment-sized group (e.g. right after the minibatch
         gather, on another stream); later calls with planned=True reuse it.  No-op for static groups."""
-        if self.plan is None or self.n == 0 or self.total == 0:
+        if self.plan is None or self.n == 0 or self.total == 0 or self._static_plan:
             return False
         s = stream if stream is not None else L.stream_handle()
         fn = L.lib().nmgp_gemm_plan_lat if self.lat else L.lib().nmgp_gemm_plan
@@ -299,7 +310,7 @@ class GemmGroup:
             return
         s = stream if stream is not None else L.stream_handle()
         segp = ctypes.c_void_p(self.seg.data_ptr()) if self.seg is not None else None
-        pre = "_planned_" if (planned and self.plan is not None) else "_"
+        pre = "_planned_" if ((planned or self._static_plan) and self.plan is not None) else "_"
         if self.lat:
             fn = getattr(L.lib(), "nmgp_gemm_grouped_lat" + pre + _sfx(self.dtype))
             plan = ctypes.c_void_p(self.plan.data_ptr()) if self.plan is not None else None
