@@ -103,6 +103,52 @@ def test_gemm_kblocks_and_segments_grouped(ops):
 
 
 @pytest.mark.parametrize("dt", [F64, torch.float32])
+def test_gemm_group_kt_cap_max_grid_ascale(ops, dt):
+    """GemmGroup(kt_cap=) (split-K so no workgroup runs more than kt_cap k-tiles), GemmGroup(max_grid=)
+    (fewer workgroups striding over the tiles: device plan for row-segmented groups, a static plan
+    otherwise) and NMGP_ASCALE (A scaled per (row, k-block) when staged) against torch references on
+    k-blocked, row-segmented and k-segmented problems."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L
+    g = torch.Generator().manual_seed(21)
+    D, B, M = 4, 700, 128
+    W = torch.randn(D, B, M, generator=g, dtype=F64)
+    S = torch.randn(D, M, M, generator=g, dtype=F64)
+    F = torch.randn(D, B, generator=g, dtype=F64)                    # per-(block, row) A scales
+    seg = torch.tensor([0, 100, 330, 520, 700], dtype=torch.int32)
+    Wd, Sd, Fd, segd = W.to(dt).to(DEV), S.to(dt).to(DEV), F.to(dt).to(DEV), seg.to(DEV)
+    Wc, Sc, Fc = Wd.double().cpu(), Sd.double().cpu(), Fd.double().cpu()
+    tol = 1e-13 if dt == F64 else 3e-6
+    for kw in (dict(), dict(kt_cap=2), dict(max_grid=7), dict(kt_cap=3, max_grid=5)):
+        out1 = torch.zeros(B, M, dtype=dt, device=DEV)
+        out2 = torch.zeros(D, M, M, dtype=dt, device=DEV)
+        descs = []
+        for i in range(D):   # rows of segment i: sum_{d <= i} diag(F[d]) W[d] tril(S[d])^T
+            d = ops.gemm_desc(out1, Wd, Sd, B, M, (i + 1) * M, (M, 1, B * M), (1, M, M * M), (M, 1),
+                              flags=L.B_UPPER, kb=(M, M), row_seg=i)
+            d.kscale, d.sAS_kb = ops._addr(Fd), B
+            d.flags |= L.ASCALE
+            descs.append(d)
+        # out2[d] = W[d][rows of segments d..]^T W[d][same rows]   (long k: split by kt_cap)
+        descs += [ops.gemm_desc(out2, Wd, Wd, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), k_seg=d, seg_span=D - d,
+                                offs=(d * B * M, d * B * M, d * M * M), flags=L.OUT_TRIL) for d in range(D)]
+        grp = ops.GemmGroup(descs, DEV, dt, seg=segd, kernel="tile", **kw)
+        if "kt_cap" in kw:
+            assert max(x.ksplit for x in grp.descs) > 1
+        if "max_grid" in kw:
+            assert grp.plan is not None and grp.grid == kw["max_grid"]
+        grp()
+        sc = seg.tolist()
+        ref1 = torch.zeros(B, M, dtype=F64)
+        for i in range(D):
+            r0, r1 = sc[i], sc[i + 1]
+            ref1[r0:r1] = sum((Fc[d][r0:r1, None] * Wc[d][r0:r1]) @ torch.tril(Sc[d]).t() for d in range(i + 1))
+        assert rel(out1, ref1) < tol, kw
+        for d in range(D):
+            r0 = sc[d]
+            assert rel(out2[d], torch.tril(Wc[d][r0:].t() @ Wc[d][r0:])) < tol, (kw, d)
+
+
+@pytest.mark.parametrize("dt", [F64, torch.float32])
 def test_gemm_grouped_device_plan(ops, dt):
     """Row-segmented groups sized on device (plan kernel + grid-stride tiles) equal the static launch
     bit for bit, including an empty segment, a segment longer than the static estimate and split-K."""
