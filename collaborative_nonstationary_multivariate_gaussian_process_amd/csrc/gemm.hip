@@ -226,7 +226,9 @@ __device__ inline void mainloop_fast(const nmgp_gemm_desc& d, const Tile& tl, co
 #pragma unroll
       for (int v = 0; v < V; ++v) rs[e * V + v] = ksc[tl.k0 + min(kload + b_k(e * V + v), tl.K - 1)];
     }
-    if (AS) ras[e] = ksc[(int64_t)(kbA_on ? kload / tl.kbA : 0) * d.sAS_kb + asr + min(a_mn(e * V), amax)];   // (A k-contiguous)
+    // (A k-contiguous; the fetch runs up to two k-tiles past kend -- their values are masked -- so the block
+    //  index is clamped to the last k like the k-scale index above)
+    if (AS) ras[e] = ksc[(int64_t)(kbA_on ? min(kload, tl.K - 1) / tl.kbA : 0) * d.sAS_kb + asr + min(a_mn(e * V), amax)];
   };
   auto step1 = [&]() {
     kload += GBK;
