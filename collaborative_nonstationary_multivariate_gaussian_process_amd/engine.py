@@ -310,6 +310,9 @@ class DsviEngine:
                 bl.append(H.pairwise_desc(self.Afac[NF + k], self.Z, self.Z, mode=L.RBF, hyp=th, hyp_off=hoff,
                                           hyp_log=True, diag_add=self.jitter))
         p["build_rbf"] = H.PairwiseGroup(bl, dev)
+        if not self.p64:     # (early-begin schedule: the K22 builders need only theta, the K12 ones the minibatch)
+            p["build_rbf22"] = H.PairwiseGroup(bl[1::2], dev)
+            p["build_rbf12"] = H.PairwiseGroup(bl[0::2], dev)
         p64 = self.p64
         if p64:
             # the fp64 path of fp32 engines: K12 / K22 + lam I of the RBF priors in fp64 (K22 straight into
@@ -712,6 +715,29 @@ class DsviEngine:
             self.noise.numel(), ctypes.c_uint64(seed), vp(counter.data_ptr()), vp(self._begin_done.data_ptr()),
             vp(self._grad.data_ptr()), self._grad.numel(), s), "step_begin")
 
+    def _begin_launch(self, s):
+        seed, counter = self._begin_args
+        self.begin_step(seed, counter, stream=s)
+
+    def begin_forward_backward(self, seed, counter):
+        """begin_step + forward_backward(zero_grad=False).  NMGP_EARLY_BEGIN=1 (fp64 training engines): the
+        early-begin schedule, the step-begin launch on its own stream beside the theta-only head of the forward
+        chain.  Bit-identical, but 6% slower on the PM2.5 bench (1313 vs 1400 it/s, profiles/r03zh_early_begin_ab.txt):
+        in the replayed graph the extra root node and its cross-queue edges start the head ~10 us later, not
+        earlier.  Default: the two back to back on the current stream."""
+        early = (os.environ.get("NMGP_EARLY_BEGIN", "0") == "1" and not self.p64
+                 and getattr(self, "_dataset", None) is not None)
+        if not early:
+            self.begin_step(seed, counter)
+            return self.forward_backward(zero_grad=False)
+        self._begin_args = (seed, counter)
+        key = ("fb_early", self._theta.data_ptr(), self._grad.data_ptr(), self.frozen_mask, self.N)
+        if getattr(self, "_sched_key_early", None) != key:
+            self._sched_early = self._schedule(0, early=True)
+            self._sched_key_early = key
+        self._run(self._sched_early, None, None)
+        return self.out
+
     def device_noise(self, seed, counter):
         H.normal_(self.noise, seed, counter=counter)   # dtype-dispatched Philox normals
 
@@ -719,10 +745,14 @@ class DsviEngine:
     def _call(self, fn, a, s):
         L.check(fn(ctypes.byref(a), s), fn.__name__)
 
-    def _schedule(self, elbo_mode, with_kl=True, cached=False):
+    def _schedule(self, elbo_mode, with_kl=True, cached=False, early=False):
         """The ordered launch list of one step.  Items are (name, kind, callable(stream), where) with
         where in {"main", "side"}, plus ("fork",) / ("join",) markers: the D+Q variational factors that
-        only the KL terms need are factored on a side stream, overlapping the forward chain."""
+        only the KL terms need are factored on a side stream, overlapping the forward chain.
+        early (training, fp64 engines with a bound dataset): the step-begin launch (minibatch gather, noise,
+        gradient zeroing) runs on its own stream ("pre") beside the theta-only head of the forward chain --
+        Sigma_v, the prior K22 builders, the first fused Cholesky -- and only the launches that read the
+        minibatch, the noise or the gradient wait for it ("begun")."""
         lib = L.lib()
         D, M, NF = self.D, self.M, self.NF
         MM = M * M
@@ -834,6 +864,9 @@ class DsviEngine:
         kf0, kf1 = p["kl_range"]
         need_side = (not elbo_mode) or (with_kl and kf1 > kf0)
         steps = []
+        if early:
+            steps += [("sig", "main", "fork0"), ("wait", "pre", "fork0"),
+                      ("begin", "row", lambda s: self._begin_launch(s), "pre"), ("sig", "pre", "begun")]
         # (fp64 engines only: in fp32 Sigma_v's summation order shows through ell_Z = exp(v), so fp32
         # engines keep forming it exactly as the reference-checked grouped single launch does)
         v_on_side = need_side and not elbo_mode and self.dt == torch.float64
@@ -847,14 +880,22 @@ class DsviEngine:
             else:
                 steps.append(("syrk_side", "gemm", gemm("syrk_side"), "side"))
             if pre_planned:
+                if early:
+                    steps.append(("wait", "side", "begun"))
                 steps += [("plans", "gemm_plan", plans, "side"), ("sig", "side", "plans")]
+            elif early:
+                steps.append(("wait", "side", "begun"))
             steps.append(("chol_side", "chol", chol(kf0, kf1 - kf0), "side"))
             if not elbo_mode:
                 steps.append(("xs_side", "gemm", gemm("xs_side"), "side"))
         if self.p64:
             steps += [("conv_in", "convert", conv_in, "main"),
                       ("build_rbf64", "pairwise", pw64("build_rbf64"), "main")]
-        steps.append(("build_rbf", "pairwise", pw("build_rbf"), "main"))
+        if early:
+            steps += [("build_rbf22", "pairwise", pw("build_rbf22"), "main"),
+                      ("wait", "side2", "begun"), ("build_rbf12", "pairwise", pw("build_rbf12"), "side2")]
+        else:
+            steps.append(("build_rbf", "pairwise", pw("build_rbf"), "main"))
         if v_on_side:
             steps.append(("wait", "main", "syrk"))
         else:
@@ -872,6 +913,8 @@ class DsviEngine:
             ("chol", "chol", chol_main, "main"),
             ("sig", "main", "chol"),
         ]
+        if early:
+            steps.append(("wait", "main", "begun"))          # (v reads z_v)
         if crit:
             steps += [("v", "row", row(getattr(lib, "nmgp_dsvi_hyper_" + self.sfx)), "main"), ("sig", "main", "v")]
         steps.append(("wait", "side2", "chol"))
@@ -1174,7 +1217,8 @@ class DsviEngine:
                 self._side = torch.cuda.Stream(device=self.dev)
                 self._side2 = torch.cuda.Stream(device=self.dev)
                 self._side3 = torch.cuda.Stream(device=self.dev)
-            streams = {"main": main, "side": self._side, "side2": self._side2, "side3": self._side3}
+                self._pre = torch.cuda.Stream(device=self.dev)
+            streams = {"main": main, "side": self._side, "side2": self._side2, "side3": self._side3, "pre": self._pre}
             handles = {k: ctypes.c_void_p(v.cuda_stream) for k, v in streams.items()}
         events = {}
         for item in steps:

@@ -515,8 +515,7 @@ class DsviTrainer:
         mdl = self.model
         if getattr(eng, "_dataset", None) is not None and noise is None and timer is None:
             # one launch: gather + Philox noise + counter advance + gradient zeroing
-            eng.begin_step(mdl._noise_seed, mdl._noise_counter)
-            eng.forward_backward(zero_grad=False)
+            eng.begin_forward_backward(mdl._noise_seed, mdl._noise_counter)
             return eng.out[0]
         if getattr(eng, "_dataset", None) is not None:
             eng.gather_batch()
