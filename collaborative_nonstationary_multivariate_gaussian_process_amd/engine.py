@@ -869,9 +869,18 @@ class DsviEngine:
                       ("begin", "row", lambda s: self._begin_launch(s), "pre"), ("sig", "pre", "begun")]
         # (fp64 engines only: in fp32 Sigma_v's summation order shows through ell_Z = exp(v), so fp32
         # engines keep forming it exactly as the reference-checked grouped single launch does)
-        v_on_side = need_side and not elbo_mode and self.dt == torch.float64
+        # A/B knob NMGP_HEAD (round 3): 1 = the RBF builders (main) captured before the side stream's launches,
+        # so that they, not Sigma_v on the side stream, are the step-begin node's first child and keep its
+        # hardware queue (the graph put them behind a 23 us cross-queue barrier); 2 = also Sigma_v on main
+        head = os.environ.get("NMGP_HEAD", "0") if (not early and not self.p64) else "0"
+        v_on_side = need_side and not elbo_mode and self.dt == torch.float64 and head != "2"
+        rbf_first = head in ("1", "2")
+        if rbf_first:
+            if need_side:
+                steps.append(("sig", "main", "fork"))
+            steps.append(("build_rbf", "pairwise", pw("build_rbf"), "main"))
         if need_side:
-            steps += [("sig", "main", "fork"), ("wait", "side", "fork")]
+            steps += ([] if rbf_first else [("sig", "main", "fork")]) + [("wait", "side", "fork")]
             if v_on_side:
                 # Sigma_v first on the side stream (one small latency-kernel launch beside the RBF
                 # builders on the main stream, which waits only for it), then the other factors
@@ -894,7 +903,7 @@ class DsviEngine:
         if early:
             steps += [("build_rbf22", "pairwise", pw("build_rbf22"), "main"),
                       ("wait", "side2", "begun"), ("build_rbf12", "pairwise", pw("build_rbf12"), "side2")]
-        else:
+        elif not rbf_first:
             steps.append(("build_rbf", "pairwise", pw("build_rbf"), "main"))
         if v_on_side:
             steps.append(("wait", "main", "syrk"))
