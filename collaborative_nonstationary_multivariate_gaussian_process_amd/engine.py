@@ -873,7 +873,8 @@ class DsviEngine:
         # so that they, not Sigma_v on the side stream, are the step-begin node's first child and keep its
         # hardware queue (the graph put them behind a 23 us cross-queue barrier); 2 = also Sigma_v on main
         head = os.environ.get("NMGP_HEAD", "0") if (not early and not self.p64) else "0"
-        v_on_side = need_side and not elbo_mode and self.dt == torch.float64 and head != "2"
+        v_on_side = need_side and not elbo_mode and self.dt == torch.float64 and head != "2" \
+            and os.environ.get("NMGP_V_SIDE", "1") != "0"
         rbf_first = head in ("1", "2")
         if rbf_first:
             if need_side:
