@@ -82,6 +82,15 @@ def _auto_ksplit(k_eff, group_tiles, work_per_wg):
     return 1
 
 
+def _cap_ksplit(ksplit, k_eff, kt_cap):
+    """Split-K factor raised so that no chunk of a k range of k_eff runs more than ~kt_cap k-tiles of
+    GEMM_BK (GemmGroup(kt_cap=)); at most 16 chunks, never lowered."""
+    if kt_cap <= 0:
+        return ksplit
+    kt = -(-max(k_eff, 1) // GEMM_BK)
+    return max(ksplit, min(16, -(-kt // kt_cap)))
+
+
 LAT_TILE = 32       # output tile of the latency kernel (csrc/gemm_lat.hip LTM / LTN)
 LAT_PANEL = 64      # panel alignment the latency kernel needs of k-blocked operands
 LAT_WAVES, LAT_KP = 8, 32   # waves per workgroup and k-panel width (gemm_lat.hip launch config 1)
@@ -204,8 +213,7 @@ class GemmGroup:
         for i, d in enumerate(descs):
             if d.ksplit <= 1:
                 d.ksplit = _auto_ksplit(eff[i][1], group_tiles, work_per_wg)
-            if kt_cap > 0:
-                d.ksplit = max(d.ksplit, min(16, -(-(-(-eff[i][1] // GEMM_BK)) // kt_cap)))
+            d.ksplit = _cap_ksplit(d.ksplit, eff[i][1], kt_cap)
         # longest k-loop per workgroup first: those workgroups are dispatched first instead of
         # forming the launch's tail (problems of one group write disjoint outputs, so their order in
         # the launch is free)

@@ -157,3 +157,18 @@ def test_driver_data_pickle_loader_reads_reference_toy_pickle():
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", "toy_forward.npz"))
     assert np.array_equal(np.concatenate([a.reshape(-1) for a in obj[0]]), g["x"])
     assert np.array_equal(np.concatenate([a.reshape(-1) for a in obj[1]]), g["y"])
+
+
+def test_split_k_rules():
+    """GemmGroup's split-K choices (hip_ops): the automatic rule splits only tiny groups and problems far
+    beyond the balanced per-workgroup share; the k-tile cap (kt_cap, round 3: 20 for the fp64 P-bar_G
+    group) only raises a split, to at most 16 chunks.  PM2.5 P-bar_G: output D-1 runs k = 5 x 256 = 40 k-tiles
+    -> 2 chunks, output 0 (8 k-tiles) stays whole."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import hip_ops as H
+    assert H._auto_ksplit(1280, 640, 5) == 1                 # PM2.5 P-bar_G under the automatic rule
+    assert H._cap_ksplit(1, 1280, 20) == 2 and H._cap_ksplit(1, 256, 20) == 1
+    assert H._cap_ksplit(1, 1024, 20) == 2 and H._cap_ksplit(1, 768, 20) == 2
+    assert H._cap_ksplit(3, 256, 20) == 3                    # never lowered
+    assert H._cap_ksplit(1, 10 ** 6, 2) == 16                # at most 16 chunks
+    assert H._cap_ksplit(5, 10 ** 6, 0) == 5                 # 0: no cap
+    assert H._auto_ksplit(2000, 16, 100) > 1                 # tiny groups split long k loops
