@@ -505,6 +505,19 @@ def cpu_baseline(seconds, xs, ys, z):
                       f"D=5, M=256, B=2000 config; mean {1000 * float(np.mean(steady)):.1f} ms/it"}
 
 
+def _relaunch_under_torchrun(n):
+    """`python bench.py --gpus N` without a launcher: run the same command under torchrun with N ranks on
+    127.0.0.1 as a child process (no exec: the parent has not touched the GPU, and never will)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -524,7 +537,16 @@ def main():
     ap.add_argument("--elbo-D", type=int, default=128, help="channels of the ELBO leg (default: ECoG-full 128)")
     args = ap.parse_args()
 
+    # --gpus N is honoured before anything touches the GPU: without a launcher, N > 1 re-runs this
+    # script under torchrun as a CHILD process (one rank per GPU) and exits with its status; under a
+    # launcher whose WORLD_SIZE disagrees with N the run is refused instead of reporting the wrong N
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_relaunch_under_torchrun(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; refusing to report n_gpus={world}",
+              file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -575,9 +597,11 @@ def main():
 
     if world > 1:
         dist.broadcast(model._theta, 0)
-    graph = None
+    graph, upd_graph = None, None
     if not args.eager:
         graph = trainer.capture(eng, include_update=(world == 1))
+        if world > 1:
+            upd_graph = trainer.capture_update(world)
 
     def step(i):
         if graph is not None:
@@ -585,8 +609,12 @@ def main():
         else:
             trainer.grad_step(eng)
         if world > 1:
-            DD.allreduce_mean_(model._grad)                  # one RCCL all-reduce of the flat gradient
-            trainer.update()
+            if upd_graph is not None:
+                DD.allreduce_sum_(model._grad)               # one RCCL all-reduce of the flat gradient
+                upd_graph.replay()                           # 1/world + Adam, replayed from their own graph
+            else:
+                DD.allreduce_mean_(model._grad)
+                trainer.update()
         elif graph is None:
             trainer.update()
 

@@ -30,7 +30,7 @@ class GemmDesc(ctypes.Structure):
                 ("alpha", c_dbl), ("beta", c_dbl), ("gamma", c_dbl), ("diag_add", c_dbl),
                 ("tiles_m", c_int), ("tiles_n", c_int), ("tile_start", c_int), ("seg_span", c_int),
                 ("ksplit", c_int), ("pad2_", c_int), ("ws", c_vp), ("counters", c_vp),
-                ("sA_b", c_i64), ("sB_b", c_i64), ("sC_b", c_i64), ("batch", c_int), ("sAS_kb", c_int)]
+                ("sA_b", c_i64), ("sB_b", c_i64), ("sC_b", c_i64), ("batch", c_int), ("pad3_", c_int)]
 
 
 class PairwiseDesc(ctypes.Structure):
@@ -65,14 +65,13 @@ class DsviArgs(ctypes.Structure):
                 ("scal_off", c_i64 * 8), ("T", c_vp),
                 ("pair_q0", c_int), ("n_wfac", c_int), ("kl_v", c_int), ("pair_pad", c_int), ("T64", c_vp),
                 ("kl_f0", c_int), ("kl_f1", c_int), ("v64", c_vp), ("ellZ64", c_vp), ("K12_64", c_vp),
-                ("t64", c_vp), ("scal64", c_vp), ("wscale", c_vp)]
+                ("t64", c_vp), ("scal64", c_vp)]
 
 
 # flags (include/nmgp_hip.h)
 A_LOWER, A_UPPER, B_LOWER, B_UPPER = 1, 2, 4, 8
 OUT_LOWER, OUT_TRIL, KSCALE, EPI, EPI_E_LOWER, DIAG_ADD, EPI_RS_NEG = 16, 32, 64, 128, 256, 512, 1024
 LAT_COLPACK = 2048
-ASCALE = 4096
 RBF, GIBBS = 0, 1
 DIST_DIFF, DIST_EXPAND = 0, 1
 HYP_LOG = 1

@@ -1027,155 +1027,6 @@ __device__ __attribute__((always_inline)) inline void chol3_trtri_role(T* Am, T*
   }
 }
 
-// The inverse role with a one-step prefetch (used with the lookahead factor role): while block step kb
-// computes, every wave already polls for column kb+1 and has its loads of L[:, kb+1] / L_kk^-1 in flight
-// (registers, double-buffered LDS), so a factor role that runs ahead costs no load round trip per step.
-// Each wave polls the progress word itself (no workgroup barrier, whose fence would also drain the X
-// stores of the previous step).  Same arithmetic as chol3_trtri_role.
-template <typename T>
-__device__ __attribute__((always_inline)) inline bool poll_flag(unsigned long long* flag, int need, int nt) {
-  for (int spin = 0; spin < (1 << 26); ++spin) {
-    const unsigned long long f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (f >= kFlagTag + (unsigned long long)need && f <= kFlagTag + (unsigned long long)nt) return true;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  return false;
-}
-
-template <typename T, int NTPW>
-__device__ __attribute__((always_inline)) inline void chol5_trtri_role(T* Am, T* Xm, int n, int64_t lda,
-                                                                       int64_t ldx, int par, unsigned char* smem_raw) {
-  using acc_t = typename Mfma<T>::acc_t;
-  constexpr int PER = 256 * 16 / (RW * 64);
-  const int nt = (n + 15) >> 4, NR = nt * 16;
-  T* Ps0 = (T*)smem_raw;                 // 2 x NR x CP: L[:, kb] by parity
-  T* Xrow = Ps0 + 2 * NR * CP;           // NR x CP
-  T* LiT0 = Xrow + NR * CP;              // 2 x 16 x CP: (L_kk^-1)^T by parity
-  unsigned long long* flag = ctl_flag(Xm, n);
-  unsigned long long* done = ctl_done(Xm, n);
-  const __amdgpu_buffer_rsrc_t rAm = make_rsrc(Am, ((int64_t)(n - 1) * lda + n) * (int64_t)sizeof(T));
-  const __amdgpu_buffer_rsrc_t rXm = make_rsrc(Xm, ((int64_t)(n - 1) * ldx + n) * (int64_t)sizeof(T));
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  int ntp = 0;
-  for (int j = par; j < nt; j += 2) ntp += nt - j;
-  int ib[NTPW], jb[NTPW];
-  acc_t acc[NTPW];
-#pragma unroll
-  for (int u = 0; u < NTPW; ++u) {
-    const int tp = w + RW * u;
-    ib[u] = -1;
-    jb[u] = -1;
-    if (tp < ntp) {
-      tri_decode_par(tp, par, ib[u], jb[u]);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gr = ib[u] * 16 + Mfma<T>::row(lane, r), gc = jb[u] * 16 + (lane & 15);
-        acc[u][r] = gr == gc ? (T)1 : (T)0;
-      }
-    }
-  }
-  for (int i = 2 * w + par; i < n; i += 2 * RW)
-    for (int j = ((i >> 4) + 1) * 16 + lane; j < n; j += 64) {
-      if (i != 0 || j < n - 2 * kCtl<T>) Xm[(int64_t)i * ldx + j] = 0;
-      Am[(int64_t)i * lda + j] = 0;
-    }
-  bool ok = true;
-  T v[PER], vl = (T)0;
-  auto fetch = [&](int kb) {
-    const int nrow = NR - kb * 16;
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      const int idx = t + q * RW * 64, lr = idx >> 4, c = idx & 15;
-      const int gr = kb * 16 + lr, gc = kb * 16 + c;
-      const uint32_t off =
-          (idx < nrow * 16 && gr < n && gc < n) ? (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)) : 0x80000000u;
-      v[q] = bload_sc1<T>(rAm, off);
-    }
-    if (t < 256) {
-      const int r = t >> 4, c = t & 15;
-      const int gr = kb * 16 + r, gc = kb * 16 + c;
-      const uint32_t off = (gr < n && gc < n) ? (uint32_t)(((int64_t)gr * ldx + gc) * sizeof(T)) : 0x80000000u;
-      vl = bload_sc1<T>(rXm, off);
-      if (gr >= n || gc >= n) vl = (gr == gc) ? (T)1 : (T)0;
-    }
-  };
-  auto stash = [&](int kb) {
-    const int nrow = NR - kb * 16;
-    T* Ps = Ps0 + (kb & 1) * NR * CP;
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      const int idx = t + q * RW * 64;
-      if (idx < nrow * 16) Ps[(idx >> 4) * CP + (idx & 15)] = v[q];
-    }
-    if (t < 256) LiT0[(kb & 1) * 16 * CP + (t & 15) * CP + (t >> 4)] = vl;
-  };
-  ok &= poll_flag<T>(flag, 1, nt);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  fetch(0);
-  stash(0);
-  for (int kb = 0; kb < nt; ++kb) {
-    lds_barrier();                   // step kb's panel is in LDS; step kb-1's Xrow / panel reads are done
-    if (w == 0) CHOL4_STAMP(3 + par, kb, 0);
-    const T* Ps = Ps0 + (kb & 1) * NR * CP;
-    const T* LiT = LiT0 + (kb & 1) * 16 * CP;
-    const bool pre = kb + 1 < nt;
-    if (pre) {
-      ok &= poll_flag<T>(flag, kb + 2, nt);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      fetch(kb + 1);                 // in flight during this step's MFMA work
-    }
-    if (w == 0) CHOL4_STAMP(3 + par, kb, 1);
-#pragma unroll
-    for (int u = 0; u < NTPW; ++u) {
-      if (ib[u] == kb) {
-        const int xj = __builtin_amdgcn_readfirstlane(jb[u] - kb) + kb;
-        acc_t x = {0, 0, 0, 0};
-        if (xj == kb) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) x[r] = LiT[(lane & 15) * CP + Mfma<T>::row(lane, r)];
-        } else {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) x = Mfma<T>::mma(LiT[Mfma<T>::row(lane, s) * CP + (lane & 15)], acc[u][s], x);
-        }
-        acc[u] = x;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Xrow[(xj * 16 + Mfma<T>::row(lane, r)) * CP + (lane & 15)] = x[r];
-      }
-    }
-    lds_barrier();
-#pragma unroll
-    for (int u = 0; u < NTPW; ++u) {
-      if (ib[u] > kb && jb[u] >= 0 && jb[u] <= kb) {
-        const int ra = __builtin_amdgcn_readfirstlane(ib[u] - kb) * 16 + (lane & 15);
-        const int xj = __builtin_amdgcn_readfirstlane(jb[u] - kb) + kb;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int kr = Mfma<T>::row(lane, s);
-          acc[u] = Mfma<T>::mma(-Ps[ra * CP + kr], Xrow[(xj * 16 + kr) * CP + (lane & 15)], acc[u]);
-        }
-      }
-    }
-    const int ncol = kb >= par ? (kb - par) / 2 + 1 : 0;
-    for (int idx = t; idx < ncol * 256; idx += RW * 64) {
-      const int j = par + 2 * (idx >> 8), k = (idx >> 4) & 15, c = idx & 15;
-      const int gr = kb * 16 + k, gc = j * 16 + c;
-      if (gr < n && gc < n) Xm[(int64_t)gr * ldx + gc] = Xrow[(j * 16 + k) * CP + c];
-    }
-    if (pre) stash(kb + 1);
-    if (w == 0) CHOL4_STAMP(3 + par, kb, 2);
-  }
-  if (!ok && lane == 0) spin_gave_up(NMGP_STATUS_CHOL_SPIN);
-  __syncthreads();                   // every wave of this consumer is done with the progress word
-  if (t == 0) {
-    const unsigned long long old = __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == kDoneTag + 1ull) {
-      __hip_atomic_store(flag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
 template <typename T, int NTPW, int NTPW1>
 __global__ __launch_bounds__(RW * 64) void chol_inv3_kernel(T* A, int n, int64_t lda, int64_t strideA, T* X,
                                                             int64_t ldx, int64_t strideX, int32_t* info, int col_off,
@@ -1516,368 +1367,6 @@ __global__ __launch_bounds__(RW * 64) void chol_inv7_kernel(T* A, int n, int64_t
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// Lookahead factor role (round 3).  The factor workgroup (12 waves) splits the block step by role so
-// that the panel of column k+1 runs while the trailing update of step k is still on the matrix cores:
-//   wave 0 (diagonal wave): the pivot chain.  Lanes 0..15 hold the 16 rows of the diagonal block,
-//     lanes 16..31 sixteen identity rows (which come out as L_kk^-T); the column loop is
-//     chol2_potrf_role's forward substitution with the next pivot formed before the current column's
-//     scaling (sqrt_recip + mul + fma per column on the critical path).  It leaves in LDS the table
-//     [inv_j, L_{j+1..15, j}] (136 values) that the panel rows need, L_kk and L_kk^-T.
-//   waves 1..3 (row waves): the panel rows below the diagonal block, two slots of 64 rows per wave.
-//     They load their rows of column k while the diagonal wave runs, then apply the same column loop
-//     with the table values read as LDS broadcasts (no cross-lane traffic), and write L[:, k] to LDS.
-//   waves 4..11 (update waves): own every lower 16x16 tile in MFMA accumulators (17 per wave).  Step k:
-//     apply L[:, k] to the tiles of block column k+1 and hand them to waves 0..3 (LDS), then the rest of
-//     the trailing update, then publish their share of L[:, k] and L_kk^-1 to global (coalesced) for
-//     the inverse workgroups (chol5_trtri_role).
-// In-workgroup hand-offs are LDS counters (release / acquire, bounded spins): colcnt[p] counts the update
-// waves' spills of columns of parity p, diag the diagonal steps done, rows the row-wave steps done, pub
-// the drained publishes (the last update wave to drain column k-1 raises the global progress word to k).
-// LDS double buffers by parity: column k+2 reuses column k's buffers only once every update wave spilled
-// column k+2, i.e. finished step k (its publish included).  Every operation is chol2_potrf_role's in the
-// same order, so L and L^-1 are bit-identical to the three-role kernel's.
-constexpr int kWaves6 = 12;             // waves of every workgroup of chol_inv6_kernel
-constexpr int kRowW = 3;                // row waves
-constexpr int kUpdW = kWaves6 - 1 - kRowW;   // update waves
-constexpr int kRowSlots = 2;            // 3 x 2 x 64 = 384 >= 240 panel rows
-constexpr int kTab = 136;               // [inv_j, L_{j+1..15, j}] for j = 0..15
-
-__device__ inline bool lds_wait_ge(int* p, int target) {
-  for (int spin = 0; spin < (1 << 24); ++spin) {
-    if (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  return false;
-}
-__device__ inline int tab_off(int j) { return j * 16 - j * (j - 1) / 2; }   // start of column j's entries
-
-template <typename T, int R, int J0 = 0, int J1 = 16>
-__device__ __attribute__((always_inline)) inline void rows_apply(T (&a)[kRowSlots][16], const T* tab) {
-#pragma unroll
-  for (int j = J0; j < J1; ++j) {
-    const T inv = tab[tab_off(j)];
-#pragma unroll
-    for (int s = 0; s < R; ++s) a[s][j] = a[s][j] * inv;
-#pragma unroll
-    for (int c = j + 1; c < 16; ++c) {
-      const T lcj = tab[tab_off(j) + c - j];
-#pragma unroll
-      for (int s = 0; s < R; ++s) a[s][c] = fma(-a[s][j], lcj, a[s][c]);
-    }
-  }
-}
-
-template <typename T, int NTPW>
-__device__ __attribute__((always_inline)) inline void chol6_potrf_role(T* Am, T* Xm, int n, int64_t lda, int64_t ldx,
-                                                                       int32_t* info, int col_off, int info_first,
-                                                                       int mat, unsigned char* smem_raw) {
-  using acc_t = typename Mfma<T>::acc_t;
-  const int nt = (n + 15) >> 4, NR = nt * 16;
-  T* colbuf0 = (T*)smem_raw;           // 2 x NR x CP: block column k (parity k & 1) before its panel
-  T* Ps0 = colbuf0 + 2 * NR * CP;      // 2 x NR x CP: L[:, k] (local rows, diagonal block first)
-  T* LiT0 = Ps0 + 2 * NR * CP;         // 2 x 16 x CP: L_kk^-T rows by parity
-  T* Tab0 = LiT0 + 32 * CP;            // 2 x 136: the diagonal wave's table by parity
-  // [0], [1] colcnt by parity, [2] diag, [3] rows, [4] pub, [5] table column groups published (4 columns
-  // each, k * 4 + g + 1), [6] diagonal tiles spilled ahead (k + 1: tile (k+1, k+1) with step k applied),
-  // [7] update-wave steps finished (their last reads of Ps / LiT of that step done)
-  int* ctl = (int*)(Tab0 + 2 * kTab);
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  if (t < 16) ctl[t] = 0;
-  __syncthreads();
-  const __amdgpu_buffer_rsrc_t rAm = make_rsrc(Am, ((int64_t)(n - 1) * lda + n) * (int64_t)sizeof(T));
-  if (w == 0) {
-    // ------------------------------------------------------------------ diagonal wave
-    // the pivot chain is the kernel's critical path: it wins issue arbitration over the update waves'
-    // MFMAs on its SIMD (without it the chain ran ~2x slower while the trailing update was in flight)
-    __builtin_amdgcn_s_setprio(3);
-    int first_fail = 0;
-    bool ok = true;
-    for (int k = 0; k < nt; ++k) {
-      if (k == 0) {
-        ok &= lds_wait_ge(&ctl[0], kUpdW);                    // the prologue spill of block column 0
-      } else {
-        ok &= lds_wait_ge(&ctl[6], k);                        // tile (k, k), spilled ahead by its owner
-        // Ps / LiT / Tab of this parity were last read by the update waves in step k - 2
-        if (k >= 2) ok &= lds_wait_ge(&ctl[7], kUpdW * (k - 1));
-      }
-      CHOL4_STAMP(0, k, 0);
-      const T* cb = colbuf0 + (k & 1) * NR * CP;
-      T a[16];
-      {
-        const T keep = lane < 16 ? (T)1 : (T)0;
-        const T* src = cb + (lane & 15) * CP;
-#pragma unroll
-        for (int c = 0; c < 16; ++c) a[c] = fma(src[c], keep, (lane - 16 == c) ? (T)1 : (T)0);
-      }
-      T* tab = Tab0 + (k & 1) * kTab;
-      unsigned int bad = 0;
-      T d = readlane(a[0], 0);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        T bn = (T)0, an = (T)0;
-        if (j < 15) {
-          bn = readlane(a[j], j + 1);
-          an = readlane(a[j + 1], j + 1);
-        }
-        bad |= (d > (T)0) ? 0u : (1u << j);
-        T sj, inv;
-        sqrt_recip(d, sj, inv);
-        if (j < 15) {
-          const T ln = bn * inv;
-          d = fma(-ln, ln, an);
-        }
-        if (lane == 0) tab[tab_off(j)] = inv;
-        a[j] = (lane == j) ? sj : a[j] * inv;
-        if (lane > j && lane < 16) tab[tab_off(j) + lane - j] = a[j];     // L_{lane, j}
-        if ((j & 3) == 3 && j < 15) {
-          // columns j-3..j of the table are complete: the row waves start on them now instead of after
-          // the whole 16-column chain
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          if (lane == 0) __hip_atomic_store(&ctl[5], k * 4 + (j >> 2) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-#pragma unroll
-        for (int c = j + 1; c < 16; ++c) a[c] = fma(-a[j], readlane(a[j], c), a[c]);
-      }
-      CHOL4_STAMP(0, k, 1);
-      if (bad && first_fail == 0) {
-        const int j0 = __builtin_ctz(bad);
-        if (k * 16 + j0 < n) first_fail = k * 16 + j0 + 1;
-      }
-      T* ps = Ps0 + (k & 1) * NR * CP;
-      T* LiT = LiT0 + (k & 1) * 16 * CP;
-      if (lane < 16) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) ps[lane * CP + c] = c > lane ? (T)0 : a[c];
-      } else if (lane < 32) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) LiT[(lane - 16) * CP + c] = a[c];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) __hip_atomic_store(&ctl[2], k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      CHOL4_STAMP(0, k, 2);
-    }
-    if (lane == 0) {
-      if (!ok) spin_gave_up(NMGP_STATUS_CHOL_SPIN);
-      if (info) {
-        if (info_first) info[mat] = first_fail ? first_fail + col_off : 0;
-        else if (first_fail && info[mat] == 0) info[mat] = first_fail + col_off;
-      }
-    }
-    return;
-  }
-  if (w <= kRowW) {
-    // ------------------------------------------------------------------ row waves
-    __builtin_amdgcn_s_setprio(2);
-    const int rw = w - 1;
-    bool ok = true;
-    for (int k = 0; k < nt; ++k) {
-      const int nrow = NR - 16 * k, nr = nrow - 16;          // panel rows below the diagonal block
-      const int H = (nr + kRowW - 1) / kRowW;                // rows of this wave: [rw H, min(nr, rw H + H))
-      const int o0 = rw * H, o1 = min(nr, o0 + H);
-      const int nslot = o1 > o0 ? ((o1 - o0 - 1) >> 6) + 1 : 0;   // wave-uniform, <= 2
-      ok &= lds_wait_ge(&ctl[k & 1], kUpdW * ((k >> 1) + 1));
-      const T* cb = colbuf0 + (k & 1) * NR * CP;
-      T a[kRowSlots][16];
-#pragma unroll
-      for (int s = 0; s < kRowSlots; ++s) {
-        const int o = o0 + s * 64 + lane;
-        const T* src = cb + (16 + min(o, nr - 1 < 0 ? 0 : nr - 1)) * CP;
-#pragma unroll
-        for (int c = 0; c < 16; ++c) a[s][c] = (s < nslot) ? src[c] : (T)0;
-      }
-      // the diagonal wave's table of column k, four table columns at a time as they are published
-      const T* tab = Tab0 + (k & 1) * kTab;
-      ok &= lds_wait_ge(&ctl[5], k * 4 + 1);
-      if (w == 1) CHOL4_STAMP(1, k, 0);
-      if (nslot == 2) rows_apply<T, 2, 0, 4>(a, tab);
-      else if (nslot == 1) rows_apply<T, 1, 0, 4>(a, tab);
-      ok &= lds_wait_ge(&ctl[5], k * 4 + 2);
-      if (nslot == 2) rows_apply<T, 2, 4, 8>(a, tab);
-      else if (nslot == 1) rows_apply<T, 1, 4, 8>(a, tab);
-      ok &= lds_wait_ge(&ctl[5], k * 4 + 3);
-      if (nslot == 2) rows_apply<T, 2, 8, 12>(a, tab);
-      else if (nslot == 1) rows_apply<T, 1, 8, 12>(a, tab);
-      ok &= lds_wait_ge(&ctl[2], k + 1);
-      if (nslot == 2) rows_apply<T, 2, 12, 16>(a, tab);
-      else if (nslot == 1) rows_apply<T, 1, 12, 16>(a, tab);
-      T* ps = Ps0 + (k & 1) * NR * CP;
-#pragma unroll
-      for (int s = 0; s < kRowSlots; ++s) {
-        const int o = o0 + s * 64 + lane;
-        if (s < nslot && o < o1) {
-#pragma unroll
-          for (int c = 0; c < 16; ++c) ps[(16 + o) * CP + c] = a[s][c];
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) __hip_atomic_fetch_add(&ctl[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (w == 1) CHOL4_STAMP(1, k, 1);
-    }
-    if (!ok && lane == 0) spin_gave_up(NMGP_STATUS_CHOL_SPIN);
-    return;
-  }
-  // ------------------------------------------------------------------ update waves
-  const int sw = w - 1 - kRowW;
-  const int ntiles = nt * (nt + 1) / 2;
-  // tile coordinates packed (ib << 8 | jb, -1 = none): one scalar register per tile instead of two
-  int tij[NTPW];
-  acc_t acc[NTPW];
-#pragma unroll
-  for (int u = 0; u < NTPW; ++u) {
-    const int tt = sw + kUpdW * u;
-    int i_ = -1, j_ = -1;
-    if (tt < ntiles) tri_decode(tt, i_, j_);
-    tij[u] = tt < ntiles ? (i_ << 8) | j_ : -1;
-  }
-#define IB(u) (tij[u] < 0 ? -1 : (tij[u] >> 8))
-#define JB(u) (tij[u] < 0 ? -1 : (tij[u] & 255))
-#pragma unroll
-  for (int u = 0; u < NTPW; ++u) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int gr = IB(u) * 16 + Mfma<T>::row(lane, r), gc = JB(u) * 16 + (lane & 15);
-      const bool in = IB(u) >= 0 && gr < n && gc < n;
-      acc[u][r] = bload<T>(rAm, in ? (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)) : 0x80000000u);
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < NTPW; ++u) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int gr = IB(u) * 16 + Mfma<T>::row(lane, r), gc = JB(u) * 16 + (lane & 15);
-      if (IB(u) >= 0 && !(gr < n && gc < n)) acc[u][r] = gr == gc ? (T)1 : (T)0;   // padding past n
-    }
-  }
-  // block column 0 goes to waves 0..3 as loaded
-#pragma unroll
-  for (int u = 0; u < NTPW; ++u) {
-    if (JB(u) == 0) {
-      const int dib = __builtin_amdgcn_readfirstlane(IB(u));
-#pragma unroll
-      for (int r = 0; r < 4; ++r) colbuf0[(dib * 16 + Mfma<T>::row(lane, r)) * CP + (lane & 15)] = acc[u][r];
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if (lane == 0) __hip_atomic_fetch_add(&ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  const __amdgpu_buffer_rsrc_t rXm = make_rsrc(Xm, ((int64_t)(n - 1) * ldx + n) * (int64_t)sizeof(T));
-  unsigned long long* flag = ctl_flag(Xm, n);
-  // this wave's stores of column kcol - 1 are complete; the last update wave to get there raises the
-  // inverse workgroups' progress word to kcol
-  auto drained = [&](int kcol) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-      const int old = __hip_atomic_fetch_add(&ctl[4], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (old == kUpdW * kcol - 1)
-        __hip_atomic_store(flag, kFlagTag + (unsigned long long)kcol, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  };
-  // L[:, k] (final output A) and L_kk^-1 (= the final X[k, k]) from LDS, this wave's share, 16
-  // consecutive lanes per row
-  auto publish = [&](int k) {
-    const int nrow = NR - 16 * k;
-    const T* ps = Ps0 + (k & 1) * NR * CP;
-    const T* LiT = LiT0 + (k & 1) * 16 * CP;
-    for (int e = sw * 64 + lane; e < nrow * 16; e += kUpdW * 64) {
-      const int lr = e >> 4, c = e & 15;
-      const int gr = k * 16 + lr, gc = k * 16 + c;
-      if (gr < n && gc < n) bstore_sc1<T>(rAm, (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)), ps[lr * CP + c]);
-    }
-    for (int e = sw * 64 + lane; e < 256; e += kUpdW * 64) {
-      const int r = e >> 4, c = e & 15;                // X[k, k](r, c) = L_kk^-1(r, c) = LiT(c, r)
-      const int gr = k * 16 + r, gc = k * 16 + c;
-      if (gr < n && gc < n) bstore_sc1<T>(rXm, (uint32_t)(((int64_t)gr * ldx + gc) * sizeof(T)), LiT[c * CP + r]);
-    }
-  };
-  bool ok = true;
-  for (int k = 0; k + 1 < nt; ++k) {
-    ok &= lds_wait_ge(&ctl[3], kRowW * (k + 1));            // (implies the diagonal wave's step k)
-    if (sw == 0) CHOL4_STAMP(2, k, 0);
-    const T* ps = Ps0 + (k & 1) * NR * CP;
-    T* cb = colbuf0 + ((k + 1) & 1) * NR * CP;
-    // 1. block column k+1 first: the next panel's input.  Its diagonal tile before the others: the
-    // diagonal wave starts step k+1 on it alone (ctl[6])
-#pragma unroll
-    for (int u = 0; u < NTPW; ++u) {
-      if (JB(u) == k + 1 && IB(u) == k + 1) {
-        const int ra = 16 + (lane & 15);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int kr = Mfma<T>::row(lane, s);
-          acc[u] = Mfma<T>::mma(-ps[ra * CP + kr], ps[ra * CP + kr], acc[u]);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) cb[Mfma<T>::row(lane, r) * CP + (lane & 15)] = acc[u][r];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_store(&ctl[6], k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < NTPW; ++u) {
-      if (JB(u) == k + 1 && IB(u) > k + 1) {
-        const int ra = __builtin_amdgcn_readfirstlane(IB(u) - k) * 16 + (lane & 15);
-        const int rb = 16 + (lane & 15);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int kr = Mfma<T>::row(lane, s);
-          acc[u] = Mfma<T>::mma(-ps[ra * CP + kr], ps[rb * CP + kr], acc[u]);
-        }
-        const int dib = __builtin_amdgcn_readfirstlane(IB(u) - k - 1);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) cb[(dib * 16 + Mfma<T>::row(lane, r)) * CP + (lane & 15)] = acc[u][r];
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) __hip_atomic_fetch_add(&ctl[(k + 1) & 1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (sw == 0) CHOL4_STAMP(2, k, 1);
-    if (k > 0) drained(k);             // (off the panel hand-off: column k-1 was published a step ago)
-    // 2. the rest of the trailing update, overlapped with the panel of column k+1
-#pragma unroll
-    for (int u = 0; u < NTPW; ++u) {
-      if (JB(u) > k + 1) {
-        const int ra = __builtin_amdgcn_readfirstlane(IB(u) - k) * 16 + (lane & 15);
-        const int rb = __builtin_amdgcn_readfirstlane(JB(u) - k) * 16 + (lane & 15);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int kr = Mfma<T>::row(lane, s);
-          acc[u] = Mfma<T>::mma(-ps[ra * CP + kr], ps[rb * CP + kr], acc[u]);
-        }
-      }
-    }
-    if (sw == 0) CHOL4_STAMP(2, k, 2);
-    publish(k);        // (Ps / LiT of this parity are rewritten only after every update wave counted step k)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) __hip_atomic_fetch_add(&ctl[7], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-  ok &= lds_wait_ge(&ctl[3], kRowW * nt);                   // the last panel
-  if (nt > 1) drained(nt - 1);
-  publish(nt - 1);
-  drained(nt);
-  if (sw == 0) CHOL4_STAMP(2, nt, 0);
-  if (!ok && lane == 0) spin_gave_up(NMGP_STATUS_CHOL_SPIN);
-#undef IB
-#undef JB
-}
-
-template <typename T, int NTPW, int NTPW1>
-__global__ __launch_bounds__(kWaves6 * 64) void chol_inv6_kernel(T* A, int n, int64_t lda, int64_t strideA, T* X,
-                                                                 int64_t ldx, int64_t strideX, int32_t* info,
-                                                                 int col_off, int info_first) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  const int mat = blockIdx.x / 3, role = blockIdx.x - 3 * mat;
-  T* Am = A + (int64_t)mat * strideA;
-  T* Xm = X + (int64_t)mat * strideX;
-  if (role == 0) {
-    if (threadIdx.x == 0) __hip_atomic_store(ctl_done(Xm, n), kDoneTag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    chol6_potrf_role<T, NTPW>(Am, Xm, n, lda, ldx, info, col_off, info_first, mat, smem_raw);
-  } else {
-    // the inverse role is written for RW waves: the others end here (ended waves leave the barriers)
-    if (threadIdx.x >= RW * 64) return;
-    chol5_trtri_role<T, NTPW1>(Am, Xm, n, lda, ldx, role - 1, smem_raw);
-  }
-}
-
 template <typename T, int NTPW>
 __global__ __launch_bounds__(RW * 64) void chol_inv2_kernel(T* A, int n, int64_t lda, int64_t strideA, T* X,
                                                             int64_t ldx, int64_t strideX, int32_t* info, int col_off,
@@ -2000,24 +1489,6 @@ static void chol_inv3_go(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx
                      sA, X, ldx, sX, info, col_off, info_first);
 }
 
-template <typename T> static size_t chol_inv4_smem(int n) {
-  const int nt = (n + 15) >> 4;
-  return (size_t)(4 * nt * 16 * CP + 32 * CP + 2 * kTab) * sizeof(T) + 64;
-}
-
-template <typename T, int NTPW, int NTPW1>
-static void chol_inv4_go(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx, int64_t sX, int64_t batch,
-                         int32_t* info, size_t sm, hipStream_t s, int col_off, int info_first) {
-  static bool attr_done = false;
-  if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)chol_inv6_kernel<T, NTPW, NTPW1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr_done = true;
-  }
-  hipLaunchKernelGGL((chol_inv6_kernel<T, NTPW, NTPW1>), dim3((unsigned)(3 * batch)), dim3(kWaves6 * 64), sm, s, A, n,
-                     lda, sA, X, ldx, sX, info, col_off, info_first);
-}
-
 template <typename T, int NTPW1, int NTPWU>
 static void chol_inv7_go(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ldx, int64_t sX, int64_t batch,
                          int32_t* info, size_t sm, hipStream_t s, int col_off, int info_first) {
@@ -2041,13 +1512,6 @@ static bool use_four_role(int n, int64_t batch) {
   const char* e = getenv("NMGP_CHOL_4ROLE");
   if (e) return atoi(e) != 0;
   return n >= 192;
-}
-
-// The lookahead factor role (chol_inv4_kernel) is the default wherever the three-role kernel runs;
-// NMGP_CHOL_LA=0 restores chol_inv3_kernel (A/B).
-static bool use_lookahead() {
-  const char* e = getenv("NMGP_CHOL_LA");   // read per launch: tests switch it in-process
-  return e && atoi(e) != 0;                 // (opt-in until measured faster on the box)
 }
 
 // the multi-role kernels keep 64-bit control words in X's row 0: f32 needs them 8-byte aligned
@@ -2075,19 +1539,6 @@ static int chol_inv_small(T* A, int n, int64_t lda, int64_t sA, T* X, int64_t ld
         chol_inv7_go<T, 5, 4>(A, n, lda, sA, X, ldx, sX, batch, info, sm7, s, col_off, info_first);
       else
         chol_inv7_go<T, 9, 10>(A, n, lda, sA, X, ldx, sX, batch, info, sm7, s, col_off, info_first);
-      NMGP_CHECK_LAUNCH();
-      return NMGP_OK;
-    }
-    if (two_role && use_three_role(n, batch) && !getenv("NMGP_CHOL_FUSED1") && use_lookahead()) {
-      const size_t sm4 = chol_inv4_smem<T>(n) > sm_min ? chol_inv4_smem<T>(n) : sm_min;
-      // update-wave tiles ceil(ntiles / kUpdW); inverse-role tiles as the three-role kernel's thresholds
-      static_assert(kUpdW * 5 >= RW * 5 && kUpdW * 9 >= RW * 9 && kUpdW * 17 >= 136, "tile ownership");
-      if (ntiles <= RW * 5)
-        chol_inv4_go<T, 5, 3>(A, n, lda, sA, X, ldx, sX, batch, info, sm4, s, col_off, info_first);
-      else if (ntiles <= RW * 9)
-        chol_inv4_go<T, 9, 5>(A, n, lda, sA, X, ldx, sX, batch, info, sm4, s, col_off, info_first);
-      else
-        chol_inv4_go<T, 17, 9>(A, n, lda, sA, X, ldx, sX, batch, info, sm4, s, col_off, info_first);
       NMGP_CHECK_LAUNCH();
       return NMGP_OK;
     }

@@ -372,30 +372,21 @@ __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
   if (elbo) return;
   __syncthreads();
 
-  // ---- phase 3: W-hat = diag(2 adjoint) W -- as the (2D, B) scale table the backward GEMMs apply to
-  // their W operand (wscale; 0 for s > o) or, without it, W / W_P scaled in place (rows s > o zeroed:
-  // they are not computed by the W GEMM) -- and the P-bar initial rows
+  // ---- phase 3: W-hat = diag(2 adjoint) W, W / W_P scaled in place (rows s > o zeroed: they are not
+  // computed by the W GEMM), and the P-bar initial rows
   const T cg = scal[0], c0 = scal[1], c1 = scal[2];
-  if (a.wscale) {
-    T* ws = (T*)a.wscale;
-    for (int s = t; s < D; s += 256) {
-      ws[(int64_t)s * B + r] = s <= o ? sv[s] : (T)0;
-      ws[(int64_t)(D + s) * B + r] = s <= o ? sv[D + s] : (T)0;
+  for (int s = 0; s <= o; ++s) {
+    const T fg = sv[s], fp = sv[D + s];
+    T* wg = WG + (int64_t)s * BM + (int64_t)r * M;
+    T* wp = WP + (int64_t)s * BM + (int64_t)r * M;
+    for (int c = t; c < M; c += 256) {
+      wg[c] *= fg;
+      wp[c] *= fp;
     }
-  } else {
-    for (int s = 0; s <= o; ++s) {
-      const T fg = sv[s], fp = sv[D + s];
-      T* wg = WG + (int64_t)s * BM + (int64_t)r * M;
-      T* wp = WP + (int64_t)s * BM + (int64_t)r * M;
-      for (int c = t; c < M; c += 256) {
-        wg[c] *= fg;
-        wp[c] *= fp;
-      }
-    }
-    for (int s = o + 1; s < D; ++s) {
-      T* wg = WG + (int64_t)s * BM + (int64_t)r * M;
-      for (int c = t; c < M; c += 256) wg[c] = (T)0;
-    }
+  }
+  for (int s = o + 1; s < D; ++s) {
+    T* wg = WG + (int64_t)s * BM + (int64_t)r * M;
+    for (int c = t; c < M; c += 256) wg[c] = (T)0;
   }
   T* PbG = (T*)a.Pbar + 3 * BM + (int64_t)r * M;
   T* Pb0 = (T*)a.Pbar + 1 * BM + (int64_t)r * M;

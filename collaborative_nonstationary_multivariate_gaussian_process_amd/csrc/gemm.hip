@@ -154,8 +154,8 @@ __device__ inline bool fast_ok(const nmgp_gemm_desc& d, const Tile& tl) {
 // triangular operand's diagonal); rows past m / columns past n need none: they only feed outputs
 // that are never stored.  Two LDS stages: the MFMAs of k-tile t run while tile t+1 is written from
 // registers to the other stage and tile t+2 is fetched into them; one barrier per k-tile.  KS:
-// k-scaled B.  AS: A scaled per (row, k-block) (NMGP_ASCALE).
-template <typename T, bool KS, bool AS, typename Acc>
+// k-scaled B.
+template <typename T, bool KS, typename Acc>
 __device__ inline void mainloop_fast(const nmgp_gemm_desc& d, const Tile& tl, const UnitMap& um, T* S, int lane,
                                      int wr, int wc, Acc& c00, Acc& c01, Acc& c10, Acc& c11) {
   constexpr int V = 16 / (int)sizeof(T);  // elements per unit
@@ -214,11 +214,8 @@ __device__ inline void mainloop_fast(const nmgp_gemm_desc& d, const Tile& tl, co
     }
   };
   u32x4 ra[NU], rb[NU];
-  T rs[8], ras[NU];
+  T rs[8];
   int kload = tl.kbeg;  // k-tile the issue() calls fetch
-  // AS: row scales of A's k-block kbuA (advanced with the fetch position); rows past m read row m-1
-  const int64_t asr = tl.r0 + tl.i0;
-  const int amax = tl.m - 1 - tl.i0;
   auto issue = [&](int e) {
     ra[e] = __builtin_amdgcn_raw_buffer_load_b128(rA, oA + e * osA, 0, 0);
     rb[e] = __builtin_amdgcn_raw_buffer_load_b128(rB, oB + e * osB, 0, 0);
@@ -226,9 +223,6 @@ __device__ inline void mainloop_fast(const nmgp_gemm_desc& d, const Tile& tl, co
 #pragma unroll
       for (int v = 0; v < V; ++v) rs[e * V + v] = ksc[tl.k0 + min(kload + b_k(e * V + v), tl.K - 1)];
     }
-    // (A k-contiguous; the fetch runs up to two k-tiles past kend -- their values are masked -- so the block
-    //  index is clamped to the last k like the k-scale index above)
-    if (AS) ras[e] = ksc[(int64_t)(kbA_on ? min(kload, tl.K - 1) / tl.kbA : 0) * d.sAS_kb + asr + min(a_mn(e * V), amax)];
   };
   auto step1 = [&]() {
     kload += GBK;
@@ -258,7 +252,6 @@ __device__ inline void mainloop_fast(const nmgp_gemm_desc& d, const Tile& tl, co
       b = keep_if(b, (okm_st >> (8 + s)) & 1u);
     }
     if (KS) b *= rs[s];
-    if (AS) a *= ras[e];
     N[wa + e * wsa + v * wva] = a;
     N[GBK * LP + wb + e * wsb + v * wvb] = b;
   };
@@ -330,7 +323,6 @@ __device__ inline void mainloop_general(const nmgp_gemm_desc& d, const Tile& tl,
   const GPtr<const T> Bm = (GPtr<const T>)d.B;
   const GPtr<const T> ksc = (GPtr<const T>)(d.kscale ? d.kscale : d.B);
   const bool ksf = (tl.flags & NMGP_KSCALE) != 0;
-  const bool asf = (tl.flags & NMGP_ASCALE) != 0;
   const bool kbA_on = tl.kbA < tl.K, kbB_on = tl.kbB < tl.K;
   auto load = [&](int kt, T (&ra)[8], T (&rb)[8], T (&rs)[8], unsigned& okm) {
     okm = 0;
@@ -340,7 +332,6 @@ __device__ inline void mainloop_general(const nmgp_gemm_desc& d, const Tile& tl,
       const int gkc = min(gk, tl.K - 1);
       const int kb = kbA_on ? gkc / tl.kbA : 0, kk = gkc - kb * (kbA_on ? tl.kbA : 0);
       ra[e] = A[(tl.r0 + min(gi, tl.m - 1)) * d.sA_i + (tl.k0 + kk) * d.sA_k + (int64_t)kb * d.sA_kb];
-      if (asf) ra[e] *= ksc[(int64_t)kb * d.sAS_kb + tl.r0 + min(gi, tl.m - 1)];
       okm |= a_ok(tl.flags, gi, kk, tl.m, gk < tl.kend) ? (1u << e) : 0u;
     }
 #pragma unroll
@@ -472,14 +463,11 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, const nmgp_gemm_
   using acc_t = typename Mfma<T>::acc_t;
   acc_t acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc10 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
   if (kbeg < kend) {
-    // (A-scaled with A not k-contiguous: general loop)
-    const bool kb_fast = fast_ok<T>(d, tl) && !((flags & NMGP_ASCALE) && d.sA_k != 1);
+    const bool kb_fast = fast_ok<T>(d, tl);
     if (kb_fast && (flags & NMGP_KSCALE))
-      mainloop_fast<T, true, false>(d, tl, um, smem, lane, wr, wc, acc00, acc01, acc10, acc11);
-    else if (kb_fast && (flags & NMGP_ASCALE))
-      mainloop_fast<T, false, true>(d, tl, um, smem, lane, wr, wc, acc00, acc01, acc10, acc11);
+      mainloop_fast<T, true>(d, tl, um, smem, lane, wr, wc, acc00, acc01, acc10, acc11);
     else if (kb_fast)
-      mainloop_fast<T, false, false>(d, tl, um, smem, lane, wr, wc, acc00, acc01, acc10, acc11);
+      mainloop_fast<T, false>(d, tl, um, smem, lane, wr, wc, acc00, acc01, acc10, acc11);
     else
       mainloop_general<T>(d, tl, em, smem, lane, wr, wc, acc00, acc01, acc10, acc11);
   }

@@ -135,15 +135,10 @@ class DsviEngine:
         self.Abar = e(4, M, M)
         self.WG = e(D, B, M)
         self.WP = e(D, B, M)
-        # W-hat fold (round 3): recon writes the per-(factor, row) scales 2 g-bar / 2 s2p-bar into wsc and
-        # the backward GEMMs apply them to the W operand (NMGP_ASCALE for P-bar, NMGP_KSCALE for L-bar)
-        # instead of recon rewriting W / W_P as W-hat in place (46 MB of stores per PM2.5 step).  Not on the
-        # 128x128 L-bar kernel of the large fp32 engines (no operand scale there) nor with the latency-kernel
-        # P-bar knob; NMGP_WHAT_FOLD=0 restores the in-place W-hat.
-        big_side = self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0"
-        self.what_fold = (not big_side and os.environ.get("NMGP_WHAT_FOLD", "0") == "1"
-                          and int(os.environ.get("NMGP_BWD_LAT_WGS", "0")) == 0)
-        self.wsc = e(2 * D, B) if self.what_fold else None
+        # HCP / ECoG shapes (fp32, M >= 512): the D+Q factor products run on the 128x128 f32 MFMA kernel at
+        # per-factor offsets (BigBatch) instead of the grouped 64x64 tiles.  NMGP_BIG_SIDE=0 keeps them on the
+        # grouped kernel: the only schedule switch left, for tests/test_gpu_engine.py's equivalence check
+        self.big_side = self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0"
         self.Y = e(D + 1 + 2 * self.NPC, M)
         self.T2 = e(M, M)
         self.v, self.ellZ = e(M), e(M)
@@ -170,9 +165,8 @@ class DsviEngine:
         # fp32 engines factor the four GP priors (t, L0, L1, G) in fp64 and round L, L^-1 back: the
         # explicit-inverse projections K12 (K22 + 1e-4 I)^-1 of smooth priors otherwise lose
         # ~cond(K22) * eps32 (HCP-like fixture: P_G off by 40% with an fp32 factorization, 5e-4 with
-        # an fp64 one -- DESIGN.md §5).  NMGP_PRIOR_FP64=0 turns it off (A/B only).
-        self.prior64 = dtype == F32 and os.environ.get("NMGP_PRIOR_FP64", "1") != "0"
-        self.p64 = self.prior64 and os.environ.get("NMGP_PROJ_FP64", "1") != "0"
+        # an fp64 one -- DESIGN.md §5).
+        self.prior64 = self.p64 = dtype == F32
         if self.prior64:
             # with p64 a fifth fp64 slot in front holds Sigma_v + 1e-4 I: [v | t | L0 | L1 | G] is then
             # one contiguous batch whose first four slots factor in one launch, like the fp32 slots
@@ -190,7 +184,6 @@ class DsviEngine:
         # the v sample (fp64 factor of Sigma_v) and the prior adjoint chains (R, A-bar, builder backward,
         # hyper-parameter partial sums) are fp64 as well (tests/analysis/ecog_hyper_sensitivity.py: the
         # hyper-parameter gradients cancel to ~1e-7 of their terms; fp32 adjoints left them 14-30% off).
-        # NMGP_PROJ_FP64=0: the round-2 all-fp32 projections and adjoints (A/B only).
         if self.p64:
             z64 = lambda *s: torch.zeros(*s, dtype=F64, device=self.dev)
             self.x64, self.hyp64, self.ellX64, self.ellZ64 = z64(B), z64(8), z64(B), z64(M)
@@ -265,7 +258,6 @@ class DsviEngine:
             a.v64, a.ellZ64, a.K12_64 = self.v_A64.data_ptr(), self.ellZ64.data_ptr(), self.K12_64.data_ptr()
             a.t64, a.scal64 = self.t64.data_ptr(), self.scal64.data_ptr()
         a.kl_f0, a.kl_f1 = 0, self.NF - 1
-        a.wscale = self.wsc.data_ptr() if self.wsc is not None else 0
         kp = self._elbo_kl if elbo_mode else None
         if kp is not None:                       # this rank's share of compute_ELBO's KL terms
             a.kl_f0, a.kl_f1 = kp[0], kp[1]
@@ -310,9 +302,6 @@ class DsviEngine:
                 bl.append(H.pairwise_desc(self.Afac[NF + k], self.Z, self.Z, mode=L.RBF, hyp=th, hyp_off=hoff,
                                           hyp_log=True, diag_add=self.jitter))
         p["build_rbf"] = H.PairwiseGroup(bl, dev)
-        if not self.p64:     # (early-begin schedule: the K22 builders need only theta, the K12 ones the minibatch)
-            p["build_rbf22"] = H.PairwiseGroup(bl[1::2], dev)
-            p["build_rbf12"] = H.PairwiseGroup(bl[0::2], dev)
         p64 = self.p64
         if p64:
             # the fp64 path of fp32 engines: K12 / K22 + lam I of the RBF priors in fp64 (K22 straight into
@@ -368,7 +357,7 @@ class DsviEngine:
             d5.append(xs(FV))
             p["xs_side"] = G([xs(f) for f in range(FV)])
         p["inv3"] = G(d5) if d5 else None
-        if self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0":
+        if self.big_side:
             # HCP / ECoG shapes: the D+Q factor products are 1000s of M x M triangular products --
             # the 128x128 f32 MFMA kernel at per-factor parameter offsets instead of 64x64 grouped tiles
             offs_f, slots = fac_off[:FV], [f * MM for f in range(FV)]
@@ -436,61 +425,36 @@ class DsviEngine:
         # B2: P-bar += W-hat L^T ; L-bar = P^T W-hat ; mu-bar = P^T adjoints
         # rows of output i: P-bar_G += sum_{d <= i} W-hat_d L_d^T (W-hat_d holds only the rows of outputs
         # >= d, so k runs over the (i + 1) latent blocks that are non-zero there, not all D)
-        wsc = self.wsc
-
-        def ascaled(d, off):             # W-hat fold: A = W rows scaled by wsc[off + k-block * B + row]
-            if wsc is not None:
-                d.kscale, d.sAS_kb = H._addr(wsc, off), B
-                d.flags |= L.ASCALE
-            return d
-        ksc = (lambda off: (wsc, off)) if wsc is not None else (lambda off: None)
-        d17 = [ascaled(g(self.Pbar, self.WG, th, B, M, (i + 1) * M, (M, 1, BM), (1, M, MM), (M, 1), flags=L.B_UPPER,
-                         kb=(M, M), beta=1.0, offs=(0, sW, 3 * BM), row_seg=i), 0) for i in range(D)]
+        d17G = [g(self.Pbar, self.WG, th, B, M, (i + 1) * M, (M, 1, BM), (1, M, MM), (M, 1), flags=L.B_UPPER,
+                  kb=(M, M), beta=1.0, offs=(0, sW, 3 * BM), row_seg=i) for i in range(D)]
+        d17P = []
         for i in range(i0, i1):
-            d17.append(ascaled(g(self.Pbar, self.WP, th, B, M, M, (M, 1, 0), (1, M, 0), (M, 1), flags=L.B_UPPER,
-                                 beta=1.0, offs=(i * BM, sU + pq(i, i) * MM, 2 * BM), row_seg=i), (D + i) * B))
+            d17P.append(g(self.Pbar, self.WP, th, B, M, M, (M, 1, 0), (1, M, 0), (M, 1), flags=L.B_UPPER,
+                          beta=1.0, offs=(i * BM, sU + pq(i, i) * MM, 2 * BM), row_seg=i))
             if i > 0:
-                d17.append(ascaled(g(self.Pbar, self.WP, th, B, M, i * M, (M, 1, BM), (1, M, MM), (M, 1),
-                                     flags=L.B_UPPER, kb=(M, M), beta=1.0, offs=(0, sU + pq(i, 0) * MM, 1 * BM),
-                                     row_seg=i), D * B))
-        # the P-bar products feed R (main chain); the L-bar / mu-bar products below only accumulate
-        # gradient rows, so they run on the side stream beside bwd_R .. bwd_v2
-        # A/B knob NMGP_BWD_LAT_WGS=<n>: run P-bar on the latency kernel with split-K sized for ~n workgroups
-        # (its k runs over up to D latent blocks: 5 rounds of panels per workgroup unsplit at PM2.5)
-        bwd_lat = int(os.environ.get("NMGP_BWD_LAT_WGS", "0"))
-        p["bwd_w"] = G(d17) if not bwd_lat else H.GemmGroup(d17, dev, self.dt, seg=seg, target_wgs=bwd_lat,
-                                                             kernel="lat")
-        # split (round 3, NMGP_BWD_SPLIT): the latent P-bar_G products feed R_G on the main chain; the pair
-        # P-bar_0/1 products feed only the L0 / L1 prior adjoints and run on the third side stream
-        # k-tile caps (split-K so no workgroup runs a longer k loop; 0 = the balanced automatic split): P-bar_G
-        # is on the main chain, its output-(D-1) tiles otherwise run all D latent blocks (40 k-tiles at PM2.5).
-        # fp64 default 20 (PM2.5 A/B on the box, 3 x 300 steps interleaved, two boxes: 1370-1379 -> 1386-1400 it/s;
-        # 8 / 12 / 16 / 24 / 32 and caps on the side-stream P-bar_0/1 and L-bar groups no better:
-        # profiles/r03za_kt_cap_ab.txt).  fp32 engines keep the automatic split (their gates were measured with it).
-        capG = int(os.environ.get("NMGP_KT_CAP_WG", "20" if self.dt == torch.float64 else "0"))
-        capP = int(os.environ.get("NMGP_KT_CAP_WP", "0"))
-        capL = int(os.environ.get("NMGP_KT_CAP_LBAR", "0"))
-        p["bwd_wG"] = H.GemmGroup(d17[:D], dev, self.dt, seg=seg, kt_cap=capG)
-        # grid caps (A/B knobs): at most that many workgroups for the side-stream P-bar_0/1 and L-bar groups
-        gP = int(os.environ.get("NMGP_WP_GRID", "0"))
-        gL = int(os.environ.get("NMGP_LBAR_GRID", "0"))
-        p["bwd_wP"] = H.GemmGroup(d17[D:], dev, self.dt, seg=seg, kt_cap=capP, max_grid=gP) if len(d17) > D else None
+                d17P.append(g(self.Pbar, self.WP, th, B, M, i * M, (M, 1, BM), (1, M, MM), (M, 1),
+                              flags=L.B_UPPER, kb=(M, M), beta=1.0, offs=(0, sU + pq(i, 0) * MM, 1 * BM), row_seg=i))
+        # the latent P-bar_G products feed R_G on the main chain; the pair P-bar_0/1 products feed only the
+        # L0 / L1 prior adjoints and run on the third side stream.  P-bar_G caps its k loops at 20 k-tiles per
+        # workgroup in fp64 (output D-1's tiles otherwise run all D latent blocks, 40 k-tiles at PM2.5; round-3
+        # A/B on the box: 1370-1379 -> 1386-1400 it/s, profiles/r03za_kt_cap_ab.txt).  fp32 engines keep the
+        # automatic split (their gates were measured with it).
+        p["bwd_wG"] = H.GemmGroup(d17G, dev, self.dt, seg=seg, kt_cap=20 if self.dt == torch.float64 else 0)
+        p["bwd_wP"] = G(d17P) if d17P else None
         d17 = []
         for d in range(D):
             d17.append(g(gr, self.P, self.WG, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_TRIL, beta=1.0,
-                         offs=(3 * BM, d * BM, sW + d * MM), k_seg=d, seg_span=D - d, kscale=ksc(d * B)))
+                         offs=(3 * BM, d * BM, sW + d * MM), k_seg=d, seg_span=D - d))
             d17.append(g(gr, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1), beta=1.0,
                          offs=(3 * BM, d * B, muW + d * M), k_seg=d, seg_span=D - d))
         for (i, j) in pairs:
             typ = 2 if i == j else 1
             d17.append(g(gr, self.P, self.WP, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_TRIL, beta=1.0,
-                         offs=(typ * BM, j * BM, sU + pq(i, j) * MM), k_seg=i, kscale=ksc((D + j) * B)))
+                         offs=(typ * BM, j * BM, sU + pq(i, j) * MM), k_seg=i))
             d17.append(g(gr, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1), beta=1.0,
                          offs=(typ * BM, (D + j) * B, muU + pq(i, j) * M), k_seg=i))
-        if not (self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0"):
-            p["bwd_lbar"] = H.GemmGroup(d17, dev, self.dt, seg=seg, kt_cap=capL, max_grid=gL)
-        elif wsc is not None:
-            raise RuntimeError("W-hat fold: the 128x128 L-bar products take no operand scale")
+        if not self.big_side:
+            p["bwd_lbar"] = G(d17)
         else:
             # the D + Q L-bar products P^T W (k over each factor's row segment) on the 128x128 kernel,
             # the M x 1 mu-bar products stay one grouped launch
@@ -535,7 +499,7 @@ class DsviEngine:
                                   offs=(0, 0, M))])
             p["kl_t64b"] = G64([g(self.Abt64, self.dY64, self.dY64, M, M, 1, (1, M, 0), (M, 1, 0), (M, 1),
                                   alpha=-0.5, beta=1.0, offs=(M, M, 0))]) if self.kl_owner else None
-        if self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0":
+        if self.big_side:
             # KL L-bar of all NF factors: -C_f^-T Xs_f + diag(1/C_ii^2) L_f on the 128x128 kernel
             slots = [f * MM for f in range(NFK)]
             p["kl_lbar"] = H.BigBatch(self.Cinv, self.Xs, gr, slots, slots, fac_off[:NFK], M, M, M, lda=M, ldb=M,
@@ -715,28 +679,12 @@ class DsviEngine:
             self.noise.numel(), ctypes.c_uint64(seed), vp(counter.data_ptr()), vp(self._begin_done.data_ptr()),
             vp(self._grad.data_ptr()), self._grad.numel(), s), "step_begin")
 
-    def _begin_launch(self, s):
-        seed, counter = self._begin_args
-        self.begin_step(seed, counter, stream=s)
-
     def begin_forward_backward(self, seed, counter):
-        """begin_step + forward_backward(zero_grad=False).  NMGP_EARLY_BEGIN=1 (fp64 training engines): the
-        early-begin schedule, the step-begin launch on its own stream beside the theta-only head of the forward
-        chain.  Bit-identical, but 6% slower on the PM2.5 bench (1313 vs 1400 it/s, profiles/r03zh_early_begin_ab.txt):
-        in the replayed graph the extra root node and its cross-queue edges start the head ~10 us later, not
-        earlier.  Default: the two back to back on the current stream."""
-        early = (os.environ.get("NMGP_EARLY_BEGIN", "0") == "1" and not self.p64
-                 and getattr(self, "_dataset", None) is not None)
-        if not early:
-            self.begin_step(seed, counter)
-            return self.forward_backward(zero_grad=False)
-        self._begin_args = (seed, counter)
-        key = ("fb_early", self._theta.data_ptr(), self._grad.data_ptr(), self.frozen_mask, self.N)
-        if getattr(self, "_sched_key_early", None) != key:
-            self._sched_early = self._schedule(0, early=True)
-            self._sched_key_early = key
-        self._run(self._sched_early, None, None)
-        return self.out
+        """begin_step + forward_backward(zero_grad=False), back to back on the current stream.  (Round 3 measured
+        the step-begin launch on its own stream beside the theta-only head of the forward chain: bit-identical,
+        6% slower -- profiles/r03zh_early_begin_ab.txt.)"""
+        self.begin_step(seed, counter)
+        return self.forward_backward(zero_grad=False)
 
     def device_noise(self, seed, counter):
         H.normal_(self.noise, seed, counter=counter)   # dtype-dispatched Philox normals
@@ -745,14 +693,11 @@ class DsviEngine:
     def _call(self, fn, a, s):
         L.check(fn(ctypes.byref(a), s), fn.__name__)
 
-    def _schedule(self, elbo_mode, with_kl=True, cached=False, early=False):
-        """The ordered launch list of one step.  Items are (name, kind, callable(stream), where) with
-        where in {"main", "side"}, plus ("fork",) / ("join",) markers: the D+Q variational factors that
-        only the KL terms need are factored on a side stream, overlapping the forward chain.
-        early (training, fp64 engines with a bound dataset): the step-begin launch (minibatch gather, noise,
-        gradient zeroing) runs on its own stream ("pre") beside the theta-only head of the forward chain --
-        Sigma_v, the prior K22 builders, the first fused Cholesky -- and only the launches that read the
-        minibatch, the noise or the gradient wait for it ("begun")."""
+    def _schedule(self, elbo_mode, with_kl=True, cached=False):
+        """The ordered launch list of one step.  Items are (name, kind, callable(stream), where) with where
+        one of the four streams, plus ("sig", stream, tag) / ("wait", stream, tag) event edges: the D+Q
+        variational factors that only the KL terms need are factored on a side stream, overlapping the
+        forward chain; the backward's independent chains run on three side streams."""
         lib = L.lib()
         D, M, NF = self.D, self.M, self.NF
         MM = M * M
@@ -768,13 +713,11 @@ class DsviEngine:
             return lambda s: L.check(fn(ctypes.byref(a), s), fn.__name__)
 
         # segment-sized groups of the training step whose tile plans are computed ahead, on the side
-        # stream right after the minibatch gather (off the main chain): quad and bwd_w
+        # stream right after the minibatch gather (off the main chain).  (quad_P plans inline on side2:
+        # waiting there for the side stream's plans would be a side <-> side2 edge)
         pre_planned = set()
-        if not elbo_mode and os.environ.get("NMGP_PLAN_AHEAD", "1") != "0":
-            # (quad_P plans inline on side2: waiting there for the side stream's plans would be a
-            # side <-> side2 edge, which hipGraph instantiation does not survive on this stack)
-            split_bw = os.environ.get("NMGP_SIDE3", "1") != "0" and os.environ.get("NMGP_BWD_SPLIT", "1") != "0"
-            pre_planned = {nm for nm in (("quad", "quad_W", "bwd_wG", "bwd_wP") if split_bw else ("quad", "quad_W", "bwd_w"))
+        if not elbo_mode:
+            pre_planned = {nm for nm in ("quad", "quad_W", "bwd_wG", "bwd_wP")
                            if isinstance(p.get(nm), H.GemmGroup) and p[nm].plan is not None}
 
         def gemm(name):
@@ -864,80 +807,49 @@ class DsviEngine:
         kf0, kf1 = p["kl_range"]
         need_side = (not elbo_mode) or (with_kl and kf1 > kf0)
         steps = []
-        if early:
-            steps += [("sig", "main", "fork0"), ("wait", "pre", "fork0"),
-                      ("begin", "row", lambda s: self._begin_launch(s), "pre"), ("sig", "pre", "begun")]
-        # (fp64 engines only: in fp32 Sigma_v's summation order shows through ell_Z = exp(v), so fp32
-        # engines keep forming it exactly as the reference-checked grouped single launch does)
-        # A/B knob NMGP_HEAD (round 3): 1 = the RBF builders (main) captured before the side stream's launches,
-        # so that they, not Sigma_v on the side stream, are the step-begin node's first child and keep its
-        # hardware queue (the graph put them behind a 23 us cross-queue barrier); 2 = also Sigma_v on main
-        head = os.environ.get("NMGP_HEAD", "0") if (not early and not self.p64) else "0"
-        v_on_side = need_side and not elbo_mode and self.dt == torch.float64 and head != "2" \
-            and os.environ.get("NMGP_V_SIDE", "1") != "0"
-        rbf_first = head in ("1", "2")
-        if rbf_first:
-            if need_side:
-                steps.append(("sig", "main", "fork"))
-            steps.append(("build_rbf", "pairwise", pw("build_rbf"), "main"))
+        # Streams: main (the forward / backward dependency chain), side (variational factors, KL, L-bar, v
+        # chain), side2 (t-prior projections, t-row, K_G12, pair quad forms; in the backward the G-prior
+        # adjoint), side3 (pair P-bar and the L0 / L1 prior adjoints).  side2 and side3 synchronise with the
+        # main stream and one-way with side, never side <-> side2 both ways.  In a replayed graph
+        # a node's FIRST-created child keeps its hardware queue and every other child starts on another queue
+        # behind a cross-queue barrier (10-20 us per hop in the r03 traces), so the critical-path child of each
+        # fork is captured first (v after chol, quad_W after projG, bwd_R after bwd_wG, bwd_t1 after tbwd).
+        # Sigma_v: fp64 engines form it first on the side stream (one small launch beside the RBF builders);
+        # in fp32 its summation order shows through ell_Z = exp(v), so fp32 engines keep the grouped main launch
+        v_on_side = need_side and not elbo_mode and self.dt == torch.float64
         if need_side:
-            steps += ([] if rbf_first else [("sig", "main", "fork")]) + [("wait", "side", "fork")]
+            steps += [("sig", "main", "fork"), ("wait", "side", "fork")]
             if v_on_side:
-                # Sigma_v first on the side stream (one small latency-kernel launch beside the RBF
-                # builders on the main stream, which waits only for it), then the other factors
-                steps += [("syrk", "gemm", gemm("syrk"), "side"), ("sig", "side", "syrk"),
-                          ("syrk_side", "gemm", gemm("syrk_side"), "side")]
-            else:
-                steps.append(("syrk_side", "gemm", gemm("syrk_side"), "side"))
+                steps += [("syrk", "gemm", gemm("syrk"), "side"), ("sig", "side", "syrk")]
+            steps.append(("syrk_side", "gemm", gemm("syrk_side"), "side"))
             if pre_planned:
-                if early:
-                    steps.append(("wait", "side", "begun"))
                 steps += [("plans", "gemm_plan", plans, "side"), ("sig", "side", "plans")]
-            elif early:
-                steps.append(("wait", "side", "begun"))
             steps.append(("chol_side", "chol", chol(kf0, kf1 - kf0), "side"))
             if not elbo_mode:
                 steps.append(("xs_side", "gemm", gemm("xs_side"), "side"))
         if self.p64:
             steps += [("conv_in", "convert", conv_in, "main"),
                       ("build_rbf64", "pairwise", pw64("build_rbf64"), "main")]
-        if early:
-            steps += [("build_rbf22", "pairwise", pw("build_rbf22"), "main"),
-                      ("wait", "side2", "begun"), ("build_rbf12", "pairwise", pw("build_rbf12"), "side2")]
-        elif not rbf_first:
-            steps.append(("build_rbf", "pairwise", pw("build_rbf"), "main"))
-        if v_on_side:
-            steps.append(("wait", "main", "syrk"))
-        else:
-            steps.append(("syrk", "gemm", gemm("syrk"), "main"))
+        steps.append(("build_rbf", "pairwise", pw("build_rbf"), "main"))
+        steps.append(("wait", "main", "syrk") if v_on_side else ("syrk", "gemm", gemm("syrk"), "main"))
         # forward chain: chol -> v -> K_G22 -> chol_G -> invG -> projG.  The t-prior projections, the
         # t-row (ell_X) and K_G12 run on the second side stream beside v / K_G22 / chol_G: they are
         # needed only from invG on (T_G = K_G12 C_G^-T)
-        # In a replayed graph a node's FIRST-created child stays on the node's hardware queue and every other
-        # child starts on another queue behind a cross-queue barrier (≈ 10-20 us per hop in the r03 kernel
-        # traces).  crit: the critical-path child of each fork is created first (v after chol, quad_W after
-        # projG, bwd_R after bwd_w, bwd_t1 after the t-row backward); stream order and every event edge are
-        # unchanged, only the capture order of independent launches moves.  NMGP_CRIT_FIRST=0: the old order.
-        crit = os.environ.get("NMGP_CRIT_FIRST", "1") != "0"
         steps += [
             ("chol", "chol", chol_main, "main"),
             ("sig", "main", "chol"),
+            ("v", "row", row(getattr(lib, "nmgp_dsvi_hyper_" + self.sfx)), "main"),
+            ("sig", "main", "v"),
+            ("wait", "side2", "chol"),
         ]
-        if early:
-            steps.append(("wait", "main", "begun"))          # (v reads z_v)
-        if crit:
-            steps += [("v", "row", row(getattr(lib, "nmgp_dsvi_hyper_" + self.sfx)), "main"), ("sig", "main", "v")]
-        steps.append(("wait", "side2", "chol"))
         if self.p64:
             steps += [("inv3_64", "gemm", gemm("inv3_64"), "side2"),
                       ("proj3_64", "gemm", gemm("proj3_64"), "side2"),
                       ("conv3", "convert", round_back(0, 3), "side2")]
         if p["inv3"] is not None:
             steps.append(("inv3", "gemm", gemm("inv3"), "side2"))
-        steps.append(("proj3", "gemm", gemm("proj3"), "side2"))
-        if not crit:
-            steps += [("v", "row", row(getattr(lib, "nmgp_dsvi_hyper_" + self.sfx)), "main"), ("sig", "main", "v")]
         steps += [
+            ("proj3", "gemm", gemm("proj3"), "side2"),
             ("build_g22", "pairwise", (pw64 if self.p64 else pw)("build_g22"), "main"),
             ("wait", "side2", "v"),
             ("trow", "row", row(getattr(lib, "nmgp_dsvi_trow_" + self.sfx)), "side2"),
@@ -948,7 +860,8 @@ class DsviEngine:
         if self.p64:
             steps.append(("build_g12_64", "pairwise", pw64("build_g12_64"), "side2"))
         steps.append(("sig", "side2", "g12"))
-        if not elbo_mode and os.environ.get("NMGP_QUAD_SPLIT", "1") != "0":
+        if not elbo_mode:
+            # the pair factors W_P = P_{0,1} L_ij need only the L0 / L1 projections: beside the Gibbs chain
             steps += [("quad_P", "gemm", gemm("quad_P"), "side2"), ("sig", "side2", "quadP")]
         steps += [
             ("chol_G", "chol", chol_g, "main"),
@@ -961,9 +874,6 @@ class DsviEngine:
         else:
             steps.append(("invG", "gemm", gemm("invG"), "main"))
         steps.append(("projG", "gemm", gemm("projG"), "main"))
-        if os.environ.get("NMGP_SIDE2_FWD", "1") == "0":
-            steps = self._remap(steps, 0, len(steps), "side2", "main")
-        n_fwd = len(steps)
         if elbo_mode:
             steps.append(("quad", "gemm", gemm("quad"), "main"))
             if need_side:
@@ -985,16 +895,13 @@ class DsviEngine:
             return steps
         # KL branch on the side stream once all prior factors and Y = A^-1 mu exist (after projG):
         # KL terms, prior-diagonal adjoints, the variational factors' KL L-bar (first writer of those
-        # gradient rows -- bwd_lbar follows it on the same stream, so the accumulation order is fixed) and the KL part of
-        # the prior adjoints Abar (bwd_pr waits for it)
-        quad_split = os.environ.get("NMGP_QUAD_SPLIT", "1") != "0"
+        # gradient rows -- bwd_lbar follows it on the same stream, so the accumulation order is fixed) and the
+        # KL part of the prior adjoints Abar (the main stream waits for it before R_G is signalled)
         steps.append(("sig", "main", "kl_in"))
-        quad_first = crit and quad_split
-        if quad_first:
-            if pre_planned:
-                steps.append(("wait", "main", "plans"))
-            steps.append(("quad_W", "gemm", gemm("quad_W"), "main"))
+        if pre_planned:
+            steps.append(("wait", "main", "plans"))
         steps += [
+            ("quad_W", "gemm", gemm("quad_W"), "main"),
             ("wait", "side", "kl_in"),
             ("kl", "row", row(getattr(lib, "nmgp_dsvi_kl_" + self.sfx)), "side"),
             ("delta", "row", row(getattr(lib, "nmgp_dsvi_delta_" + self.sfx)), "side"),
@@ -1004,215 +911,79 @@ class DsviEngine:
                       ("kl_t64a", "gemm", gemm("kl_t64a"), "side")]
             if p["kl_t64b"] is not None:
                 steps.append(("kl_t64b", "gemm", gemm("kl_t64b"), "side"))
-        # round 3 (NMGP_LBAR_EARLY): the KL parts of A-bar (kl_abar, bwd_kly: they need delta and Y, not the KL
-        # L-bar) on the third side stream, so the side stream reaches bwd_lbar -- the step's longest
-        # backward GEMM, ahead of the v chain -- right after recon
-        lbar_early = os.environ.get("NMGP_LBAR_EARLY", "0") == "1" and os.environ.get("NMGP_SIDE3", "1") != "0" \
-            and os.environ.get("NMGP_BWD_SPLIT", "1") != "0"
-        if lbar_early:
-            steps += [
-                ("sig", "side", "delta_done"),
-                ("kl_lbar", "gemm", gemm("kl_lbar"), "side"),
-                ("sig", "side", "kl_lbar"),
-                ("wait", "side3", "delta_done"),
-                ("kl_abar", "gemm", gemm("kl_abar"), "side3"),
-                ("bwd_kly", "gemm", gemm("bwd_kly"), "side3"),
-                ("sig", "side3", "kl_done"),
-            ]
-        else:
-            steps += [
-                ("kl_lbar", "gemm", gemm("kl_lbar"), "side"),
-                ("sig", "side", "kl_lbar"),
-                ("kl_abar", "gemm", gemm("kl_abar"), "side"),
-                ("bwd_kly", "gemm", gemm("bwd_kly"), "side"),
-                ("sig", "side", "kl_done"),
-            ]
-        if pre_planned and not quad_first:
-            steps.append(("wait", "main", "plans"))
-        if quad_first:
-            steps.append(("wait", "main", "quadP"))
-        elif quad_split:
-            steps += [("quad_W", "gemm", gemm("quad_W"), "main"), ("wait", "main", "quadP")]
-        else:
-            steps.append(("quad", "gemm", gemm("quad"), "main"))
-        side3 = os.environ.get("NMGP_SIDE3", "1") != "0"
-        bwd_split = side3 and os.environ.get("NMGP_BWD_SPLIT", "1") != "0"
         steps += [
+            ("kl_lbar", "gemm", gemm("kl_lbar"), "side"),
+            ("sig", "side", "kl_lbar"),
+            ("kl_abar", "gemm", gemm("kl_abar"), "side"),
+            ("bwd_kly", "gemm", gemm("bwd_kly"), "side"),
+            ("sig", "side", "kl_done"),
+            ("wait", "main", "quadP"),
             ("recon", "row", row(getattr(lib, "nmgp_dsvi_recon_" + self.sfx)), "main"),
             ("sig", "main", "recon"),
-            ("bwd_wG", "gemm", gemm("bwd_wG"), "main") if bwd_split else ("bwd_w", "gemm", gemm("bwd_w"), "main"),
-        ]
-        if bwd_split:
-            steps.append(("bwd_R", "gemm", gemm("bwd_R"), "main"))
-        steps += [
+            ("bwd_wG", "gemm", gemm("bwd_wG"), "main"),
+            ("bwd_R", "gemm", gemm("bwd_R"), "main"),
             # L-bar / mu-bar gradient rows: after the KL L-bar (their first writer, same stream) and recon.
-            # (Deferring them until after bwd_w, to leave it the whole chip, measured 2% slower: the
-            # main chain after bwd_w is latency-bound either way.)
             ("wait", "side", "recon"),
             # the recon row partials and the KL slabs summed here, off the main chain (finalize adds them)
             ("prefinal", "row", row(getattr(lib, "nmgp_dsvi_prefinal_" + self.sfx)), "side"),
             ("bwd_lbar", "gemm", gemm("bwd_lbar"), "side"),
             ("sig", "side", "lbar_done"),
-            ("sig", "main", "bwd_w"),
         ]
-        # G prior: R_G -> the K_G12 builder backward (ell_X adjoints) stays on the main chain; the prior
-        # adjoint Abar_G -= P_G^T R_G and the K_G22 builder backward (ell_Z adjoints: the v chain only)
-        # run on the second side stream
-        # A/B on the box (tools/ab_env.sh NMGP_SIDE3, 3 x 300 steps each): 0.815-0.818 -> 0.798-0.802 ms
         BM = self.B * M
-
-        def lchain(where, kl_wait=None):
-            # (p64: P-bar_0/1, the KL parts of A-bar_0/1 and the row coefficients c0 / c1 widened first)
-            # kl_wait: the stream waits for the KL parts of A-bar_0/1 (event kl_done) only after R_0/1 = P-bar Ainv,
-            # which does not read them
-            wP = [("wPbL", "convert", widen(self.Pbar, self.PbL64, 2 * BM, BM), where),
-                  ("wrcL", "convert", widen(self.rowbuf, self.rcL64, 2 * self.B, (2 * D + 1) * self.B), where)] \
-                if self.p64 else []
-            wA = [("wAbL", "convert", widen(self.Abar, self.AbL64, 2 * MM, MM), where)] if self.p64 else []
-            kw = [("wait", where, kl_wait)] if kl_wait else []
-            return wP + [("bwd_R_L", "gemm", gemm("bwd_R_L"), where)] + kw + wA + \
-                [("bwd_pr_L", "gemm", gemm("bwd_pr_L"), where),
-                 ("bwd_build_L", "pairwise_bwd", (pw64 if self.p64 else pw)("bwd_build_L"), where),
-                 ("sig", where, "L_done")]
-        if bwd_split:
-            # the pair P-bar_0/1 products start on the third side stream right after recon (beside bwd_wG),
-            # then -- with the KL parts of A-bar_0/1 (kl_done, a one-way side -> side3 edge) -- the L0 / L1
-            # prior adjoints
-            steps += [("wait", "side3", "recon")]
-            if p["bwd_wP"] is not None:
-                steps.append(("bwd_wP", "gemm", gemm("bwd_wP"), "side3"))
-            # round 3 (NMGP_RL_EARLY=1): R_0/1 follow bwd_wP with no other dependency (waiting for kl_done before
-            # them gives the node two parents and the graph puts it on bwd_R's hardware queue, behind the main
-            # chain); it then overlaps bwd_R and the step measured 1389 -> 1373 it/s, so off by default
-            if lbar_early:
-                steps += lchain("side3")                     # (kl_done is this stream's own)
-            elif os.environ.get("NMGP_RL_EARLY", "0") == "1":
-                steps += lchain("side3", kl_wait="kl_done")
-            else:
-                steps += [("wait", "side3", "kl_done")]
-                steps += lchain("side3")
-        elif side3:
-            # the L0 / L1 prior adjoints (R_0, R_1 -> P^T R -> builder backward: hyper-parameter partials
-            # only) need P-bar_0/1 (bwd_w) and the KL parts of Abar (kl_done): a third side stream starts
-            # them right after bwd_w.  On side2 they queued behind the G-prior adjoint and, in the graph,
-            # shared a hardware queue with the t chain (finalize waited ~50 us for them, r02b timeline).
-            # Like side2 it synchronises with the main stream only.
-            steps += [("wait", "main", "kl_done"), ("sig", "main", "bwd_w_kl")]
-            if crit:
-                steps.append(("bwd_R", "gemm", gemm("bwd_R"), "main"))
-            steps.append(("wait", "side3", "bwd_w_kl"))
-            steps += lchain("side3")
-        if not (side3 and crit) and not bwd_split:
-            steps.append(("bwd_R", "gemm", gemm("bwd_R"), "main"))
+        # the pair P-bar_0/1 products start on the third side stream right after recon (beside bwd_wG), then --
+        # with the KL parts of A-bar_0/1 (kl_done, a one-way side -> side3 edge) -- the L0 / L1 prior adjoints
+        # R_0/1 -> P^T R -> builder backward (hyper-parameter partials only; p64: P-bar_0/1, the KL parts of
+        # A-bar_0/1 and the row coefficients c0 / c1 widened first)
+        steps.append(("wait", "side3", "recon"))
+        if p["bwd_wP"] is not None:
+            steps.append(("bwd_wP", "gemm", gemm("bwd_wP"), "side3"))
+        steps.append(("wait", "side3", "kl_done"))
+        if self.p64:
+            steps += [("wPbL", "convert", widen(self.Pbar, self.PbL64, 2 * BM, BM), "side3"),
+                      ("wrcL", "convert", widen(self.rowbuf, self.rcL64, 2 * self.B, (2 * D + 1) * self.B), "side3")]
+        steps.append(("bwd_R_L", "gemm", gemm("bwd_R_L"), "side3"))
+        if self.p64:
+            steps.append(("wAbL", "convert", widen(self.Abar, self.AbL64, 2 * MM, MM), "side3"))
         steps += [
-            # (the second side stream synchronises with the main stream only: a side <-> side2 event
-            # edge made hipGraph instantiation crash on this stack; the KL prior adjoints are long done
-            # when bwd_R finishes, so the main stream's wait on them costs nothing)
+            ("bwd_pr_L", "gemm", gemm("bwd_pr_L"), "side3"),
+            ("bwd_build_L", "pairwise_bwd", (pw64 if self.p64 else pw)("bwd_build_L"), "side3"),
+            ("sig", "side3", "L_done"),
+            # (the KL prior adjoints are long finished when bwd_R is done: the main stream's wait is free)
             ("wait", "main", "kl_done"),
             ("sig", "main", "R_G"),
-        ]
-        # round 3 (NMGP_PR_MAIN=1): the G-prior adjoint (bwd_pr -> K_G22 builder backward, the longer of the two
-        # chains after R_G, ahead of the v chain) stays on the main stream with no cross-queue hop; the K_G12
-        # builder backward and the t-row backward move to side2 (tb signalled there)
-        pr_main = os.environ.get("NMGP_PR_MAIN", "0") == "1"
-        if pr_main:
-            steps += [
-                ("bwd_pr", "gemm", gemm("bwd_pr"), "main"),
-                ("bwd_build22", "pairwise_bwd", pw("bwd_build22"), "main"),
-                ("sig", "main", "g22"),
-                ("wait", "side2", "R_G"),
-                ("bwd_build12", "pairwise_bwd", pw("bwd_build12"), "side2"),
-                ("tbwd", "row", row(getattr(lib, "nmgp_dsvi_tbwd_" + self.sfx)), "side2"),
-                ("sig", "side2", "tb"),
-            ]
-        else:
-            steps += [
-                ("bwd_build12", "pairwise_bwd", pw("bwd_build12"), "main"),
-                ("wait", "side2", "R_G"),
-                ("bwd_pr", "gemm", gemm("bwd_pr"), "side2"),
-                ("bwd_build22", "pairwise_bwd", pw("bwd_build22"), "side2"),
-                ("sig", "side2", "g22"),
-            ]
-        if not side3:
-            # the L0 / L1 prior adjoints feed only their hyper-parameter partials (scal_part slots and
-            # row-coefficient rows of their own): second side stream after the G prior adjoint (R_G was
-            # signalled after bwd_w and the KL parts of Abar), so the v chain on the side stream does not
-            # queue behind them
-            steps += lchain("side2")
-        steps += [] if pr_main else [
+            # G prior: R_G -> the K_G12 builder backward (ell_X adjoints) stays on the main chain; the prior
+            # adjoint Abar_G -= P_G^T R_G and the K_G22 builder backward (ell_Z adjoints: the v chain only) run
+            # on the second side stream
+            ("bwd_build12", "pairwise_bwd", pw("bwd_build12"), "main"),
+            ("wait", "side2", "R_G"),
+            ("bwd_pr", "gemm", gemm("bwd_pr"), "side2"),
+            ("bwd_build22", "pairwise_bwd", pw("bwd_build22"), "side2"),
+            ("sig", "side2", "g22"),
+            # after the t-row backward the t-prior chain (bwd_t1 -> bwd_t2 -> builder backward) and the v-factor
+            # Cholesky backward (P_t^T tbar -> vbwd -> bwd_v1 -> bwd_v2, reading vbar and the Gibbs partials)
+            # share no buffer: the v chain runs on the side stream (after bwd_lbar there, which keeps the order
+            # of the sqrt_v gradient accumulation fixed: kl_lbar, bwd_lbar, bwd_v2), waiting for the K_G22
+            # builder backward itself (a one-way side2 -> side edge), followed by the KL mean gradients
             ("tbwd", "row", row(getattr(lib, "nmgp_dsvi_tbwd_" + self.sfx)), "main"),
-            # after the t-row backward the t-prior chain (bwd_t1 -> bwd_t2 -> builder backward) and the
-            # v-factor Cholesky backward (P_t^T tbar -> vbwd -> bwd_v1 -> bwd_v2, reading vbar and the
-            # Gibbs partials) share no buffer: the v chain runs on the side stream (after bwd_lbar there,
-            # which keeps the order of the sqrt_v gradient accumulation fixed: kl_lbar, bwd_lbar,
-            # bwd_v2), followed by the KL mean gradients of the mu rows
-            # (starting P_t^T tbar before the K_G22 builder backward is done -- the g22 partials relayed to
-            # the v-backward kernel through the main stream -- measured slower in the graph: 0.84 ms and,
-            # with the third side stream, 0.94 ms per step; more cross-queue edges)
-        ]
-        # round 3 (NMGP_G22_SIDE, default on): the v chain waits for the K_G22 builder backward itself (a
-        # one-way side2 -> side edge; only the side <-> side2 ping-pong breaks torch's capture), so the main
-        # stream's t-prior chain no longer waits for the G-prior adjoint relayed through it
-        g22_side = os.environ.get("NMGP_G22_SIDE", "1") != "0"
-        if not g22_side and not pr_main:
-            steps.append(("wait", "main", "g22"))
-        if not pr_main:
-            steps.append(("sig", "main", "tb"))
-        if crit:
-            steps.append(("bwd_t1", "gemm", gemm("bwd_t1"), "main"))
-        steps.append(("wait", "side", "tb"))
-        if g22_side:
-            steps.append(("wait", "side", "g22"))
-        steps += [
+            ("sig", "main", "tb"),
+            ("bwd_t1", "gemm", gemm("bwd_t1"), "main"),
+            ("wait", "side", "tb"),
+            ("wait", "side", "g22"),
             ("bwd_vt", "gemm", gemm("bwd_vt"), "side"),
             ("vbwd", "row", row(getattr(lib, "nmgp_dsvi_vbwd_" + self.sfx)), "side"),
             ("bwd_v1", "gemm", gemm("bwd_v1"), "side"),
             ("bwd_v2", "gemm", gemm("bwd_v2"), "side"),
             ("mugrad", "row", row(getattr(lib, "nmgp_dsvi_mugrad_" + self.sfx)), "side"),
             ("sig", "side", "v_done"),
-        ]
-        if not crit:
-            steps.append(("bwd_t1", "gemm", gemm("bwd_t1"), "main"))
-        steps += [
             ("bwd_t2", "gemm", gemm("bwd_t2"), "main"),
             ("bwd_tbuild", "pairwise_bwd", (pw64 if self.p64 else pw)("bwd_tbuild"), "main"),
             ("wait", "main", "v_done"),
             ("wait", "main", "lbar_done"),
             ("wait", "main", "L_done"),
-        ]
-        if g22_side and not pr_main:
-            steps.append(("wait", "main", "g22"))          # (explicit join of side2; long done)
-        steps += [
+            ("wait", "main", "g22"),          # (explicit join of side2; long done)
             ("finalize", "row", row(getattr(lib, "nmgp_dsvi_finalize_" + self.sfx)), "main"),
         ]
-        if pr_main:
-            # the t-prior chain (bwd_t1 -> bwd_t2 -> builder backward) follows the t-row backward on side2
-            out = []
-            for it in steps:
-                if it[0] == "finalize":
-                    out.append(("wait", "main", "t_done"))
-                if len(it) == 4 and it[0] in ("bwd_t1", "bwd_t2", "bwd_tbuild"):
-                    it = (it[0], it[1], it[2], "side2")
-                out.append(it)
-                if it[0] == "bwd_tbuild":
-                    out.append(("sig", "side2", "t_done"))
-            steps = out
-        if os.environ.get("NMGP_SIDE2_BWD", "1") == "0":
-            steps = self._remap(steps, n_fwd, len(steps), "side2", "main")
         return steps
-
-    @staticmethod
-    def _remap(steps, lo, hi, frm, to):
-        """Run the items [lo, hi) of `frm` on stream `to` instead (A/B of stream placements)."""
-        out = []
-        for i, it in enumerate(steps):
-            if lo <= i < hi:
-                if it[0] in ("sig", "wait") and it[1] == frm:
-                    it = (it[0], to, it[2])
-                elif len(it) == 4 and it[3] == frm:
-                    it = (it[0], it[1], it[2], to)
-            out.append(it)
-        return out
 
     def _run(self, steps, stream, timer):
         """Enqueue `steps`.  timer=None: on the four streams.  A timer with concurrent=False: serially on
@@ -1227,8 +998,7 @@ class DsviEngine:
                 self._side = torch.cuda.Stream(device=self.dev)
                 self._side2 = torch.cuda.Stream(device=self.dev)
                 self._side3 = torch.cuda.Stream(device=self.dev)
-                self._pre = torch.cuda.Stream(device=self.dev)
-            streams = {"main": main, "side": self._side, "side2": self._side2, "side3": self._side3, "pre": self._pre}
+            streams = {"main": main, "side": self._side, "side2": self._side2, "side3": self._side3}
             handles = {k: ctypes.c_void_p(v.cuda_stream) for k, v in streams.items()}
         events = {}
         for item in steps:

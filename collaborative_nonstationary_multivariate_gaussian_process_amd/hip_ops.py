@@ -43,7 +43,6 @@ def gemm_desc(C, A, B, m, n, k, sA, sB, sC, *, flags=0, alpha=1.0, beta=0.0, kb=
     d.m, d.n, d.k = int(m), int(n), int(k)
     d.kbA, d.kbB = kb
     d.flags = flags | (L.KSCALE if kscale is not None else 0)
-    assert not (d.flags & L.KSCALE and d.flags & L.ASCALE), "KSCALE and ASCALE share the kscale table"
     d.row_seg, d.k_seg, d.seg_span = row_seg, k_seg, seg_span
     d.alpha, d.beta, d.diag_add = alpha, beta, diag_add
     if epi is not None:
@@ -63,9 +62,9 @@ def gemm_desc(C, A, B, m, n, k, sA, sB, sC, *, flags=0, alpha=1.0, beta=0.0, kb=
 
 
 GEMM_BK = 32   # k-tile of gemm_kernel (csrc/gemm.hip GBK)
-# tuning knob (tools/gemm_probe.py; tools/ab_env.sh on the PM2.5 bench, round 2: 2.0 -> 1283-1291 it/s,
-# 4.0 -> 1300-1302, 8.0 -> 1298-1329, no large-k split 1315-1322, 3 x 300 steps each; HCP unchanged)
-_KSPLIT_FACTOR = float(os.environ.get("NMGP_KSPLIT_FACTOR", "8.0"))
+# split a problem's k loop beyond this many times the balanced per-workgroup share (tools/gemm_probe.py; PM2.5
+# bench A/B in round 2: 2.0 -> 1283-1291 it/s, 4.0 -> 1300-1302, 8.0 -> 1298-1329, no large-k split 1315-1322)
+_KSPLIT_FACTOR = 8.0
 
 
 def _auto_ksplit(k_eff, group_tiles, work_per_wg):
@@ -91,15 +90,19 @@ def _cap_ksplit(ksplit, k_eff, kt_cap):
     return max(ksplit, min(16, -(-kt // kt_cap)))
 
 
+# row-segmented groups get the device tile plan only from this many static tiles on (round 2 A/B: 128 / 256 /
+# 512 / 1024 within noise on the PM2.5 bench)
+_DYN_MIN_TILES = 1024
+
 LAT_TILE = 32       # output tile of the latency kernel (csrc/gemm_lat.hip LTM / LTN)
 LAT_PANEL = 64      # panel alignment the latency kernel needs of k-blocked operands
 LAT_WAVES, LAT_KP = 8, 32   # waves per workgroup and k-panel width (gemm_lat.hip launch config 1)
-_LAT_MODE = os.environ.get("NMGP_GEMM_LAT", "auto")        # "0": never, "force": wherever eligible
+_LAT_MODE = "auto"        # "0": never (the tests compare the two kernels), "force": wherever eligible
 # a workgroup of the latency kernel loads each round of panels (LAT_WAVES x LAT_KP of k) in one go and
 # waits for it; groups that leave more rounds than this per workgroup after split-K (many output tiles
 # AND long k: the P-bar / L-bar products over several latent blocks or the minibatch) stay on the
 # LDS-pipelined tile kernel (per-group A/B on the box: tools/gemm_group_probe.py)
-_LAT_MAX_ROUNDS = int(os.environ.get("NMGP_GEMM_LAT_MAX_ROUNDS", "2"))
+_LAT_MAX_ROUNDS = 2
 
 
 def _lat_split(descs, seg, target_wgs):
@@ -119,16 +122,13 @@ def _lat_split(descs, seg, target_wgs):
     return ks, worst
 
 
-_LAT_COLPACK = os.environ.get("NMGP_LAT_COLPACK", "1") != "0"
-
-
 def _lat_colpack_groups(d):
-    """Column-tile groups of a B-triangular latency-kernel problem (csrc/gemm_lat.hip, NMGP_LAT_COLPACK): with
+    """Column-tile groups of a B-triangular latency-kernel problem (csrc/gemm_lat.hip, NMGP_LAT_COLPACK flag): with
     B_LOWER the column tile j of an n == k == 32 T problem has T - j k panels (B_UPPER: j + 1), so {0}, {g, T - g}
     and, for even T, {T / 2} each fill at most the 8 waves of a workgroup.  0 when the problem does not qualify."""
     f = d.flags
     bmask = f & (L.B_LOWER | L.B_UPPER)
-    if not _LAT_COLPACK or bmask not in (L.B_LOWER, L.B_UPPER):
+    if bmask not in (L.B_LOWER, L.B_UPPER):
         return 0
     if f & (L.A_LOWER | L.A_UPPER | L.OUT_LOWER | L.OUT_TRIL) or d.k_seg >= 0 or d.ksplit > 1:
         return 0
@@ -145,7 +145,7 @@ def _lat_eligible(d, esz):
     """Can gemm_lat.hip run this descriptor?  Non-negative strides, k-blocks that panels never
     straddle, and operand extents (incl. the rows / k a tile may touch past the problem) addressable
     by a 32-bit buffer offset."""
-    if d.batch > 1 or d.flags & L.ASCALE:      # (no A operand scale in the latency kernel)
+    if d.batch > 1:
         return False
     st = (d.sA_i, d.sA_k, d.sA_kb, d.sB_k, d.sB_j, d.sB_kb)
     if min(st) < 0:
@@ -176,7 +176,7 @@ class GemmGroup:
                  max_grid=0):
         """Split-K is chosen per problem so that the launch has ~target_wgs workgroups when the
         outputs alone are too few tiles (the M x B x M products P^T R with K = B).  kt_cap > 0 (tile
-        kernel): split every problem so that no workgroup runs more than ~kt_cap k-tiles -- for groups
+        kernel only; forces it): split every problem so that no workgroup runs more than ~kt_cap k-tiles -- for groups
         on the step's critical path, where the longest tile's k loop, not the chip's fill, sets the
         launch time.  max_grid > 0 (tile kernel): at most that many workgroups, striding over the tiles
         (longest k loops first) -- for off-critical-path groups whose long-lived workgroups would otherwise
@@ -185,6 +185,14 @@ class GemmGroup:
         self.seg = seg
         self.lat = False
         self._static_plan = False
+        # the group owns copies: split-K, tile counts, workspaces and flags are set per group, so a descriptor
+        # list shared by two groups (or reused by the caller) never carries one group's choices into another
+        descs = [L.GemmDesc.from_buffer_copy(d) for d in descs]
+        if kt_cap or max_grid:
+            # split caps and grid caps are tile-kernel features: never let "auto" drop them silently
+            if kernel == "lat":
+                raise ValueError("GemmGroup: kt_cap / max_grid apply to the tile kernel only")
+            kernel = "tile"
         esz = 8 if dtype == _F64 else 4
         if kernel != "tile" and _LAT_MODE != "0" and descs:
             ok = all(_lat_eligible(d, esz) for d in descs)
@@ -254,7 +262,7 @@ class GemmGroup:
         elif seg is not None and dyn_plan and any(d.row_seg >= 0 for d in descs):
             ksp = {id(d): max(d.ksplit, 1) for d in descs}
             expect = sum(eff[order[i]][0] * ksp[id(d)] for i, d in enumerate(descs))
-            if dyn_plan == "force" or (t >= int(os.environ.get("NMGP_DYN_MIN_TILES", 1024)) and expect < 0.5 * t):
+            if dyn_plan == "force" or (t >= _DYN_MIN_TILES and expect < 0.5 * t):
                 self.plan = torch.zeros(len(descs) + 1, dtype=torch.int32, device=device)
                 self.grid = int(min(t, max(256, min(4096, round(1.15 * expect)))))
 
@@ -274,6 +282,7 @@ class GemmGroup:
             d.tiles_m = -(-d.m // LAT_TILE) if d.m > 0 else 0
             d.tiles_n = -(-d.n // LAT_TILE) if d.n > 0 else 0
             d.ksplit = ksplits[i]
+            d.flags &= ~L.LAT_COLPACK                # (set below only when this group packs the problem)
             groups = _lat_colpack_groups(d)
             if groups:
                 d.flags |= L.LAT_COLPACK          # tiles_n = column-tile groups (5 instead of 8 at M = 256)
@@ -295,7 +304,7 @@ class GemmGroup:
         self.dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
         self.plan, self.grid = None, 0
         if self.seg is not None and dyn_plan and any(d.row_seg >= 0 for d in descs):
-            if dyn_plan == "force" or (t >= int(os.environ.get("NMGP_DYN_MIN_TILES", 1024)) and expect < 0.5 * t):
+            if dyn_plan == "force" or (t >= _DYN_MIN_TILES and expect < 0.5 * t):
                 self.plan = torch.zeros(len(descs) + 1, dtype=torch.int32, device=device)
                 self.grid = int(min(-(-t // 8) * 8, max(256, min(8192, 8 * round(1.15 * expect / 8)))))
 

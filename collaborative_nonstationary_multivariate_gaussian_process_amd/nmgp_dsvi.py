@@ -602,6 +602,22 @@ class DsviTrainer:
         self.graphs[id(eng)] = g
         return g
 
+    def capture_update(self, world=1):
+        """The Adam update alone as a HIP graph: the data-parallel step replays the gradient graph, runs ONE
+        sum all-reduce of the flat gradient, then replays this -- the 1/world scaling of the summed gradient
+        and Adam (code/nmgp_dsvi.py:847-854's backward -> optimizer.step with the collective between them) --
+        so no optimizer launch is issued eagerly."""
+        key = ("update", int(world))
+        g = self.graphs.get(key)
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                if world > 1:
+                    self.model._grad.div_(world)
+                self.update()
+            self.graphs[key] = g
+        return g
+
 
 class _IndexData(Dataset):
     """Row indices 0..n-1.  A DataLoader over it with the same length, batch size, shuffle flag and
@@ -820,7 +836,10 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
                     trainer.update()
                 else:
                     eng = pipe.step(sl)
-                    if world > 1:
+                    if world > 1 and use_graph:
+                        DD.allreduce_sum_(model._grad, group)
+                        trainer.capture_update(world).replay()     # 1/world + Adam as one graph
+                    elif world > 1:
                         DD.allreduce_mean_(model._grad, group)
                         trainer.update()
                 losses_dev.append(eng.out[0].clone())

@@ -69,10 +69,6 @@ enum {
                           * 32 T, T <= 8, no other mask: tiles_n counts column-tile GROUPS -- {0}, {g, T-g}
                           * for g = 1..(T-1)/2 and {T/2} for even T (B_UPPER mirrored) -- whose k panels add up
                           * to <= 8, one group per workgroup                                                  */
-  NMGP_ASCALE = 4096     /* 64x64 kernel only, exclusive with NMGP_KSCALE: multiply op(A)(i,k) by
-                          * kscale[(k / kbA) * sAS_kb + row(i)] (row(i) = the absolute row: row_seg start + i),
-                          * a per-(row, k-block) scale applied when A is staged.  The DSVI backward reads the
-                          * W-hat = diag(2 adjoint) W rows this way (round 3) instead of a scaled copy of W. */
 };
 
 typedef struct nmgp_gemm_desc {
@@ -96,8 +92,7 @@ typedef struct nmgp_gemm_desc {
   /* batch (single-problem launches only): problem b uses A + b*sA_b, B + b*sB_b, C + b*sC_b;
    * batch <= 1 means one problem.  Split-K and batch are exclusive.                           */
   int64_t sA_b, sB_b, sC_b;
-  int32_t batch;
-  int32_t sAS_kb;        /* NMGP_ASCALE: stride of the scale table per k-block of A (elements)     */
+  int32_t batch, pad3_;
 } nmgp_gemm_desc;
 
 /* d_desc: device array of nprob descriptors (tiles_m/tiles_n/tile_start filled by the host,
@@ -376,11 +371,6 @@ typedef struct nmgp_dsvi_args {
   const void* K12_64;
   void* t64;
   void* scal64;
-  /* W-hat scales (round 3; NULL = scale W / W_P in place): (2 D, B) -- rows 0..D-1 the latent scales
-     2 g-bar_s of each row (0 for s > the row's output), rows D..2D-1 the pair scales 2 s2p-bar_s.
-     recon writes them instead of W-hat = diag(scale) W, and the backward GEMMs apply them to their
-     W operand (NMGP_ASCALE for P-bar, NMGP_KSCALE for L-bar)                                         */
-  void* wscale;
 } nmgp_dsvi_args;
 
 int nmgp_dsvi_hyper_f64(const nmgp_dsvi_args* a, hipStream_t s);      /* hyper values + v sample   */

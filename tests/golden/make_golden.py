@@ -653,3 +653,4 @@ if __name__ == "__main__":
     case_modelpt_file()
     case_hcp_like()
     case_driver_hyper()
+    case_ecog_like()

@@ -230,64 +230,6 @@ def test_fp32_big_side_products_match_grouped(monkeypatch):
     assert _rel(res[0][1], res[1][1]) < 1e-3
 
 
-@pytest.mark.parametrize("M,dtype", [(64, torch.float64), (24, torch.float64), (128, torch.float32)])
-def test_what_fold_bit_identical(monkeypatch, M, dtype):
-    """NMGP_WHAT_FOLD=1 (recon writes the W-hat scales, the P-bar GEMMs scale their A operand per
-    (row, k-block) -- NMGP_ASCALE -- and the L-bar GEMMs their B operand per k -- NMGP_KSCALE) gives
-    the same loss and gradients bit for bit as W-hat = diag(2 adjoint) W formed in place by recon:
-    the product fl(w * f) is the same number either way.  M=64: the fast main loop (k-blocks aligned
-    to the k-tile); M=24: the general loop.  (The latency kernel, which small P-bar groups would
-    otherwise take without the fold, is switched off for both runs: it sums in another order.)"""
-    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP
-    from collaborative_nonstationary_multivariate_gaussian_process_amd import hip_ops
-    monkeypatch.setattr(hip_ops, "_LAT_MODE", "0")
-    rng = np.random.default_rng(5)
-    D, n = 3, 90
-    X = [np.sort(rng.uniform(0, 1, n)).reshape(-1, 1) for _ in range(D)]
-    Y = [np.sin(5 * x + d) + 0.2 * rng.standard_normal(x.shape) for d, x in enumerate(X)]
-    res = []
-    for fold in ("1", "0"):
-        monkeypatch.setenv("NMGP_WHAT_FOLD", fold)
-        model = NMGP(number_observations=D * n, dim_outputs=D, Z=np.linspace(0, 1, M), seed=4,
-                     device="cuda:0", noise="device", dtype=dtype)
-        loss = model(X, Y)
-        assert all(e.what_fold == (fold == "1") for e in model._engines.values())
-        loss.backward()
-        torch.cuda.synchronize()
-        res.append((float(loss), torch.cat([p.grad.reshape(-1).double() for p in model.parameters()]).cpu()))
-    assert np.isfinite(res[0][0]) and res[0][0] == res[1][0]
-    assert torch.equal(res[0][1], res[1][1])
-
-
-@pytest.mark.parametrize("env", [{"NMGP_RL_EARLY": "1"}, {"NMGP_LBAR_EARLY": "1"}, {"NMGP_PR_MAIN": "1"},
-                                 {"NMGP_HEAD": "1"}, {"NMGP_HEAD": "2"}, {"NMGP_V_SIDE": "0"},
-                                 {"NMGP_LBAR_GRID": "16", "NMGP_WP_GRID": "16"}])
-def test_schedule_variants_bit_identical(monkeypatch, env):
-    """The round-3 schedule knobs (stream placement, capture order, workgroup caps of the side-stream
-    groups) move launches between streams but keep every accumulation into a shared row in one fixed
-    order: loss and gradient equal the default schedule's bit for bit (D=3, M=64, fp64)."""
-    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP
-    rng = np.random.default_rng(8)
-    D, n, M = 3, 120, 64
-    X = [np.sort(rng.uniform(0, 1, n)).reshape(-1, 1) for _ in range(D)]
-    Y = [np.cos(4 * x + d) + 0.2 * rng.standard_normal(x.shape) for d, x in enumerate(X)]
-    res = []
-    for on in (True, False):
-        for k, v in env.items():
-            if on:
-                monkeypatch.setenv(k, v)
-            else:
-                monkeypatch.delenv(k, raising=False)
-        model = NMGP(number_observations=D * n, dim_outputs=D, Z=np.linspace(0, 1, M), seed=6,
-                     device="cuda:0", noise="device", dtype=torch.float64)
-        loss = model(X, Y)
-        loss.backward()
-        torch.cuda.synchronize()
-        res.append((float(loss), torch.cat([p.grad.reshape(-1) for p in model.parameters()]).cpu()))
-    assert np.isfinite(res[0][0]) and res[0][0] == res[1][0]
-    assert torch.equal(res[0][1], res[1][1])
-
-
 def test_step_begin_matches_separate_launches():
     """nmgp_step_begin (one launch) == batch gather + Philox noise + noise-counter advance + grad
     zeroing as separate launches: bit-identical minibatch, segment table, noise, counters."""

@@ -103,35 +103,33 @@ def test_gemm_kblocks_and_segments_grouped(ops):
 
 
 @pytest.mark.parametrize("dt", [F64, torch.float32])
-def test_gemm_group_kt_cap_max_grid_ascale(ops, dt):
-    """GemmGroup(kt_cap=) (split-K so no workgroup runs more than kt_cap k-tiles), GemmGroup(max_grid=)
+def test_gemm_group_kt_cap_max_grid(ops, dt):
+    """GemmGroup(kt_cap=) (split-K so no workgroup runs more than kt_cap k-tiles) and GemmGroup(max_grid=)
     (fewer workgroups striding over the tiles: device plan for row-segmented groups, a static plan
-    otherwise) and NMGP_ASCALE (A scaled per (row, k-block) when staged) against torch references on
-    k-blocked, row-segmented and k-segmented problems."""
+    otherwise) against torch references on k-blocked, row-segmented and k-segmented problems; the
+    caller's descriptors are left untouched (the group works on copies)."""
     from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L
     g = torch.Generator().manual_seed(21)
     D, B, M = 4, 700, 128
     W = torch.randn(D, B, M, generator=g, dtype=F64)
     S = torch.randn(D, M, M, generator=g, dtype=F64)
-    F = torch.randn(D, B, generator=g, dtype=F64)                    # per-(block, row) A scales
     seg = torch.tensor([0, 100, 330, 520, 700], dtype=torch.int32)
-    Wd, Sd, Fd, segd = W.to(dt).to(DEV), S.to(dt).to(DEV), F.to(dt).to(DEV), seg.to(DEV)
-    Wc, Sc, Fc = Wd.double().cpu(), Sd.double().cpu(), Fd.double().cpu()
+    Wd, Sd, segd = W.to(dt).to(DEV), S.to(dt).to(DEV), seg.to(DEV)
+    Wc, Sc = Wd.double().cpu(), Sd.double().cpu()
     tol = 1e-13 if dt == F64 else 3e-6
     for kw in (dict(), dict(kt_cap=2), dict(max_grid=7), dict(kt_cap=3, max_grid=5)):
         out1 = torch.zeros(B, M, dtype=dt, device=DEV)
         out2 = torch.zeros(D, M, M, dtype=dt, device=DEV)
         descs = []
-        for i in range(D):   # rows of segment i: sum_{d <= i} diag(F[d]) W[d] tril(S[d])^T
-            d = ops.gemm_desc(out1, Wd, Sd, B, M, (i + 1) * M, (M, 1, B * M), (1, M, M * M), (M, 1),
-                              flags=L.B_UPPER, kb=(M, M), row_seg=i)
-            d.kscale, d.sAS_kb = ops._addr(Fd), B
-            d.flags |= L.ASCALE
-            descs.append(d)
+        for i in range(D):   # rows of segment i: sum_{d <= i} W[d] tril(S[d])^T
+            descs.append(ops.gemm_desc(out1, Wd, Sd, B, M, (i + 1) * M, (M, 1, B * M), (1, M, M * M), (M, 1),
+                                       flags=L.B_UPPER, kb=(M, M), row_seg=i))
         # out2[d] = W[d][rows of segments d..]^T W[d][same rows]   (long k: split by kt_cap)
         descs += [ops.gemm_desc(out2, Wd, Wd, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), k_seg=d, seg_span=D - d,
                                 offs=(d * B * M, d * B * M, d * M * M), flags=L.OUT_TRIL) for d in range(D)]
-        grp = ops.GemmGroup(descs, DEV, dt, seg=segd, kernel="tile", **kw)
+        grp = ops.GemmGroup(descs, DEV, dt, seg=segd, **kw)     # (kt_cap / max_grid force the tile kernel)
+        assert not grp.lat or not kw
+        assert all(d.ksplit == 0 and d.tile_start == 0 for d in descs)
         if "kt_cap" in kw:
             assert max(x.ksplit for x in grp.descs) > 1
         if "max_grid" in kw:
@@ -141,7 +139,7 @@ def test_gemm_group_kt_cap_max_grid_ascale(ops, dt):
         ref1 = torch.zeros(B, M, dtype=F64)
         for i in range(D):
             r0, r1 = sc[i], sc[i + 1]
-            ref1[r0:r1] = sum((Fc[d][r0:r1, None] * Wc[d][r0:r1]) @ torch.tril(Sc[d]).t() for d in range(i + 1))
+            ref1[r0:r1] = sum(Wc[d][r0:r1] @ torch.tril(Sc[d]).t() for d in range(i + 1))
         assert rel(out1, ref1) < tol, kw
         for d in range(D):
             r0 = sc[d]
@@ -338,35 +336,6 @@ def test_chol_inv_fused(ops, n, batch):
     assert rel(X, torch.linalg.inv(ref)) < 1e-11
     assert float(torch.triu(Ad.cpu(), 1).abs().max()) == 0.0
     assert float(torch.triu(X.cpu(), 1).abs().max()) == 0.0
-
-
-@pytest.mark.parametrize("n,batch", [(128, 1), (176, 3), (192, 2), (250, 1), (256, 1), (256, 4), (256, 25)])
-@pytest.mark.parametrize("dt", [F64, torch.float32])
-def test_chol_inv_lookahead_matches_three_role(ops, n, batch, dt, monkeypatch):
-    """The lookahead factor role (chol_inv4_kernel: panel wave concurrent with the MFMA update waves) does
-    the three-role kernel's arithmetic in the same order: L and L^-1 are bit-identical, and both match
-    LAPACK; a non-PD matrix in the batch reports the same info."""
-    A = _spd(n, batch, 11 * n + batch).to(dt)
-    if batch > 2:
-        A[1, n // 2, n // 2] = -5.0                    # not PD from column n // 2 on
-    res = []
-    monkeypatch.setenv("NMGP_CHOL_4ROLE", "0")         # (the four-role kernel would run in both)
-    for la in ("1", "0"):
-        monkeypatch.setenv("NMGP_CHOL_LA", la)
-        Ad = A.clone().to(DEV)
-        X, info = ops.chol_inv_(Ad)
-        torch.cuda.synchronize()
-        res.append((Ad.cpu(), X.cpu(), info.cpu()))
-    (L1, X1, i1), (L0, X0, i0) = res
-    assert torch.equal(i1, i0)
-    if batch > 2:
-        assert int(i1[1]) == n // 2 + 1 and int(i1[0]) == 0
-    ok = [b for b in range(batch) if int(i1[b]) == 0]
-    assert torch.equal(L1[ok], L0[ok]) and torch.equal(X1[ok], X0[ok])
-    ref = torch.linalg.cholesky(A[ok].double())
-    tl, tx = (1e-13, 1e-11) if dt == F64 else (1e-5, 1e-4)
-    assert rel(L1[ok], ref) < tl and rel(X1[ok], torch.linalg.inv(ref)) < tx
-    assert float(torch.triu(L1[ok], 1).abs().max()) == 0.0 and float(torch.triu(X1[ok], 1).abs().max()) == 0.0
 
 
 @pytest.mark.parametrize("n,batch", [(128, 1), (176, 3), (192, 2), (250, 1), (256, 1), (256, 4), (256, 25)])

@@ -225,25 +225,6 @@ def test_device_pipeline_graph_equals_eager(bs):
     assert all(np.diff(res[1][2]) >= 0) and len(res[1][2]) == 3 * nb
 
 
-def test_early_begin_schedule_bit_identical(monkeypatch):
-    """NMGP_EARLY_BEGIN=1 (round 3, opt-in: the step-begin launch -- gather, Philox noise, gradient zeroing --
-    on its own stream beside the theta-only head of the forward chain, which waits for it only where it reads
-    the minibatch, the noise or the gradient): graph-replayed training gives the default's losses and
-    parameters bit for bit, with the ragged last minibatch included."""
-    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import inference
-    X, Y = _hcp_like()
-    hyper = {"length_scales_L0_log": -2.0, "length_scales_L1_log": -2.0, "length_scales_tildeell_log": -2.0}
-    res = []
-    for early in ("1", "0"):
-        monkeypatch.setenv("NMGP_EARLY_BEGIN", early)
-        torch.manual_seed(0)
-        m, losses, _ = inference(X, Y, np.linspace(0, 1, 32), 350, 4, hyperpars=hyper, lr=0.01, itnum=3,
-                                 show_ELBO=False, device="cuda:0", noise="device", use_graph=True)
-        res.append((m._theta.detach().cpu().clone(), np.array([float(v) for v in losses])))
-    assert np.array_equal(res[0][1], res[1][1]) and np.all(np.isfinite(res[0][1]))
-    assert torch.equal(res[0][0], res[1][0])
-
-
 def test_device_pipeline_batches_are_the_reference_minibatches():
     """The first step of the device pipeline sees the reference DataLoader's first minibatch, grouped
     by output as vec2list makes it (seeded global generator)."""

@@ -172,3 +172,17 @@ def test_split_k_rules():
     assert H._cap_ksplit(1, 10 ** 6, 2) == 16                # at most 16 chunks
     assert H._cap_ksplit(5, 10 ** 6, 0) == 5                 # 0: no cap
     assert H._auto_ksplit(2000, 16, 100) > 1                 # tiny groups split long k loops
+
+
+def test_bench_refuses_gpus_world_mismatch():
+    """bench.py --gpus N under a launcher whose WORLD_SIZE differs exits non-zero before touching the GPU
+    (it never reports n_gpus != N); without a launcher N > 1 re-runs under torchrun (checked on the box)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2
+    assert "refusing" in r.stderr
