@@ -129,6 +129,47 @@ def stress_cholesky(dev, reps=5):
             "speedup_vs_cpu": round(t_cpu * 1e3 / t_fac, 1)}
 
 
+def kron_mv_leg(dev, P=5, N=8192, reps=20):
+    """The Kronecker mat-vec of the legacy Kronecker likelihood (SIM_code/Utility/kronecker_operation.py:72-85,
+    distributions.py:26-52): (B kron K) y with B (P x P), K (N x N), fp64, on the fused one-pass kernel
+    (csrc/kron.hip kron_mv_kernel).  HBM-bound: algorithmic bytes per call = 8 (N^2 + P N + P^2 + P N) --
+    K read once, y read, out written.  Timed with HIP events around a graph of `reps` launches on the
+    stream they run on."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import hip_ops as H
+    g = torch.Generator(device=dev).manual_seed(3)
+    Bm = torch.randn(P, P, generator=g, dtype=torch.float64, device=dev)
+    K = torch.randn(N, N, generator=g, dtype=torch.float64, device=dev)
+    y = torch.randn(P * N, generator=g, dtype=torch.float64, device=dev)
+    out = torch.empty(P * N, dtype=torch.float64, device=dev)
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        H.kron_mv(Bm, K, y, out=out)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    gr = H.HipGraph(dev)
+    with gr.capture():
+        for _ in range(reps):
+            H.kron_mv(Bm, K, y, out=out)
+    with torch.cuda.stream(s):
+        gr.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        gr.replay()
+        e1.record(s)
+    torch.cuda.synchronize(dev)
+    us = 1000.0 * e0.elapsed_time(e1) / reps
+    ref = torch.kron(Bm[:2, :2].cpu(), K[:64, :64].cpu()) @ torch.cat([y[:64], y[N:N + 64]]).cpu()
+    chk = H.kron_mv(Bm[:2, :2].contiguous(), K[:64, :64].contiguous(), torch.cat([y[:64], y[N:N + 64]])).cpu()
+    nbytes = 8.0 * (N * N + P * N + P * P + P * N)
+    gbs = nbytes / (us * 1e-6) / 1e9
+    del K
+    return {"workload": f"kron_mv: (B kron K) y, B {P}x{P}, K {N}x{N}, fp64 (legacy Kronecker likelihood)",
+            "kernel": "kron_mv_kernel<double, 2> (one pass over K, 16-byte rows, DPP wave reductions)",
+            "us_per_call": round(us, 2), "algorithmic_bytes": int(nbytes), "achieved_GBs": round(gbs, 1),
+            "peak_GBs": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4), "bound": "hbm",
+            "check_rel_err": float((chk - ref).norm() / ref.norm())}
+
+
 def _stress_syrk_pmc():
     """MFMA-busy of the trailing-update SYRK launches INSIDE the M=4096 factorization (k = 128), time-weighted,
     from the committed rocprofv3 PMC pass (tools/syrk_inside_pmc.sh: SQ_VALU_MFMA_BUSY_CYCLES /
@@ -533,6 +574,7 @@ def main():
     ap.add_argument("--no-hcp", action="store_true", help="skip the HCP-shaped training leg (configs[2])")
     ap.add_argument("--no-ecog", action="store_true", help="skip the ECoG-shaped training leg (configs[3])")
     ap.add_argument("--no-pair", action="store_true", help="skip the pair-sharded ECoG training leg (N > 1 only)")
+    ap.add_argument("--no-kron", action="store_true", help="skip the Kronecker mat-vec leg")
     ap.add_argument("--pair-D", type=int, default=128, help="channels of the pair-sharded leg (default: ECoG-full 128)")
     ap.add_argument("--elbo-D", type=int, default=128, help="channels of the ELBO leg (default: ECoG-full 128)")
     args = ap.parse_args()
@@ -811,6 +853,13 @@ def main():
     if rank == 0 and world == 1 and not args.no_stress:
         stress = stress_cholesky(dev)
 
+    kron = None
+    if rank == 0 and world == 1 and not args.no_kron:
+        try:
+            kron = kron_mv_leg(dev)
+        except Exception as exc:
+            kron = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+
     if rank == 0:
         rec = {"metric": "DSVI ELBO iterations/sec (PM2.5-shaped, fp64, 1 iteration = fwd+bwd+Adam on B=2000)",
                "value": round(value, 3), "unit": "it/s", "n_gpus": world, "steps": args.steps,
@@ -821,6 +870,7 @@ def main():
                           "global_batch": B * world, "parallelism": f"dp{world}" if world > 1 else "single",
                           "hip_graph": used_graph},
                "roofline": roofline, "cpu_baseline": cpu, "cholesky": chol, "cholesky_stress": stress,
+               "kron_mv": kron,
                "elbo_sample_sharded": elbo,
                "hcp_train": hcp, "ecog_train": ecog,
                "pair_sharded_train": pair,

@@ -78,6 +78,10 @@ HYP_LOG = 1
 
 _SIGS = {
     "nmgp_version": (c_int, []),
+    "nmgp_graph_begin": (c_int, [c_vp]),
+    "nmgp_graph_end": (c_int, [c_vp, ctypes.POINTER(c_vp)]),
+    "nmgp_graph_launch": (c_int, [c_vp, c_vp]),
+    "nmgp_graph_destroy": (c_int, [c_vp]),
     "nmgp_device_status": (c_int, [ctypes.POINTER(ctypes.c_uint32), c_int]),
     "nmgp_sizeof_gemm_desc": (c_i64, []),
     "nmgp_sizeof_pairwise_desc": (c_i64, []),

@@ -1652,7 +1652,6 @@ size_t gemm_big_ws_bytes();
 int potrf_step_f32(float* P, float* C, const float* X, int64_t lda, int n2, int nb, int c1, int32_t* flag,
                    hipStream_t s);
 int potrf_strip_f32(const float* L, float* C, int64_t lda, int m, int c1, hipStream_t s);
-bool potrf_step32_active();
 
 // f32 recursion (same algebra as chol_inv_rec below) with the products on the 128x128 MFMA kernel
 // of gemm_big.hip, split-K into `ws` where the tile grid would not fill the chip.
@@ -1755,22 +1754,32 @@ static int chol_inv_launch(T* A, int64_t n, int64_t lda, int64_t sA, T* X, int64
 
 // ---------------------------------------------------------------------------------------------
 // Large single-matrix Cholesky (the M=4096 stress configuration; LAPACK potrf semantics, upper
-// triangle zeroed): right-looking, 128-wide block columns, one step of lookahead on two streams.
-// Step j (rows/columns below block j: n2):
-//   main:  [L_jj, X_jj] = fused leaf(A_jj)                      (register-resident, one workgroup)
-//          L_j = A_j X_jj^T                                      (panel GEMM)
-//          A(:, j+1) -= L_j L_j(0:128)^T                         (lookahead: next block column)
-//          (f32: both in one launch, potrf_step_kernel; f64: two GEMMs, A_j staged in P)
-//   side:  A(j+2:, j+2:) -= L_j(128:) L_j(128:)^T                (trailing SYRK, lower tiles only)
-// The trailing SYRK of step j runs while the main stream factors block j+1 (leaf + panel); the
-// lookahead update of step j+1 (which writes block column j+2) waits for it.  Everything else is
-// stream-ordered.  f32 products run on the 128x128 MFMA kernel (stream-K where the tile grid
-// would not fill the chip; one split-K workspace per stream), f64 on the 64x64 f64 MFMA kernel.
+// triangle zeroed).  128-wide block columns; the diagonal blocks are the fused register-resident
+// factor + inverse kernel ("leaf"), the panel below a block is L_j = A_j X_jj^T.
+//
+// f32 (the stress configuration, round 4): two levels.  Outer panels of PPW = 512 columns are factored
+// right-looking at 128-column granularity with every update kept INSIDE the panel; the panel's 512
+// columns then update the rest of the matrix in k = 512 products on the 128x128 MFMA kernel (a k = 128
+// trailing SYRK per block step ran at 12-28% MFMA-busy; at k = 512 the kernel's k loop amortises its
+// tile loads).  Per outer panel p (columns [c0, pe), pe = c0 + 512):
+//   main:   for each block j of the panel: leaf(j) -> step(j) = panel rows of block j + lookahead of
+//           block column j+1 when it lies inside the panel (potrf_step32_kernel, one launch)
+//   side:   after step(j): the near strips -- the panel's block columns j+2 .. (k = 128, potrf_strip32),
+//           issued after leaf(j+1) so that the leaf -> step hand-off keeps one hardware queue in a graph
+//   after the panel's last step:
+//   main:   NP_first = A[pe:, pe:pe+128] -= L_p[pe:] L_p[pe:pe+128]^T   (k = 512; the next leaf needs it)
+//   side:   NP_rest  = the other three block columns of panel p+1       (k = 512; beside that leaf)
+//   side2:  far SYRK = A[pe+512:, pe+512:] -= L_p L_p^T, lower tiles     (k = 512; a whole panel of slack)
+// Ordering: the step kernel that writes a column waits for the side stream's last writer of it (strip
+// or NP_rest); NP(p) waits for the far SYRK of panel p-1 (which wrote panel p+1's columns).
+// f64: one level (round 1): panel and lookahead as two GEMMs on the 64x64 f64 kernel, panel staged
+// through P, the trailing SYRK of step j on the side stream while block j+1 is factored.
 constexpr int PNB = 128;
+constexpr int PPW = 512;
 
 struct PotrfSide {
-  hipStream_t side = nullptr;
-  hipEvent_t ev_main = nullptr, ev_side = nullptr, ev_tail = nullptr;
+  hipStream_t side = nullptr, side2 = nullptr;
+  hipEvent_t ev_main = nullptr, ev_side = nullptr, ev_tail = nullptr, ev_np = nullptr, ev_far = nullptr;
 };
 
 static int potrf_side_ctx(PotrfSide*& out) {
@@ -1782,9 +1791,9 @@ static int potrf_side_ctx(PotrfSide*& out) {
   PotrfSide& c = ctx[dev];
   if (c.side == nullptr) {
     if (hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking) != hipSuccess) return NMGP_ERR_LAUNCH;
-    if (hipEventCreateWithFlags(&c.ev_main, hipEventDisableTiming) != hipSuccess) return NMGP_ERR_LAUNCH;
-    if (hipEventCreateWithFlags(&c.ev_side, hipEventDisableTiming) != hipSuccess) return NMGP_ERR_LAUNCH;
-    if (hipEventCreateWithFlags(&c.ev_tail, hipEventDisableTiming) != hipSuccess) return NMGP_ERR_LAUNCH;
+    if (hipStreamCreateWithFlags(&c.side2, hipStreamNonBlocking) != hipSuccess) return NMGP_ERR_LAUNCH;
+    for (hipEvent_t* e : {&c.ev_main, &c.ev_side, &c.ev_tail, &c.ev_np, &c.ev_far})
+      if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return NMGP_ERR_LAUNCH;
   }
   out = &c;
   return NMGP_OK;
@@ -1796,7 +1805,7 @@ template <typename T>
 static size_t potrf_blocked_ws(int64_t n) {
   const int64_t nblk = (n + PNB - 1) / PNB;
   size_t b = al256((size_t)nblk * PNB * PNB * sizeof(T)) + al256((size_t)n * PNB * sizeof(T));
-  if (std::is_same<T, float>::value) b += 2 * al256(gemm_big_ws_bytes()) + 256;   // + step-kernel flag
+  if (std::is_same<T, float>::value) b += 3 * al256(gemm_big_ws_bytes()) + 256;   // + step-kernel flag
   return b;
 }
 
@@ -1819,124 +1828,142 @@ __global__ __launch_bounds__(256) void zero_upper_kernel(T* A, int n, int64_t ld
   for (int j = i + 1 + (int)threadIdx.x; j < n; j += 256) A[(int64_t)i * lda + j] = (T)0;
 }
 
-static bool leaf_roles() {
-  static int v = -1;
-  if (v < 0) v = getenv("NMGP_POTRF_LEAF_ROLES") && atoi(getenv("NMGP_POTRF_LEAF_ROLES")) == 0 ? 0 : 1;
-  return v == 1;
-}
+// f32 leaves reserve enough LDS that no trailing-update workgroup (2 x 36 KB stages) shares their CUs: the
+// side streams' products run beside the leaf on the other CUs (round 2 A/B: 1.64 -> 1.51 ms)
+constexpr size_t kLeafLds = 88 * 1024;
 
-static bool potrf_strip() {
-  static int v = -1;
-  if (v < 0) v = getenv("NMGP_POTRF_STRIP") && atoi(getenv("NMGP_POTRF_STRIP")) == 0 ? 0 : 1;
-  return v == 1;
-}
+#define NMGP_HIP_TRY(x) \
+  do {                  \
+    if ((x) != hipSuccess) return NMGP_ERR_LAUNCH; \
+  } while (0)
+#define NMGP_TRY(x)                    \
+  do {                                 \
+    const int rc_ = (x);               \
+    if (rc_ != NMGP_OK) return rc_;    \
+  } while (0)
 
-// f32 leaves reserve enough LDS that no trailing-SYRK workgroup (2 x 36 KB stages) shares their CUs: the
-// rest of the previous step's SYRK runs beside the leaf (NMGP_POTRF_LEAF_LDS bytes, 0 = the leaf's own size)
-static size_t leaf_lds_reserve() {
-  static long v = -1;
-  if (v < 0) v = getenv("NMGP_POTRF_LEAF_LDS") ? atol(getenv("NMGP_POTRF_LEAF_LDS")) : 88 * 1024;
-  return (size_t)v;
-}
-
-static bool syrk_after_leaf() {
-  static int v = -1;
-  if (v < 0) v = getenv("NMGP_POTRF_SYRK_FIRST") && atoi(getenv("NMGP_POTRF_SYRK_FIRST")) == 1 ? 0 : 1;
-  return v == 1;
+static int potrf_two_level_f32(float* A, int n, int64_t lda, int32_t* info, void* ws, hipStream_t s) {
+  PotrfSide* ctx = nullptr;
+  NMGP_TRY(potrf_side_ctx(ctx));
+  const int nblk = (n + PNB - 1) / PNB;
+  char* w = (char*)ws;
+  float* Xd = (float*)w;
+  w += al256((size_t)nblk * PNB * PNB * sizeof(float)) + al256((size_t)n * PNB * sizeof(float));
+  void* ws_main = w;
+  void* ws_side = w + al256(gemm_big_ws_bytes());
+  void* ws_far = w + 2 * al256(gemm_big_ws_bytes());
+  int32_t* step_flag = (int32_t*)(w + 3 * al256(gemm_big_ws_bytes()));
+  bool side_used = false, np_used = false, far_used = false;
+  // near strips of the last step, issued after the next leaf
+  struct { const float* L; float* C; int m, cols; bool on; } ps{nullptr, nullptr, 0, 0, false};
+  auto issue_strips = [&]() -> int {
+    if (!ps.on) return NMGP_OK;
+    ps.on = false;
+    NMGP_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->ev_main, 0));
+    for (int c = 0; c < ps.cols; c += PNB) {
+      const int cw = min(PNB, ps.cols - c);
+      NMGP_TRY(potrf_strip_f32(ps.L + (int64_t)c * lda, ps.C + (int64_t)c * lda + c, lda, ps.m - c, cw, ctx->side));
+      // the next step kernel's lookahead writes the first strip column: it waits for that one only
+      if (c == 0) NMGP_HIP_TRY(hipEventRecord(ctx->ev_side, ctx->side));
+    }
+    side_used = true;
+    return NMGP_OK;
+  };
+  for (int c0 = 0; c0 < n; c0 += PPW) {
+    const int pw = min(PPW, n - c0), pe = c0 + pw;
+    for (int j0 = c0; j0 < pe; j0 += PNB) {
+      const int jb = j0 / PNB, nbj = min(PNB, n - j0), r0 = j0 + nbj, n2 = n - r0;
+      float* Xj = Xd + (int64_t)jb * PNB * PNB;
+      // the diagonal leaf on the multi-role kernel (factor + two inverse workgroups)
+      NMGP_TRY(chol_inv_small<float>(A + (int64_t)j0 * lda + j0, nbj, lda, 0, Xj, PNB, 0, 1, info, s, j0, jb == 0,
+                                     true, kLeafLds));
+      NMGP_TRY(issue_strips());
+      if (n2 == 0) break;
+      float* Lj = A + (int64_t)r0 * lda + j0;   // block column j below the diagonal block
+      const int c1 = r0 < pe ? min(PNB, pe - r0) : 0;
+      // the last side-stream writer of block column j+1: the strip of step j-1, or NP_rest of the last panel
+      if (c1 > 0 && side_used) NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_side, 0));
+      if (c1 > 0 && j0 == c0 && np_used) NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_np, 0));
+      NMGP_TRY(potrf_step_f32(Lj, A + (int64_t)r0 * lda + r0, Xj, lda, n2, nbj, c1, step_flag, s));
+      const int ncols = pe - (r0 + c1);
+      if (ncols > 0 || r0 == pe) NMGP_HIP_TRY(hipEventRecord(ctx->ev_main, s));
+      if (ncols > 0)
+        ps = {Lj + (int64_t)c1 * lda, A + (int64_t)(r0 + c1) * lda + (r0 + c1), n2 - c1, ncols, true};
+      if (r0 == pe) {
+        // the panel is factored: its 512 columns update the next panel (main + side) and the rest (side2)
+        const float* Lp = A + (int64_t)pe * lda + c0;
+        const int nb1 = min(PNB, n - pe);
+        if (far_used) NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_far, 0));
+        NMGP_TRY(pgemm<float>(Lp, lda, Lp, lda, A + (int64_t)pe * lda + pe, lda, n - pe, nb1, pw, NMGP_OUT_LOWER,
+                              -1.0, 1.0, ws_main, s));
+        const int q0 = pe + nb1, q1 = min(pe + PPW, n);
+        if (q1 > q0) {
+          const float* Lq = Lp + (int64_t)nb1 * lda;
+          NMGP_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->ev_main, 0));
+          if (far_used) NMGP_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->ev_far, 0));
+          NMGP_TRY(pgemm<float>(Lq, lda, Lq, lda, A + (int64_t)q0 * lda + q0, lda, n - q0, q1 - q0, pw,
+                                NMGP_OUT_LOWER, -1.0, 1.0, ws_side, ctx->side));
+          NMGP_HIP_TRY(hipEventRecord(ctx->ev_np, ctx->side));
+          np_used = side_used = true;
+        }
+        if (q1 < n) {
+          const float* Lf = Lp + (int64_t)(q1 - pe) * lda;
+          NMGP_HIP_TRY(hipStreamWaitEvent(ctx->side2, ctx->ev_main, 0));
+          NMGP_TRY(pgemm<float>(Lf, lda, Lf, lda, A + (int64_t)q1 * lda + q1, lda, n - q1, n - q1, pw, NMGP_OUT_LOWER,
+                                -1.0, 1.0, ws_far, ctx->side2));
+          NMGP_HIP_TRY(hipEventRecord(ctx->ev_far, ctx->side2));
+          far_used = true;
+        }
+      }
+    }
+  }
+  NMGP_TRY(issue_strips());
+  if (side_used) {
+    NMGP_HIP_TRY(hipEventRecord(ctx->ev_tail, ctx->side));
+    NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_tail, 0));
+  }
+  if (far_used) NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_far, 0));
+  hipLaunchKernelGGL(zero_upper_kernel<float>, dim3((unsigned)n), dim3(256), 0, s, A, n, lda);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
 }
 
 template <typename T>
 static int potrf_blocked(T* A, int n, int64_t lda, int32_t* info, void* ws, hipStream_t s) {
+  if constexpr (std::is_same<T, float>::value) return potrf_two_level_f32(A, n, lda, info, ws, s);
   PotrfSide* ctx = nullptr;
-  int rc = potrf_side_ctx(ctx);
-  if (rc != NMGP_OK) return rc;
+  NMGP_TRY(potrf_side_ctx(ctx));
   const int nblk = (n + PNB - 1) / PNB;
   char* w = (char*)ws;
   T* Xd = (T*)w;
   w += al256((size_t)nblk * PNB * PNB * sizeof(T));
   T* P = (T*)w;
-  w += al256((size_t)n * PNB * sizeof(T));
-  void* ws_main = nullptr;
-  void* ws_side = nullptr;
-  int32_t* step_flag = nullptr;
-  if (std::is_same<T, float>::value) {
-    ws_main = w;
-    ws_side = w + al256(gemm_big_ws_bytes());
-    step_flag = (int32_t*)((char*)ws_side + al256(gemm_big_ws_bytes()));
-  }
   bool side_used = false;
-  const bool strip = std::is_same<T, float>::value && potrf_step32_active() && potrf_strip();
-  // the trailing SYRK of step j is issued after the leaf of step j+1: both follow the step kernel of
-  // step j, and in a captured graph the first-issued child keeps the parent's queue -- the leaf -> step
-  // hand-off of the serial chain then stays on one queue (the cross-queue wait moves to the SYRK)
-  struct { const T* Lb; T* C; int n3, nbj, jb; bool on; } pend{nullptr, nullptr, 0, 0, -1, false};
-  auto issue_syrk = [&]() -> int {
-    if (!pend.on) return NMGP_OK;
-    pend.on = false;
-    if (hipStreamWaitEvent(ctx->side, ctx->ev_main, 0) != hipSuccess) return NMGP_ERR_LAUNCH;
-    int r;
-    if (std::is_same<T, float>::value && strip) {
-      // block column j+2 first (the next step kernel's lookahead writes it: it waits for this strip only),
-      // then the rest of the trailing SYRK (columns >= j+3), which the step after next waits for
-      const int cs = min(PNB, pend.n3), n4 = pend.n3 - cs;
-      if ((r = potrf_strip_f32((const float*)pend.Lb, (float*)pend.C, lda, pend.n3, cs, ctx->side)) != NMGP_OK) return r;
-      if (hipEventRecord(ctx->ev_side, ctx->side) != hipSuccess) return NMGP_ERR_LAUNCH;
-      if (n4 > 0) {
-        const T* Lb2 = pend.Lb + (int64_t)cs * lda;
-        if ((r = pgemm<T>(Lb2, lda, Lb2, lda, pend.C + (int64_t)cs * lda + cs, lda, n4, n4, pend.nbj, NMGP_OUT_LOWER,
-                          -1.0, 1.0, ws_side, ctx->side)) != NMGP_OK)
-          return r;
-      }
-    } else {
-      r = pgemm<T>(pend.Lb, lda, pend.Lb, lda, pend.C, lda, pend.n3, pend.n3, pend.nbj, NMGP_OUT_LOWER, -1.0, 1.0,
-                   ws_side, ctx->side);
-      if (r != NMGP_OK) return r;
-      if (hipEventRecord(ctx->ev_side, ctx->side) != hipSuccess) return NMGP_ERR_LAUNCH;
-    }
-    if (hipEventRecord(ctx->ev_tail, ctx->side) != hipSuccess) return NMGP_ERR_LAUNCH;
-    side_used = true;
-    return NMGP_OK;
-  };
   for (int jb = 0; jb < nblk; ++jb) {
     const int j0 = jb * PNB, nbj = min(PNB, n - j0), r0 = j0 + nbj, n2 = n - r0;
-    T* Ajj = A + (int64_t)j0 * lda + j0;
     T* Xj = Xd + (int64_t)jb * PNB * PNB;
-    // the diagonal leaf on the multi-role kernel (factor + two inverse workgroups; role 0 waits on
-    // nobody, so a side-stream SYRK holding the CUs only delays it) unless NMGP_POTRF_LEAF_ROLES=0
-    if ((rc = chol_inv_small<T>(Ajj, nbj, lda, 0, Xj, PNB, 0, 1, info, s, j0, jb == 0, leaf_roles(),
-                                std::is_same<T, float>::value ? leaf_lds_reserve() : 0)) != NMGP_OK)
-      return rc;
-    if ((rc = issue_syrk()) != NMGP_OK) return rc;
+    NMGP_TRY(chol_inv_small<T>(A + (int64_t)j0 * lda + j0, nbj, lda, 0, Xj, PNB, 0, 1, info, s, j0, jb == 0));
     if (n2 == 0) break;
     T* Lj = A + (int64_t)r0 * lda + j0;   // block column j below the diagonal block
     const int c1 = min(PNB, n2), n3 = n2 - c1;
-    if constexpr (std::is_same<T, float>::value) {
-      // panel + lookahead in one launch (gemm_big.hip potrf_step_kernel: one 128-wide tile column,
-      // each workgroup reads its rows of A_j in full before overwriting them -- in place).  The
-      // trailing SYRK of step j-1 wrote block column j+1, so the launch follows it.
-      if (side_used && hipStreamWaitEvent(s, ctx->ev_side, 0) != hipSuccess) return NMGP_ERR_LAUNCH;
-      if ((rc = potrf_step_f32(Lj, A + (int64_t)r0 * lda + r0, Xj, lda, n2, nbj, c1, step_flag, s)) != NMGP_OK)
-        return rc;
-    } else {
-      // the f64 kernel's 64-wide tiles would let one workgroup overwrite rows another is still
-      // reading: the panel is staged through P
-      if ((rc = block_copy<T>(Lj, lda, 0, P, PNB, 0, n2, nbj, 1, s)) != NMGP_OK) return rc;
-      if ((rc = pgemm<T>(P, PNB, Xj, PNB, Lj, lda, n2, nbj, nbj, NMGP_B_UPPER, 1.0, 0.0, ws_main, s)) != NMGP_OK)
-        return rc;
-      // the trailing SYRK of step j-1 wrote block column j+1: the lookahead update must follow it
-      if (side_used && hipStreamWaitEvent(s, ctx->ev_side, 0) != hipSuccess) return NMGP_ERR_LAUNCH;
-      if ((rc = pgemm<T>(Lj, lda, Lj, lda, A + (int64_t)r0 * lda + r0, lda, n2, c1, nbj, 0, -1.0, 1.0, ws_main, s)) !=
-          NMGP_OK)
-        return rc;
-    }
+    // the f64 kernel's 64-wide tiles would let one workgroup overwrite rows another is still reading: the
+    // panel is staged through P
+    NMGP_TRY(block_copy<T>(Lj, lda, 0, P, PNB, 0, n2, nbj, 1, s));
+    NMGP_TRY(pgemm<T>(P, PNB, Xj, PNB, Lj, lda, n2, nbj, nbj, NMGP_B_UPPER, 1.0, 0.0, nullptr, s));
+    // the trailing SYRK of step j-1 wrote block column j+1: the lookahead update must follow it
+    if (side_used) NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_side, 0));
+    NMGP_TRY(pgemm<T>(Lj, lda, Lj, lda, A + (int64_t)r0 * lda + r0, lda, n2, c1, nbj, 0, -1.0, 1.0, nullptr, s));
     if (n3 > 0) {
-      if (hipEventRecord(ctx->ev_main, s) != hipSuccess) return NMGP_ERR_LAUNCH;
-      pend = {Lj + (int64_t)c1 * lda, A + (int64_t)(r0 + c1) * lda + (r0 + c1), n3, nbj, jb, true};
-      if (!(std::is_same<T, float>::value && syrk_after_leaf()) && (rc = issue_syrk()) != NMGP_OK) return rc;
+      NMGP_HIP_TRY(hipEventRecord(ctx->ev_main, s));
+      NMGP_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->ev_main, 0));
+      const T* Lb = Lj + (int64_t)c1 * lda;
+      NMGP_TRY(pgemm<T>(Lb, lda, Lb, lda, A + (int64_t)(r0 + c1) * lda + (r0 + c1), lda, n3, n3, nbj, NMGP_OUT_LOWER,
+                        -1.0, 1.0, nullptr, ctx->side));
+      NMGP_HIP_TRY(hipEventRecord(ctx->ev_side, ctx->side));
+      side_used = true;
     }
   }
-  if ((rc = issue_syrk()) != NMGP_OK) return rc;
-  if (side_used && hipStreamWaitEvent(s, ctx->ev_tail, 0) != hipSuccess) return NMGP_ERR_LAUNCH;
+  if (side_used) NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_side, 0));
   hipLaunchKernelGGL(zero_upper_kernel<T>, dim3((unsigned)n), dim3(256), 0, s, A, n, lda);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;

@@ -660,6 +660,7 @@ __global__ __launch_bounds__(256) void potrf_step32_kernel(PotrfStepArgs pa) {
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[q >> 1][q & 1][r]), rP,
                                               (uint32_t)(((int64_t)i * pa.lda + j) * 4), 0, 16 /* sc1 */);
     }
+  if (pa.c1 == 0) return;   // panel only: no lookahead column, no hand-off (the flags stay untouched)
   const bool pub = (int)blockIdx.x < npub;
   if (pub) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -727,44 +728,27 @@ __global__ __launch_bounds__(256) void potrf_strip32_kernel(const float* L, floa
   ps_store_c<RB>(rC, cv, coff, acc);
 }
 
-// rows per workgroup of the step / strip kernels (NMGP_POTRF_ROWS=16 or 32; 16 halves the MFMA work per
-// workgroup and measured the same 1.52-1.54 ms at M = 4096: the kernels are bound by their memory round
-// trips and the L_0 hand-off, not by the products)
-static int ps_rows() {
-  static int v = -1;
-  if (v < 0) v = getenv("NMGP_POTRF_ROWS") && atoi(getenv("NMGP_POTRF_ROWS")) == 16 ? 16 : 32;
-  return v;
-}
-
+// 32 rows per workgroup of the step / strip kernels (round 2: 16 rows halved the MFMA work per workgroup and
+// measured the same 1.52-1.54 ms at M = 4096 -- the kernels are bound by their memory round trips and the L_0
+// hand-off, not by the products)
 int potrf_strip_f32(const float* L, float* C, int64_t lda, int m, int c1, hipStream_t s) {
   if (m <= 0 || c1 <= 0) return NMGP_OK;
-  const int R = ps_rows();
-  if (R == 16)
-    hipLaunchKernelGGL(potrf_strip32_kernel<1>, dim3((unsigned)((m + 15) / 16)), dim3(256), 0, s, L, C, lda, m, c1);
-  else
-    hipLaunchKernelGGL(potrf_strip32_kernel<2>, dim3((unsigned)((m + 31) / 32)), dim3(256), 0, s, L, C, lda, m, c1);
+  hipLaunchKernelGGL(potrf_strip32_kernel<2>, dim3((unsigned)((m + 31) / 32)), dim3(256), 0, s, L, C, lda, m, c1);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
 
-bool potrf_step32_active() {
-  static int v = -1;
-  if (v < 0) v = getenv("NMGP_POTRF_STEP128") && atoi(getenv("NMGP_POTRF_STEP128")) == 1 ? 1 : 0;
-  return v == 0;
-}
-
+// c1 = 0: the panel product only (no lookahead column)
 int potrf_step_f32(float* P, float* C, const float* X, int64_t lda, int n2, int nb, int c1, int32_t* flag,
                    hipStream_t s) {
   if (n2 <= 0) return NMGP_OK;
   PotrfStepArgs pa{P, C, X, lda, n2, nb, c1, flag};
-  if (potrf_step32_active() && nb == 128) {
-    if (ps_rows() == 16)
-      hipLaunchKernelGGL(potrf_step32_kernel<1>, dim3((unsigned)((n2 + 15) / 16)), dim3(256), 0, s, pa);
-    else
-      hipLaunchKernelGGL(potrf_step32_kernel<2>, dim3((unsigned)((n2 + 31) / 32)), dim3(256), 0, s, pa);
+  if (nb == 128) {
+    hipLaunchKernelGGL(potrf_step32_kernel<2>, dim3((unsigned)((n2 + 31) / 32)), dim3(256), 0, s, pa);
     NMGP_CHECK_LAUNCH();
     return NMGP_OK;
   }
+  // (a narrower last block: the 128-row tile form)
   const size_t lds = 2 * BSTAGE * sizeof(float);
   static bool attr = false;
   if (!attr) {

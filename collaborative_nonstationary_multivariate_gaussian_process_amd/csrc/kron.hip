@@ -3,9 +3,10 @@
 //                           element in the reference's operand order, so results are bit-exact;
 //                           each thread writes 4 consecutive elements of one output row.
 //   kronecker_product_diag  out[i*n2+k] = d1[i] * d2[k]
-//   kron_mv                 (B kron K) y without forming B kron K: Y = y.view(P2,N2)^T,
-//                           A = (K Y) B^T on the matrix cores (two GEMMs), out = vec(A^T) in the
-//                           reference's reshape order (bit-exact index mapping).
+//   kron_mv                 (B kron K) y without forming B kron K: Y = y.view(P2,N2)^T, A = (K Y) B^T,
+//                           out = vec(A^T) in the reference's reshape order (bit-exact index mapping).
+//                           P2 <= 8 (the legacy likelihood's few outputs): ONE pass over K (round 4,
+//                           kron_mv_kernel below) -- the HBM-bound case; wider B: two MFMA GEMMs.
 #include "common.hpp"
 
 namespace nmgp {
@@ -44,6 +45,67 @@ static int kron_product(const T* t1, int64_t r1, int64_t c1, const T* t2, int64_
   return NMGP_OK;
 }
 
+// Fused Kronecker mat-vec for small P2 (the legacy likelihood: B is P x P over a few outputs, K is N x N).
+// Each wave owns KR consecutive rows n of K and streams them once from HBM in 16-byte loads (lanes over k);
+// y's P2 rows are re-read from L2 for every KR rows (KR-fold reuse).  Per lane: KR x P2 partial sums of
+// work[n, m] = sum_k K[n,k] y[m N2 + k]; a DPP wave reduction (common.hpp wave_sum) completes them in every
+// lane, and lane p < P1 writes out[p N1 + n] = sum_m B[p,m] work[n,m] -- the second GEMM in registers.
+// Bound: HBM, N1 N2 s bytes of K (+ y, B, out: P2 N2 + P1 P2 + P1 N1 elements).
+constexpr int KMV_MAXP = 8;   // P2 limit of the fused path
+constexpr int KMV_ROWS = 4;   // rows of K per wave
+
+template <typename T, int V>
+__global__ __launch_bounds__(256) void kron_mv_kernel(const T* __restrict__ B, int P1, int P2, const T* __restrict__ K,
+                                                      int N1, int N2, const T* __restrict__ y, T* __restrict__ out) {
+  struct alignas(sizeof(T) * V) Vec { T e[V]; };
+  const int lane = threadIdx.x & 63;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int n0 = wave * KMV_ROWS;
+  if (n0 >= N1) return;
+  T acc[KMV_ROWS][KMV_MAXP];
+#pragma unroll
+  for (int r = 0; r < KMV_ROWS; ++r)
+#pragma unroll
+    for (int m = 0; m < KMV_MAXP; ++m) acc[r][m] = (T)0;
+  const int nv = N2 / V;
+  for (int kv = lane; kv < nv; kv += 64) {
+    Vec kr[KMV_ROWS];
+#pragma unroll
+    for (int r = 0; r < KMV_ROWS; ++r) {
+      const int n = min(n0 + r, N1 - 1);                      // (rows past N1 duplicate the last row; unused)
+      kr[r] = *(const Vec*)(K + (int64_t)n * N2 + (int64_t)kv * V);
+    }
+#pragma unroll
+    for (int m = 0; m < KMV_MAXP; ++m) {
+      if (m < P2) {
+        const Vec yv = *(const Vec*)(y + (int64_t)m * N2 + (int64_t)kv * V);
+#pragma unroll
+        for (int r = 0; r < KMV_ROWS; ++r)
+#pragma unroll
+          for (int e = 0; e < V; ++e) acc[r][m] = fma(kr[r].e[e], yv.e[e], acc[r][m]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < KMV_ROWS; ++r)
+#pragma unroll
+    for (int m = 0; m < KMV_MAXP; ++m)
+      if (m < P2) acc[r][m] = wave_sum(acc[r][m]);
+  // the second stage: lanes p < P1 (strided over P1 > 64) form out[p N1 + n]
+  for (int p = lane; p < P1; p += 64) {
+#pragma unroll
+    for (int r = 0; r < KMV_ROWS; ++r) {
+      const int n = n0 + r;
+      if (n >= N1) break;
+      T o = (T)0;
+#pragma unroll
+      for (int m = 0; m < KMV_MAXP; ++m)
+        if (m < P2) o = fma(B[(int64_t)p * P2 + m], acc[r][m], o);
+      out[(int64_t)p * N1 + n] = o;
+    }
+  }
+}
+
 template <typename T>
 static int kron_mv(const T* B, int64_t P1, int64_t P2, const T* K, int64_t N1, int64_t N2, const T* y, T* out, T* work,
                    hipStream_t s, int (*gemm)(const nmgp_gemm_desc*, const int32_t*, hipStream_t)) {
@@ -51,8 +113,21 @@ static int kron_mv(const T* B, int64_t P1, int64_t P2, const T* K, int64_t N1, i
   if (!K) return -4;
   if (!y) return -7;
   if (!out) return -8;
-  if (!work) return -9;
   if (P1 == 0 || N1 == 0) return NMGP_OK;
+  if (P2 >= 1 && P2 <= KMV_MAXP && N2 >= 1 && N1 < (1LL << 30) && N2 < (1LL << 30)) {
+    const unsigned grid = (unsigned)((N1 + 4 * KMV_ROWS - 1) / (4 * KMV_ROWS));
+    constexpr int V = 16 / (int)sizeof(T);
+    const bool vec = N2 % V == 0 && ((uintptr_t)K & 15) == 0 && ((uintptr_t)y & 15) == 0;
+    if (vec)
+      hipLaunchKernelGGL((kron_mv_kernel<T, V>), dim3(grid), dim3(256), 0, s, B, (int)P1, (int)P2, K, (int)N1, (int)N2,
+                         y, out);
+    else
+      hipLaunchKernelGGL((kron_mv_kernel<T, 1>), dim3(grid), dim3(256), 0, s, B, (int)P1, (int)P2, K, (int)N1, (int)N2,
+                         y, out);
+    NMGP_CHECK_LAUNCH();
+    return NMGP_OK;
+  }
+  if (!work) return -9;
   // work(n, m) = sum_k K[n,k] * y[m*N2 + k]        (N1 x P2)
   nmgp_gemm_desc d{};
   d.A = K; d.B = y; d.C = work;

@@ -742,19 +742,87 @@ def kron_product(t1, t2):
     return out
 
 
-def kron_mv(B, K, y):
+KRON_MV_FUSED_MAXP = 8      # csrc/kron.hip KMV_MAXP
+
+
+def kron_mv(B, K, y, out=None):
     L.require_device(B, "B")
     B, K, y = B.contiguous(), K.contiguous(), y.contiguous()
     P1, P2 = B.shape
     N1, N2 = K.shape
     assert y.numel() == P2 * N2
-    out = torch.empty(P1 * N1, dtype=B.dtype, device=B.device)
-    work = torch.empty(N1 * P2, dtype=B.dtype, device=B.device)
+    if out is None:
+        out = torch.empty(P1 * N1, dtype=B.dtype, device=B.device)
+    # P2 <= 8: one fused launch streaming K once (csrc/kron.hip kron_mv_kernel); wider B: two GEMMs via `work`
+    work = torch.empty(N1 * P2, dtype=B.dtype, device=B.device) if P2 > KRON_MV_FUSED_MAXP else None
     fn = getattr(L.lib(), "nmgp_kron_mv_" + _sfx(B.dtype))
     L.check(fn(ctypes.c_void_p(B.data_ptr()), P1, P2, ctypes.c_void_p(K.data_ptr()), N1, N2,
-               ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(work.data_ptr()),
-               L.stream_handle()), "kron_mv")
+               ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+               ctypes.c_void_p(work.data_ptr()) if work is not None else None, L.stream_handle()), "kron_mv")
     return out
+
+
+# ------------------------------------------------------------------------------------ graphs
+class HipGraph:
+    """A captured launch sequence replayed as one HIP graph, captured through the library's own C ABI
+    (nmgp_graph_begin / _end / _launch) instead of torch.cuda.CUDAGraph: torch's capture_end crashed on a
+    side <-> side2 event ping-pong of the step schedule that the HIP runtime captures cleanly.
+
+        g = HipGraph(device)
+        with g.capture():          # the body runs on g.stream (torch's current stream inside the block)
+            body()                 # launches, event records / waits across streams; no allocation, no sync
+        g.replay()                 # on torch's current stream
+
+    The body's side streams must join back into the capture stream before the block ends."""
+
+    def __init__(self, device=None):
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.stream = torch.cuda.Stream(device=self.device)
+        self.exec = None
+
+    class _Capture:
+        def __init__(self, g):
+            self.g = g
+
+        def __enter__(self):
+            g = self.g
+            if g.exec is not None:
+                raise RuntimeError("HipGraph already holds a captured graph")
+            cur = torch.cuda.current_stream(g.device)
+            g.stream.wait_stream(cur)           # everything enqueued before the capture comes first
+            torch.cuda.synchronize(g.device)    # (and is finished: a capture must not wait on pending work)
+            self.ctx = torch.cuda.stream(g.stream)
+            self.ctx.__enter__()
+            L.check(L.lib().nmgp_graph_begin(ctypes.c_void_p(g.stream.cuda_stream)), "graph_begin")
+            return g
+
+        def __exit__(self, et, ev, tb):
+            g = self.g
+            ex = ctypes.c_void_p()
+            rc = L.lib().nmgp_graph_end(ctypes.c_void_p(g.stream.cuda_stream), ctypes.byref(ex))
+            self.ctx.__exit__(et, ev, tb)
+            if et is None:
+                L.check(rc, "graph_end")
+                g.exec = ex
+            return False
+
+    def capture(self):
+        return HipGraph._Capture(self)
+
+    def replay(self, stream=None):
+        if self.exec is None:
+            raise RuntimeError("HipGraph.replay before capture")
+        s = stream if stream is not None else L.stream_handle(self.device)
+        L.check(L.lib().nmgp_graph_launch(self.exec, s), "graph_launch")
+
+    def __del__(self):
+        ex = getattr(self, "exec", None)
+        if ex is not None and L._lib is not None:
+            try:
+                L._lib.nmgp_graph_destroy(ex)
+            except Exception:
+                pass
+            self.exec = None
 
 
 # ------------------------------------------------------------------------------------ optimiser / rng

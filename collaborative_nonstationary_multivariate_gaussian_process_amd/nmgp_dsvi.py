@@ -596,8 +596,8 @@ class DsviTrainer:
         cur.wait_stream(s)
         for t, v in saved:
             t.copy_(v)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        g = H.HipGraph(mdl.device_)          # captured through the HIP runtime (nmgp_graph_*), not torch
+        with g.capture():
             body(eng)
         self.graphs[id(eng)] = g
         return g
@@ -610,8 +610,8 @@ class DsviTrainer:
         key = ("update", int(world))
         g = self.graphs.get(key)
         if g is None:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            g = H.HipGraph(self.model.device_)
+            with g.capture():
                 if world > 1:
                     self.model._grad.div_(world)
                 self.update()

@@ -292,7 +292,8 @@ int nmgp_colsum_f32(const float* a, int64_t rows, int64_t cols, double beta, flo
  * kronecker_product (SIM_code/Utility/kronecker_operation.py:5-22): out[(i*r2+k)*(c1*c2)+j*c2+l] =
  *   t1[i,j]*t2[k,l]  (one multiply per element: bit-exact)
  * kronecker_product_diag (:25-33): out[i*n2+k] = d1[i]*d2[k]
- * kron_mv (:72-85): out = (B kron K) y, B (P1 x P2), K (N1 x N2), y (P2*N2) -> (P1*N1)       */
+ * kron_mv (:72-85): out = (B kron K) y, B (P1 x P2), K (N1 x N2), y (P2*N2) -> (P1*N1).  P2 <= 8: one
+ *   fused launch streaming K once (work unused, may be NULL); otherwise two GEMMs through work (N1*P2). */
 int nmgp_kron_product_f64(const double* t1, int64_t r1, int64_t c1, const double* t2, int64_t r2, int64_t c2,
                           double* out, hipStream_t stream);
 int nmgp_kron_product_diag_f64(const double* d1, int64_t n1, const double* d2, int64_t n2, double* out,
@@ -438,6 +439,17 @@ int nmgp_batch_gather_f64(const double* Xb, const double* Yb, const int32_t* Ib,
 int nmgp_batch_gather_f32(const float* Xb, const float* Yb, const int32_t* Ib, const int32_t* Sb, int64_t B,
                           int64_t nseg, int64_t nbatch, int64_t* batch_counter, float* x, float* y,
                           int32_t* row_out, int32_t* seg, hipStream_t stream);
+
+/* Whole-step HIP graphs (the reference runs its step eagerly, code/nmgp_dsvi.py:829-854; the build captures
+ * noise -> forward -> backward -> Adam once and replays it).  Capture goes straight through the HIP runtime:
+ * begin on `stream` (thread-local mode; other streams join through event waits and must join back before
+ * the end), end + instantiate into an executable graph handle, launch it on a stream, destroy it.  The body
+ * must not allocate or synchronise.  Returns NMGP_ERR_LAUNCH on a runtime failure; a failed end of capture
+ * leaves nothing behind.                                                                                  */
+int nmgp_graph_begin(hipStream_t stream);
+int nmgp_graph_end(hipStream_t stream, void** exec_out);
+int nmgp_graph_launch(void* exec, hipStream_t stream);
+int nmgp_graph_destroy(void* exec);
 
 #ifdef __cplusplus
 }

@@ -719,6 +719,25 @@ def test_kron(ops):
     assert rel(mv, torch.kron(Bk, Kk) @ y) < 1e-13
 
 
+@pytest.mark.parametrize("P1,P2,N1,N2", [(5, 5, 4096, 4096), (3, 8, 37, 61), (70, 2, 131, 64), (6, 9, 50, 40),
+                                         (1, 1, 1, 1), (8, 3, 1000, 1001)])
+@pytest.mark.parametrize("dt", [F64, torch.float32])
+def test_kron_mv_fused_and_gemm_paths(ops, P1, P2, N1, N2, dt):
+    """kron_mv (kronecker_operation.py:72-85): P2 <= 8 takes the fused one-pass kernel (16-byte rows when N2
+    allows, scalar otherwise; row tails; P1 > 64 lanes strided), P2 > 8 the two-GEMM path; both in the
+    reference's reshape order against the oracle restatement and the dense (B kron K) y."""
+    g = torch.Generator().manual_seed(P1 * 1000 + P2 * 100 + N1 + N2)
+    Bk = torch.randn(P1, P2, generator=g, dtype=F64)
+    Kk = torch.randn(N1, N2, generator=g, dtype=F64)
+    y = torch.randn(P2 * N2, generator=g, dtype=F64)
+    mv = ops.kron_mv(Bk.to(dt).to(DEV), Kk.to(dt).to(DEV), y.to(dt).to(DEV)).double().cpu()
+    Bc, Kc, yc = Bk.to(dt).double(), Kk.to(dt).double(), y.to(dt).double()
+    tol = 1e-13 if dt == F64 else 2e-5          # (fp32: sums of up to 8 x 4096 products)
+    assert rel(mv, O.kron_mv(Bc, Kc, yc)) < tol
+    if N1 * N2 <= 10 ** 6:
+        assert rel(mv, torch.kron(Bc, Kc) @ yc) < tol
+
+
 def test_adam_matches_torch(ops):
     g = torch.Generator().manual_seed(8)
     p0 = torch.randn(1000, generator=g, dtype=F64)
@@ -802,3 +821,70 @@ def test_kronecker_gaussian_legacy_sizes(ops, P, N):
     lp = float(DI.multivariate_normal_logpdf0(y, mu, Bm, K, s2))
     assert lp == pytest.approx(float(O.multivariate_normal_logpdf0(y, mu, Bm, K, s2)), rel=1e-10)
     assert float(DI.multivariate_normal_logpdf2(y, mu, Bm, K, s2)) == pytest.approx(lp, rel=1e-9)
+
+
+def test_hip_graph_side_stream_ping_pong(ops):
+    """hip_ops.HipGraph (capture through the library's nmgp_graph_* C ABI): a side -> side2 -> side event
+    ping-pong -- the pattern torch's CUDAGraph.capture_end crashed on -- captures,
+    instantiates and replays with the stream order intact."""
+    x = torch.zeros(4096, dtype=F64, device=DEV)
+    y = torch.zeros(4096, dtype=F64, device=DEV)
+    s1, s2 = torch.cuda.Stream(device=DEV), torch.cuda.Stream(device=DEV)
+    g = ops.HipGraph(DEV)
+    with g.capture():
+        main = torch.cuda.current_stream(DEV)
+        e0 = torch.cuda.Event()
+        e0.record(main)
+        s1.wait_event(e0)
+        s2.wait_event(e0)
+        with torch.cuda.stream(s1):
+            x.add_(1.0)
+            e1 = torch.cuda.Event()
+            e1.record(s1)
+        with torch.cuda.stream(s2):
+            s2.wait_event(e1)                  # side -> side2
+            y.add_(x)
+            e2 = torch.cuda.Event()
+            e2.record(s2)
+        with torch.cuda.stream(s1):
+            s1.wait_event(e2)                  # side2 -> side
+            x.mul_(2.0)
+            e3 = torch.cuda.Event()
+            e3.record(s1)
+        main.wait_event(e3)
+        main.wait_event(e2)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    # per replay: x += 1; y += x; x *= 2  ->  (x, y) = (2, 1), (6, 4), (14, 11)
+    assert torch.all(x == 14.0) and torch.all(y == 11.0)
+
+
+def test_training_step_graph_is_captured_through_hip(ops):
+    """DsviTrainer.capture builds the step graph with hip_ops.HipGraph (not torch.cuda.CUDAGraph), with the
+    schedule's direct side <-> side2 edges; replaying it equals the eager step bit for bit (D=3, M=64)."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP, DsviTrainer
+    rng = np.random.default_rng(8)
+    D, n, M, B = 3, 120, 64, 240
+    xs = [torch.from_numpy(np.sort(rng.uniform(0, 1, n))) for _ in range(D)]
+    ys = [torch.from_numpy(np.cos(4 * x.numpy() + d) + 0.2 * rng.standard_normal(n)) for d, x in enumerate(xs)]
+    res = []
+    for graph in (True, False):
+        model = NMGP(number_observations=D * n, dim_outputs=D, Z=np.linspace(0, 1, M), minibatch_size=B, seed=6,
+                     device=DEV, noise="device")
+        tr = DsviTrainer(model, 0.01)
+        eng = model.engine(B)
+        x, y, sizes = model._prepare(xs, ys)
+        eng.load_batch(x, y, sizes)
+        if graph:
+            g = tr.capture(eng, include_update=False)
+            assert isinstance(g, ops.HipGraph)
+            sched = eng._schedule(0)
+            waits = {(it[1], it[2]) for it in sched if it[0] == "wait"}
+            assert ("side2", "kl_done") in waits and ("side", "g22") in waits      # the ping-pong edges
+            g.replay()
+        else:
+            tr.grad_step(eng)
+        torch.cuda.synchronize()
+        res.append((float(eng.out[0]), model._grad.detach().cpu().clone()))
+    assert res[0][0] == res[1][0] and torch.equal(res[0][1], res[1][1])

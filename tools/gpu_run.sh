@@ -9,6 +9,7 @@
 #   timeline   step timeline from the prof kernel trace    -> gpurun_out/<tag>_step_timeline.txt
 #   stress     stress potrf kernel trace + MFMA pass       -> gpurun_out/stress/             (tools/stress_trace.sh)
 #   hcp        HCP / ECoG training kernel traces          -> gpurun_out/hcp/                (tools/hcp_trace.sh)
+#   potrf      stress potrf tests, timing, trace, MFMA    -> gpurun_out/<tag>_stress_*     (tools/stress_potrf.sh)
 #   n2         bench.py's N = 2 path rehearsed with two gloo ranks sharing cuda:0
 #   n4         the same with four gloo ranks
 # Every GPU step runs under its own timeout and the script stops at the first failing step.
@@ -44,6 +45,9 @@ for step in "$@"; do
       head -3 gpurun_out/${TAG}_step_timeline.txt ;;
     stress)
       run stress bash tools/stress_trace.sh > gpurun_out/${TAG}_stress.log 2>&1 || { tail -20 gpurun_out/${TAG}_stress.log; exit 1; } ;;
+    potrf)
+      run potrf bash tools/stress_potrf.sh $TAG > gpurun_out/${TAG}_potrf.log 2>&1 || { tail -30 gpurun_out/${TAG}_potrf.log; exit 1; }
+      tail -25 gpurun_out/${TAG}_potrf.log ;;
     hcp)
       run hcp bash tools/hcp_trace.sh > gpurun_out/${TAG}_hcp.log 2>&1 || { tail -20 gpurun_out/${TAG}_hcp.log; exit 1; } ;;
     n2|n4)

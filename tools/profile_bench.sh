@@ -10,7 +10,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-ARGS="--steps 30 --warmup 5 --no-cpu-baseline --no-stress --no-elbo --no-api --no-hcp --no-ecog"
+ARGS="--steps 30 --warmup 5 --no-cpu-baseline --no-stress --no-elbo --no-api --no-hcp --no-ecog --no-kron"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $R/bench.py $ARGS > $OUT/bench_under_trace.json 2> $OUT/trace.err
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $R/bench.py $ARGS --no-breakdown > $OUT/bench_under_fetch.json 2> $OUT/fetch.err
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 $R/bench.py $ARGS --no-breakdown > $OUT/bench_under_write.json 2> $OUT/write.err
