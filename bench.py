@@ -360,7 +360,9 @@ def pair_sharded_train(dev, world, rank, dist, D=128, M=1024, rows=391, B=512, s
     coefficient pairs sharded over the ranks by output range (pair_shard.PairShard): each rank holds its
     pairs' parameters / Adam state / factors, draws b_r = B N_r / N rows of its outputs, and the
     replicated gradient (mu_W, sqrt_W, mu_v, sqrt_v, hyper-parameters) is summed with one RCCL
-    all-reduce per step.  fp32, eager launches; timed over `steps` steps after one warm-up step,
+    all-reduce per step.  fp32; each rank's rows resident in HBM, one on-device minibatch gather per step,
+    the rank-local step and Adam replayed as HIP graphs around the all-reduce (PairShard.bind_rows /
+    capture); timed over `steps` steps after one warm-up step,
     barrier + synchronize on both sides, max over ranks.  A rank that fails to build its share makes
     every rank skip the leg (flag all-reduce) instead of leaving the others in a collective."""
     import gc
@@ -393,9 +395,9 @@ def pair_sharded_train(dev, world, rank, dist, D=128, M=1024, rows=391, B=512, s
                        device=dev, frozen=("length_scales_tildeell_log", "length_scales_L0_log", "length_scales_L1_log"),
                        ranges=ranges, pairs_local=True)
         del p
-        idx = np.sort(np.random.default_rng(5 + rank).choice(n_r, b_r, replace=False))
-        sh.load([xs[i0 + k][idx[(idx >= k * rows) & (idx < (k + 1) * rows)] - k * rows] for k in range(i1 - i0)],
-                [ys[i0 + k][idx[(idx >= k * rows) & (idx < (k + 1) * rows)] - k * rows] for k in range(i1 - i0)])
+        # the rank's rows stay in HBM; each step gathers its minibatch on the device and replays as HIP graphs
+        nb = sh.bind_rows(xs[i0:i1], ys[i0:i1], seed=5)
+        sh.capture()
     except Exception as exc:                      # e.g. out of memory on a small world
         ok.zero_()
         err = f"{type(exc).__name__}: {exc}"[:300]
@@ -406,12 +408,14 @@ def pair_sharded_train(dev, world, rank, dist, D=128, M=1024, rows=391, B=512, s
         gc.collect()
         torch.cuda.empty_cache()
         return {"error": err or "another rank could not build its share"}
-    sh.step()                                     # warm-up: plans, first launches
+    sh.step()                                     # warm-up: first replays
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.time()
-    for _ in range(steps):
+    for it in range(steps):
+        if (it + 1) % nb == 0:
+            sh.new_epoch()
         loss = sh.step()
     torch.cuda.synchronize()
     if world > 1:

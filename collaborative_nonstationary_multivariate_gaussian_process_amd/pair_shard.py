@@ -148,6 +148,52 @@ class PairShard:
         self.engine.load_batch(x, y, sizes, noise=noise, index=list(range(i0, i1)))
         self._host_noise = noise is not None
 
+    def bind_rows(self, xs, ys, b_r=None, seed=0):
+        """SURVEY f4 for a pair-sharded rank: ALL of this rank's rows (xs / ys: one array per owned output, in
+        order) stay resident in HBM, and every epoch is a device permutation cut into minibatches of b_r rows
+        (default: the engine's B), each grouped by output as vec2list groups them and given its segment table
+        -- bound to the engine (DsviEngine.bind_dataset), so a step starts with ONE on-device gather and the
+        whole step replays from a HIP graph (capture()).  The minibatch stratification is the one `load`
+        documents: rank r draws its b_r rows from its own N_r.  Returns the number of minibatches per epoch."""
+        i0, i1 = self.pair_range
+        assert len(xs) == len(ys) == i1 - i0, "one row list per owned output"
+        B = self.B if b_r is None else int(b_r)
+        assert B == self.B, "the engine's minibatch size is fixed at construction (B_r)"
+        dev, dt = self.dev, self.dt
+        sizes = [len(np.asarray(x).reshape(-1)) for x in xs]
+        cat = lambda a: torch.as_tensor(np.concatenate([np.asarray(v, np.float64).reshape(-1) for v in a]))
+        self._rows = (cat(xs).to(dev, dt), cat(ys).to(dev, dt),
+                      torch.as_tensor(np.repeat(np.arange(i0, i1), sizes)).to(dev))
+        n = int(sum(sizes))
+        nb = n // B
+        if nb < 1:
+            raise ValueError(f"rank {self.rank} holds {n} rows, fewer than one minibatch of {B}")
+        self._epoch_gen = torch.Generator(device=dev)
+        self._epoch_gen.manual_seed(int(seed) + 7919 * (self.rank + 1))
+        self._bufs = (torch.empty(nb, B, dtype=dt, device=dev), torch.empty(nb, B, dtype=dt, device=dev),
+                      torch.empty(nb, B, dtype=torch.int32, device=dev),
+                      torch.empty(nb, self.D + 1, dtype=torch.int32, device=dev))
+        self._bctr = self.engine.bind_dataset(*self._bufs)
+        self._ar = torch.arange(self.D + 1, device=dev)
+        self._host_noise = False
+        self.new_epoch()
+        return nb
+
+    def new_epoch(self):
+        """Refill the bound minibatches from a fresh device permutation of this rank's rows (no host copy)."""
+        X, Y, I = self._rows
+        Xb, Yb, Ib, Sb = self._bufs
+        nb, B = Xb.shape
+        idx = torch.randperm(X.numel(), generator=self._epoch_gen, device=self.dev)[:nb * B].view(nb, B)
+        ids = I[idx]
+        order = torch.sort(ids, dim=1, stable=True).indices
+        idx, ids = idx.gather(1, order), ids.gather(1, order)
+        Xb.copy_(X[idx])
+        Yb.copy_(Y[idx])
+        Ib.copy_(ids)
+        Sb.copy_(torch.searchsorted(ids, self._ar.expand(nb, -1).contiguous()))
+        self._bctr.zero_()
+
     def draw_noise(self):
         """z_v from the seed every rank shares (one v sample for the whole model), the row / pair noise
         from a rank-distinct stream; then advance the shared counter."""
@@ -157,28 +203,75 @@ class PairShard:
         H.counter_add_(self.noise_counter, 1)
 
     # ------------------------------------------------------------------------------------ step
-    def grad_step(self, reduce=True):
-        """-SELBO of the whole model (summed over ranks) and this rank's gradient: owned pairs exact,
-        replicated parameters summed over ranks.  reduce=False: this share's own terms only (the
-        caller sums them, e.g. several shares simulated in one process)."""
+    def _grad_body(self):
+        """The rank-local part of a step: [on-device minibatch gather] + noise + fused forward / backward."""
+        if getattr(self.engine, "_dataset", None) is not None:
+            self.engine.gather_batch()
         if not getattr(self, "_host_noise", False):
             self.draw_noise()
         self.engine.forward_backward()
-        loss = self.engine.out[0:1].clone()
-        if reduce and self.world > 1:
+
+    def _reduce(self, loss):
+        if self.world > 1:
             import torch.distributed as dist
             for t in self._rep:
                 dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
             dist.all_reduce(loss, op=dist.ReduceOp.SUM, group=self.group)
+
+    def grad_step(self, reduce=True):
+        """-SELBO of the whole model (summed over ranks) and this rank's gradient: owned pairs exact,
+        replicated parameters summed over ranks.  reduce=False: this share's own terms only (the
+        caller sums them, e.g. several shares simulated in one process)."""
+        self._grad_body()
+        loss = self.engine.out[0:1].clone()
+        if reduce:
+            self._reduce(loss)
         return loss[0]
 
     def update(self):
         H.adam_(self.theta, self.grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps)
 
+    def capture(self):
+        """Capture the rank-local step (gather + noise + forward / backward) and the Adam update as two HIP
+        graphs (hip_ops.HipGraph); step() then replays them around the replicated-gradient all-reduce.  Needs
+        device noise; the warm-up runs outside the capture and restores the noise / batch counters, so the
+        first replay is the next real step."""
+        if getattr(self, "_host_noise", False):
+            raise ValueError("graph capture needs device noise (no host noise loaded)")
+        ds = getattr(self.engine, "_dataset", None)
+        saved = [(self.noise_counter, self.noise_counter.clone())]
+        if ds is not None:
+            saved.append((ds[4], ds[4].clone()))
+        cur = torch.cuda.current_stream(self.dev)
+        st = torch.cuda.Stream(device=self.dev)
+        st.wait_stream(cur)
+        with torch.cuda.stream(st):
+            for _ in range(2):
+                self._grad_body()
+        cur.wait_stream(st)
+        for t, v in saved:
+            t.copy_(v)
+        g = H.HipGraph(self.dev)
+        with g.capture():
+            self._grad_body()
+        u = H.HipGraph(self.dev)
+        with u.capture():
+            self.update()
+        self._graphs = (g, u)
+        return self._graphs
+
     def step(self):
-        loss = self.grad_step()
-        self.update()
-        return loss
+        """One training step: graph replays when captured (capture()), eager launches otherwise."""
+        graphs = getattr(self, "_graphs", None)
+        if graphs is None:
+            loss = self.grad_step()
+            self.update()
+            return loss
+        graphs[0].replay()
+        loss = self.engine.out[0:1].clone()
+        self._reduce(loss)
+        graphs[1].replay()
+        return loss[0]
 
     def check(self):
         self.engine.check_info()
