@@ -60,9 +60,16 @@ __device__ inline float4 ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX));
 }
 
-// Lower-triangle tile index -> (tile row, tile column), row-major over the lower triangle.
+// Lower-triangle tile index -> (tile row, tile column), row-major over the lower triangle.  A tall OUT_LOWER
+// output (m > n: the blocked potrf's next-panel updates) continues below the triangle with full tile rows.
 __device__ inline void tile_coords(const BigGemmArgs& g, int tile, int& tm, int& tn) {
   if (g.flags & NMGP_OUT_LOWER) {
+    const int T = g.tiles_n, tri = T * (T + 1) / 2;
+    if (tile >= tri) {
+      tm = T + (tile - tri) / T;
+      tn = (tile - tri) - (tm - T) * T;
+      return;
+    }
     tm = (int)((sqrtf(8.0f * (float)tile + 1.0f) - 1.0f) * 0.5f);
     while ((tm + 1) * (tm + 2) / 2 <= tile) ++tm;
     while (tm * (tm + 1) / 2 > tile) --tm;
@@ -792,7 +799,7 @@ static int gemm_big_f32_ex(const float* A, int64_t lda, const float* B, int64_t 
                            const int64_t* offC, float diag_add, int batch, void* ws, hipStream_t s,
                            const BigEpi& ep = BigEpi()) {
   if (m <= 0 || n <= 0 || batch <= 0) return NMGP_OK;
-  if ((flags & NMGP_OUT_LOWER) && m != n) return -1;
+  if ((flags & NMGP_OUT_LOWER) && m < n) return -1;   // (m > n: the triangle, then full tile rows below it)
   BigGemmArgs g;
   g.A = A; g.B = B; g.C = C;
   g.offA = offA; g.offB = offB; g.offC = offC;
@@ -809,7 +816,8 @@ static int gemm_big_f32_ex(const float* A, int64_t lda, const float* B, int64_t 
   g.alpha = alpha; g.beta = beta;
   g.tiles_m = (m + BBM - 1) / BBM;
   g.tiles_n = (n + BBN - 1) / BBN;
-  g.tiles = (flags & NMGP_OUT_LOWER) ? g.tiles_m * (g.tiles_m + 1) / 2 : g.tiles_m * g.tiles_n;
+  g.tiles = (flags & NMGP_OUT_LOWER) ? g.tiles_n * (g.tiles_n + 1) / 2 + (g.tiles_m - g.tiles_n) * g.tiles_n
+                                      : g.tiles_m * g.tiles_n;
   int S = 1, sk = 0;
   const int64_t total = (int64_t)g.tiles * batch;
   const int nkt = (k + BBK - 1) / BBK;

@@ -437,6 +437,24 @@ def test_gemm_big_masks_and_syrk(ops, flags, b_kcontig):
         assert rel(C, ref) < 2e-6
 
 
+@pytest.mark.parametrize("m,n,k", [(700, 300, 200), (3584, 128, 512), (3456, 384, 512), (256, 256, 64)])
+def test_gemm_big_out_lower_tall(ops, m, n, k):
+    """OUT_LOWER on a tall output (m >= n: the blocked potrf's next-panel updates C -= L_p L_q^T): the
+    lower triangle of the top n x n block and every row below it are updated, the strict upper part of
+    the top block is untouched; stream-K / split-K tile counts cover the triangle plus the full rows."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L
+    g = torch.Generator().manual_seed(m + n + k)
+    A = torch.randn(m, k, generator=g)
+    C0 = torch.randn(m, n, generator=g)
+    Ad, C = A.to(DEV), C0.to(DEV)
+    ops.gemm_big(Ad, Ad[:n].contiguous(), C, flags=L.OUT_LOWER, alpha=-1.0, beta=1.0)
+    got = C.cpu().double()
+    ref = C0.double() - A.double() @ A[:n].double().t()
+    lo = torch.ones(m, n, dtype=torch.bool).tril()
+    assert rel(got[lo], ref[lo]) < 2e-6
+    assert torch.equal(got[~lo], C0.double()[~lo])
+
+
 def test_gemm_big_split_k_deterministic_and_batched(ops):
     # few tiles, long k: split-K runs (workspace) and must be bit-reproducible and equal to no-split within f32 rounding
     g = torch.Generator().manual_seed(5)
