@@ -8,7 +8,7 @@
 #   pmc        MFMA-busy pass of the PM2.5 step            -> gpurun_out/pm25pmc/            (tools/pm25_pmc.sh)
 #   timeline   step timeline from the prof kernel trace    -> gpurun_out/<tag>_step_timeline.txt
 #   stress     stress potrf kernel trace + MFMA pass       -> gpurun_out/stress/             (tools/stress_trace.sh)
-#   hcp        HCP / ECoG training kernel traces          -> gpurun_out/hcp/                (tools/hcp_trace.sh)
+#   train      HCP / ECoG training kernel breakdowns      -> gpurun_out/<tag>_{hcp,ecog}_train_kernels.json
 #   potrf      stress potrf tests, timing, trace, MFMA    -> gpurun_out/<tag>_stress_*     (tools/stress_potrf.sh)
 #   n2         bench.py's N = 2 path rehearsed with two gloo ranks sharing cuda:0
 #   n4         the same with four gloo ranks
@@ -48,8 +48,15 @@ for step in "$@"; do
     potrf)
       run potrf bash tools/stress_potrf.sh $TAG > gpurun_out/${TAG}_potrf.log 2>&1 || { tail -30 gpurun_out/${TAG}_potrf.log; exit 1; }
       tail -25 gpurun_out/${TAG}_potrf.log ;;
-    hcp)
-      run hcp bash tools/hcp_trace.sh > gpurun_out/${TAG}_hcp.log 2>&1 || { tail -20 gpurun_out/${TAG}_hcp.log; exit 1; } ;;
+    train)
+      run train bash tools/train_trace.sh $TAG > gpurun_out/${TAG}_train.log 2>&1 || { tail -20 gpurun_out/${TAG}_train.log; exit 1; }
+      tail -28 gpurun_out/${TAG}_train.log ;;
+    quick)
+      # the round's new GPU tests first (a fault here stops the script before the long steps)
+      run quick timeout -k 10 300 python -u -m pytest tests/test_gpu_primitives.py -q -x --timeout 200 \
+        --timeout-method thread -k "${QUICK_K:-potrf}" > gpurun_out/${TAG}_quick.log 2>&1 \
+        || { tail -30 gpurun_out/${TAG}_quick.log; exit 1; }
+      tail -3 gpurun_out/${TAG}_quick.log ;;
     n2|n4)
       n=${step#n}
       # never the measured configuration: gloo ranks sharing one GPU, shapes small enough for n ranks per card
