@@ -716,7 +716,7 @@ class DsviEngine:
         # stream right after the minibatch gather (off the main chain)
         pre_planned = set()
         if not elbo_mode:
-            pre_planned = {nm for nm in ("quad", "quad_W", "quad_P", "bwd_wG", "bwd_wP")
+            pre_planned = {nm for nm in ("quad", "quad_W", "bwd_wG", "bwd_wP")
                            if isinstance(p.get(nm), H.GemmGroup) and p[nm].plan is not None}
 
         def gemm(name):
@@ -808,9 +808,10 @@ class DsviEngine:
         steps = []
         # Streams: main (the forward / backward dependency chain), side (variational factors, KL, L-bar, v
         # chain), side2 (t-prior projections, t-row, K_G12, pair quad forms; in the backward the G-prior
-        # adjoint), side3 (pair P-bar and the L0 / L1 prior adjoints).  The step is captured through the HIP
-        # runtime (hip_ops.HipGraph), so side and side2 may wait on each other both ways (round 4: torch's
-        # capture crashed on that ping-pong and the edges were relayed through main).  In a replayed graph
+        # adjoint), side3 (pair P-bar and the L0 / L1 prior adjoints).  side2 and side3 synchronise with the
+        # main stream and one-way with side, never side <-> side2 both ways: hipStreamEndCapture of the HIP
+        # runtime this process runs (torch's bundled ROCm 7.0 libamdhip64) segfaults on such a ping-pong, so
+        # those edges are relayed through main (quad_P plans inline on side2).  In a replayed graph
         # a node's FIRST-created child keeps its hardware queue and every other child starts on another queue
         # behind a cross-queue barrier (10-20 us per hop in the r03 traces), so the critical-path child of each
         # fork is captured first (v after chol, quad_W after projG, bwd_R after bwd_wG, bwd_t1 after tbwd).
@@ -862,8 +863,6 @@ class DsviEngine:
         steps.append(("sig", "side2", "g12"))
         if not elbo_mode:
             # the pair factors W_P = P_{0,1} L_ij need only the L0 / L1 projections: beside the Gibbs chain
-            if "quad_P" in pre_planned:
-                steps.append(("wait", "side2", "plans"))
             steps += [("quad_P", "gemm", gemm("quad_P"), "side2"), ("sig", "side2", "quadP")]
         steps += [
             ("chol_G", "chol", chol_g, "main"),
@@ -950,13 +949,14 @@ class DsviEngine:
             ("bwd_pr_L", "gemm", gemm("bwd_pr_L"), "side3"),
             ("bwd_build_L", "pairwise_bwd", (pw64 if self.p64 else pw)("bwd_build_L"), "side3"),
             ("sig", "side3", "L_done"),
+            # (the KL part of Abar_G reaches side2 through main: the KL branch is long finished when bwd_R is)
+            ("wait", "main", "kl_done"),
             ("sig", "main", "R_G"),
             # G prior: R_G -> the K_G12 builder backward (ell_X adjoints) stays on the main chain; the prior
-            # adjoint Abar_G -= P_G^T R_G (after the KL part of Abar_G: a side -> side2 edge) and the K_G22
-            # builder backward (ell_Z adjoints: the v chain only) run on the second side stream
+            # adjoint Abar_G -= P_G^T R_G and the K_G22 builder backward (ell_Z adjoints: the v chain only) run
+            # on the second side stream
             ("bwd_build12", "pairwise_bwd", pw("bwd_build12"), "main"),
             ("wait", "side2", "R_G"),
-            ("wait", "side2", "kl_done"),
             ("bwd_pr", "gemm", gemm("bwd_pr"), "side2"),
             ("bwd_build22", "pairwise_bwd", pw("bwd_build22"), "side2"),
             ("sig", "side2", "g22"),

@@ -329,7 +329,7 @@ def test_hcp_like_fp64_engine_matches_reference():
     g, eng, grad = _hcp_like_engine(torch.float64)
     errs = _digest_errs(eng, grad, g)
     print("hcp_like fp64 errors", errs)
-    assert errs["loss"] < 1e-9, errs             # measured 6.6e-11
+    assert errs["loss"] < 1e-10, errs            # SURVEY §8c fp64 gate; measured 6.6e-11
     bad = {k: e for k, e in errs.items() if k != "loss" and e > 3e-9}    # measured <= 2.9e-10
     assert not bad, f"fp64 gradient digest mismatch {bad} (all {errs})"
 
