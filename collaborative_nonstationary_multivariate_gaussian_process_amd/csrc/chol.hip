@@ -1801,12 +1801,17 @@ static int potrf_side_ctx(PotrfSide*& out) {
 
 static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 
+// Workspace: [f32: three split-K / stream-K workspaces of the 128x128 kernel (their counters must be zero on
+// entry and are left zero) + the step kernel's flag] [the leaves' inverses X_jj] [f64: the panel staging P].
+// The fixed-size part comes first so that a workspace reused for another n (hip_ops.big_workspace keeps one
+// per device) finds its counters where the previous call left them zero.
+static size_t potrf_fixed_ws(bool f32) { return f32 ? 3 * al256(gemm_big_ws_bytes()) + 256 : 0; }
+
 template <typename T>
 static size_t potrf_blocked_ws(int64_t n) {
   const int64_t nblk = (n + PNB - 1) / PNB;
-  size_t b = al256((size_t)nblk * PNB * PNB * sizeof(T)) + al256((size_t)n * PNB * sizeof(T));
-  if (std::is_same<T, float>::value) b += 3 * al256(gemm_big_ws_bytes()) + 256;   // + step-kernel flag
-  return b;
+  return potrf_fixed_ws(std::is_same<T, float>::value) + al256((size_t)nblk * PNB * PNB * sizeof(T)) +
+         al256((size_t)n * PNB * sizeof(T));
 }
 
 // C(m x nn) = alpha * A(m x k, row stride lda) op(B) + beta * C, op(B)(k, c) = B[c * ldb + k]
@@ -1845,14 +1850,12 @@ constexpr size_t kLeafLds = 88 * 1024;
 static int potrf_two_level_f32(float* A, int n, int64_t lda, int32_t* info, void* ws, hipStream_t s) {
   PotrfSide* ctx = nullptr;
   NMGP_TRY(potrf_side_ctx(ctx));
-  const int nblk = (n + PNB - 1) / PNB;
   char* w = (char*)ws;
-  float* Xd = (float*)w;
-  w += al256((size_t)nblk * PNB * PNB * sizeof(float)) + al256((size_t)n * PNB * sizeof(float));
   void* ws_main = w;
   void* ws_side = w + al256(gemm_big_ws_bytes());
   void* ws_far = w + 2 * al256(gemm_big_ws_bytes());
   int32_t* step_flag = (int32_t*)(w + 3 * al256(gemm_big_ws_bytes()));
+  float* Xd = (float*)(w + potrf_fixed_ws(true));
   bool side_used = false, np_used = false, far_used = false;
   // near strips of the last step, issued after the next leaf
   struct { const float* L; float* C; int m, cols; bool on; } ps{nullptr, nullptr, 0, 0, false};
@@ -1869,6 +1872,27 @@ static int potrf_two_level_f32(float* A, int n, int64_t lda, int32_t* info, void
     side_used = true;
     return NMGP_OK;
   };
+  // The far trailing update of the last finished panel (k = 512), cut into column pieces of about equal
+  // work.  Piece i is issued after the i-th step kernel of the next panel, so it runs beside a leaf (3
+  // workgroups whose CUs it cannot share: kLeafLds) instead of starving the step kernels of CUs -- a whole
+  // update issued at once held every CU in persistent stream-K workgroups while the next step kernels
+  // waited (2.11 ms per M = 4096 factorization in the first measurement of this schedule).
+  struct Piece { const float* L; float* C; int m, cols, k; };
+  Piece far_q[PPW / PNB];
+  int far_n = 0, far_i = 0;
+  bool piece_due = false;               // a piece follows the next leaf
+  struct { const float* L; float* C; int m, cols, k; bool on; } np{nullptr, nullptr, 0, 0, 0, false};
+  auto issue_far_piece = [&]() -> int {
+    piece_due = false;
+    if (far_i >= far_n) return NMGP_OK;
+    const Piece& q = far_q[far_i++];
+    NMGP_HIP_TRY(hipStreamWaitEvent(ctx->side2, ctx->ev_main, 0));
+    NMGP_TRY(pgemm<float>(q.L, lda, q.L, lda, q.C, lda, q.m, q.cols, q.k, NMGP_OUT_LOWER, -1.0, 1.0, ws_far,
+                          ctx->side2));
+    if (far_i == far_n) NMGP_HIP_TRY(hipEventRecord(ctx->ev_far, ctx->side2));
+    far_used = true;
+    return NMGP_OK;
+  };
   for (int c0 = 0; c0 < n; c0 += PPW) {
     const int pw = min(PPW, n - c0), pe = c0 + pw;
     for (int j0 = c0; j0 < pe; j0 += PNB) {
@@ -1877,7 +1901,19 @@ static int potrf_two_level_f32(float* A, int n, int64_t lda, int32_t* info, void
       // the diagonal leaf on the multi-role kernel (factor + two inverse workgroups)
       NMGP_TRY(chol_inv_small<float>(A + (int64_t)j0 * lda + j0, nbj, lda, 0, Xj, PNB, 0, 1, info, s, j0, jb == 0,
                                      true, kLeafLds));
+      // side-stream work that follows the previous main-stream launch is issued after this leaf: in a replayed
+      // graph the first-issued child of a node keeps the node's hardware queue, so the leaf -> step hand-off of
+      // the serial chain stays on one queue (the cross-queue wait moves to the side work)
       NMGP_TRY(issue_strips());
+      if (np.on) {                            // NP_rest: after NP_first, beside this leaf
+        np.on = false;
+        NMGP_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->ev_main, 0));
+        NMGP_TRY(pgemm<float>(np.L, lda, np.L, lda, np.C, lda, np.m, np.cols, np.k, NMGP_OUT_LOWER, -1.0, 1.0,
+                              ws_side, ctx->side));
+        NMGP_HIP_TRY(hipEventRecord(ctx->ev_np, ctx->side));
+        np_used = side_used = true;
+      }
+      if (piece_due) NMGP_TRY(issue_far_piece());
       if (n2 == 0) break;
       float* Lj = A + (int64_t)r0 * lda + j0;   // block column j below the diagonal block
       const int c1 = r0 < pe ? min(PNB, pe - r0) : 0;
@@ -1885,39 +1921,52 @@ static int potrf_two_level_f32(float* A, int n, int64_t lda, int32_t* info, void
       if (c1 > 0 && side_used) NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_side, 0));
       if (c1 > 0 && j0 == c0 && np_used) NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_np, 0));
       NMGP_TRY(potrf_step_f32(Lj, A + (int64_t)r0 * lda + r0, Xj, lda, n2, nbj, c1, step_flag, s));
+      NMGP_HIP_TRY(hipEventRecord(ctx->ev_main, s));
       const int ncols = pe - (r0 + c1);
-      if (ncols > 0 || r0 == pe) NMGP_HIP_TRY(hipEventRecord(ctx->ev_main, s));
       if (ncols > 0)
         ps = {Lj + (int64_t)c1 * lda, A + (int64_t)(r0 + c1) * lda + (r0 + c1), n2 - c1, ncols, true};
-      if (r0 == pe) {
-        // the panel is factored: its 512 columns update the next panel (main + side) and the rest (side2)
-        const float* Lp = A + (int64_t)pe * lda + c0;
-        const int nb1 = min(PNB, n - pe);
-        if (far_used) NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_far, 0));
-        NMGP_TRY(pgemm<float>(Lp, lda, Lp, lda, A + (int64_t)pe * lda + pe, lda, n - pe, nb1, pw, NMGP_OUT_LOWER,
-                              -1.0, 1.0, ws_main, s));
-        const int q0 = pe + nb1, q1 = min(pe + PPW, n);
-        if (q1 > q0) {
-          const float* Lq = Lp + (int64_t)nb1 * lda;
-          NMGP_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->ev_main, 0));
-          if (far_used) NMGP_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->ev_far, 0));
-          NMGP_TRY(pgemm<float>(Lq, lda, Lq, lda, A + (int64_t)q0 * lda + q0, lda, n - q0, q1 - q0, pw,
-                                NMGP_OUT_LOWER, -1.0, 1.0, ws_side, ctx->side));
-          NMGP_HIP_TRY(hipEventRecord(ctx->ev_np, ctx->side));
-          np_used = side_used = true;
-        }
-        if (q1 < n) {
-          const float* Lf = Lp + (int64_t)(q1 - pe) * lda;
-          NMGP_HIP_TRY(hipStreamWaitEvent(ctx->side2, ctx->ev_main, 0));
-          NMGP_TRY(pgemm<float>(Lf, lda, Lf, lda, A + (int64_t)q1 * lda + q1, lda, n - q1, n - q1, pw, NMGP_OUT_LOWER,
-                                -1.0, 1.0, ws_far, ctx->side2));
-          NMGP_HIP_TRY(hipEventRecord(ctx->ev_far, ctx->side2));
-          far_used = true;
+      if (r0 < pe) {
+        piece_due = far_i < far_n;            // beside the next leaf
+        continue;
+      }
+      // the panel is factored: its 512 columns update the next panel (main, then side) and the rest (side2)
+      while (far_i < far_n) NMGP_TRY(issue_far_piece());   // (normally none left: one per step but the last)
+      const float* Lp = A + (int64_t)pe * lda + c0;
+      const int nb1 = min(PNB, n - pe);
+      if (far_used) NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_far, 0));
+      NMGP_TRY(pgemm<float>(Lp, lda, Lp, lda, A + (int64_t)pe * lda + pe, lda, n - pe, nb1, pw, NMGP_OUT_LOWER,
+                            -1.0, 1.0, ws_main, s));
+      const int q0 = pe + nb1, q1 = min(pe + PPW, n);
+      if (q1 > q0) {
+        // NP_rest beside the next leaf, after NP_first (which it would slow down on the critical path)
+        NMGP_HIP_TRY(hipEventRecord(ctx->ev_main, s));
+        const float* Lq = Lp + (int64_t)nb1 * lda;
+        np = {Lq, A + (int64_t)q0 * lda + q0, n - q0, q1 - q0, pw, true};
+      }
+      if (q1 < n) {
+        // the far update A[q1:, q1:] -= L_p L_p^T in pieces of about equal work (column ranges [a, b), rows a..)
+        const int N = n - q1, pieces = max(1, (q1 - pe) / PNB - 1);
+        const double target = 0.5 * (double)N * N / pieces;
+        far_n = far_i = 0;
+        int a = 0;
+        double acc = 0.0;
+        for (int b = 0; b < N;) {
+          const int cw = min(PNB, N - b);
+          acc += (double)cw * (N - b) - 0.5 * cw * cw;
+          b += cw;
+          if ((acc >= target && far_n < pieces - 1) || b == N) {
+            far_q[far_n++] = {Lp + (int64_t)(q1 + a - pe) * lda, A + (int64_t)(q1 + a) * lda + (q1 + a), N - a, b - a,
+                              pw};
+            a = b;
+            acc = 0.0;
+          }
         }
       }
     }
   }
+  while (far_i < far_n) NMGP_TRY(issue_far_piece());
   NMGP_TRY(issue_strips());
+  if (np.on) return NMGP_ERR_LAUNCH;    // (cannot happen: NP_rest exists only when a next panel does)
   if (side_used) {
     NMGP_HIP_TRY(hipEventRecord(ctx->ev_tail, ctx->side));
     NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_tail, 0));
@@ -1934,7 +1983,7 @@ static int potrf_blocked(T* A, int n, int64_t lda, int32_t* info, void* ws, hipS
   PotrfSide* ctx = nullptr;
   NMGP_TRY(potrf_side_ctx(ctx));
   const int nblk = (n + PNB - 1) / PNB;
-  char* w = (char*)ws;
+  char* w = (char*)ws + potrf_fixed_ws(false);
   T* Xd = (T*)w;
   w += al256((size_t)nblk * PNB * PNB * sizeof(T));
   T* P = (T*)w;
