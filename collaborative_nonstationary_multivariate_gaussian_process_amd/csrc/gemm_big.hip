@@ -23,6 +23,14 @@
 
 namespace nmgp {
 
+#ifdef NMGP_BIG_TRACE  // per-workgroup wall-clock phases (tools/big_trace.hip only)
+__device__ unsigned long long* g_big_trace;
+#define BIG_STAMP(i) \
+  if (threadIdx.x == 0) g_big_trace[(blockIdx.x + gridDim.x * blockIdx.y) * 8 + (i)] = wall_clock64()
+#else
+#define BIG_STAMP(i)
+#endif
+
 constexpr int BBM = 128, BBN = 128, BBK = 32, BP = 36;   // tile and LDS pitch (floats, 144 B rows)
 constexpr int BSTAGE = (BBM + BBN) * BP;                  // floats per LDS stage
 constexpr int BSLOT = BBM * BBN;                          // floats per split-K partial tile
@@ -218,6 +226,7 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, float* big_sm
     load(kt0);
     store_lds(big_smem, kt0);
     __syncthreads();
+    BIG_STAMP(1);
     int st = 0;
     const int ko = 16 * (lane >> 5), rl = lane & 31;
     for (int kt = kt0; kt < kt1; kt += BBK) {
@@ -386,6 +395,7 @@ __device__ inline void zero_acc(f32x16 (&acc)[2][2]) {
 template <bool AK, bool BK, int MODE>
 __global__ __launch_bounds__(256, 2) void gemm_big_kernel(BigGemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) float big_smem[];
+  BIG_STAMP(0);
   // XCD-aware block order: hardware places block b on XCD b % 8; give each XCD a contiguous run
   int bid = blockIdx.x;
   const int nb = gridDim.x;
@@ -463,6 +473,7 @@ __global__ __launch_bounds__(256, 2) void gemm_big_kernel(BigGemmArgs g) {
     const int i0 = tm * BBM, j0 = tn * BBN;
     zero_acc(acc);
     big_mainloop<AK, BK, MODE>(g, big_smem, bat, i0, j0, kend, kt0, kt1, acc);
+    BIG_STAMP(2);
     bool store = true;
     if (nparts > 1) {
       const int64_t slot0 = (bat * g.tiles + tile) * (int64_t)S;
@@ -474,9 +485,14 @@ __global__ __launch_bounds__(256, 2) void gemm_big_kernel(BigGemmArgs g) {
       int32_t* ctr = sk ? g.counters + c0 : g.counters + bat * g.tiles + tile;
       store = big_combine(g, me, nparts, ctr, slot_of, acc);
     }
+    BIG_STAMP(3);
     if (store) big_epilogue<MODE>(g, bat, i0, j0, acc);
     it += step;
   }
+#ifdef NMGP_BIG_TRACE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  BIG_STAMP(4);
+#endif
 }
 
 // ------------------------------------------------------------------ blocked potrf: panel + lookahead

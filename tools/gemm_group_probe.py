@@ -2,7 +2,9 @@
 the 64x64 tile kernel and on the latency kernel (same descriptors), each replayed REPS times inside a
 HIP graph so launch overhead is excluded; prints algorithmic GFLOP, us per launch and TF/s.
 
-usage (GPU box): python tools/gemm_group_probe.py [group ...] [--reps 50]
+usage (GPU box): python tools/gemm_group_probe.py [group ...] [--reps 50] [--kt-caps 8,16,32]
+--kt-caps: also time the tile kernel with GemmGroup(kt_cap=c) for each c (split so that no workgroup runs
+more than ~c k-tiles), as "tile_cap<c>" entries.
 Outputs of the groups are scratch here (the probe runs the launches back to back on the same buffers).
 """
 import json
@@ -21,6 +23,9 @@ def main():
     import collaborative_nonstationary_multivariate_gaussian_process_amd.hip_ops as H
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 50
+    caps = ([int(c) for c in sys.argv[sys.argv.index("--kt-caps") + 1].split(",")]
+            if "--kt-caps" in sys.argv else [])
+    args = [a for a in args if not (a[0].isdigit() or a == ",")]
     D, M, B, n = 5, 256, 2000, 2000
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(0)
@@ -45,9 +50,13 @@ def main():
         if args and name not in args:
             continue
         row = {"group": name, "nprob": grp.n, "gflop": round(2.0 * grp.macs(seg_host) / 1e9, 4)}
-        for kern in ("tile", "lat"):
+        for kern in ["tile", "lat"] + [f"tile_cap{c}" for c in caps]:
             try:
-                g2 = H.GemmGroup(list(grp.descs), dev, eng.dt, seg=grp.seg, kernel=kern)
+                descs = [type(d).from_buffer_copy(d) for d in grp.descs]
+                if kern.startswith("tile_cap"):
+                    g2 = H.GemmGroup(descs, dev, eng.dt, seg=grp.seg, kernel="tile", kt_cap=int(kern[8:]))
+                else:
+                    g2 = H.GemmGroup(descs, dev, eng.dt, seg=grp.seg, kernel=kern)
             except ValueError:
                 continue
             with torch.cuda.stream(s):

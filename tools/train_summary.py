@@ -10,7 +10,7 @@ import sys
 
 
 def short(name):
-    nm = name.replace("void ", "").replace("nmgp::", "")
+    nm = name.replace("void ", "").replace("nmgp::", "").replace("(anonymous namespace)::", "")
     return nm.split("(")[0][:90]
 
 
