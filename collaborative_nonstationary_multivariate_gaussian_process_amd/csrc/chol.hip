@@ -1757,29 +1757,27 @@ static int chol_inv_launch(T* A, int64_t n, int64_t lda, int64_t sA, T* X, int64
 // triangle zeroed).  128-wide block columns; the diagonal blocks are the fused register-resident
 // factor + inverse kernel ("leaf"), the panel below a block is L_j = A_j X_jj^T.
 //
-// f32 (the stress configuration, round 4): two levels.  Outer panels of PPW = 512 columns are factored
-// right-looking at 128-column granularity with every update kept INSIDE the panel; the panel's 512
-// columns then update the rest of the matrix in k = 512 products on the 128x128 MFMA kernel (a k = 128
-// trailing SYRK per block step ran at 12-28% MFMA-busy; at k = 512 the kernel's k loop amortises its
-// tile loads).  Per outer panel p (columns [c0, pe), pe = c0 + 512):
-//   main:   for each block j of the panel: leaf(j) -> step(j) = panel rows of block j + lookahead of
-//           block column j+1 when it lies inside the panel (potrf_step32_kernel, one launch)
-//   side:   after step(j): the near strips -- the panel's block columns j+2 .. (k = 128, potrf_strip32),
-//           issued after leaf(j+1) so that the leaf -> step hand-off keeps one hardware queue in a graph
-//   after the panel's last step:
-//   main:   NP_first = A[pe:, pe:pe+128] -= L_p[pe:] L_p[pe:pe+128]^T   (k = 512; the next leaf needs it)
-//   side:   NP_rest  = the other three block columns of panel p+1       (k = 512; beside that leaf)
-//   side2:  far SYRK = A[pe+512:, pe+512:] -= L_p L_p^T, lower tiles     (k = 512; a whole panel of slack)
-// Ordering: the step kernel that writes a column waits for the side stream's last writer of it (strip
-// or NP_rest); NP(p) waits for the far SYRK of panel p-1 (which wrote panel p+1's columns).
+// f32 (the stress configuration): right-looking, lookahead depth 1.  Per block step j:
+//   main:  leaf(j) -> step(j) = L_j = A_j X_jj^T for every row below + A(rows, block column j+1) -= L_j L_{j+1,j}^T
+//          (potrf_step32_kernel, one launch; the next leaf needs only the updated block column j+1)
+//   side:  after leaf(j+1): the strip of block column j+2 (k = 128, potrf_strip32_kernel; the next step kernel
+//          waits for it) and the rest of the trailing SYRK (columns >= j+3, gemm_big), two block steps of slack.
+// Measured and not kept (round 4, profiles/r04a_stress_potrf_two_level_*, profiles/r04d_stress_*):
+//   * two levels -- 512-column outer panels, the panel's updates of the rest of the matrix deferred into k = 512
+//     products: 2.31 ms against 1.51.  A 128 x 128 tile of a k = 512 product takes >= 36 us on one CU
+//     (tools/big_trace.hip), so the next panel's first block column put 38-48 us per panel on the serial chain,
+//     and the deferred products held CUs the step kernels needed;
+//   * the step kernel split into the rows of block j+1 (4 workgroups, on the chain) and the rest (a side
+//     stream): 1.69 ms.  The step kernel is bound by its memory round trips (load, write-through store,
+//     hand-off, read-back, store: 14 us alone), not by its width, so the 4-workgroup launch took as long as the
+//     full one, and 21-24 us beside the side stream's SYRK.
 // f64: one level (round 1): panel and lookahead as two GEMMs on the 64x64 f64 kernel, panel staged
 // through P, the trailing SYRK of step j on the side stream while block j+1 is factored.
 constexpr int PNB = 128;
-constexpr int PPW = 512;
 
 struct PotrfSide {
-  hipStream_t side = nullptr, side2 = nullptr;
-  hipEvent_t ev_main = nullptr, ev_side = nullptr, ev_tail = nullptr, ev_np = nullptr, ev_far = nullptr;
+  hipStream_t side = nullptr;
+  hipEvent_t ev_main = nullptr, ev_side = nullptr, ev_tail = nullptr;
 };
 
 static int potrf_side_ctx(PotrfSide*& out) {
@@ -1791,8 +1789,7 @@ static int potrf_side_ctx(PotrfSide*& out) {
   PotrfSide& c = ctx[dev];
   if (c.side == nullptr) {
     if (hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking) != hipSuccess) return NMGP_ERR_LAUNCH;
-    if (hipStreamCreateWithFlags(&c.side2, hipStreamNonBlocking) != hipSuccess) return NMGP_ERR_LAUNCH;
-    for (hipEvent_t* e : {&c.ev_main, &c.ev_side, &c.ev_tail, &c.ev_np, &c.ev_far})
+    for (hipEvent_t* e : {&c.ev_main, &c.ev_side, &c.ev_tail})
       if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return NMGP_ERR_LAUNCH;
   }
   out = &c;
@@ -1847,131 +1844,58 @@ constexpr size_t kLeafLds = 88 * 1024;
     if (rc_ != NMGP_OK) return rc_;    \
   } while (0)
 
-static int potrf_two_level_f32(float* A, int n, int64_t lda, int32_t* info, void* ws, hipStream_t s) {
+static int potrf_one_level_f32(float* A, int n, int64_t lda, int32_t* info, void* ws, hipStream_t s) {
   PotrfSide* ctx = nullptr;
   NMGP_TRY(potrf_side_ctx(ctx));
   char* w = (char*)ws;
-  void* ws_main = w;
   void* ws_side = w + al256(gemm_big_ws_bytes());
-  void* ws_far = w + 2 * al256(gemm_big_ws_bytes());
   int32_t* step_flag = (int32_t*)(w + 3 * al256(gemm_big_ws_bytes()));
   float* Xd = (float*)(w + potrf_fixed_ws(true));
-  bool side_used = false, np_used = false, far_used = false;
-  // near strips of the last step, issued after the next leaf
-  struct { const float* L; float* C; int m, cols; bool on; } ps{nullptr, nullptr, 0, 0, false};
-  auto issue_strips = [&]() -> int {
-    if (!ps.on) return NMGP_OK;
-    ps.on = false;
+  const int nblk = (n + PNB - 1) / PNB;
+  bool side_used = false;
+  // the trailing update of step j, issued after the leaf of step j+1 (see below)
+  struct { const float* Lb; float* C; int n3; bool on; } pend{nullptr, nullptr, 0, false};
+  auto issue_update = [&]() -> int {
+    if (!pend.on) return NMGP_OK;
+    pend.on = false;
     NMGP_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->ev_main, 0));
-    for (int c = 0; c < ps.cols; c += PNB) {
-      const int cw = min(PNB, ps.cols - c);
-      NMGP_TRY(potrf_strip_f32(ps.L + (int64_t)c * lda, ps.C + (int64_t)c * lda + c, lda, ps.m - c, cw, ctx->side));
-      // the next step kernel's lookahead writes the first strip column: it waits for that one only
-      if (c == 0) NMGP_HIP_TRY(hipEventRecord(ctx->ev_side, ctx->side));
+    // block column j+2 first (the next step kernel's lookahead writes it and waits for this strip only), then
+    // the rest of the trailing SYRK (columns >= j+3), which the step after next waits for
+    const int cs = min(PNB, pend.n3), n4 = pend.n3 - cs;
+    NMGP_TRY(potrf_strip_f32(pend.Lb, pend.C, lda, pend.n3, cs, ctx->side));
+    NMGP_HIP_TRY(hipEventRecord(ctx->ev_side, ctx->side));
+    if (n4 > 0) {
+      const float* Lb2 = pend.Lb + (int64_t)cs * lda;
+      NMGP_TRY(pgemm<float>(Lb2, lda, Lb2, lda, pend.C + (int64_t)cs * lda + cs, lda, n4, n4, PNB, NMGP_OUT_LOWER,
+                            -1.0, 1.0, ws_side, ctx->side));
     }
+    NMGP_HIP_TRY(hipEventRecord(ctx->ev_tail, ctx->side));
     side_used = true;
     return NMGP_OK;
   };
-  // The far trailing update of the last finished panel (k = 512), cut into column pieces of about equal
-  // work.  Piece i is issued after the i-th step kernel of the next panel, so it runs beside a leaf (3
-  // workgroups whose CUs it cannot share: kLeafLds) instead of starving the step kernels of CUs -- a whole
-  // update issued at once held every CU in persistent stream-K workgroups while the next step kernels
-  // waited (2.11 ms per M = 4096 factorization in the first measurement of this schedule).
-  struct Piece { const float* L; float* C; int m, cols, k; };
-  Piece far_q[PPW / PNB];
-  int far_n = 0, far_i = 0;
-  bool piece_due = false;               // a piece follows the next leaf
-  struct { const float* L; float* C; int m, cols, k; bool on; } np{nullptr, nullptr, 0, 0, 0, false};
-  auto issue_far_piece = [&]() -> int {
-    piece_due = false;
-    if (far_i >= far_n) return NMGP_OK;
-    const Piece& q = far_q[far_i++];
-    NMGP_HIP_TRY(hipStreamWaitEvent(ctx->side2, ctx->ev_main, 0));
-    NMGP_TRY(pgemm<float>(q.L, lda, q.L, lda, q.C, lda, q.m, q.cols, q.k, NMGP_OUT_LOWER, -1.0, 1.0, ws_far,
-                          ctx->side2));
-    if (far_i == far_n) NMGP_HIP_TRY(hipEventRecord(ctx->ev_far, ctx->side2));
-    far_used = true;
-    return NMGP_OK;
-  };
-  for (int c0 = 0; c0 < n; c0 += PPW) {
-    const int pw = min(PPW, n - c0), pe = c0 + pw;
-    for (int j0 = c0; j0 < pe; j0 += PNB) {
-      const int jb = j0 / PNB, nbj = min(PNB, n - j0), r0 = j0 + nbj, n2 = n - r0;
-      float* Xj = Xd + (int64_t)jb * PNB * PNB;
-      // the diagonal leaf on the multi-role kernel (factor + two inverse workgroups)
-      NMGP_TRY(chol_inv_small<float>(A + (int64_t)j0 * lda + j0, nbj, lda, 0, Xj, PNB, 0, 1, info, s, j0, jb == 0,
-                                     true, kLeafLds));
-      // side-stream work that follows the previous main-stream launch is issued after this leaf: in a replayed
-      // graph the first-issued child of a node keeps the node's hardware queue, so the leaf -> step hand-off of
-      // the serial chain stays on one queue (the cross-queue wait moves to the side work)
-      NMGP_TRY(issue_strips());
-      if (np.on) {                            // NP_rest: after NP_first, beside this leaf
-        np.on = false;
-        NMGP_HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->ev_main, 0));
-        NMGP_TRY(pgemm<float>(np.L, lda, np.L, lda, np.C, lda, np.m, np.cols, np.k, NMGP_OUT_LOWER, -1.0, 1.0,
-                              ws_side, ctx->side));
-        NMGP_HIP_TRY(hipEventRecord(ctx->ev_np, ctx->side));
-        np_used = side_used = true;
-      }
-      if (piece_due) NMGP_TRY(issue_far_piece());
-      if (n2 == 0) break;
-      float* Lj = A + (int64_t)r0 * lda + j0;   // block column j below the diagonal block
-      const int c1 = r0 < pe ? min(PNB, pe - r0) : 0;
-      // the last side-stream writer of block column j+1: the strip of step j-1, or NP_rest of the last panel
-      if (c1 > 0 && side_used) NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_side, 0));
-      if (c1 > 0 && j0 == c0 && np_used) NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_np, 0));
-      NMGP_TRY(potrf_step_f32(Lj, A + (int64_t)r0 * lda + r0, Xj, lda, n2, nbj, c1, step_flag, s));
+  for (int jb = 0; jb < nblk; ++jb) {
+    const int j0 = jb * PNB, nbj = min(PNB, n - j0), r0 = j0 + nbj, n2 = n - r0;
+    float* Xj = Xd + (int64_t)jb * PNB * PNB;
+    // the diagonal leaf on the multi-role kernel (factor + two inverse workgroups)
+    NMGP_TRY(chol_inv_small<float>(A + (int64_t)j0 * lda + j0, nbj, lda, 0, Xj, PNB, 0, 1, info, s, j0, jb == 0, true,
+                                   kLeafLds));
+    // the previous step's trailing update follows the previous step kernel like this leaf does; issued after the
+    // leaf, because in a replayed graph the first-issued child of a node keeps the node's hardware queue, so the
+    // leaf -> step hand-off of the serial chain stays on one queue (the cross-queue wait moves to the update)
+    NMGP_TRY(issue_update());
+    if (n2 == 0) break;
+    float* Lj = A + (int64_t)r0 * lda + j0;   // block column j below the diagonal block
+    const int c1 = min(PNB, n2), n3 = n2 - c1;
+    // panel + lookahead of block column j+1 in one launch; the strip of step j-1 wrote that column
+    if (side_used) NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_side, 0));
+    NMGP_TRY(potrf_step_f32(Lj, A + (int64_t)r0 * lda + r0, Xj, lda, n2, nbj, c1, step_flag, s));
+    if (n3 > 0) {
       NMGP_HIP_TRY(hipEventRecord(ctx->ev_main, s));
-      const int ncols = pe - (r0 + c1);
-      if (ncols > 0)
-        ps = {Lj + (int64_t)c1 * lda, A + (int64_t)(r0 + c1) * lda + (r0 + c1), n2 - c1, ncols, true};
-      if (r0 < pe) {
-        piece_due = far_i < far_n;            // beside the next leaf
-        continue;
-      }
-      // the panel is factored: its 512 columns update the next panel (main, then side) and the rest (side2)
-      while (far_i < far_n) NMGP_TRY(issue_far_piece());   // (normally none left: one per step but the last)
-      const float* Lp = A + (int64_t)pe * lda + c0;
-      const int nb1 = min(PNB, n - pe);
-      if (far_used) NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_far, 0));
-      NMGP_TRY(pgemm<float>(Lp, lda, Lp, lda, A + (int64_t)pe * lda + pe, lda, n - pe, nb1, pw, NMGP_OUT_LOWER,
-                            -1.0, 1.0, ws_main, s));
-      const int q0 = pe + nb1, q1 = min(pe + PPW, n);
-      if (q1 > q0) {
-        // NP_rest beside the next leaf, after NP_first (which it would slow down on the critical path)
-        NMGP_HIP_TRY(hipEventRecord(ctx->ev_main, s));
-        const float* Lq = Lp + (int64_t)nb1 * lda;
-        np = {Lq, A + (int64_t)q0 * lda + q0, n - q0, q1 - q0, pw, true};
-      }
-      if (q1 < n) {
-        // the far update A[q1:, q1:] -= L_p L_p^T in pieces of about equal work (column ranges [a, b), rows a..)
-        const int N = n - q1, pieces = max(1, (q1 - pe) / PNB - 1);
-        const double target = 0.5 * (double)N * N / pieces;
-        far_n = far_i = 0;
-        int a = 0;
-        double acc = 0.0;
-        for (int b = 0; b < N;) {
-          const int cw = min(PNB, N - b);
-          acc += (double)cw * (N - b) - 0.5 * cw * cw;
-          b += cw;
-          if ((acc >= target && far_n < pieces - 1) || b == N) {
-            far_q[far_n++] = {Lp + (int64_t)(q1 + a - pe) * lda, A + (int64_t)(q1 + a) * lda + (q1 + a), N - a, b - a,
-                              pw};
-            a = b;
-            acc = 0.0;
-          }
-        }
-      }
+      pend = {Lj + (int64_t)c1 * lda, A + (int64_t)(r0 + c1) * lda + (r0 + c1), n3, true};
     }
   }
-  while (far_i < far_n) NMGP_TRY(issue_far_piece());
-  NMGP_TRY(issue_strips());
-  if (np.on) return NMGP_ERR_LAUNCH;    // (cannot happen: NP_rest exists only when a next panel does)
-  if (side_used) {
-    NMGP_HIP_TRY(hipEventRecord(ctx->ev_tail, ctx->side));
-    NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_tail, 0));
-  }
-  if (far_used) NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_far, 0));
+  NMGP_TRY(issue_update());
+  if (side_used) NMGP_HIP_TRY(hipStreamWaitEvent(s, ctx->ev_tail, 0));
   hipLaunchKernelGGL(zero_upper_kernel<float>, dim3((unsigned)n), dim3(256), 0, s, A, n, lda);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
@@ -1979,7 +1903,7 @@ static int potrf_two_level_f32(float* A, int n, int64_t lda, int32_t* info, void
 
 template <typename T>
 static int potrf_blocked(T* A, int n, int64_t lda, int32_t* info, void* ws, hipStream_t s) {
-  if constexpr (std::is_same<T, float>::value) return potrf_two_level_f32(A, n, lda, info, ws, s);
+  if constexpr (std::is_same<T, float>::value) return potrf_one_level_f32(A, n, lda, info, ws, s);
   PotrfSide* ctx = nullptr;
   NMGP_TRY(potrf_side_ctx(ctx));
   const int nblk = (n + PNB - 1) / PNB;

@@ -296,6 +296,41 @@ __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S,
   __syncthreads();   // s_last is reused by the next tile of a stream-K workgroup
   if (!last) return false;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint32_t off = (uint32_t)(t * 64 * 4);
+  if (S <= 4) {
+    // per half-tile (acc[a][*]) all S partials -- this workgroup's own as stored above -- are loaded at once and
+    // then summed in contributor order: two memory round trips instead of S - 1 (the same sums, bit for bit)
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      u32x4g v[4][8];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (c >= S) continue;
+        const __amdgpu_buffer_rsrc_t rws = make_rsrc(g.ws + (int64_t)slot_of(c) * BSLOT, (int64_t)BSLOT * 4);
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            v[c][b * 4 + q] = __builtin_amdgcn_raw_buffer_load_b128(rws, off + ((a * 2 + b) * 4 + q) * 16, 0, 16);
+      }
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        f32x16 sum;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sum[r] = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (c >= S) continue;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sum[4 * q + e] += __uint_as_float(v[c][b * 4 + q][e]);
+        }
+        acc[a][b] = sum;
+      }
+    }
+    return true;
+  }
   f32x16 sum[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -312,7 +347,6 @@ __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S,
       continue;
     }
     const __amdgpu_buffer_rsrc_t rws = make_rsrc(g.ws + (int64_t)slot_of(c) * BSLOT, (int64_t)BSLOT * 4);
-    const uint32_t off = (uint32_t)(t * 64 * 4);
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -331,10 +365,8 @@ __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S,
   return true;
 }
 
-// C = alpha * acc + beta * C (+ diag_add, + the KL epilogue) on the stored part of the tile.  With
-// beta != 0 the 16 C values of one accumulator block are loaded together before its stores (4 round
-// trips per tile instead of 64 serialized load->store pairs: the compiler cannot move a C load above
-// a C store it may alias), which also keeps the epilogue within the 2-waves/SIMD register budget.
+// C = alpha * acc + beta * C (+ diag_add, + the KL epilogue) on the stored part of the tile.  The C loads are
+// issued together before any store (the compiler cannot move a C load above a C store it may alias).
 template <int MODE>
 __device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, int i0, int j0, f32x16 (&acc)[2][2]) {
   const int t = threadIdx.x, lane = t & 63;
@@ -347,6 +379,26 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, 
   const bool eLo = g.flags & NMGP_EPI_E_LOWER;
   const float* Eb = EPI ? g.E + (g.offE ? g.offE[bat] : 0) : nullptr;
   const float* rs = EPI ? g.RS + (g.offRS ? g.offRS[bat] : 0) : nullptr;
+  // with beta != 0 all 64 C values of the thread are loaded before the first store: one memory round trip per
+  // tile (per accumulator block, the compiler kept 4 dependent load -> store rounds: 6.4 us of a 36 us k = 512
+  // tile, tools/big_trace.hip)
+  f32x16 cv[2][2];
+  if (g.beta != 0.0f) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int ib = i0 + 64 * wr + 32 * a + 4 * (lane >> 5);
+        const int j = j0 + 64 * wc + 32 * b + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int i = ib + (r & 3) + 8 * (r >> 2);
+          // (elements that OUT_TRIL zeroes are not read: a third of C's traffic in the batched L-bar forms)
+          const bool ok = i < g.m && j < g.n && (!lower || j <= i) && !(tril && j > i);
+          cv[a][b][r] = ok ? __builtin_nontemporal_load(Cb + (int64_t)i * g.sCi + (int64_t)j * g.sCj) : 0.0f;
+        }
+      }
+  }
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -354,17 +406,7 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, 
       const int ib = i0 + 64 * wr + 32 * a + 4 * (lane >> 5);
       const int j = j0 + 64 * wc + 32 * b + (lane & 31);
       f32x16 v = acc[a][b] * g.alpha;
-      if (g.beta != 0.0f) {
-        f32x16 cv;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int i = ib + (r & 3) + 8 * (r >> 2);
-          // (elements that OUT_TRIL zeroes are not read: a third of C's traffic in the batched L-bar forms)
-          const bool ok = i < g.m && j < g.n && (!lower || j <= i) && !(tril && j > i);
-          cv[r] = ok ? __builtin_nontemporal_load(Cb + (int64_t)i * g.sCi + (int64_t)j * g.sCj) : 0.0f;
-        }
-        v += g.beta * cv;
-      }
+      if (g.beta != 0.0f) v += g.beta * cv[a][b];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = ib + (r & 3) + 8 * (r >> 2);
