@@ -291,22 +291,14 @@ def elbo_sharded(dev, world, rank, dist, D=128, M=1024, rows=391, samples=64):
 FP32_MFMA_PEAK_TFLOPS = 157.3         # MI355X dense FP32 matrix peak (spec)
 
 
-def graph_train(dev, cfg, steps, warmup=2):
-    """A training configuration of BASELINE.json beside the headline (one GPU, fp32, graph-replayed steps,
-    the epoch's minibatches resident in HBM, device Philox noise, Adam inside the graph):
-      hcp  configs[2]: D=50 outputs x 10,000 timepoints (500k rows), M=512, B=5000, length scales 3/M;
-      ecog configs[3]: D=128 channels x 391 rows (N=50,048), M=1024, B=512, length scales 3/M.
-    Packed pair layout (the pairs are initialised on the device; HCP's dense layout runs the same kernels
-    at the same speed).  Step TFLOP/s uses SURVEY §8d's algorithmic forward FLOPs x 3 (backward ~ 2x
-    forward): HCP 263 GFLOP, ECoG 6.15 TFLOP forward per step."""
-    import gc
+def train_setup(dev, cfg):
+    """Model, trainer and engine of one fp32 training configuration (graph_train below; tools/gemm_group_probe.py
+    --cfg): synthetic rows, the epoch's minibatches bound in HBM (device gather + Philox noise per step)."""
     from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP, DsviTrainer
-    Dc, n, Mc, Bc, fwd_gflop = {"hcp": (50, 10000, 512, 5000, 263.0), "ecog": (128, 391, 1024, 512, 6150.0)}[cfg]
+    Dc, n, Mc, Bc, fwd_gflop = TRAIN_CFGS[cfg]
     rng = np.random.default_rng(2024)
     xs = [np.arange(n) / n if cfg == "hcp" else np.sort(rng.uniform(0, 1, n)) for _ in range(Dc)]
     ys = [np.sin(6 * x + 0.1 * d) + 0.3 * rng.standard_normal(n) for d, x in enumerate(xs)]
-    torch.cuda.reset_peak_memory_stats(dev)
-    t0 = time.time()
     m = NMGP(number_observations=Dc * n, dim_outputs=Dc, Z=np.linspace(0, 1, Mc), minibatch_size=Bc, seed=22,
              device=dev, noise="device", dtype=torch.float32, pair_layout="packed")
     for k in ["length_scales_tildeell_log", "length_scales_L0_log", "length_scales_L1_log"]:
@@ -325,6 +317,60 @@ def graph_train(dev, cfg, steps, warmup=2):
         bs.append(np.concatenate([[0], np.cumsum(np.bincount(I[idx], minlength=Dc))]))
     f = lambda a, t: torch.tensor(np.stack(a), dtype=t, device=dev)
     eng.bind_dataset(f(bx, torch.float32), f(by, torch.float32), f(bi, torch.int32), f(bs, torch.int32))
+    return m, tr, eng
+
+
+TRAIN_CFGS = {"hcp": (50, 10000, 512, 5000, 263.0), "ecog": (128, 391, 1024, 512, 6150.0)}
+
+
+def train_roofline(eng, cfg):
+    """The dominant kernel of an fp32 training step (BASELINE configs[2] / [3]) against the fp32 MFMA peak: the
+    grouped 64x64 tile GEMM (gemm_kernel<float, true>; the committed rocprofv3 breakdown of the graphed step,
+    profiles/r*_{cfg}_train_kernels.json from tools/train_trace.sh, names it).  Algorithmic flops per step = 2 m n k
+    over the descriptors of every group the engine runs on that kernel (triangular zeros and skipped output
+    halves not counted, row segments of this minibatch); divided by the kernel's busy time per step in the
+    profile (sum of its launch durations)."""
+    import glob
+    seg_host = eng.seg.cpu().numpy()
+    gf, n, names = 0.0, 0, []
+    for nm, grp in eng.gemm_groups():
+        parts = grp.parts if hasattr(grp, "parts") else [grp]
+        for p_ in parts:
+            if hasattr(p_, "macs") and not getattr(p_, "lat", False) and p_.dtype == torch.float32:
+                gf += 2.0 * p_.macs(seg_host) / 1e9
+                n += 1
+                names.append(nm)
+    out = {"kernel": "gemm_kernel<float, true> (grouped 64x64 MFMA f32 GEMM)", "bound": "mfma",
+           "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "algorithmic_gflop_per_step": round(gf, 3),
+           "launches_per_step": n, "groups": sorted(set(names)), "traffic": None}
+    profs = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{cfg}_train_kernels.json")))
+    if profs:
+        rows = json.load(open(profs[-1]))["kernels"]
+        k = [r for r in rows if r["kernel"].startswith("gemm_kernel<float, true>")]
+        if k:
+            ms = k[0]["ms_per_step"]
+            ach = gf / ms                                   # GFLOP / ms = TFLOP/s
+            out.update({"profile_ms_per_step": ms, "profile_launches_per_step": k[0]["launches_per_step"],
+                        "profile_share_of_busy": k[0]["share_of_busy"], "achieved": round(ach, 3),
+                        "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                        "timing": "rocprofv3 --kernel-trace busy time of the kernel per graphed step, "
+                                  + os.path.relpath(profs[-1], ROOT)})
+    return out
+
+
+def graph_train(dev, cfg, steps, warmup=2):
+    """A training configuration of BASELINE.json beside the headline (one GPU, fp32, graph-replayed steps,
+    the epoch's minibatches resident in HBM, device Philox noise, Adam inside the graph):
+      hcp  configs[2]: D=50 outputs x 10,000 timepoints (500k rows), M=512, B=5000, length scales 3/M;
+      ecog configs[3]: D=128 channels x 391 rows (N=50,048), M=1024, B=512, length scales 3/M.
+    Packed pair layout (the pairs are initialised on the device; HCP's dense layout runs the same kernels
+    at the same speed).  Step TFLOP/s uses SURVEY §8d's algorithmic forward FLOPs x 3 (backward ~ 2x
+    forward): HCP 263 GFLOP, ECoG 6.15 TFLOP forward per step."""
+    import gc
+    Dc, n, Mc, Bc, fwd_gflop = TRAIN_CFGS[cfg]
+    torch.cuda.reset_peak_memory_stats(dev)
+    t0 = time.time()
+    m, tr, eng = train_setup(dev, cfg)
     g = tr.capture(eng, include_update=True)
     t_setup = time.time() - t0
     for _ in range(warmup):
@@ -339,6 +385,7 @@ def graph_train(dev, cfg, steps, warmup=2):
     m.check_numerics()
     loss = float(eng.out[0])
     tf = 3.0 * fwd_gflop / 1e3 / el
+    roof = train_roofline(eng, cfg)
     out = {"workload": f"{cfg.upper()}-shaped training step (BASELINE.json configs[{2 if cfg == 'hcp' else 3}]): D={Dc}, "
                        f"Q={Dc * (Dc + 1) // 2} pairs, M={Mc}, N={Dc * n}, B={Bc}, fp32, packed pairs, HIP graph",
            "steps": steps, "warmup": warmup, "s_per_step": round(el, 5), "it_per_s": round(1.0 / el, 3),
@@ -348,7 +395,7 @@ def graph_train(dev, cfg, steps, warmup=2):
            "frac_of_fp32_peak": round(tf / FP32_MFMA_PEAK_TFLOPS, 4),
            "flop_convention": "SURVEY §8d: 3 x algorithmic forward FLOPs (backward ~ 2 x forward)",
            "setup_s": round(t_setup, 1), "params": int(m._theta.numel()),
-           "peak_mem_GB": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)}
+           "peak_mem_GB": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1), "roofline": roof}
     del g, tr, eng, m
     gc.collect()
     torch.cuda.empty_cache()
