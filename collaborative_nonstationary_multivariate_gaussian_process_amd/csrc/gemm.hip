@@ -696,19 +696,6 @@ __global__ __launch_bounds__(256) void gemm_plan_kernel(const nmgp_gemm_desc* __
   if (t == 0) dyn_start[nprob] = carry;
 }
 
-// Extra dynamic LDS per workgroup (experiment knob NMGP_GEMM_LDS_RESERVE=bytes, applied to grids of at
-// most NMGP_GEMM_LDS_RESERVE_MAXWG workgroups): reserving LDS forces one workgroup per CU.
-static size_t lds_reserve(int wgs) {
-  static int bytes = -1, maxwg = 0;
-  if (bytes < 0) {
-    const char* e = getenv("NMGP_GEMM_LDS_RESERVE");
-    const char* m = getenv("NMGP_GEMM_LDS_RESERVE_MAXWG");
-    bytes = e ? atoi(e) : 0;
-    maxwg = m ? atoi(m) : 256;
-  }
-  return (bytes > 0 && wgs <= maxwg) ? (size_t)bytes : 0;
-}
-
 // Workgroups of the grouped kernel that are certainly resident at once: CUs x min(occupancy API, 2)
 // (LDS and VGPRs allow two 256-thread workgroups per CU; the API can report one block too many).
 template <typename T>
@@ -741,7 +728,7 @@ static int launch_grouped(const nmgp_gemm_desc* d_desc, int nprob, int total_til
   a.seg = d_seg;
   a.dyn_start = nullptr;
   a.inl = nmgp_gemm_desc{};
-  hipLaunchKernelGGL((gemm_kernel<T, true>), dim3(total_tiles), dim3(256), lds_reserve(total_tiles), s, a, d_desc);
+  hipLaunchKernelGGL((gemm_kernel<T, true>), dim3(total_tiles), dim3(256), 0, s, a, d_desc);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
@@ -768,7 +755,7 @@ static int launch_grouped_dyn(const nmgp_gemm_desc* d_desc, int nprob, int total
   a.seg = d_seg;
   a.dyn_start = d_plan;
   a.inl = nmgp_gemm_desc{};
-  hipLaunchKernelGGL((gemm_kernel<T, true>), dim3(grid), dim3(256), lds_reserve(grid), s, a, d_desc);
+  hipLaunchKernelGGL((gemm_kernel<T, true>), dim3(grid), dim3(256), 0, s, a, d_desc);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }

@@ -406,19 +406,9 @@ int launch_lat(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles, const i
     a.dyn_start = d_plan;
     if (grid > 0) wgs = min(wgs, ((grid + 7) / 8) * 8);   // a multiple of 8 keeps each workgroup on one XCD chunk
   }
-  // launch configuration (experiment knob NMGP_GEMM_LAT_CFG): 2 = 8 waves x 32-wide panels with
-  // registers capped at 128 so two workgroups share a CU (default; PM2.5 step +1% over 1); 1 = the
-  // same at one workgroup per CU.  hip_ops.GemmGroup sizes split-K for 8 waves x 32.
-  static int cfg = -1;
-  if (cfg < 0) {
-    const char* e = getenv("NMGP_GEMM_LAT_CFG");
-    cfg = e ? atoi(e) : 2;
-  }
-  const int32_t* dp = a.dyn_start;
-  if (cfg == 2)
-    hipLaunchKernelGGL((gemm_lat_kernel<T, 8, 32, 4>), dim3(wgs), dim3(512), 0, s, a, d_desc, dp);
-  else
-    hipLaunchKernelGGL((gemm_lat_kernel<T, 8, 32, 2>), dim3(wgs), dim3(512), 0, s, a, d_desc, dp);
+  // 8 waves x 32-wide panels with registers capped at 128 so two workgroups share a CU (round 2: PM2.5 step +1%
+  // over one workgroup per CU).  hip_ops.GemmGroup sizes split-K for 8 waves x 32.
+  hipLaunchKernelGGL((gemm_lat_kernel<T, 8, 32, 4>), dim3(wgs), dim3(512), 0, s, a, d_desc, a.dyn_start);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }

@@ -1,6 +1,6 @@
 """A/B timing of the fused factor+inverse launch (H.chol_inv_) at the DSVI step's shapes (GPU box):
-NMGP_CHOL_4ROLE=1 (four-role kernel: separate update workgroup, chol_inv7_kernel), NMGP_CHOL_LA=1 (lookahead
-factor role, chol_inv4_kernel) and the three-role chol_inv3_kernel.
+NMGP_CHOL_4ROLE=1 (four-role kernel: separate update workgroup, chol_inv7_kernel) and =0 (the three-role
+chol_inv3_kernel).  (The round-3 lookahead variant, chol_inv4_kernel, was removed in round 4.)
 Each variant is captured in a HIP graph of `reps` launches (plus the restore copies, timed separately
 and subtracted).  Usage: python tools/chol_ab.py [n:batch:dtype ...]  (default 256:4:f64 256:1:f64)"""
 import json
@@ -57,10 +57,10 @@ for c in cases:
     n, b, d = c.split(":")
     dt = torch.float64 if d == "f64" else torch.float32
     rec = {"n": int(n), "batch": int(b), "dtype": d}
-    for four, la, tag in (("1", "0", "four_role"), ("0", "1", "la1"), ("0", "0", "la0")):
-        os.environ["NMGP_CHOL_4ROLE"], os.environ["NMGP_CHOL_LA"] = four, la
+    for four, tag in (("1", "four_role"), ("0", "three_role")):
+        os.environ["NMGP_CHOL_4ROLE"] = four
         us, resid, ie = time_one(int(n), int(b), dt)
-        os.environ.pop("NMGP_CHOL_4ROLE"), os.environ.pop("NMGP_CHOL_LA")
+        os.environ.pop("NMGP_CHOL_4ROLE")
         rec[f"{tag}_us"] = round(us, 2)
         rec[f"{tag}_inv_err"] = ie
     print(json.dumps(rec), flush=True)

@@ -6,6 +6,10 @@
 // main loop, end of split-K publish, end -- summarised as spreads over the grid.
 #include "gemm.hip"
 
+#ifndef TT
+#define TT double   // -DTT=float: the f32 kernel
+#endif
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -16,17 +20,17 @@ int main(int argc, char** argv) {
   const int ks = argc > 4 ? atoi(argv[4]) : 1;
   const int transA = argc > 5 ? atoi(argv[5]) : 0;
   const int nprob = argc > 6 ? atoi(argv[6]) : 1;   // copies of the problem in one grouped launch
-  double *A, *B, *C, *ws;
+  TT *A, *B, *C, *ws;
   int32_t* ctr;
   const int tm = (m + 63) / 64, tn = (n + 63) / 64, nblk1 = tm * tn * ks, nblk = nblk1 * nprob;
-  hipMalloc(&A, (size_t)m * k * 8);
-  hipMalloc(&B, (size_t)k * n * 8);
-  hipMalloc(&C, (size_t)m * n * 8);
-  hipMalloc(&ws, (size_t)tm * tn * ks * 4096 * 8 * nprob);
+  hipMalloc(&A, (size_t)m * k * sizeof(TT));
+  hipMalloc(&B, (size_t)k * n * sizeof(TT));
+  hipMalloc(&C, (size_t)m * n * sizeof(TT));
+  hipMalloc(&ws, (size_t)tm * tn * ks * 4096 * sizeof(TT) * nprob);
   hipMalloc(&ctr, (size_t)tm * tn * 4 * nprob);
   hipMemset(ctr, 0, (size_t)tm * tn * 4 * nprob);
-  hipMemset(A, 0, (size_t)m * k * 8);
-  hipMemset(B, 0, (size_t)k * n * 8);
+  hipMemset(A, 0, (size_t)m * k * sizeof(TT));
+  hipMemset(B, 0, (size_t)k * n * sizeof(TT));
   const int NT = 1024 + 4 * nblk;
   unsigned long long* tr;
   hipMalloc(&tr, NT * 8);
@@ -52,9 +56,9 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  for (int r = 0; r < 3; ++r) nmgp::launch_grouped<double>(dd, nprob, nblk, nullptr, 0);
+  for (int r = 0; r < 3; ++r) nmgp::launch_grouped<TT>(dd, nprob, nblk, nullptr, 0);
   hipEventRecord(e0);
-  nmgp::launch_grouped<double>(dd, nprob, nblk, nullptr, 0);
+  nmgp::launch_grouped<TT>(dd, nprob, nblk, nullptr, 0);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms;
@@ -63,7 +67,7 @@ int main(int argc, char** argv) {
   {
     // untraced: average of 20 back-to-back launches
     hipEventRecord(e0);
-    for (int r = 0; r < 20; ++r) nmgp::launch_grouped<double>(dd, nprob, nblk, nullptr, 0);
+    for (int r = 0; r < 20; ++r) nmgp::launch_grouped<TT>(dd, nprob, nblk, nullptr, 0);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms20;
