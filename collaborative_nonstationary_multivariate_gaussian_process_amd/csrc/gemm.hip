@@ -79,10 +79,12 @@ __device__ inline void mma_tile(const T* As, const T* Bs, int lane, int wr, int 
                                 Acc& c11, const Stage& stage = Stage()) {
   const T* pa = As + (lane >> 4) * LP + wr * 32 + (lane & 15);
   const T* pb = Bs + (lane >> 4) * LP + wc * 32 + (lane & 15);
-  // fragments of k-steps s and s+1 in registers; step s+2 is read while step s multiplies
-  T f[2][4];
+  // fragments of k-steps s .. s+PF-1 in registers; step s+PF is read while step s multiplies (round 4: PF 2 -> 3,
+  // the LDS latency of a fragment read outlasted one 4-MFMA step behind the staging writes)
+  constexpr int PF = 3;
+  T f[PF][4];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < PF; ++u) {
     const int o = u * 4 * LP;
     f[u][0] = pa[o];
     f[u][1] = pa[o + 16];
@@ -91,10 +93,10 @@ __device__ inline void mma_tile(const T* As, const T* Bs, int lane, int wr, int 
   }
 #pragma unroll
   for (int s = 0; s < GBK / 4; ++s) {
-    const int u = s & 1;
+    const int u = s % PF;
     const T a0 = f[u][0], a1 = f[u][1], b0 = f[u][2], b1 = f[u][3];
-    if (s + 2 < GBK / 4) {
-      const int o = (s + 2) * 4 * LP;
+    if (s + PF < GBK / 4) {
+      const int o = (s + PF) * 4 * LP;
       f[u][0] = pa[o];
       f[u][1] = pa[o + 16];
       f[u][2] = pb[o];
