@@ -1001,6 +1001,44 @@ static int convert_launch(const S* src, D* dst, int64_t n, hipStream_t s) {
   return NMGP_OK;
 }
 
+// ------------------------------------------------------------------------------------ P-bar_G reduction
+// The latent P-bar of the backward (code/nmgp_dsvi.py:227-238 autograd through MGP_mu_sigma2 / MGP_d): the rows of
+// output i receive sum_{d <= i} W-hat_d L_d^T.  The engine forms each factor's product once for all rows that use
+// it, Z_d = W-hat_d[rows of outputs >= d] L_d^T (one grouped GEMM, k = M), and this kernel adds, per row r of
+// output i, Z_0[r] + Z_1[r] + ... + Z_i[r] (in d order) onto P[r] -- instead of one k = (i + 1) M product per
+// output, whose k loop (up to D M) ran on a single workgroup per output tile.  One block per (row, 256 columns).
+template <typename T>
+__global__ __launch_bounds__(256) void pbar_reduce_kernel(const T* __restrict__ Z, int64_t sZ, T* __restrict__ P,
+                                                          int64_t ldp, const int32_t* __restrict__ seg, int D, int M) {
+  const int r = blockIdx.x;
+  const int j = blockIdx.y * 256 + threadIdx.x;
+  if (r >= seg[D] || j >= M) return;
+  int i = 0;                                   // the output of row r: the last d with seg[d] <= r
+  for (int d = 1; d < D; ++d) i = seg[d] <= r ? d : i;
+  T acc = P[(int64_t)r * ldp + j];
+  const T* z = Z + (int64_t)r * M + j;
+  for (int d = 0; d <= i; ++d) acc += z[(int64_t)d * sZ];
+  P[(int64_t)r * ldp + j] = acc;
+}
+
+template <typename T>
+static int pbar_reduce_launch(const T* Z, int64_t sZ, T* P, int64_t ldp, const int32_t* seg, int D, int B, int M,
+                              hipStream_t s) {
+  if (!Z) return -1;
+  if (sZ < (int64_t)B * M) return -2;
+  if (!P) return -3;
+  if (ldp < M) return -4;
+  if (!seg) return -5;
+  if (D <= 0) return -6;
+  if (B < 0) return -7;
+  if (M <= 0) return -8;
+  if (B == 0) return NMGP_OK;
+  hipLaunchKernelGGL(pbar_reduce_kernel<T>, dim3((unsigned)B, (unsigned)((M + 255) / 256)), dim3(256), 0, s, Z, sZ, P,
+                     ldp, seg, D, M);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
+
 // ------------------------------------------------------------------------------------ batch gather
 // One block: every thread reads the batch index first, the copy is grid-strided over the block,
 // then (after a barrier) thread 0 advances the counter for the next step.
@@ -1318,6 +1356,14 @@ int nmgp_convert_f32_to_f64(const float* src, double* dst, int64_t n, hipStream_
 }
 int nmgp_convert_f64_to_f32(const double* src, float* dst, int64_t n, hipStream_t s) {
   return nmgp::convert_launch<double, float>(src, dst, n, s);
+}
+int nmgp_pbar_reduce_f64(const double* Z, int64_t sZ, double* P, int64_t ldp, const int32_t* seg, int D, int B, int M,
+                         hipStream_t s) {
+  return nmgp::pbar_reduce_launch<double>(Z, sZ, P, ldp, seg, D, B, M, s);
+}
+int nmgp_pbar_reduce_f32(const float* Z, int64_t sZ, float* P, int64_t ldp, const int32_t* seg, int D, int B, int M,
+                         hipStream_t s) {
+  return nmgp::pbar_reduce_launch<float>(Z, sZ, P, ldp, seg, D, B, M, s);
 }
 int nmgp_counter_add(int64_t* c, int64_t inc, hipStream_t s) {
   if (!c) return -1;

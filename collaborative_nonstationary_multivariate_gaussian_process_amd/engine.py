@@ -135,6 +135,7 @@ class DsviEngine:
         self.Abar = e(4, M, M)
         self.WG = e(D, B, M)
         self.WP = e(D, B, M)
+        self.Zg = e(D, B, M)            # per-factor P-bar_G products W-hat_d L_d^T (rows of outputs >= d)
         # HCP / ECoG shapes (fp32, M >= 512): the D+Q factor products run on the 128x128 f32 MFMA kernel at
         # per-factor offsets (BigBatch) instead of the grouped 64x64 tiles.  NMGP_BIG_SIDE=0 keeps them on the
         # grouped kernel: the only schedule switch left, for tests/test_gpu_engine.py's equivalence check
@@ -423,10 +424,13 @@ class DsviEngine:
             self._plans[key] = p
             return p
         # B2: P-bar += W-hat L^T ; L-bar = P^T W-hat ; mu-bar = P^T adjoints
-        # rows of output i: P-bar_G += sum_{d <= i} W-hat_d L_d^T (W-hat_d holds only the rows of outputs
-        # >= d, so k runs over the (i + 1) latent blocks that are non-zero there, not all D)
-        d17G = [g(self.Pbar, self.WG, th, B, M, (i + 1) * M, (M, 1, BM), (1, M, MM), (M, 1), flags=L.B_UPPER,
-                  kb=(M, M), beta=1.0, offs=(0, sW, 3 * BM), row_seg=i) for i in range(D)]
+        # rows of output i: P-bar_G += sum_{d <= i} W-hat_d L_d^T.  Round 4: each latent factor's product is formed
+        # once for every row that uses it, Z_d = W-hat_d[rows of outputs >= d] L_d^T (W-hat_d holds only those
+        # rows; k = M per problem, short tiles), and nmgp_pbar_reduce adds Z_0 + ... + Z_i onto each row of output
+        # i.  The round-3 form ran one k = (i + 1) M product per output: at PM2.5 a 40-k-tile loop per output tile
+        # on the main chain (64 us, split-K capped), at ECoG (4 rows per output) up to 4096 k-tiles per tile.
+        d17G = [g(self.Zg, self.WG, th, B, M, M, (M, 1, 0), (1, M, 0), (M, 1), flags=L.B_UPPER,
+                  offs=(d * BM, sW + d * MM, d * BM), row_seg=d, seg_span=D - d) for d in range(D)]
         d17P = []
         for i in range(i0, i1):
             d17P.append(g(self.Pbar, self.WP, th, B, M, M, (M, 1, 0), (1, M, 0), (M, 1), flags=L.B_UPPER,
@@ -439,7 +443,7 @@ class DsviEngine:
         # workgroup in fp64 (output D-1's tiles otherwise run all D latent blocks, 40 k-tiles at PM2.5; round-3
         # A/B on the box: 1370-1379 -> 1386-1400 it/s, profiles/r03za_kt_cap_ab.txt).  fp32 engines keep the
         # automatic split (their gates were measured with it).
-        p["bwd_wG"] = H.GemmGroup(d17G, dev, self.dt, seg=seg, kt_cap=20 if self.dt == torch.float64 else 0)
+        p["bwd_wG"] = G(d17G)
         p["bwd_wP"] = G(d17P) if d17P else None
         d17 = []
         for d in range(D):
@@ -724,6 +728,14 @@ class DsviEngine:
                 return lambda s: p[name](s, planned=True)
             return lambda s: p[name](s)
 
+        pbar_fn = getattr(lib, "nmgp_pbar_reduce_" + self.sfx)
+        esz = self.Pbar.element_size()
+
+        def pbar_reduce(s):
+            # P-bar_G (slot 3) rows += Z_0 + ... + Z_i, i the row's output
+            L.check(pbar_fn(vp(self.Zg.data_ptr()), self.B * M, vp(self.Pbar.data_ptr() + 3 * self.B * M * esz), M,
+                            vp(self.seg.data_ptr()), D, self.B, M, s), "pbar_reduce")
+
         def plans(s):
             for nm in sorted(pre_planned):
                 p[nm].plan_now(s)
@@ -922,6 +934,7 @@ class DsviEngine:
             ("recon", "row", row(getattr(lib, "nmgp_dsvi_recon_" + self.sfx)), "main"),
             ("sig", "main", "recon"),
             ("bwd_wG", "gemm", gemm("bwd_wG"), "main"),
+            ("bwd_wGr", "row", pbar_reduce, "main"),
             ("bwd_R", "gemm", gemm("bwd_R"), "main"),
             # L-bar / mu-bar gradient rows: after the KL L-bar (their first writer, same stream) and recon.
             ("wait", "side", "recon"),

@@ -413,6 +413,14 @@ int nmgp_counter_add(int64_t* counter, int64_t inc, hipStream_t stream);
  * fp32 engines (HCP / ECoG shapes) factor the four GP priors K22 + 1e-4 I in fp64: the fp32
  * explicit-inverse projections K12 (K22 + 1e-4 I)^-1 of code/utils.py:117-119 otherwise lose
  * ~cond(K22) * eps.                                                            */
+/* P-bar_G of the DSVI backward (autograd of code/nmgp_dsvi.py:227-238 through utils.MGP_mu_sigma2,
+ * code/utils.py:128-146): for every row r of output i (rows grouped by output, seg[0..D]),
+ * P[r, :] += Z[0][r, :] + Z[1][r, :] + ... + Z[i][r, :] in that order, where Z[d] = W-hat_d L_d^T (stride sZ
+ * elements between factors, row stride M) was formed for the rows of outputs >= d.  0 or -(argument). */
+int nmgp_pbar_reduce_f64(const double* Z, int64_t sZ, double* P, int64_t ldp, const int32_t* seg, int D, int B, int M,
+                         hipStream_t stream);
+int nmgp_pbar_reduce_f32(const float* Z, int64_t sZ, float* P, int64_t ldp, const int32_t* seg, int D, int B, int M,
+                         hipStream_t stream);
 int nmgp_convert_f32_to_f64(const float* src, double* dst, int64_t n, hipStream_t stream);
 int nmgp_convert_f64_to_f32(const double* src, float* dst, int64_t n, hipStream_t stream);
 /* On-device minibatch pipeline (replaces the host DataLoader + vec2list split of
