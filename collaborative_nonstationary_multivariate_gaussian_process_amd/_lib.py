@@ -168,6 +168,8 @@ _SIGS = {
     "nmgp_counter_add": (c_int, [c_vp, c_i64, c_vp]),
     "nmgp_pbar_reduce_f64": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_vp]),
     "nmgp_pbar_reduce_f32": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_vp]),
+    "nmgp_lbar_reduce_f64": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_vp]),
+    "nmgp_lbar_reduce_f32": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_vp]),
     "nmgp_convert_f32_to_f64": (c_int, [c_vp, c_vp, c_i64, c_vp]),
     "nmgp_convert_f64_to_f32": (c_int, [c_vp, c_vp, c_i64, c_vp]),
     "nmgp_step_begin_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_u64, c_vp, c_vp, c_vp, c_i64, c_vp]),

@@ -1039,6 +1039,66 @@ static int pbar_reduce_launch(const T* Z, int64_t sZ, T* P, int64_t ldp, const i
   return NMGP_OK;
 }
 
+// ------------------------------------------------------------------------------------ L-bar reduction
+// The latent factors' L-bar and mu-bar of the backward (code/nmgp_dsvi.py:198-215 autograd of W = mu + L eps and
+// MGP_d's L-products): factor d collects P_G^T W-hat_d over the rows of every output i >= d.  The engine forms one
+// product per (i, d) over output i's rows only, Y_{i,d} = P_G[rows of i]^T W-hat_d[rows of i] (k = the output's
+// rows: every workgroup of the grouped GEMM runs a short k loop, where one product per d ran k = the rows of
+// outputs d..D-1 on a single workgroup per output tile), and this kernel adds Y_{d,d} + ... + Y_{D-1,d} (in i order)
+// onto factor d's gradient: the lower triangle of an M x M block at gA + d * sA (upper triangle set to 0, as the
+// OUT_TRIL GEMM it replaces) and the M-vector at gB + d * sB.  Slot (i, d) is Y + (first(d) + i - d) * sY, first(d)
+// = sum_{d' < d} (D - d'), matrix first, vector at offset M * M.  Blocks [0, nA) cover the matrices, the rest the
+// vectors; blockIdx.y = d.
+template <typename T>
+__global__ __launch_bounds__(256) void lbar_reduce_kernel(const T* __restrict__ Y, int64_t sY, T* __restrict__ gA,
+                                                          int64_t sA, T* __restrict__ gB, int64_t sB, int D, int M,
+                                                          int nA) {
+  const int d = blockIdx.y;
+  const int64_t first = (int64_t)d * D - (int64_t)d * (d - 1) / 2;
+  const T* y = Y + first * sY;
+  const int64_t MM = (int64_t)M * M;
+  if ((int)blockIdx.x < nA) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= MM) return;
+    const int r = (int)(e / M), c = (int)(e % M);
+    T* o = gA + (int64_t)d * sA + e;
+    if (c > r) {
+      *o = (T)0;
+      return;
+    }
+    T acc = *o;
+    for (int i = d; i < D; ++i) acc += y[(int64_t)(i - d) * sY + e];
+    *o = acc;
+  } else {
+    const int e = ((int)blockIdx.x - nA) * 256 + threadIdx.x;
+    if (e >= M) return;
+    T* o = gB + (int64_t)d * sB + e;
+    T acc = *o;
+    for (int i = d; i < D; ++i) acc += y[(int64_t)(i - d) * sY + MM + e];
+    *o = acc;
+  }
+}
+
+template <typename T>
+static int lbar_reduce_launch(const T* Y, int64_t sY, T* gA, int64_t sA, T* gB, int64_t sB, int D, int M,
+                              hipStream_t s) {
+  if (!Y) return -1;
+  if (sY < (int64_t)M * M + M) return -2;
+  if (!gA) return -3;
+  if (sA < (int64_t)M * M) return -4;
+  if (!gB) return -5;
+  if (sB < M) return -6;
+  if (D <= 0) return -7;
+  if (M <= 0) return -8;
+  const int64_t nA = ((int64_t)M * M + 255) / 256;
+  if (nA > (1 << 30)) return -8;
+  const int nB = (M + 255) / 256;
+  hipLaunchKernelGGL(lbar_reduce_kernel<T>, dim3((unsigned)(nA + nB), (unsigned)D), dim3(256), 0, s, Y, sY, gA, sA, gB,
+                     sB, D, M, (int)nA);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
+
 // ------------------------------------------------------------------------------------ batch gather
 // One block: every thread reads the batch index first, the copy is grid-strided over the block,
 // then (after a barrier) thread 0 advances the counter for the next step.
@@ -1364,6 +1424,14 @@ int nmgp_pbar_reduce_f64(const double* Z, int64_t sZ, double* P, int64_t ldp, co
 int nmgp_pbar_reduce_f32(const float* Z, int64_t sZ, float* P, int64_t ldp, const int32_t* seg, int D, int B, int M,
                          hipStream_t s) {
   return nmgp::pbar_reduce_launch<float>(Z, sZ, P, ldp, seg, D, B, M, s);
+}
+int nmgp_lbar_reduce_f64(const double* Y, int64_t sY, double* gA, int64_t sA, double* gB, int64_t sB, int D, int M,
+                         hipStream_t s) {
+  return nmgp::lbar_reduce_launch<double>(Y, sY, gA, sA, gB, sB, D, M, s);
+}
+int nmgp_lbar_reduce_f32(const float* Y, int64_t sY, float* gA, int64_t sA, float* gB, int64_t sB, int D, int M,
+                         hipStream_t s) {
+  return nmgp::lbar_reduce_launch<float>(Y, sY, gA, sA, gB, sB, D, M, s);
 }
 int nmgp_counter_add(int64_t* c, int64_t inc, hipStream_t s) {
   if (!c) return -1;

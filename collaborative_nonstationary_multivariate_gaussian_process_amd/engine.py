@@ -140,6 +140,12 @@ class DsviEngine:
         # per-factor offsets (BigBatch) instead of the grouped 64x64 tiles.  NMGP_BIG_SIDE=0 keeps them on the
         # grouped kernel: the only schedule switch left, for tests/test_gpu_engine.py's equivalence check
         self.big_side = self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0"
+        # per-(output, factor) L-bar products of the grouped backward (bwd_lbar), summed by nmgp_lbar_reduce: D(D+1)/2
+        # slots of M x M + M.  Only where the slots stay small (PM2.5: 15 slots, 7.9 MB); many outputs with few
+        # rows each (HCP-like D = 50) keep one product per factor, whose k loop is then short anyway
+        nsl = D * (D + 1) // 2
+        self.Ylb = e(nsl * (M * M + M)) if (not self.big_side and nsl * (M * M + M) * self.dt.itemsize
+                                                   <= (64 << 20)) else None
         self.Y = e(D + 1 + 2 * self.NPC, M)
         self.T2 = e(M, M)
         self.v, self.ellZ = e(M), e(M)
@@ -446,11 +452,27 @@ class DsviEngine:
         p["bwd_wG"] = G(d17G)
         p["bwd_wP"] = G(d17P) if d17P else None
         d17 = []
-        for d in range(D):
-            d17.append(g(gr, self.P, self.WG, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_TRIL, beta=1.0,
-                         offs=(3 * BM, d * BM, sW + d * MM), k_seg=d, seg_span=D - d))
-            d17.append(g(gr, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1), beta=1.0,
-                         offs=(3 * BM, d * B, muW + d * M), k_seg=d, seg_span=D - d))
+        if self.Ylb is not None:
+            # round 4: one product per (output i, factor d <= i) over output i's rows into slot (i, d) of Ylb,
+            # summed in i order onto factor d's gradient by nmgp_lbar_reduce -- every workgroup runs a k loop of
+            # one output's rows, where one product per d ran the rows of outputs d..D-1 (at PM2.5 a 32-k-tile loop
+            # per output tile of factor 0: the longest workgroup of the step).  The slots' upper triangles are
+            # never written (OUT_LOWER: no zero tiles); the reduction sets the gradient's upper triangle to 0
+            SY = MM + M
+            for d in range(D):
+                first = d * D - d * (d - 1) // 2
+                for i in range(d, D):
+                    s_ = (first + i - d) * SY
+                    d17.append(g(self.Ylb, self.P, self.WG, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_LOWER,
+                                 offs=(3 * BM, d * BM, s_), k_seg=i))
+                    d17.append(g(self.Ylb, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1),
+                                 offs=(3 * BM, d * B, s_ + MM), k_seg=i))
+        else:
+            for d in range(D):
+                d17.append(g(gr, self.P, self.WG, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_TRIL, beta=1.0,
+                             offs=(3 * BM, d * BM, sW + d * MM), k_seg=d, seg_span=D - d))
+                d17.append(g(gr, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1), beta=1.0,
+                             offs=(3 * BM, d * B, muW + d * M), k_seg=d, seg_span=D - d))
         for (i, j) in pairs:
             typ = 2 if i == j else 1
             d17.append(g(gr, self.P, self.WP, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_TRIL, beta=1.0,
@@ -736,6 +758,14 @@ class DsviEngine:
             L.check(pbar_fn(vp(self.Zg.data_ptr()), self.B * M, vp(self.Pbar.data_ptr() + 3 * self.B * M * esz), M,
                             vp(self.seg.data_ptr()), D, self.B, M, s), "pbar_reduce")
 
+        lbar_fn = getattr(lib, "nmgp_lbar_reduce_" + self.sfx)
+
+        def lbar_reduce(s):
+            # latent L-bar / mu-bar gradient rows += Y_{d,d} + ... + Y_{D-1,d} (bwd_lbar's per-output products)
+            gp = self._grad.data_ptr()
+            L.check(lbar_fn(vp(self.Ylb.data_ptr()), M * M + M, vp(gp + self.offs["sqrt_W"][0] * esz), M * M,
+                            vp(gp + self.offs["mu_W"][0] * esz), M, D, M, s), "lbar_reduce")
+
         def plans(s):
             for nm in sorted(pre_planned):
                 p[nm].plan_now(s)
@@ -940,9 +970,14 @@ class DsviEngine:
             ("wait", "side", "recon"),
             # the recon row partials and the KL slabs summed here, off the main chain (finalize adds them)
             ("prefinal", "row", row(getattr(lib, "nmgp_dsvi_prefinal_" + self.sfx)), "side"),
-            ("bwd_lbar", "gemm", gemm("bwd_lbar"), "side"),
-            ("sig", "side", "lbar_done"),
         ]
+        lbar_steps = [("bwd_lbar", "gemm", gemm("bwd_lbar"), "side")]
+        if self.Ylb is not None:
+            lbar_steps.append(("bwd_lbr", "row", lbar_reduce, "side"))
+        lbar_steps.append(("sig", "side", "lbar_done"))
+        # (bwd_lbar after R_G instead, so that it does not compete with the P-bar_G -> R_G chain for CUs: 1380 ->
+        # 1270 it/s, profiles/r04s_lbar_per_output_ab.txt)
+        steps += lbar_steps
         BM = self.B * M
         # the pair P-bar_0/1 products start on the third side stream right after recon (beside bwd_wG), then --
         # with the KL parts of A-bar_0/1 (kl_done, a one-way side -> side3 edge) -- the L0 / L1 prior adjoints

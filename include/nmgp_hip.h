@@ -421,6 +421,15 @@ int nmgp_pbar_reduce_f64(const double* Z, int64_t sZ, double* P, int64_t ldp, co
                          hipStream_t stream);
 int nmgp_pbar_reduce_f32(const float* Z, int64_t sZ, float* P, int64_t ldp, const int32_t* seg, int D, int B, int M,
                          hipStream_t stream);
+/* L-bar / mu-bar of the latent factors in the DSVI backward (autograd of code/nmgp_dsvi.py:198-215, W = mu + L eps
+ * and MGP_d's L-products): factor d's gradient collects Y_{i,d} = P_G[rows of i]^T W-hat_d[rows of i] over outputs
+ * i = d .. D-1.  Slot (i, d) is Y + (first(d) + i - d) * sY, first(d) = sum_{d' < d} (D - d'): an M x M matrix, then an
+ * M-vector at offset M * M.  Adds, in i order, the matrices' lower triangles onto gA + d * sA (upper triangle set to
+ * 0) and the vectors onto gB + d * sB.  0 or -(argument).                                                          */
+int nmgp_lbar_reduce_f64(const double* Y, int64_t sY, double* gA, int64_t sA, double* gB, int64_t sB, int D, int M,
+                         hipStream_t stream);
+int nmgp_lbar_reduce_f32(const float* Y, int64_t sY, float* gA, int64_t sA, float* gB, int64_t sB, int D, int M,
+                         hipStream_t stream);
 int nmgp_convert_f32_to_f64(const float* src, double* dst, int64_t n, hipStream_t stream);
 int nmgp_convert_f64_to_f32(const double* src, float* dst, int64_t n, hipStream_t stream);
 /* On-device minibatch pipeline (replaces the host DataLoader + vec2list split of

@@ -756,6 +756,70 @@ def test_kron_mv_fused_and_gemm_paths(ops, P1, P2, N1, N2, dt):
         assert rel(mv, torch.kron(Bc, Kc) @ yc) < tol
 
 
+@pytest.mark.parametrize("sizes", [[400, 350, 500, 300, 450], [0, 7, 0, 129, 1], [3] * 40])
+@pytest.mark.parametrize("dt", [F64, torch.float32])
+def test_pbar_reduce_adds_each_rows_factor_products_in_order(ops, sizes, dt):
+    """nmgp_pbar_reduce (the per-factor P-bar_G form of the backward): every row r of output i gets
+    P[r] + Z_0[r] + ... + Z_i[r], summed left to right -- empty outputs and ragged segments included."""
+    import ctypes
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L
+    D, M = len(sizes), 300
+    B = sum(sizes)
+    seg = torch.tensor(np.concatenate([[0], np.cumsum(sizes)]), dtype=torch.int32)
+    g = torch.Generator().manual_seed(D * 31 + B)
+    Z = torch.randn(D, B, M, generator=g, dtype=dt)
+    P = torch.randn(B, M, generator=g, dtype=dt)
+    ref = P.clone()
+    for i in range(D):
+        for d in range(i + 1):
+            ref[seg[i]:seg[i + 1]] += Z[d, seg[i]:seg[i + 1]]
+    Zd, Pd, sd = Z.to(DEV), P.to(DEV), seg.to(DEV)
+    fn = L.lib().nmgp_pbar_reduce_f64 if dt == F64 else L.lib().nmgp_pbar_reduce_f32
+    vp = ctypes.c_void_p
+    L.check(fn(vp(Zd.data_ptr()), B * M, vp(Pd.data_ptr()), M, vp(sd.data_ptr()), D, B, M, L.stream_handle()),
+            "pbar_reduce")
+    assert torch.equal(Pd.cpu(), ref)
+    assert fn(vp(Zd.data_ptr()), B * M - 1, vp(Pd.data_ptr()), M, vp(sd.data_ptr()), D, B, M,
+              L.stream_handle()) == -2
+
+
+@pytest.mark.parametrize("D,M", [(5, 256), (1, 300), (7, 33)])
+@pytest.mark.parametrize("dt", [F64, torch.float32])
+def test_lbar_reduce_adds_each_factors_output_products_in_order(ops, D, M, dt):
+    """nmgp_lbar_reduce (the per-(output, factor) L-bar form of the backward): factor d's M x M gradient block gets
+    its lower triangle + Y_{d,d} + ... + Y_{D-1,d} (left to right) and its upper triangle set to 0, as the OUT_TRIL
+    product it replaces; its M-vector gets the slots' vectors the same way.  Padding between blocks untouched."""
+    import ctypes
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L
+    MM, SY = M * M, M * M + M
+    nsl = D * (D + 1) // 2
+    g = torch.Generator().manual_seed(D * 7 + M)
+    Y = torch.randn(nsl * SY, generator=g, dtype=dt)
+    sA, sB = MM + 5, M + 3                       # gradient blocks with gaps between them
+    gA = torch.randn(D * sA, generator=g, dtype=dt)
+    gB = torch.randn(D * sB, generator=g, dtype=dt)
+    refA, refB = gA.clone(), gB.clone()
+    low = torch.tril(torch.ones(M, M, dtype=torch.bool)).reshape(-1)
+    for d in range(D):
+        first = d * D - d * (d - 1) // 2
+        a = refA[d * sA:d * sA + MM]
+        b = refB[d * sB:d * sB + M]
+        for i in range(d, D):
+            s = (first + i - d) * SY
+            a += Y[s:s + MM]
+            b += Y[s + MM:s + SY]
+        a[~low] = 0
+    Yd, gAd, gBd = Y.to(DEV), gA.to(DEV), gB.to(DEV)
+    fn = L.lib().nmgp_lbar_reduce_f64 if dt == F64 else L.lib().nmgp_lbar_reduce_f32
+    vp = ctypes.c_void_p
+    L.check(fn(vp(Yd.data_ptr()), SY, vp(gAd.data_ptr()), sA, vp(gBd.data_ptr()), sB, D, M, L.stream_handle()),
+            "lbar_reduce")
+    assert torch.equal(gAd.cpu(), refA)
+    assert torch.equal(gBd.cpu(), refB)
+    assert fn(vp(Yd.data_ptr()), SY - 1, vp(gAd.data_ptr()), sA, vp(gBd.data_ptr()), sB, D, M,
+              L.stream_handle()) == -2
+
+
 def test_adam_matches_torch(ops):
     g = torch.Generator().manual_seed(8)
     p0 = torch.randn(1000, generator=g, dtype=F64)

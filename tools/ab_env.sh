@@ -7,7 +7,7 @@ cd $R
 mkdir -p gpurun_out
 V=$1; shift
 N=${REPS:-3}
-ARGS="--steps 300 --warmup 20 --no-cpu-baseline --no-stress --no-elbo --no-api --no-breakdown"
+ARGS="--steps 300 --warmup 20 --no-cpu-baseline --no-stress --no-elbo --no-api --no-breakdown --no-hcp --no-ecog --no-kron"
 for i in $(seq $N); do
   for val in "$@"; do
     env $V=$val timeout -k 10 120 python bench.py $ARGS > gpurun_out/ab_${V}_${val}_$i.json 2> gpurun_out/ab_err.log
