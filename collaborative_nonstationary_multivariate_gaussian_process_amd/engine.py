@@ -1017,8 +1017,8 @@ class DsviEngine:
             ("sig", "main", "tb"),
             ("bwd_t1", "gemm", gemm("bwd_t1"), "main"),
             ("wait", "side", "tb"),
+            ("bwd_vt", "gemm", gemm("bwd_vt"), "side"),      # (reads P_t and tbar only: beside the G-prior chain)
             ("wait", "side", "g22"),
-            ("bwd_vt", "gemm", gemm("bwd_vt"), "side"),
             ("vbwd", "row", row(getattr(lib, "nmgp_dsvi_vbwd_" + self.sfx)), "side"),
             ("bwd_v1", "gemm", gemm("bwd_v1"), "side"),
             ("bwd_v2", "gemm", gemm("bwd_v2"), "side"),
