@@ -24,6 +24,17 @@
 
 
 namespace nmgp {
+#ifdef NMGP_LAT_TRACE
+// tools/lat_trace.hip only: shader-cycle stamps of wave 0 of every workgroup's first tile (8 per workgroup)
+__device__ unsigned long long* g_lat_trace;
+#define LAT_STAMP(i)                                                                          \
+  if (threadIdx.x == 0 && first_tile) {                                                       \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                               \
+    g_lat_trace[blockIdx.x * 8 + (i)] = __builtin_readcyclecounter();                         \
+  }
+#else
+#define LAT_STAMP(i)
+#endif
 namespace {
 
 constexpr int LTM = 32, LTN = 32;
@@ -63,8 +74,9 @@ __device__ inline void loadv(T (&v)[NV], __amdgpu_buffer_rsrc_t r, uint32_t off,
 
 template <typename T, int LW, int LKP>
 __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_desc* __restrict__ descs,
-                                         const int32_t* __restrict__ dyn, T* red, int tile) {
+                                         const int32_t* __restrict__ dyn, T* red, int tile, bool first_tile) {
   constexpr int NV = LKP / 4;   // k values per lane and operand block in one panel
+  LAT_STAMP(0);
   int lo = 0, hi = args.nprob - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -76,6 +88,7 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
   lo = __builtin_amdgcn_readfirstlane(lo);
   const nmgp_gemm_desc d = descs[lo];
   tile -= dyn ? dyn[lo] : d.tile_start;
+  LAT_STAMP(1);
   const int ksplit = d.ksplit > 1 ? d.ksplit : 1;
   const int ks = tile % ksplit;
   tile /= ksplit;
@@ -196,6 +209,7 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
         const int64_t col = j0 + 16 * bj + li;
         loadv<T, NV>(b[bj], rB, (uint32_t)(((int64_t)kbl * d.sB_k + col * d.sB_j + (int64_t)bb * d.sB_kb) * sz), stB, bC);
       }
+      LAT_STAMP(2);
       if (flags & NMGP_KSCALE) {
         const int kg = kp + NV * g;
 #pragma unroll
@@ -242,6 +256,7 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
       }
     }
   }
+  LAT_STAMP(3);
   // partial tiles of the waves -> LDS, summed in wave order per output tile
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -250,6 +265,7 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
       red[w * (LTM * LTN) + (16 * (q >> 1) + Mfma<T>::row(lane, r)) * LTN + 16 * (q & 1) + li] = acc[q >> 1][q & 1][r];
   }
   lds_barrier();
+  LAT_STAMP(4);
   constexpr int NE = (LTM * LTN) / (64 * LW);   // output values per thread and tile
   const int ntl = (jt[1] >= 0) ? 2 : 1;
   for (int qt = 0; qt < ntl; ++qt) {
@@ -300,6 +316,7 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
         vals[q] = sum;
       }
     }
+    LAT_STAMP(5);
     const GPtr<T> C = (GPtr<T>)d.C;
     const GPtr<const T> E = (GPtr<const T>)d.epi_E;
     const GPtr<const T> rsp = (GPtr<const T>)d.epi_rs;
@@ -331,6 +348,7 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
       C[ci] = val;
     }
   }
+  LAT_STAMP(6);
 }
 
 template <typename T, int LW, int LKP, int OCC>
@@ -342,7 +360,7 @@ __global__ __launch_bounds__(64 * LW, OCC) void gemm_lat_kernel(LatArgs args,
   const int per = (total + 7) >> 3;   // tiles per XCD chunk
   for (int b = blockIdx.x; b < 8 * per; b += gridDim.x) {
     const int tile = (b & 7) * per + (b >> 3);
-    if (tile < total) lat_tile<T, LW, LKP>(args, descs, dyn, red, tile);
+    if (tile < total) lat_tile<T, LW, LKP>(args, descs, dyn, red, tile, b == (int)blockIdx.x);
     __syncthreads();
   }
 }
