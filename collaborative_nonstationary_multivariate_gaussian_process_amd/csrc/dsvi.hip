@@ -372,8 +372,9 @@ __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
   if (elbo) return;
   __syncthreads();
 
-  // ---- phase 3: W-hat = diag(2 adjoint) W, W / W_P scaled in place (rows s > o zeroed: they are not
-  // computed by the W GEMM), and the P-bar initial rows
+  // ---- phase 3: W-hat = diag(2 adjoint) W, W / W_P scaled in place, and the P-bar initial rows.  (Rows of
+  // factors s > o are neither computed by the W GEMM nor read by any backward product -- those take factor s
+  // over the rows of outputs >= s only -- so they are left alone; round 3 zeroed them.)
   const T cg = scal[0], c0 = scal[1], c1 = scal[2];
   for (int s = 0; s <= o; ++s) {
     const T fg = sv[s], fp = sv[D + s];
@@ -383,10 +384,6 @@ __global__ __launch_bounds__(256) void dsvi_recon_kernel(Args a) {
       wg[c] *= fg;
       wp[c] *= fp;
     }
-  }
-  for (int s = o + 1; s < D; ++s) {
-    T* wg = WG + (int64_t)s * BM + (int64_t)r * M;
-    for (int c = t; c < M; c += 256) wg[c] = (T)0;
   }
   T* PbG = (T*)a.Pbar + 3 * BM + (int64_t)r * M;
   T* Pb0 = (T*)a.Pbar + 1 * BM + (int64_t)r * M;
