@@ -324,9 +324,10 @@ TRAIN_CFGS = {"hcp": (50, 10000, 512, 5000, 263.0), "ecog": (128, 391, 1024, 512
 
 
 def train_roofline(eng, cfg):
-    """The dominant kernel of an fp32 training step (BASELINE configs[2] / [3]) against the fp32 MFMA peak: the
-    grouped 64x64 tile GEMM (gemm_kernel<float, true>; the committed rocprofv3 breakdown of the graphed step,
-    profiles/r*_{cfg}_train_kernels.json from tools/train_trace.sh, names it).  Algorithmic flops per step = 2 m n k
+    """The grouped 64x64 tile GEMM of an fp32 training step (BASELINE configs[2] / [3]) against the fp32 MFMA peak
+    (gemm_kernel<float, true>: HCP's dominant kernel by busy time; for ECoG second since round 4, behind the batched
+    128x128 factor products -- the committed rocprofv3 breakdown of the graphed step,
+    profiles/r*_{cfg}_train_kernels.json from tools/train_trace.sh, lists both).  Algorithmic flops per step = 2 m n k
     over the descriptors of every group the engine runs on that kernel (triangular zeros and skipped output
     halves not counted, row segments of this minibatch); divided by the kernel's busy time per step in the
     profile (sum of its launch durations)."""
