@@ -1,4 +1,5 @@
-// Per-step timeline of the lookahead factor+inverse kernel (chol_inv4_kernel) for matrix 0 of a batch
+// Per-step timeline of the multi-role factor+inverse kernel for matrix 0 of a batch (written for round 3's
+// lookahead kernel, removed in round 4; the stamps sit in the four-role kernel's shared code paths)
 // (standalone; not part of the library).  Wall clock 100 MHz (10 ns) stamps:
 //   role 0 = diagonal wave: 0 column seen, 1 chain done, 2 table / L_kk in LDS;  role 1 = row wave 1:
 //            0 table seen, 1 rows in LDS;  role 2 = update wave 4: 0 rows seen, 1 column k+1 spilled,
@@ -6,7 +7,7 @@
 //            issued, 2 step done.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DNMGP_CHOL_TRACE -I<pkg>/csrc tools/chol4_probe.hip \
 //         <pkg>/csrc/gemm.hip <pkg>/csrc/gemm_big.hip -o tools/bin/chol4_probe
-//   ./chol4_probe [n] [batch]          (NMGP_CHOL_LA=0 times the three-role kernel, no timeline)
+//   ./chol4_probe [n] [batch]          (NMGP_CHOL_4ROLE=0 times the three-role kernel, no timeline)
 #include "chol.hip"
 
 #include <cstdio>

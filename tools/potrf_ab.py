@@ -1,5 +1,5 @@
 """Stress potrf timing probe (GPU box): bench.py's M=4096 fp32 blocked Cholesky alone, graph-replayed,
-plus the residual.  Run once per setting of the step-kernel knobs (NMGP_POTRF_STEP128=1, ...) for an A/B.
+plus the residual (run once per tree for an A/B: the round-3/4 step-kernel knobs it was written for are removed).
 usage: python tools/potrf_ab.py [n ...]"""
 import json
 import os
