@@ -434,6 +434,43 @@ def test_index_argument_any_order_matches_oracle():
     assert whole < 1e-9
 
 
+@pytest.mark.parametrize("case,sizes", [("mid_forward", [5, 0, 7]), ("mid_forward", [0, 9, 3]),
+                                        ("mid_forward", [40, 1, 0]), ("pm25_forward", [120, 0, 95, 1, 64])])
+def test_ragged_minibatch_with_empty_outputs_matches_oracle(case, sizes):
+    """Minibatches whose outputs have very different row counts, some none at all (the DataLoader draw of
+    code/nmgp_dsvi.py:829-837 can leave an output empty): every row- and k-segmented product then runs on empty
+    or one-row segments -- the per-(output, factor) L-bar slots of an empty output must come out as zeros, the
+    per-factor P-bar reduction must skip it.  Loss and gradient against the oracle at SURVEY's fp64 gates."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.engine import DsviEngine
+    D, M = CASES[case][:2]
+    g = G.load(case)
+    p = G.params(g, D=D, M=M)
+    rng = np.random.default_rng(sum(sizes) * 7 + len(sizes))
+    xl = [np.sort(rng.uniform(0, 1, s)) for s in sizes]
+    yl = [rng.standard_normal(s) for s in sizes]
+    B = sum(sizes)
+    noise = rng.standard_normal(M + B + D * (D + 1) // 2 * B)
+    eng = DsviEngine(D, M, B, g["z"])
+    theta = torch.cat([p[k].reshape(-1) for k in O.PARAM_NAMES]).to("cuda")
+    grad = torch.zeros_like(theta)
+    eng.bind(theta, grad, N=float(g["N"]))
+    eng.load_batch(np.concatenate(xl), np.concatenate(yl), sizes, noise=noise)
+    eng.forward_backward()
+    torch.cuda.synchronize()
+    eng.check_info()
+    q = {k: v.clone().requires_grad_() for k, v in p.items()}
+    tape = O.TapeNoise(noise)
+    loss, _ = O.forward(q, xl, yl, g["z"], float(g["N"]), tape)
+    loss.backward()
+    assert tape.done()
+    gd = _unflatten(eng, grad)
+    lerr = abs(float(eng.out[0]) - float(loss)) / abs(float(loss))
+    whole = _rel(torch.cat([gd[k].reshape(-1) for k in O.PARAM_NAMES]),
+                 torch.cat([q[k].grad.reshape(-1) for k in O.PARAM_NAMES]))
+    print(f"PARITY ragged {case} {sizes}: loss rel {lerr:.3e}  whole-gradient rel-norm {whole:.3e}")
+    assert lerr <= SURVEY_FP64_LOSS and whole <= SURVEY_FP64_GRAD, (lerr, whole)
+
+
 @pytest.mark.parametrize("case", ["mid_forward", "pm25_forward"])
 def test_step_is_deterministic_run_to_run(case):
     """The fused step (grouped / latency-kernel GEMMs with their split-K combines, the multi-workgroup
