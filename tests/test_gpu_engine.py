@@ -434,15 +434,14 @@ def test_index_argument_any_order_matches_oracle():
     assert whole < 1e-9
 
 
-@pytest.mark.parametrize("case,sizes", [("mid_forward", [5, 0, 7]), ("mid_forward", [0, 9, 3]),
-                                        ("mid_forward", [40, 1, 0]), ("pm25_forward", [120, 0, 95, 1, 64])])
-def test_ragged_minibatch_with_empty_outputs_matches_oracle(case, sizes):
-    """Minibatches whose outputs have very different row counts, some none at all (the DataLoader draw of
-    code/nmgp_dsvi.py:829-837 can leave an output empty): every row- and k-segmented product then runs on empty
-    or one-row segments -- the per-(output, factor) L-bar slots of an empty output must come out as zeros, the
-    per-factor P-bar reduction must skip it.  Loss and gradient against the oracle at SURVEY's fp64 gates."""
+RAGGED = [("mid_forward", [5, 0, 7]), ("mid_forward", [0, 9, 3]), ("mid_forward", [40, 1, 0]),
+          ("pm25_forward", [120, 0, 95, 1, 64]), ("hcp_like_forward", [60, 0, 1, 45, 0, 30, 22, 12])]
+RAGGED_DM = {"mid_forward": (3, 64), "pm25_forward": (5, 256), "hcp_like_forward": (8, 512)}
+
+
+def _ragged_run(case, sizes, dtype):
     from collaborative_nonstationary_multivariate_gaussian_process_amd.engine import DsviEngine
-    D, M = CASES[case][:2]
+    D, M = RAGGED_DM[case]
     g = G.load(case)
     p = G.params(g, D=D, M=M)
     rng = np.random.default_rng(sum(sizes) * 7 + len(sizes))
@@ -450,8 +449,8 @@ def test_ragged_minibatch_with_empty_outputs_matches_oracle(case, sizes):
     yl = [rng.standard_normal(s) for s in sizes]
     B = sum(sizes)
     noise = rng.standard_normal(M + B + D * (D + 1) // 2 * B)
-    eng = DsviEngine(D, M, B, g["z"])
-    theta = torch.cat([p[k].reshape(-1) for k in O.PARAM_NAMES]).to("cuda")
+    eng = DsviEngine(D, M, B, g["z"], dtype=dtype)
+    theta = torch.cat([p[k].reshape(-1) for k in O.PARAM_NAMES]).to("cuda", dtype)
     grad = torch.zeros_like(theta)
     eng.bind(theta, grad, N=float(g["N"]))
     eng.load_batch(np.concatenate(xl), np.concatenate(yl), sizes, noise=noise)
@@ -465,10 +464,31 @@ def test_ragged_minibatch_with_empty_outputs_matches_oracle(case, sizes):
     assert tape.done()
     gd = _unflatten(eng, grad)
     lerr = abs(float(eng.out[0]) - float(loss)) / abs(float(loss))
-    whole = _rel(torch.cat([gd[k].reshape(-1) for k in O.PARAM_NAMES]),
+    whole = _rel(torch.cat([gd[k].reshape(-1).double() for k in O.PARAM_NAMES]),
                  torch.cat([q[k].grad.reshape(-1) for k in O.PARAM_NAMES]))
+    return eng, lerr, whole
+
+
+@pytest.mark.parametrize("case,sizes", RAGGED[:4] + [RAGGED[4]])
+def test_ragged_minibatch_with_empty_outputs_matches_oracle(case, sizes):
+    """Minibatches whose outputs have very different row counts, some none at all (the DataLoader draw of
+    code/nmgp_dsvi.py:829-837 can leave an output empty): every row- and k-segmented product then runs on empty
+    or one-row segments -- the per-(output, factor) L-bar slots of an empty output must come out as zeros, the
+    per-factor P-bar reduction must skip it (M = 512: the one-product-per-factor L-bar form).  Loss and gradient
+    against the oracle at SURVEY's fp64 gates."""
+    _, lerr, whole = _ragged_run(case, sizes, torch.float64)
     print(f"PARITY ragged {case} {sizes}: loss rel {lerr:.3e}  whole-gradient rel-norm {whole:.3e}")
     assert lerr <= SURVEY_FP64_LOSS and whole <= SURVEY_FP64_GRAD, (lerr, whole)
+
+
+@pytest.mark.parametrize("case,sizes", [RAGGED[0], RAGGED[2], RAGGED[4]])
+def test_fp32_ragged_minibatch_with_empty_outputs(case, sizes):
+    """The fp32 engine on the same ragged minibatches (M = 512: the 128x128 batched factor products with
+    per-problem k segments, several of them empty) at SURVEY's fp32 gates: loss 1e-3, whole gradient 2e-2."""
+    eng, lerr, whole = _ragged_run(case, sizes, torch.float32)
+    print(f"PARITY ragged fp32 {case} {sizes} (big_side {eng.big_side}): loss rel {lerr:.3e}  "
+          f"whole-gradient rel-norm {whole:.3e}")
+    assert lerr <= 1e-3 and whole <= 2e-2, (lerr, whole)
 
 
 @pytest.mark.parametrize("case", ["mid_forward", "pm25_forward"])
