@@ -27,6 +27,30 @@ sys.path.insert(0, ROOT)
 D, M, N_LOC, B = 5, 256, 2000, 2000
 FP64_MFMA_PEAK_TFLOPS = 78.6          # MI355X dense FP64 matrix peak (spec)
 HBM_PEAK_GBS = 8000.0
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from provenance import code_hash  # noqa: E402
+
+CODE_HASH = code_hash()
+
+
+def matched_profile(pattern):
+    """The committed profile (profiles/<pattern>) measured on THIS code: the newest file whose code_hash
+    (tools/provenance.py, written by the summary tools on the GPU box) equals the running tree's.  Without one
+    the newest file is returned with stale=True, and every figure taken from it is marked stale in the line."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    data = []
+    for f in files:
+        try:
+            data.append((f, json.load(open(f))))
+        except (OSError, ValueError):
+            continue
+    for f, d in reversed(data):
+        if isinstance(d, dict) and d.get("code_hash") == CODE_HASH:
+            return os.path.relpath(f, ROOT), d, False
+    if data:
+        return os.path.relpath(data[-1][0], ROOT), data[-1][1], True
+    return None, None, True
 
 
 def synth_data(rank):
@@ -118,6 +142,7 @@ def stress_cholesky(dev, reps=5):
                       "side stream: 32-row strip of block column j+2, then the trailing SYRK)",
             "potrf_ms": round(t_fac, 4), "gflops": round(f / (t_fac * 1e-3) / 1e9, 1),
             "residual": resid,
+            "hbm": _stress_hbm(t_fac),
             "syrk_in_factorization": _stress_syrk_pmc(),
             "syrk_in_ecog_factorization": _ecog_syrk_pmc(),
             "syrk_isolated_proxy": {"kernel": "gemm_big_kernel (128x128 f32 MFMA, stream-K)", "n": Mst, "k": Mst,
@@ -174,11 +199,10 @@ def _stress_syrk_pmc():
     """MFMA-busy of the trailing-update SYRK launches INSIDE the M=4096 factorization (k = 128), time-weighted,
     from the committed rocprofv3 PMC pass (tools/syrk_inside_pmc.sh: SQ_VALU_MFMA_BUSY_CYCLES /
     (GRBM_GUI_ACTIVE/8 * 4 * 256), one pass, no tracing domains) and the whole factorization's."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_stress_potrf_mfma_util.json")))
-    if not files:
+    src, d, stale = matched_profile("r*_stress_potrf_mfma_util.json")
+    if d is None:
         return None
-    rows = json.load(open(files[-1]))["rows"]
+    rows = d["rows"]
     nm = lambda r: r["kernel"]
     syrk = [r for r in rows if "gemm_big_kernel" in nm(r)]
     fac = [r for r in rows if any(k in nm(r) for k in ("gemm_big_kernel", "potrf_step", "potrf_strip", "chol_inv"))]
@@ -186,27 +210,56 @@ def _stress_syrk_pmc():
         1e-9, sum(r["avg_us"] * r["dispatches"] for r in rs))
     return {"kernel": "gemm_big_kernel (the factorization's own trailing SYRKs, k = 128)",
             "launches": sum(r["dispatches"] for r in syrk), "mfma_busy_time_weighted": round(tw(syrk), 4),
-            "factorization_kernels_mfma_busy": round(tw(fac), 4),
-            "source": os.path.relpath(files[-1], ROOT)}
+            "factorization_kernels_mfma_busy": round(tw(fac), 4), "source": src, "stale": stale}
+
+
+def _stress_hbm(potrf_ms):
+    """HBM traffic of one stress factorization from the committed FETCH_SIZE / WRITE_SIZE passes
+    (tools/stress_hbm.sh; FETCH x2 per the gfx950 note + WRITE) over the factorization time measured here,
+    beside the algorithmic bytes (A read once, L written once: 2 M^2 4 B)."""
+    src, d, stale = matched_profile("r*_stress_potrf_hbm.json")
+    alg = 2.0 * 4096 * 4096 * 4
+    out = {"algorithmic_bytes": int(alg), "algorithmic_GBs": round(alg / (potrf_ms * 1e-3) / 1e9, 1),
+           "peak_GBs": HBM_PEAK_GBS}
+    if d is not None:
+        t = d["traffic_bytes"]
+        out.update({"traffic_bytes": t, "read_bytes_x2corrected": d["read_bytes_x2corrected"],
+                    "write_bytes": d["write_bytes"], "achieved_GBs": round(t / (potrf_ms * 1e-3) / 1e9, 1),
+                    "frac": round(t / (potrf_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "source": src, "stale": stale})
+    return out
+
+
+# ECoG batched recursive Cholesky of the 8384 M = 1024 variational factors (chol.hip chol_inv_rec_big): its trailing
+# SYRKs A22 -= L21 L21^T per recursion level, identified by grid (threads = 256 x lower tiles x 8384 factors)
+ECOG_SYRK_LEVELS = [("top, n2 = 512, k = 512 (10 lower tiles)", 21463040, 1.0),
+                    ("level 2, n2 = 256, k = 256 (3 lower tiles)", 6438912, 1.0),
+                    # one-tile k = 128 products share a grid: SYRK, L21 panel and the inverse product, equal shapes
+                    ("level 3, n2 = 128, k = 128 (1 tile; 1 of the 3 one-tile products of the grid)", 2146304, 1 / 3.)]
 
 
 def _ecog_syrk_pmc():
-    """MFMA-busy of the trailing-update SYRK inside the batched recursive Cholesky of the ECoG-shaped step
-    (BASELINE.json configs[3]: 8384 variational factors of M = 1024; top recursion level A22 -= L21 L21^T,
-    k = 512, 10 lower 128x128 tiles per factor = grid 21463040 threads), from the committed PMC pass of one
-    training step (tools/syrk_inside_pmc.sh -> profiles/r*_ecog_step_mfma_util.json)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_ecog_step_mfma_util.json")))
-    if not files:
+    """MFMA-busy of the trailing-update SYRKs inside the batched recursive Cholesky of the ECoG-shaped step
+    (BASELINE.json configs[3]: 8384 variational factors of M = 1024), from the committed PMC pass of one
+    training step (tools/syrk_inside_pmc.sh -> profiles/r*_ecog_step_mfma_util.json): the top level and every
+    level, time-weighted."""
+    src, d, stale = matched_profile("r*_ecog_step_mfma_util.json")
+    if d is None:
         return None
-    rows = [r for r in json.load(open(files[-1]))["rows"]
-            if r["kernel"].startswith("void nmgp::gemm_big_kernel<true, true, 0>") and r["grid_threads"] == 21463040]
-    if not rows:
+    lev = []
+    for label, grid, share in ECOG_SYRK_LEVELS:
+        rs = [r for r in d["rows"] if r["kernel"].startswith("void nmgp::gemm_big_kernel<true, true, 0>")
+              and r["grid_threads"] == grid]
+        if rs:
+            us = sum(r["avg_us"] * r["dispatches"] for r in rs)
+            lev.append({"level": label, "us_total": round(us * share, 1),
+                        "mfma_busy": round(sum(r["mfma_util"] * r["avg_us"] * r["dispatches"] for r in rs) / us, 4)})
+    if not lev:
         return None
-    w = sum(r["avg_us"] * r["dispatches"] for r in rows)
-    return {"kernel": "gemm_big_kernel (batched trailing SYRK A22 -= L21 L21^T of 8384 M=1024 factors, k = 512)",
-            "mfma_busy_time_weighted": round(sum(r["mfma_util"] * r["avg_us"] * r["dispatches"] for r in rows) / w, 4),
-            "avg_us": round(w / sum(r["dispatches"] for r in rows), 1), "source": os.path.relpath(files[-1], ROOT)}
+    w = sum(x["us_total"] for x in lev)
+    return {"kernel": "gemm_big_kernel (batched trailing SYRK A22 -= L21 L21^T of 8384 M=1024 factors)",
+            "mfma_busy_time_weighted": lev[0]["mfma_busy"], "mfma_busy_top_level_k512": lev[0]["mfma_busy"],
+            "mfma_busy_all_levels_time_weighted": round(sum(x["mfma_busy"] * x["us_total"] for x in lev) / w, 4),
+            "levels": lev, "source": src, "stale": stale}
 
 
 def api_path(dev, xs, ys, z, epochs_device=100, epochs_torch=20):
@@ -324,39 +377,68 @@ TRAIN_CFGS = {"hcp": (50, 10000, 512, 5000, 263.0), "ecog": (128, 391, 1024, 512
 
 
 def train_roofline(eng, cfg):
-    """The grouped 64x64 tile GEMM of an fp32 training step (BASELINE configs[2] / [3]) against the fp32 MFMA peak
-    (gemm_kernel<float, true>: HCP's dominant kernel by busy time; for ECoG second since round 4, behind the batched
-    128x128 factor products -- the committed rocprofv3 breakdown of the graphed step,
-    profiles/r*_{cfg}_train_kernels.json from tools/train_trace.sh, lists both).  Algorithmic flops per step = 2 m n k
-    over the descriptors of every group the engine runs on that kernel (triangular zeros and skipped output
-    halves not counted, row segments of this minibatch); divided by the kernel's busy time per step in the
-    profile (sum of its launch durations)."""
-    import glob
+    """Roofline of an fp32 training step (BASELINE configs[2] / [3]) for the kernel FAMILY with the most busy time
+    in the committed rocprofv3 breakdown of the graphed step (profiles/r*_{cfg}_train_kernels.json from
+    tools/train_trace.sh, code-hash matched): every template instance of one kernel counts as one family.
+      gemm_big_kernel (128x128 f32): the batched factor products -- Sigma_f = tril(S) tril(S)^T (syrk_side),
+        Xs = C^-1 L (xs_side), the KL L-bar -C^-T Xs (kl_lbar), the pair / latent L-bar P^T W-hat (bwd_lbar) and
+        the GEMMs of the recursive factor + inverse of every variational factor (chol_side);
+      gemm_kernel<float> (grouped 64x64 f32): the row-segmented quad-form / P-bar products.
+    Algorithmic flops per step = 2 x multiply-adds over the launches of that family (triangular zeros, skipped
+    output halves and padding not counted; row / k segments of this minibatch), over the family's busy time
+    per step (sum of its launch durations: concurrent streams overlap, so this is conservative)."""
     seg_host = eng.seg.cpu().numpy()
-    gf, n, names = 0.0, 0, []
+    fams = {"gemm_big_kernel": [0.0, [], 0], "gemm_kernel<float": [0.0, [], 0]}
     for nm, grp in eng.gemm_groups():
         parts = grp.parts if hasattr(grp, "parts") else [grp]
         for p_ in parts:
-            if hasattr(p_, "macs") and not getattr(p_, "lat", False) and p_.dtype == torch.float32:
-                gf += 2.0 * p_.macs(seg_host) / 1e9
-                n += 1
-                names.append(nm)
-    out = {"kernel": "gemm_kernel<float, true> (grouped 64x64 MFMA f32 GEMM)", "bound": "mfma",
-           "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "algorithmic_gflop_per_step": round(gf, 3),
-           "launches_per_step": n, "groups": sorted(set(names)), "traffic": None}
-    profs = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{cfg}_train_kernels.json")))
-    if profs:
-        rows = json.load(open(profs[-1]))["kernels"]
-        k = [r for r in rows if r["kernel"].startswith("gemm_kernel<float, true>")]
-        if k:
-            ms = k[0]["ms_per_step"]
+            if isinstance(p_, H_BigBatch()):
+                fams["gemm_big_kernel"][0] += 2.0 * p_.macs(seg_host) / 1e9
+                fams["gemm_big_kernel"][1].append(nm)
+                fams["gemm_big_kernel"][2] += 1
+            elif hasattr(p_, "macs") and not getattr(p_, "lat", False) and p_.dtype == torch.float32:
+                fams["gemm_kernel<float"][0] += 2.0 * p_.macs(seg_host) / 1e9
+                fams["gemm_kernel<float"][1].append(nm)
+                fams["gemm_kernel<float"][2] += 1
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import hip_ops as H
+    kf0, kf1 = eng._plan(0)["kl_range"]
+    if eng.M > 256:      # chol_side: recursive factor + inverse of the variational factors on gemm_big
+        fams["gemm_big_kernel"][0] += (kf1 - kf0) * 2.0 * H.chol_inv_rec_macs(eng.M) / 1e9
+        fams["gemm_big_kernel"][1].append("chol_side (recursive factor + inverse GEMMs)")
+    src, d, stale = matched_profile(f"r*_{cfg}_train_kernels.json")
+    busy = {}
+    if d is not None:
+        for r in d["kernels"]:
+            for fam in fams:
+                if r["kernel"].startswith(fam):
+                    b_ = busy.setdefault(fam, [0.0, 0.0, 0.0])
+                    b_[0] += r["ms_per_step"]
+                    b_[1] += r["share_of_busy"]
+                    b_[2] += r["launches_per_step"]
+    lines = {}
+    for fam, (gf, names, n) in fams.items():
+        e = {"kernel": fam + ("> (grouped 64x64 MFMA f32 GEMM)" if fam.startswith("gemm_kernel")
+                              else " (128x128 MFMA f32, batched factor products)"),
+             "bound": "mfma", "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+             "algorithmic_gflop_per_step": round(gf, 3), "groups": sorted(set(names)), "traffic": None}
+        if fam in busy:
+            ms, share, launches = busy[fam]
             ach = gf / ms                                   # GFLOP / ms = TFLOP/s
-            out.update({"profile_ms_per_step": ms, "profile_launches_per_step": k[0]["launches_per_step"],
-                        "profile_share_of_busy": k[0]["share_of_busy"], "achieved": round(ach, 3),
-                        "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
-                        "timing": "rocprofv3 --kernel-trace busy time of the kernel per graphed step, "
-                                  + os.path.relpath(profs[-1], ROOT)})
+            e.update({"profile_ms_per_step": round(ms, 4), "profile_launches_per_step": launches,
+                      "profile_share_of_busy": round(share, 4), "achieved": round(ach, 3),
+                      "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "source": src, "stale": stale,
+                      "timing": "rocprofv3 --kernel-trace busy time of the family per graphed step"})
+        lines[fam] = e
+    top = max(lines, key=lambda f: busy.get(f, [0.0])[0]) if busy else "gemm_big_kernel"
+    out = dict(lines[top])
+    out["other_family"] = [lines[f] for f in lines if f != top][0]
+    out["dominant_by"] = "busy time per step in " + (src or "(no profile)")
     return out
+
+
+def H_BigBatch():
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import hip_ops as H
+    return H.BigBatch
 
 
 def graph_train(dev, cfg, steps, warmup=2):
@@ -799,63 +881,65 @@ def main():
         breakdown_names = {k: round(v, 4) for k, v in sorted(per_name.items(), key=lambda kv: -kv[1])}
 
     if roofline is not None:
-        # HBM traffic of the dominant kernel from the committed rocprofv3 PMC passes (FETCH_SIZE x2 per the
-        # gfx950 calibration note + WRITE_SIZE), averaged per launch; tools/pmc_summary.py writes them.
-        import glob
-        summaries = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pm25_bench_summary.json")))
-        if summaries:
-            with open(summaries[-1]) as fh:
-                ks = json.load(fh)["kernels"]
-            def prof(entry, pred):
-                gk = [k for k in ks if pred(k["name"])]
+        # The line's achieved / frac: the SERIALISED per-launch time of the kernel, measured live in this run (HIP
+        # events on the one stream the launches run on, `isolated` above) -- a kernel's own duration, so
+        # launches x avg_launch_us <= ms_per_step must hold (checked below).  Beside it, from the committed
+        # rocprofv3 runs of THIS code (code_hash match, tools/provenance.py; else "stale": true): the average
+        # inside the graphed timed loop, where the four streams overlap and a launch's duration includes time
+        # it waits for CUs held by other streams (tools/profile_bench.sh --kernel-trace --stats), the serialised
+        # average of the PMC pass (dispatches serialised by counter collection) and the HBM traffic per launch
+        # (FETCH_SIZE x2 per the gfx950 calibration note + WRITE_SIZE).
+        ssrc, summ, sstale = matched_profile("r*_pm25_bench_summary.json")
+        msrc, mfj, mstale = matched_profile("r*_pm25_mfma.json")
+
+        def attach(entry, pred):
+            iso = entry.pop("isolated")
+            entry["live_concurrent"] = {"avg_launch_us": entry["avg_launch_us"], "achieved": entry["achieved"],
+                                        "frac": entry["frac"], "timing": entry.pop("timing")}
+            entry["avg_launch_us"], entry["achieved"], entry["frac"] = (iso["avg_launch_us"], iso["achieved"],
+                                                                        iso["frac"])
+            entry["timing"] = ("live HIP events around each launch on its stream, the step's launches serialised "
+                               "on one stream (10 eager steps of this run)")
+            entry["launches_x_avg_us"] = round(entry["launches_per_step"] * entry["avg_launch_us"], 1)
+            entry["within_step"] = bool(entry["launches_x_avg_us"] <= 1000.0 * ms_per_step)
+            per_launch = entry["algorithmic_gflop_per_launch"] * 1e9
+            if summ is not None:
+                gk = [k for k in summ["kernels"] if pred(k["name"])]
                 calls = sum(k["calls"] for k in gk)
-                if not calls:
-                    return
-                if "hbm_write_bytes_per_launch" in gk[0]:
-                    entry["traffic"] = int(sum((k["hbm_read_bytes_per_launch_x2corrected"] +
-                                                k["hbm_write_bytes_per_launch"]) * k["calls"] for k in gk) / calls)
-                    entry["traffic_unit"] = "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
-                    entry["traffic_source"] = os.path.relpath(summaries[-1], ROOT)
-                # the same kernel's average launch duration as rocprofv3 saw it inside the graphed timed loop
-                # (tools/profile_bench.sh runs this bench under --kernel-trace --stats): the cross-check of the
-                # live concurrent-stream events above (the profile must come from the same code)
-                prof_us = 1000.0 * sum(k["total_ms"] for k in gk) / calls
-                per_launch = entry["algorithmic_gflop_per_launch"] * 1e9
-                prof_tf = per_launch / (prof_us * 1e-6) / 1e12
-                entry["profile"] = {"source": os.path.relpath(summaries[-1], ROOT), "avg_launch_us": round(prof_us, 2),
-                                    "achieved": round(prof_tf, 4), "frac": round(prof_tf / FP64_MFMA_PEAK_TFLOPS, 5)}
-            prof(roofline, lambda n: "gemm_lat_kernel<double" in n)
-            prof(roofline["tile_kernel"], lambda n: n.startswith("void nmgp::gemm_kernel<double"))
-
-            def promote(entry):
-                # the line's achieved / frac / avg_launch_us are the rocprofv3 figures (what a reader recomputes
-                # from profiles/); the live concurrent-stream HIP-event figures stay beside them as "live"
-                pf = entry.get("profile")
-                if not pf:
-                    return
-                entry["live"] = {"avg_launch_us": entry["avg_launch_us"], "achieved": entry["achieved"],
-                                 "frac": entry["frac"], "timing": entry.pop("timing", None),
-                                 "live_over_profile_us": round(entry["avg_launch_us"] / pf["avg_launch_us"], 3)}
-                entry["avg_launch_us"], entry["achieved"], entry["frac"] = pf["avg_launch_us"], pf["achieved"], pf["frac"]
-                entry["timing"] = ("rocprofv3 --kernel-trace average of this kernel inside the graphed timed loop of "
-                                   "this bench (tools/profile_bench.sh), " + pf["source"])
-            promote(roofline)
-            promote(roofline["tile_kernel"])
-        # MFMA-busy of the same kernels from the committed PMC pass (tools/pm25_pmc.sh: SQ_VALU_MFMA_BUSY_CYCLES /
-        # (GRBM_GUI_ACTIVE/8 * 4 * 256), dispatches serialised by counter collection), time-weighted per kernel
-        mf = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pm25_mfma.json")))
-        if mf:
-            rows = json.load(open(mf[-1]))["rows"]
-
-            def busy(pred):
-                rs = [r for r in rows if pred(r["kernel"])]
+                if calls:
+                    prof_us = 1000.0 * sum(k["total_ms"] for k in gk) / calls
+                    prof_tf = per_launch / (prof_us * 1e-6) / 1e12
+                    entry["in_graph_overlapped"] = {
+                        "source": ssrc, "stale": sstale, "avg_launch_us": round(prof_us, 2),
+                        "achieved": round(prof_tf, 4), "frac": round(prof_tf / FP64_MFMA_PEAK_TFLOPS, 5),
+                        "launches_x_avg_us": round(entry["launches_per_step"] * prof_us, 1),
+                        "timing": "rocprofv3 --kernel-trace average inside the graphed timed loop of this bench"}
+                    if "hbm_write_bytes_per_launch" in gk[0]:
+                        entry["traffic"] = int(sum((k["hbm_read_bytes_per_launch_x2corrected"] +
+                                                    k["hbm_write_bytes_per_launch"]) * k["calls"] for k in gk) / calls)
+                        entry["traffic_unit"] = "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
+                        entry["traffic_source"] = ssrc
+                        entry["traffic_stale"] = sstale
+            if mfj is not None:
+                rs = [r for r in mfj["rows"] if pred(r["kernel"])]
                 w = sum(r["avg_us"] * r["dispatches"] for r in rs)
-                return round(sum(r["mfma_util"] * r["avg_us"] * r["dispatches"] for r in rs) / w, 4) if w else None
-            roofline["mfma_busy"] = busy(lambda n: "gemm_lat_kernel<double" in n)
-            roofline["tile_kernel"]["mfma_busy"] = busy(lambda n: n.startswith("void nmgp::gemm_kernel<double"))
-            roofline["mfma_busy_source"] = os.path.relpath(mf[-1], ROOT)
-            if chol is not None:
-                chol["mfma_busy"] = busy(lambda n: "chol_inv7_kernel" in n or "chol_inv3_kernel" in n)
+                if w:
+                    ser_us = w / sum(r["dispatches"] for r in rs)
+                    entry["serialised_profile"] = {
+                        "source": msrc, "stale": mstale, "avg_launch_us": round(ser_us, 2),
+                        "achieved": round(per_launch / (ser_us * 1e-6) / 1e12, 4),
+                        "timing": "rocprofv3 PMC pass, dispatches serialised by counter collection"}
+                    entry["mfma_busy"] = round(sum(r["mfma_util"] * r["avg_us"] * r["dispatches"] for r in rs) / w, 4)
+                    entry["mfma_busy_source"] = msrc
+
+        attach(roofline, lambda n: "gemm_lat_kernel<double" in n)
+        attach(roofline["tile_kernel"], lambda n: n.startswith("void nmgp::gemm_kernel<double"))
+        roofline["code_hash"] = CODE_HASH
+        if chol is not None and mfj is not None:
+            rs = [r for r in mfj["rows"] if "chol_inv7_kernel" in r["kernel"] or "chol_inv3_kernel" in r["kernel"]]
+            w = sum(r["avg_us"] * r["dispatches"] for r in rs)
+            if w:
+                chol["mfma_busy"] = round(sum(r["mfma_util"] * r["avg_us"] * r["dispatches"] for r in rs) / w, 4)
 
     # free the headline workload before the large ELBO leg
     elbo = None
@@ -928,7 +1012,7 @@ def main():
                "pair_sharded_train": pair,
                "api_path": api,
                "phase_ms": breakdown,
-               "final_loss": loss_val}
+               "final_loss": loss_val, "code_hash": CODE_HASH}
         if cpu is not None:
             rec["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
         if breakdown is not None:

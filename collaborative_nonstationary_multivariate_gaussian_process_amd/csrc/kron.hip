@@ -46,84 +46,129 @@ static int kron_product(const T* t1, int64_t r1, int64_t c1, const T* t2, int64_
 }
 
 // Fused Kronecker mat-vec for small P2 (the legacy likelihood: B is P x P over a few outputs, K is N x N).
-// Each wave owns KR consecutive rows n of K and streams them once from HBM in 16-byte loads (lanes over k);
-// y's P2 rows are re-read from L2 for every KR rows (KR-fold reuse).  Per lane: KR x P2 partial sums of
-// work[n, m] = sum_k K[n,k] y[m N2 + k]; a DPP wave reduction (common.hpp wave_sum) completes them in every
-// lane, and lane p < P1 writes out[p N1 + n] = sum_m B[p,m] work[n,m] -- the second GEMM in registers.
-// Bound: HBM, N1 N2 s bytes of K (+ y, B, out: P2 N2 + P1 P2 + P1 N1 elements).
+// One workgroup owns KMV_ROWS consecutive rows n of K and its 256 threads walk those rows together in
+// 16-byte loads (thread t takes vectors t, t + 256, ... of every row), two iterations in flight: per thread
+// 2 x KMV_ROWS nontemporal K loads (K is streamed exactly once and must not evict y from L2) against P2 y
+// loads shared by the KMV_ROWS rows.  Per thread KMV_ROWS x P2 partial sums of
+// work[n, m] = sum_k K[n,k] y[m N2 + k]; DPP wave reductions (common.hpp wave_sum), then the four wave partials
+// are added in wave order through LDS (deterministic), and the second GEMM out[p N1 + n] = sum_m B[p,m]
+// work[n,m] runs on the threads of the block.  P2 is a template parameter so the accumulators are exactly
+// KMV_ROWS x P2 registers.  Bound: HBM, N1 N2 s bytes of K (+ y, B, out: P2 N2 + P1 P2 + P1 N1 elements).
+// Round 5: the round-4 form (one wave per 4 rows, P2 up to 8 in a fixed-size accumulator, one iteration in
+// flight, 512 workgroups) streamed K at 2.6 TB/s.
 constexpr int KMV_MAXP = 8;   // P2 limit of the fused path
-constexpr int KMV_ROWS = 4;   // rows of K per wave
+constexpr int KMV_ROWS = 8;   // rows of K per workgroup
 
-template <typename T, int V>
-__global__ __launch_bounds__(256) void kron_mv_kernel(const T* __restrict__ B, int P1, int P2, const T* __restrict__ K,
-                                                      int N1, int N2, const T* __restrict__ y, T* __restrict__ out) {
-  struct alignas(sizeof(T) * V) Vec { T e[V]; };
-  const int lane = threadIdx.x & 63;
-  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int n0 = wave * KMV_ROWS;
-  if (n0 >= N1) return;
-  T acc[KMV_ROWS][KMV_MAXP];
+template <typename T, int V, int P2>
+__global__ __launch_bounds__(256) void kron_mv_kernel(const T* __restrict__ B, int P1, const T* __restrict__ K, int N1,
+                                                      int N2, const T* __restrict__ y, T* __restrict__ out) {
+  typedef T Vec __attribute__((ext_vector_type(V)));
+  __shared__ T red[4][KMV_ROWS][P2];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n0 = blockIdx.x * KMV_ROWS;
+  const Vec* Kr[KMV_ROWS];
+#pragma unroll
+  for (int r = 0; r < KMV_ROWS; ++r)          // rows past N1 re-read the last row (results unused)
+    Kr[r] = (const Vec*)(K + (int64_t)min(n0 + r, N1 - 1) * N2);
+  const Vec* yv = (const Vec*)y;
+  const int nv = N2 / V;                      // vectors per row (V divides N2 on the vector path)
+  const int ys = nv;                          // y row m starts at vector m * nv
+  T acc[KMV_ROWS][P2];
 #pragma unroll
   for (int r = 0; r < KMV_ROWS; ++r)
 #pragma unroll
-    for (int m = 0; m < KMV_MAXP; ++m) acc[r][m] = (T)0;
-  const int nv = N2 / V;
-  for (int kv = lane; kv < nv; kv += 64) {
-    Vec kr[KMV_ROWS];
+    for (int m = 0; m < P2; ++m) acc[r][m] = (T)0;
+  int kv = tid;
+  for (; kv + 256 < nv; kv += 512) {          // two vectors per thread per iteration, all loads issued first
+    Vec ka[KMV_ROWS], kb[KMV_ROWS], ya[P2], yb[P2];
 #pragma unroll
     for (int r = 0; r < KMV_ROWS; ++r) {
-      const int n = min(n0 + r, N1 - 1);                      // (rows past N1 duplicate the last row; unused)
-      kr[r] = *(const Vec*)(K + (int64_t)n * N2 + (int64_t)kv * V);
+      ka[r] = __builtin_nontemporal_load(Kr[r] + kv);
+      kb[r] = __builtin_nontemporal_load(Kr[r] + kv + 256);
     }
 #pragma unroll
-    for (int m = 0; m < KMV_MAXP; ++m) {
-      if (m < P2) {
-        const Vec yv = *(const Vec*)(y + (int64_t)m * N2 + (int64_t)kv * V);
+    for (int m = 0; m < P2; ++m) {
+      ya[m] = yv[(int64_t)m * ys + kv];
+      yb[m] = yv[(int64_t)m * ys + kv + 256];
+    }
 #pragma unroll
-        for (int r = 0; r < KMV_ROWS; ++r)
+    for (int r = 0; r < KMV_ROWS; ++r)
 #pragma unroll
-          for (int e = 0; e < V; ++e) acc[r][m] = fma(kr[r].e[e], yv.e[e], acc[r][m]);
+      for (int m = 0; m < P2; ++m) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[r][m] = fma(ka[r][e], ya[m][e], acc[r][m]);
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[r][m] = fma(kb[r][e], yb[m][e], acc[r][m]);
       }
-    }
+  }
+  if (kv < nv) {                              // the odd last vector of this thread
+    Vec ka[KMV_ROWS], ya[P2];
+#pragma unroll
+    for (int r = 0; r < KMV_ROWS; ++r) ka[r] = __builtin_nontemporal_load(Kr[r] + kv);
+#pragma unroll
+    for (int m = 0; m < P2; ++m) ya[m] = yv[(int64_t)m * ys + kv];
+#pragma unroll
+    for (int r = 0; r < KMV_ROWS; ++r)
+#pragma unroll
+      for (int m = 0; m < P2; ++m)
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[r][m] = fma(ka[r][e], ya[m][e], acc[r][m]);
   }
 #pragma unroll
   for (int r = 0; r < KMV_ROWS; ++r)
 #pragma unroll
-    for (int m = 0; m < KMV_MAXP; ++m)
-      if (m < P2) acc[r][m] = wave_sum(acc[r][m]);
-  // the second stage: lanes p < P1 (strided over P1 > 64) form out[p N1 + n]
-  for (int p = lane; p < P1; p += 64) {
-#pragma unroll
-    for (int r = 0; r < KMV_ROWS; ++r) {
-      const int n = n0 + r;
-      if (n >= N1) break;
-      T o = (T)0;
-#pragma unroll
-      for (int m = 0; m < KMV_MAXP; ++m)
-        if (m < P2) o = fma(B[(int64_t)p * P2 + m], acc[r][m], o);
-      out[(int64_t)p * N1 + n] = o;
+    for (int m = 0; m < P2; ++m) {
+      const T s = wave_sum(acc[r][m]);
+      if (lane == 0) red[w][r][m] = s;
     }
+  __syncthreads();
+  // the second stage: thread (p, r) forms out[p N1 + n0 + r]; the wave partials are added in wave order
+  for (int q = tid; q < P1 * KMV_ROWS; q += 256) {
+    const int p = q / KMV_ROWS, r = q - p * KMV_ROWS;
+    if (n0 + r >= N1) continue;
+    T o = (T)0;
+#pragma unroll
+    for (int m = 0; m < P2; ++m) {
+      const T wk = ((red[0][r][m] + red[1][r][m]) + red[2][r][m]) + red[3][r][m];
+      o = fma(B[(int64_t)p * P2 + m], wk, o);
+    }
+    out[(int64_t)p * N1 + n0 + r] = o;
+  }
+}
+
+template <typename T, int V>
+static void kron_mv_fused(const T* B, int P1, int P2, const T* K, int N1, int N2, const T* y, T* out, hipStream_t s) {
+  const dim3 grid((unsigned)((N1 + KMV_ROWS - 1) / KMV_ROWS)), blk(256);
+  switch (P2) {
+#define NMGP_KMV_CASE(P)                                                                              \
+  case P:                                                                                             \
+    hipLaunchKernelGGL((kron_mv_kernel<T, V, P>), grid, blk, 0, s, B, P1, K, N1, N2, y, out);         \
+    break;
+    NMGP_KMV_CASE(1) NMGP_KMV_CASE(2) NMGP_KMV_CASE(3) NMGP_KMV_CASE(4)
+    NMGP_KMV_CASE(5) NMGP_KMV_CASE(6) NMGP_KMV_CASE(7) NMGP_KMV_CASE(8)
+#undef NMGP_KMV_CASE
   }
 }
 
 template <typename T>
 static int kron_mv(const T* B, int64_t P1, int64_t P2, const T* K, int64_t N1, int64_t N2, const T* y, T* out, T* work,
                    hipStream_t s, int (*gemm)(const nmgp_gemm_desc*, const int32_t*, hipStream_t)) {
+  if (P1 < 0 || P2 < 0) return -2;
+  if (N1 < 0 || N2 < 0) return -5;
+  if (P1 == 0 || N1 == 0) return NMGP_OK;    // empty output
+  if (!out) return -8;
+  if (P2 == 0 || N2 == 0)                    // an empty contraction (B, K or y may be NULL): out = 0
+    return hipMemsetAsync(out, 0, (size_t)(P1 * N1) * sizeof(T), s) == hipSuccess ? NMGP_OK : NMGP_ERR_LAUNCH;
   if (!B) return -1;
   if (!K) return -4;
   if (!y) return -7;
-  if (!out) return -8;
-  if (P1 == 0 || N1 == 0) return NMGP_OK;
-  if (P2 >= 1 && P2 <= KMV_MAXP && N2 >= 1 && N1 < (1LL << 30) && N2 < (1LL << 30)) {
-    const unsigned grid = (unsigned)((N1 + 4 * KMV_ROWS - 1) / (4 * KMV_ROWS));
+  if (P2 >= 1 && P2 <= KMV_MAXP && N1 < (1LL << 30) && N2 < (1LL << 30)) {
     constexpr int V = 16 / (int)sizeof(T);
     const bool vec = N2 % V == 0 && ((uintptr_t)K & 15) == 0 && ((uintptr_t)y & 15) == 0;
     if (vec)
-      hipLaunchKernelGGL((kron_mv_kernel<T, V>), dim3(grid), dim3(256), 0, s, B, (int)P1, (int)P2, K, (int)N1, (int)N2,
-                         y, out);
+      kron_mv_fused<T, V>(B, (int)P1, (int)P2, K, (int)N1, (int)N2, y, out, s);
     else
-      hipLaunchKernelGGL((kron_mv_kernel<T, 1>), dim3(grid), dim3(256), 0, s, B, (int)P1, (int)P2, K, (int)N1, (int)N2,
-                         y, out);
+      kron_mv_fused<T, 1>(B, (int)P1, (int)P2, K, (int)N1, (int)N2, y, out, s);
     NMGP_CHECK_LAUNCH();
     return NMGP_OK;
   }

@@ -445,10 +445,10 @@ class DsviEngine:
                 d17P.append(g(self.Pbar, self.WP, th, B, M, i * M, (M, 1, BM), (1, M, MM), (M, 1),
                               flags=L.B_UPPER, kb=(M, M), beta=1.0, offs=(0, sU + pq(i, 0) * MM, 1 * BM), row_seg=i))
         # the latent P-bar_G products feed R_G on the main chain; the pair P-bar_0/1 products feed only the
-        # L0 / L1 prior adjoints and run on the third side stream.  P-bar_G caps its k loops at 20 k-tiles per
-        # workgroup in fp64 (output D-1's tiles otherwise run all D latent blocks, 40 k-tiles at PM2.5; round-3
-        # A/B on the box: 1370-1379 -> 1386-1400 it/s, profiles/r03za_kt_cap_ab.txt).  fp32 engines keep the
-        # automatic split (their gates were measured with it).
+        # L0 / L1 prior adjoints and run on the third side stream.  In the per-factor Z_d form every P-bar_G
+        # problem has k = M (a short loop of M/32 k-tiles), so no k-tile cap is needed.  (History: the round-3
+        # per-output form ran k = (i + 1) M loops and capped them at 20 k-tiles per workgroup in fp64,
+        # profiles/r03za_kt_cap_ab.txt.)
         p["bwd_wG"] = G(d17G)
         p["bwd_wP"] = G(d17P) if d17P else None
         d17 = []

@@ -375,6 +375,23 @@ def desc_macs(d, seg=None):
     return int(cnt.sum()) * nblk
 
 
+def chol_inv_rec_macs(n):
+    """Multiply-adds of the GEMMs one recursive factor + inverse of an n x n matrix issues (csrc/chol.hip
+    chol_inv_rec_big / chol_inv_rec: split at n1 = the multiple of 128 nearest above n/2; L21 = A21 X11^T,
+    A22 -= L21 L21^T (lower), T = L21 X11, X21 = -X22 T; leaves n <= 128 run in the fused kernel, not counted)."""
+    import types
+    if n <= 128:
+        return 0
+    n1 = ((n // 2 + 127) // 128) * 128
+    if n1 >= n:
+        n1 = n - 128
+    n2 = n - n1
+    d = lambda m_, n_, k_, f: desc_macs(types.SimpleNamespace(m=m_, n=n_, k=k_, flags=f, row_seg=-1, k_seg=-1,
+                                                              seg_span=0, kbA=0))
+    return (chol_inv_rec_macs(n1) + chol_inv_rec_macs(n2) + d(n2, n1, n1, L.B_UPPER) + d(n2, n2, n1, L.OUT_LOWER)
+            + d(n2, n1, n1, L.B_LOWER) + d(n2, n1, n2, L.A_LOWER))
+
+
 def gemm_single(desc, dtype, seg=None):
     fn = getattr(L.lib(), "nmgp_gemm_" + _sfx(dtype))
     L.check(fn(ctypes.byref(desc), ctypes.c_void_p(seg.data_ptr()) if seg is not None else None,
@@ -529,6 +546,18 @@ class BigBatch:
             self.kseg = (seg, i32(ks), i32(sp))
         self.args = (m, n, k, lda, a_kcontig, ldb, b_kcontig, sC if sC is not None else (n, 1), flags, alpha, beta,
                      diag_add)
+
+    def macs(self, seg=None):
+        """Algorithmic multiply-adds of the batch (desc_macs per problem: triangular zeros and skipped output
+        halves not counted; per-problem k from the host copy `seg` of the segment table with kseg)."""
+        import types
+        m, n, k, _, _, _, _, _, flags, _, _, _ = self.args
+        if self.kseg is None:
+            return self.batch * desc_macs(types.SimpleNamespace(m=m, n=n, k=k, flags=flags, row_seg=-1, k_seg=-1,
+                                                                seg_span=0, kbA=0))
+        ks, sp = self.kseg[1].tolist(), self.kseg[2].tolist()
+        return sum(desc_macs(types.SimpleNamespace(m=m, n=n, k=k, flags=flags, row_seg=-1, k_seg=a, seg_span=b,
+                                                   kbA=0), seg) for a, b in zip(ks, sp))
 
     def __call__(self, stream=None):
         if self.batch == 0:
@@ -791,9 +820,12 @@ class HipGraph:
             cur = torch.cuda.current_stream(g.device)
             g.stream.wait_stream(cur)           # everything enqueued before the capture comes first
             torch.cuda.synchronize(g.device)    # (and is finished: a capture must not wait on pending work)
+            # the body must not allocate through torch: torch does not know a capture is running, so a block
+            # allocated (and freed) inside it would be handed out again while the graph still writes into it
+            self.alloc0 = torch.cuda.memory_stats(g.device).get("allocation.all.allocated", 0)
+            L.check(L.lib().nmgp_graph_begin(ctypes.c_void_p(g.stream.cuda_stream)), "graph_begin")
             self.ctx = torch.cuda.stream(g.stream)
             self.ctx.__enter__()
-            L.check(L.lib().nmgp_graph_begin(ctypes.c_void_p(g.stream.cuda_stream)), "graph_begin")
             return g
 
         def __exit__(self, et, ev, tb):
@@ -801,9 +833,19 @@ class HipGraph:
             ex = ctypes.c_void_p()
             rc = L.lib().nmgp_graph_end(ctypes.c_void_p(g.stream.cuda_stream), ctypes.byref(ex))
             self.ctx.__exit__(et, ev, tb)
-            if et is None:
-                L.check(rc, "graph_end")
-                g.exec = ex
+            if et is not None or rc != 0:
+                if rc == 0 and ex.value:        # the body raised after a clean capture: drop the graph
+                    L.lib().nmgp_graph_destroy(ex)
+                if et is None:
+                    L.check(rc, "graph_end")
+                return False
+            allocs = torch.cuda.memory_stats(g.device).get("allocation.all.allocated", 0) - self.alloc0
+            if allocs:
+                if ex.value:
+                    L.lib().nmgp_graph_destroy(ex)
+                raise RuntimeError(f"HipGraph capture body allocated {allocs} block(s) through torch; captured "
+                                   "bodies must use preallocated buffers")
+            g.exec = ex
             return False
 
     def capture(self):

@@ -738,7 +738,8 @@ def test_kron(ops):
 
 
 @pytest.mark.parametrize("P1,P2,N1,N2", [(5, 5, 4096, 4096), (3, 8, 37, 61), (70, 2, 131, 64), (6, 9, 50, 40),
-                                         (1, 1, 1, 1), (8, 3, 1000, 1001)])
+                                         (1, 1, 1, 1), (8, 3, 1000, 1001), (7, 5, 2049, 3000), (2, 4, 9, 514),
+                                         (4, 0, 10, 10), (3, 2, 10, 0), (12, 0, 5, 6)])
 @pytest.mark.parametrize("dt", [F64, torch.float32])
 def test_kron_mv_fused_and_gemm_paths(ops, P1, P2, N1, N2, dt):
     """kron_mv (kronecker_operation.py:72-85): P2 <= 8 takes the fused one-pass kernel (16-byte rows when N2
@@ -751,6 +752,9 @@ def test_kron_mv_fused_and_gemm_paths(ops, P1, P2, N1, N2, dt):
     mv = ops.kron_mv(Bk.to(dt).to(DEV), Kk.to(dt).to(DEV), y.to(dt).to(DEV)).double().cpu()
     Bc, Kc, yc = Bk.to(dt).double(), Kk.to(dt).double(), y.to(dt).double()
     tol = 1e-13 if dt == F64 else 2e-5          # (fp32: sums of up to 8 x 4096 products)
+    if P2 == 0 or N2 == 0:                      # an empty contraction: exactly zero (no work buffer needed)
+        assert mv.shape == (P1 * N1,) and torch.equal(mv, torch.zeros(P1 * N1, dtype=F64))
+        return
     assert rel(mv, O.kron_mv(Bc, Kc, yc)) < tol
     if N1 * N2 <= 10 ** 6:
         assert rel(mv, torch.kron(Bc, Kc) @ yc) < tol

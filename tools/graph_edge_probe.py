@@ -8,6 +8,14 @@ fails (no GPU work after a crash).  Output: one JSON line per pattern.
 
   python tools/graph_edge_probe.py [pattern ...]
 """
+import os as _os
+import sys as _sys
+
+if _os.environ.get("NMGP_RUN_KNOWN_CRASH") != "1":
+    # Its crashing variants segfault in hipStreamEndCapture of torch's bundled ROCm 7.0 runtime (result recorded
+    # in DESIGN.md §4).  Not run by default: a known crash is not worth GPU time (VERDICT r04 item 9).
+    print("graph edge probe: known-crash bisection, recorded in DESIGN.md §4; set NMGP_RUN_KNOWN_CRASH=1 to re-run")
+    _sys.exit(0)
 import json
 import os
 import subprocess

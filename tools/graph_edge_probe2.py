@@ -9,6 +9,14 @@ Each variant runs in its own process (a segfault ends only that variant):
   torch_ev_libk  torch events, the library's kernels
 usage: python tools/graph_edge_probe2.py            (driver: runs every variant, prints one line each)
        python tools/graph_edge_probe2.py <variant>  (one variant)"""
+import os as _os
+import sys as _sys
+
+if _os.environ.get("NMGP_RUN_KNOWN_CRASH") != "1":
+    # Its crashing variants segfault in hipStreamEndCapture of torch's bundled ROCm 7.0 runtime (result recorded
+    # in DESIGN.md §4).  Not run by default: a known crash is not worth GPU time (VERDICT r04 item 9).
+    print("graph edge probe: known-crash bisection, recorded in DESIGN.md §4; set NMGP_RUN_KNOWN_CRASH=1 to re-run")
+    _sys.exit(0)
 import ctypes
 import os
 import subprocess

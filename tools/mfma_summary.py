@@ -6,7 +6,11 @@ usage: python tools/mfma_summary.py <run_counter_collection.csv> <out.json> [--c
 import collections
 import csv
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from provenance import code_hash  # noqa: E402
 
 
 def main():
@@ -44,7 +48,7 @@ def main():
                      "avg_us": round(ns / len(ds) / 1e3, 2), "clock_ghz": round(cyc / ns, 3),
                      "mfma_util": round(busy / (cyc * 4 * cus), 4), "cu_busy": round(cu / (cyc * cus), 4)})
     json.dump({"source": src, "definition": "mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 4 * CUs)",
-               "rows": rows}, open(out, "w"), indent=1)
+               "code_hash": code_hash(), "rows": rows}, open(out, "w"), indent=1)
     if by_grid:
         rows.sort(key=lambda r: -r["avg_us"] * r["dispatches"])
     for r in rows:

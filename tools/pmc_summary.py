@@ -14,6 +14,9 @@ import os
 import sys
 from collections import defaultdict
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from provenance import code_hash  # noqa: E402
+
 
 def per_kernel(counter_dir, counter):
     f = glob.glob(os.path.join(counter_dir, "*counter_collection.csv"))[0]
@@ -29,7 +32,7 @@ def main():
     stats = list(csv.DictReader(open(glob.glob(os.path.join(trace, "*kernel_stats.csv"))[0])))
     fetch = per_kernel(fdir, "FETCH_SIZE")
     write = per_kernel(wdir, "WRITE_SIZE")
-    out = {"kernels": []}
+    out = {"code_hash": code_hash(), "kernels": []}
     for r in stats:
         name = r["Name"]
         e = {"name": name, "calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3,

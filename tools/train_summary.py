@@ -6,7 +6,11 @@ usage: python tools/train_summary.py <run_kernel_trace.csv> <train_leg.json> <ou
 import collections
 import csv
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from provenance import code_hash  # noqa: E402
 
 
 def short(name):
@@ -32,7 +36,7 @@ def main():
     wall = (t1 - t0) / 1e6 / steps
     tot = sum(busy.values()) / steps
     top = sorted(busy.items(), key=lambda kv: -kv[1])
-    out = {"source": sys.argv[1], "config": leg["workload"], "steps": steps,
+    out = {"code_hash": code_hash(), "source": sys.argv[1], "config": leg["workload"], "steps": steps,
            "wall_ms_per_step_under_trace": round(wall, 4), "bench_s_per_step": leg["s_per_step"],
            "kernel_busy_ms_per_step": round(tot, 4),
            "kernels": [{"kernel": k, "ms_per_step": round(v / steps, 4), "share_of_busy": round(v / steps / tot, 4),
