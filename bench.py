@@ -745,7 +745,6 @@ def main():
 
     from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP, DsviTrainer
     from collaborative_nonstationary_multivariate_gaussian_process_amd.engine import param_layout
-    from collaborative_nonstationary_multivariate_gaussian_process_amd import distributed as DD
 
     xs, ys = synth_data(rank)
     z = np.linspace(0, 1, M)
@@ -773,25 +772,25 @@ def main():
 
     if world > 1:
         dist.broadcast(model._theta, 0)
-    graph, upd_graph = None, None
+    graph = None
     if not args.eager:
-        graph = trainer.capture(eng, include_update=(world == 1))
         if world > 1:
-            upd_graph = trainer.capture_update(world)
+            # gradient graph (with an external event node where the sqrt_W / sqrt_U rows are final) and the
+            # 1/world + Adam graph; the bucketed RCCL all-reduce between them overlaps the backward's tail
+            graph = trainer.capture_dp(eng, world)[0]
+        else:
+            graph = trainer.capture(eng, include_update=True)
 
     def step(i):
-        if graph is not None:
+        if graph is not None and world > 1:
+            trainer.dp_graph_step(eng)                       # graph | overlapped bucketed all-reduce | update
+        elif graph is not None:
             graph.replay()
+        elif world > 1:
+            trainer.dp_grad_step(eng)                        # eager: the same buckets, hooked on lbar_done
+            trainer.update()
         else:
             trainer.grad_step(eng)
-        if world > 1:
-            if upd_graph is not None:
-                DD.allreduce_sum_(model._grad)               # one RCCL all-reduce of the flat gradient
-                upd_graph.replay()                           # 1/world + Adam, replayed from their own graph
-            else:
-                DD.allreduce_mean_(model._grad)
-                trainer.update()
-        elif graph is None:
             trainer.update()
 
     for i in range(args.warmup):

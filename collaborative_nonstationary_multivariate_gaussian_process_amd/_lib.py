@@ -82,6 +82,10 @@ _SIGS = {
     "nmgp_graph_end": (c_int, [c_vp, ctypes.POINTER(c_vp)]),
     "nmgp_graph_launch": (c_int, [c_vp, c_vp]),
     "nmgp_graph_destroy": (c_int, [c_vp]),
+    "nmgp_event_create": (c_int, [ctypes.POINTER(c_vp)]),
+    "nmgp_event_destroy": (c_int, [c_vp]),
+    "nmgp_event_record_external": (c_int, [c_vp, c_vp]),
+    "nmgp_stream_wait_event": (c_int, [c_vp, c_vp]),
     "nmgp_device_status": (c_int, [ctypes.POINTER(ctypes.c_uint32), c_int]),
     "nmgp_sizeof_gemm_desc": (c_i64, []),
     "nmgp_sizeof_pairwise_desc": (c_i64, []),

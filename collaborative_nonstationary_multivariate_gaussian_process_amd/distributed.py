@@ -59,6 +59,30 @@ def allreduce_sum_(t, group=None):
     return t
 
 
+def grad_buckets(offs, grad):
+    """The two all-reduce buckets of the flat DSVI gradient (engine.param_layout offsets `offs`):
+    big   -- the sqrt_W and sqrt_U rows: final once the side stream's L-bar products are done (the engine's
+             "lbar_done" point), > 99% of the bytes at the HCP / ECoG shapes, 64% at PM2.5;
+    small -- everything else (mu_W, mu_v, sqrt_v, mu_U, hyper-parameters): final at the end of the step.
+    Views into `grad`; together they cover it exactly once."""
+    import numpy as np
+    n_sW = int(np.prod(offs["sqrt_W"][1]))
+    n_sU = int(np.prod(offs["sqrt_U"][1]))
+    big = [grad[offs["sqrt_W"][0]:offs["sqrt_W"][0] + n_sW], grad[offs["sqrt_U"][0]:offs["sqrt_U"][0] + n_sU]]
+    small = [grad[0:offs["sqrt_W"][0]], grad[offs["mu_v"][0]:offs["sqrt_U"][0]],
+             grad[offs["sigma2_tildeell_log"][0]:]]
+    return big, small
+
+
+def bucketed_allreduce_sum_(buckets, group=None):
+    """SUM all-reduce of each view in `buckets` (in order, asynchronously); returns the works.  The element-wise
+    sums are those of one all-reduce of the whole vector."""
+    rank, world = world_info(group)
+    if world <= 1:
+        return []
+    return [dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True) for t in buckets if t.numel()]
+
+
 def sample_ids(n_sample, rank, world):
     """Monte-Carlo samples owned by `rank` (round-robin)."""
     return list(range(rank, int(n_sample), int(world)))

@@ -1063,6 +1063,9 @@ class DsviEngine:
                     hook = getattr(self, "hooks", {}).get(tag)
                     if hook is not None:           # e.g. start a gradient bucket's all-reduce
                         hook(ev)
+                    ext = getattr(self, "ext_events", {}).get(tag)
+                    if ext is not None:            # an external event node of a captured graph (dp_graph_step)
+                        ext.record(st)
                 else:
                     st.wait_event(events[tag])
                 continue

@@ -867,6 +867,32 @@ class HipGraph:
             self.exec = None
 
 
+class ExtEvent:
+    """A HIP event that a captured graph records as an EXTERNAL event node (nmgp_event_record_external): after
+    the graph is launched, `wait(stream)` makes a stream outside the graph wait for that point INSIDE the replay
+    (outside a capture the record is an ordinary event record)."""
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        L.check(L.lib().nmgp_event_create(ctypes.byref(h)), "event_create")
+        self.h = h
+
+    def record(self, stream):
+        L.check(L.lib().nmgp_event_record_external(self.h, ctypes.c_void_p(stream.cuda_stream)), "event_record")
+
+    def wait(self, stream):
+        L.check(L.lib().nmgp_stream_wait_event(ctypes.c_void_p(stream.cuda_stream), self.h), "stream_wait_event")
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value and L._lib is not None:
+            try:
+                L._lib.nmgp_event_destroy(h)
+            except Exception:
+                pass
+            self.h = None
+
+
 # ------------------------------------------------------------------------------------ optimiser / rng
 def adam_(theta, grad, m, v, step, lr, betas=(0.9, 0.999), eps=1e-8):
     fn = getattr(L.lib(), "nmgp_adam_" + _sfx(theta.dtype))

@@ -533,35 +533,71 @@ class DsviTrainer:
         stream runs the rest of the backward (R / prior adjoints / t chain / v chain / finalize).  The
         small remainder (mu rows, sqrt_v, hyper-parameters) is reduced after the step.  The element-wise
         sums are those of one all-reduce of the whole vector, so results are identical."""
-        import torch.distributed as dist
         mdl = self.model
         rank, world = DD.world_info(group)
-        o = mdl._offs
         g = mdl._grad
-        n_sW = int(np.prod(o["sqrt_W"][1]))
-        n_sU = int(np.prod(o["sqrt_U"][1]))
-        big = [g[o["sqrt_W"][0]:o["sqrt_W"][0] + n_sW], g[o["sqrt_U"][0]:o["sqrt_U"][0] + n_sU]]
-        small = [g[0:o["sqrt_W"][0]], g[o["mu_v"][0]:o["sqrt_U"][0]], g[o["sigma2_tildeell_log"][0]:]]
-        if getattr(self, "_comm", None) is None:
-            self._comm = torch.cuda.Stream(device=mdl.device_)
+        big, small = DD.grad_buckets(mdl._offs, g)
+        comm = self._comm_stream()
         works = []
 
         def start(ev):
-            with torch.cuda.stream(self._comm):
-                self._comm.wait_event(ev)
-                for t in big:
-                    works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True))
+            with torch.cuda.stream(comm):
+                comm.wait_event(ev)
+                works.extend(DD.bucketed_allreduce_sum_(big, group))
         eng.hooks = {"lbar_done": start}
         try:
             loss = self.grad_step(eng, noise=noise)
         finally:
             eng.hooks = {}
-        for t in small:
-            works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True))
+        works.extend(DD.bucketed_allreduce_sum_(small, group))
         for w in works:
             w.wait()
         g.div_(world)
         return loss
+
+    def _comm_stream(self):
+        if getattr(self, "_comm", None) is None:
+            self._comm = torch.cuda.Stream(device=self.model.device_)
+        return self._comm
+
+    def capture_dp(self, eng, world):
+        """The data-parallel step as two graphs around an overlapped, bucketed all-reduce (dp_graph_step):
+        the gradient graph of `eng` with an EXTERNAL event node at "lbar_done" (hip_ops.ExtEvent: the point
+        after which the sqrt_W / sqrt_U gradient rows are final), and the update graph (1/world + Adam)."""
+        if "lbar_done" not in getattr(eng, "ext_events", {}):
+            eng.ext_events = {"lbar_done": H.ExtEvent()}
+        g = self.capture(eng, include_update=False)
+        if not hasattr(self, "_dp_graphs"):
+            self._dp_graphs = {}
+        self._dp_graphs[id(eng)] = (g, eng.ext_events["lbar_done"], self.capture_update(world))
+        return self._dp_graphs[id(eng)]
+
+    def dp_graph_step(self, eng, group=None):
+        """One data-parallel step on the graph path (SURVEY §8e axis 2; the reference's loss.backward();
+        optimizer.step(), code/nmgp_dsvi.py:847-854, with the gradient average between them):
+          main:  replay the gradient graph ........................ | wait comm | replay 1/world + Adam
+          comm:  wait for the graph's lbar_done node -> all-reduce(sqrt_W, sqrt_U rows)
+                 wait for the graph's end -> all-reduce(the small remainder)
+        The sqrt rows' all-reduce runs while the graph's remaining backward (R, prior adjoints, t and v chains,
+        finalize: none of them touches those rows) still runs.  Sums are element-wise those of one flat
+        all-reduce, so the result equals the flat path bit for bit."""
+        mdl = self.model
+        rank, world = DD.world_info(group)
+        dpg = getattr(self, "_dp_graphs", {}).get(id(eng))
+        g, ev, upd = dpg if dpg is not None else self.capture_dp(eng, world)
+        main = torch.cuda.current_stream(mdl.device_)
+        comm = self._comm_stream()
+        big, small = DD.grad_buckets(mdl._offs, mdl._grad)
+        g.replay()
+        ev.wait(comm)                     # the graph's external lbar_done node (recorded at its launch)
+        with torch.cuda.stream(comm):
+            works = DD.bucketed_allreduce_sum_(big, group)
+            comm.wait_stream(main)        # the end of the gradient graph
+            works += DD.bucketed_allreduce_sum_(small, group)
+        for w in works:
+            w.wait()                      # (nccl: the current stream waits for the collective)
+        main.wait_stream(comm)
+        upd.replay()
 
     def update(self):
         """torch.optim.Adam update of the flat parameter vector (one HIP launch)."""
@@ -722,9 +758,13 @@ class _DevicePipeline:
             plan.append(self.slots[b.numel()])
         return plan
 
-    def step(self, sl):
+    def step(self, sl, group=None):
         tr = self.trainer
-        if self.use_graph:
+        if self.use_graph and self.world > 1:
+            # data parallel on the graph path: gradient graph, bucketed all-reduce overlapped with its tail
+            # (the sqrt rows from the graph's lbar_done node on), update graph
+            tr.dp_graph_step(sl["eng"], group)
+        elif self.use_graph:
             if sl["graph"] is None:
                 sl["graph"] = tr.capture(sl["eng"], include_update=self.include_update)
             sl["graph"].replay()
@@ -759,10 +799,9 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
     """
     rank, world = DD.world_info(group) if distributed else (0, 1)
     if use_graph is None:
-        # data parallel with a large gradient (HCP / ECoG shapes): eager launches, so the bucketed
-        # all-reduce can overlap the backward (DsviTrainer.dp_grad_step); otherwise one graph per step
-        big_grad = world > 1 and _param_bytes(dim_outputs, len(np.asarray(z).reshape(-1)), dtype) > (64 << 20)
-        use_graph = noise == "device" and not big_grad
+        # device noise: one graph per step; data parallel on the graph path overlaps the bucketed all-reduce
+        # with the backward's tail (DsviTrainer.dp_graph_step), as the eager dp_grad_step does
+        use_graph = noise == "device"
     if use_graph and noise != "device":
         raise ValueError("use_graph=True needs noise='device' (host RNG cannot be replayed)")
     X_train_vec = np.concatenate(X_train_list)
@@ -838,13 +877,9 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
                     trainer.dp_grad_step(eng, group)        # bucketed all-reduce overlapped with the backward
                     trainer.update()
                 else:
-                    eng = pipe.step(sl)
-                    if world > 1 and use_graph:
-                        DD.allreduce_sum_(model._grad, group)
-                        trainer.capture_update(world).replay()     # 1/world + Adam as one graph
-                    elif world > 1:
-                        DD.allreduce_mean_(model._grad, group)
-                        trainer.update()
+                    # (world > 1: DsviTrainer.dp_graph_step -- gradient graph, bucketed all-reduce overlapped
+                    # with its tail, 1/world + Adam graph)
+                    eng = pipe.step(sl, group)
                 losses_dev.append(eng.out[0].clone())
                 ev = torch.cuda.Event(enable_timing=True)
                 ev.record()
@@ -922,10 +957,6 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
         rmse_test_list = [np.float64(v) for v in torch.stack(rmse_dev).cpu().numpy()] if rmse_dev else []
         return model, loss_list, rmse_test_list, time_list
     return model, loss_list, time_list
-
-
-def _param_bytes(D, M, dtype):
-    return param_layout(D, M)[1] * (8 if dtype == F64 else 4)
 
 
 def _adam_state_dict(model, trainer):

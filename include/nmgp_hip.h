@@ -468,6 +468,17 @@ int nmgp_graph_end(hipStream_t stream, void** exec_out);
 int nmgp_graph_launch(void* exec, hipStream_t stream);
 int nmgp_graph_destroy(void* exec);
 
+/* Events a captured step graph records as EXTERNAL event nodes (hipEventRecordWithFlags(...,
+ * hipEventRecordExternal)): a stream outside the graph can wait on a point INSIDE a replayed step -- the
+ * data-parallel step starts the all-reduce of the gradient rows that are final at that point (the sqrt_W /
+ * sqrt_U rows after the L-bar products) while the rest of the backward still runs (SURVEY §8e axis 2; the
+ * reference's loss.backward(); optimizer.step(), code/nmgp_dsvi.py:847-854, has no such overlap).  Outside a
+ * capture the record is a plain event record.  Handles are opaque (hipEvent_t, timing disabled).         */
+int nmgp_event_create(void** event_out);
+int nmgp_event_destroy(void* event);
+int nmgp_event_record_external(void* event, hipStream_t stream);
+int nmgp_stream_wait_event(hipStream_t stream, void* event);
+
 #ifdef __cplusplus
 }
 #endif

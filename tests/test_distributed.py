@@ -350,3 +350,44 @@ def test_pair_shard_ranges_cover_outputs(D, world):
                     nxt[key] = v
         best = nxt
     assert max(loads) == best[(world, D)]
+
+
+def _bucketed_vs_flat(rank):
+    """distributed.grad_buckets + bucketed_allreduce_sum_ (the data-parallel step's two buckets) against one
+    all-reduce of the flat vector: the buckets tile the gradient exactly once; with integer-valued gradients
+    (exact sums) the result is bit-identical for any world size, with random ones bit-identical at world 2
+    (a + b commutes) and within rounding above it -- a ring reduction's summation order depends on where an
+    element falls in the ring's chunks, so bucketing may reorder a 3+-term sum.  Every rank ends identical."""
+    import numpy as np
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import distributed as DD
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.engine import param_layout
+    world = dist.get_world_size()
+    offs, n = param_layout(4, 16)
+    gen = torch.Generator().manual_seed(11 + rank)
+    cases = [torch.randint(-2 ** 20, 2 ** 20, (n,), generator=gen).to(torch.float64),
+             torch.randn(n, dtype=torch.float64, generator=gen) * (10.0 ** rank)]
+    for exact, g0 in zip((True, world == 2), cases):
+        flat = g0.clone()
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+        g = g0.clone()
+        big, small = DD.grad_buckets(offs, g)
+        cover = np.zeros(n, np.int64)
+        for t in big + small:
+            o = (t.data_ptr() - g.data_ptr()) // g.element_size()
+            cover[o:o + t.numel()] += 1
+        assert (cover == 1).all()
+        for w in DD.bucketed_allreduce_sum_(big) + DD.bucketed_allreduce_sum_(small):
+            w.wait()
+        if exact:
+            assert torch.equal(g, flat)
+        else:
+            assert float((g - flat).abs().max() / flat.abs().max()) < 1e-15
+        allg = [torch.empty_like(g) for _ in range(world)]
+        dist.all_gather(allg, g)
+        assert all(torch.equal(allg[0], t) for t in allg)
+    return True
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bucketed_allreduce_equals_flat(world):
+    assert all(_run(_bucketed_vs_flat, world=world))

@@ -162,3 +162,58 @@ def test_data_parallel_overlapped_allreduce_equals_single():
         assert np.array_equal(eager[0], graph[0])
         assert eager[1] == graph[1]
     assert np.array_equal(outs[0][0][0], outs[1][0][0])
+
+
+def _dp_graph_bucketed_vs_flat(rank):
+    """The data-parallel step on the graph path (DsviTrainer.dp_graph_step: gradient graph with an external
+    event node at lbar_done, the sqrt_W / sqrt_U bucket all-reduced from that node on while the backward's
+    tail runs, then the remainder, then the 1/world + Adam graph) against the flat form (gradient graph, ONE
+    all-reduce of the whole vector, update graph): identical parameters after 4 steps (two ranks: a + b
+    commutes, so the sums are bit-identical)."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP, DsviTrainer
+    from tests import _golden as G
+    g = G.load("toy_elbo")
+    xs, ys = G.split_lists(g)
+    half = [slice(0, len(x) // 2) if rank == 0 else slice(len(x) // 2, len(x)) for x in xs]
+    xr = [x[h] for x, h in zip(xs, half)]
+    yr = [y[h] for y, h in zip(ys, half)]
+    thetas = []
+    for bucketed in (False, True):
+        model = NMGP(number_observations=int(g["N"]), dim_outputs=2, Z=g["z"], seed=22, device="cuda:0",
+                     noise="device")
+        model._noise_seed = 22 + 7919 * rank
+        tr = DsviTrainer(model, lr=0.005)
+        x, y, sizes = model._prepare(xr, yr)
+        eng = model.engine(sum(sizes))
+        eng.load_batch(x, y, sizes)
+        if bucketed:
+            tr.capture_dp(eng, WORLD)
+        else:
+            gg, upd = tr.capture(eng, include_update=False), tr.capture_update(WORLD)
+        for _ in range(4):
+            if bucketed:
+                tr.dp_graph_step(eng)
+            else:
+                gg.replay()
+                dist.all_reduce(model._grad, op=dist.ReduceOp.SUM)
+                upd.replay()
+        torch.cuda.synchronize()
+        thetas.append(model._theta.detach().cpu().numpy())
+    return thetas
+
+
+def test_data_parallel_graph_bucketed_allreduce_equals_flat():
+    outs = _run(_dp_graph_bucketed_vs_flat)
+    for flat, bucketed in outs:
+        assert np.all(np.isfinite(flat))
+        assert np.array_equal(flat, bucketed)
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert not np.array_equal(outs[0][1], _toy_theta0())       # the steps moved the parameters
+
+
+def _toy_theta0():
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP
+    from tests import _golden as G
+    g = G.load("toy_elbo")
+    return NMGP(number_observations=int(g["N"]), dim_outputs=2, Z=g["z"], seed=22,
+                device="cuda:0")._theta.detach().cpu().numpy()

@@ -984,3 +984,43 @@ def test_training_step_graph_is_captured_through_hip(ops):
         torch.cuda.synchronize()
         res.append((float(eng.out[0]), model._grad.detach().cpu().clone()))
     assert res[0][0] == res[1][0] and torch.equal(res[0][1], res[1][1])
+
+
+def test_hip_graph_external_event_node_fires_mid_replay(ops):
+    """nmgp_event_record_external inside a capture becomes an external event node: after the graph is
+    launched, a stream OUTSIDE the graph that waits on the event runs as soon as that point of the replay is
+    reached -- not at the graph's end.  Graph: x = 1 -> [event] -> ~10 ms of GEMMs -> y = 1; the outside
+    stream copies (x, y) after its wait: x must be 1 (ordering) and y still 0 (it ran mid-replay).  This is
+    what DsviTrainer.dp_graph_step builds the overlapped all-reduce on."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L
+    x = torch.zeros(1, dtype=F64, device=DEV)
+    y = torch.zeros(1, dtype=F64, device=DEV)
+    out = torch.full((2, 3), -1.0, dtype=F64, device=DEV)
+    Ab = torch.rand(4096, 4096, device=DEV)
+    Cb = torch.zeros(4096, 4096, device=DEV)
+    ws = ops.big_workspace(DEV, L.lib().nmgp_gemm_big_workspace_size())
+    ops.gemm_big(Ab, Ab, Cb, ws=ws)                    # warm-up (attributes, workspace)
+    ev = ops.ExtEvent()
+    g = ops.HipGraph(DEV)
+    with g.capture():
+        main = torch.cuda.current_stream(DEV)
+        x.zero_()
+        y.zero_()
+        x.fill_(1.0)
+        ev.record(main)
+        for _ in range(8):
+            ops.gemm_big(Ab, Ab, Cb, ws=ws)
+        y.fill_(1.0)
+    comm = torch.cuda.Stream(device=DEV)
+    torch.cuda.synchronize()
+    for rep in range(3):
+        g.replay()
+        ev.wait(comm)
+        with torch.cuda.stream(comm):
+            out[0, rep].copy_(x[0])
+            out[1, rep].copy_(y[0])
+        torch.cuda.current_stream(DEV).wait_stream(comm)
+    torch.cuda.synchronize()
+    o = out.cpu()
+    assert torch.equal(o[0], torch.ones(3, dtype=F64)), o
+    assert torch.equal(o[1], torch.zeros(3, dtype=F64)), o
