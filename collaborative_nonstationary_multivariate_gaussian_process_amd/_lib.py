@@ -49,6 +49,10 @@ class PairwiseBwdDesc(ctypes.Structure):
                 ("tile_start", c_int), ("pad_", c_int), ("scale2", c_dbl), ("length_scale", c_dbl)]
 
 
+class PairDesc(ctypes.Structure):
+    _fields_ = [("a_off", c_i64), ("l_off", c_i64), ("c_off", c_i64), ("seg", c_int), ("pad", c_int)]
+
+
 class DsviArgs(ctypes.Structure):
     _fields_ = [("D", c_int), ("M", c_int), ("B", c_int), ("Q", c_int), ("NF", c_int), ("elbo_mode", c_int),
                 ("frozen_mask", c_int), ("pair_packed", c_int), ("N_over_B", c_dbl), ("jitter", c_dbl),
@@ -88,6 +92,17 @@ _SIGS = {
     "nmgp_stream_wait_event": (c_int, [c_vp, c_vp]),
     "nmgp_device_status": (c_int, [ctypes.POINTER(ctypes.c_uint32), c_int]),
     "nmgp_sizeof_gemm_desc": (c_i64, []),
+    "nmgp_sizeof_pair_desc": (c_i64, []),
+    "nmgp_pair_quad_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp]),
+    "nmgp_pair_quad_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp]),
+    "nmgp_pair_dot_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp]),
+    "nmgp_pair_dot_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp]),
+    "nmgp_pair_rank_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp]),
+    "nmgp_pair_rank_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp]),
+    "nmgp_pair_pbar_reduce_f64": (c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int, c_int,
+                                          c_vp]),
+    "nmgp_pair_pbar_reduce_f32": (c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int, c_int,
+                                          c_vp]),
     "nmgp_sizeof_pairwise_desc": (c_i64, []),
     "nmgp_sizeof_pairwise_bwd_desc": (c_i64, []),
     "nmgp_sizeof_dsvi_args": (c_i64, []),
@@ -167,6 +182,10 @@ _SIGS = {
     "nmgp_dsvi_prefinal_f32": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_adam_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_dbl, c_dbl, c_dbl, c_dbl, c_vp]),
     "nmgp_adam_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_dbl, c_dbl, c_dbl, c_dbl, c_vp]),
+    "nmgp_adam_lower_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_vp, c_dbl, c_dbl, c_dbl,
+                                    c_dbl, c_vp]),
+    "nmgp_adam_lower_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_vp, c_dbl, c_dbl, c_dbl,
+                                    c_dbl, c_vp]),
     "nmgp_normal_f64": (c_int, [c_vp, c_i64, c_u64, c_vp, c_i64, c_vp]),
     "nmgp_normal_f32": (c_int, [c_vp, c_i64, c_u64, c_vp, c_i64, c_vp]),
     "nmgp_counter_add": (c_int, [c_vp, c_i64, c_vp]),
@@ -201,7 +220,8 @@ def lib():
         f.restype = res
         f.argtypes = args
     for cls, fn in [(GemmDesc, "nmgp_sizeof_gemm_desc"), (PairwiseDesc, "nmgp_sizeof_pairwise_desc"),
-                    (PairwiseBwdDesc, "nmgp_sizeof_pairwise_bwd_desc"), (DsviArgs, "nmgp_sizeof_dsvi_args")]:
+                    (PairwiseBwdDesc, "nmgp_sizeof_pairwise_bwd_desc"), (DsviArgs, "nmgp_sizeof_dsvi_args"),
+                    (PairDesc, "nmgp_sizeof_pair_desc")]:
         if ctypes.sizeof(cls) != getattr(L, fn)():
             raise ImportError(f"ABI mismatch: ctypes {cls.__name__} is {ctypes.sizeof(cls)} bytes, "
                               f"library says {getattr(L, fn)()}")

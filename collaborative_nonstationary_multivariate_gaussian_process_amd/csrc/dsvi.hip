@@ -979,6 +979,90 @@ static void adam_launch(T* th, const T* g, T* m, T* v, int64_t n, const int64_t*
 
 __global__ void counter_add_kernel(int64_t* c, int64_t inc) { c[0] += inc; }
 
+// Adam over lower-triangular M x M blocks (round 5): the sqrt_W / sqrt_v / sqrt_U parameters enter the model only
+// through mat2ltri (code/utils.py:68-72), so their strictly upper triangles never get a gradient and stay where
+// torch's Adam leaves them (exp_avg = exp_avg_sq = 0: no move).  This form touches only the 16-byte vectors that
+// hold lower-triangle elements (row r: vectors 0 .. r / V) instead of streaming g, m and v over the whole block to
+// find the all-zero groups -- at the ECoG shape (8384 blocks of M = 1024) that halves the reads of the update.
+// One wave per row pair (r, M - 1 - r): M + 1 elements per wave, balanced; grid-strided over the pairs.  The
+// element update is adam_elt, so results are bit-identical to the dense kernel.
+template <typename T>
+__global__ __launch_bounds__(256) void adam_tri_kernel(T* th, const T* g, T* m, T* v, int64_t nblk, int M,
+                                                       const int64_t* step, T lr, T b1, T b2, T eps) {
+  __shared__ T s_bc[2];
+  if (threadIdx.x == 0) {
+    const double t = (double)(step[0] + 1);
+    s_bc[0] = (T)(1.0 - pow((double)b1, t));
+    s_bc[1] = (T)sqrt(1.0 - pow((double)b2, t));
+  }
+  __syncthreads();
+  const T bc1 = s_bc[0], bc2s = s_bc[1];
+  constexpr int V = 16 / (int)sizeof(T);
+  struct alignas(16) P { T e[V]; };
+  const int lane = threadIdx.x & 63;
+  const int half = (M + 1) / 2;
+  const int64_t npair = nblk * half;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); p < npair; p += nw) {
+    const int64_t b = p / half;
+    const int rp = (int)(p - b * half);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = h == 0 ? rp : M - 1 - rp;
+      if (h == 1 && r == rp) break;
+      const int64_t row = (b * M + r) * (int64_t)M / V;     // vector index of the row's start
+      const int nv = r / V + 1;
+      for (int q = lane; q < nv; q += 64) {
+        const int64_t i = row + q;
+        const P gq = ((const P*)g)[i];
+        P mq = ((const P*)m)[i];
+        P vq = ((const P*)v)[i];
+        bool any = false;
+#pragma unroll
+        for (int e = 0; e < V; ++e) any |= (bits_of(gq.e[e]) | bits_of(mq.e[e]) | bits_of(vq.e[e])) != 0;
+        if (!any) continue;
+        P tq = ((P*)th)[i];
+#pragma unroll
+        for (int e = 0; e < V; ++e) adam_elt<T>(tq.e[e], gq.e[e], mq.e[e], vq.e[e], lr, b1, b2, eps, bc1, bc2s);
+        ((P*)m)[i] = mq;
+        ((P*)v)[i] = vq;
+        ((P*)th)[i] = tq;
+      }
+    }
+  }
+}
+
+// the flat vector [0, n) with `ntri` ranges (offset, blocks) of lower-triangular M x M blocks: the dense kernel on
+// the gaps, the triangular one on the ranges, then the step counter
+template <typename T>
+static int adam_lower(T* th, const T* g, T* m, T* v, int64_t n, const int64_t* tri, int ntri, int M, int64_t* step,
+                      T lr, T b1, T b2, T eps, hipStream_t s) {
+  if (ntri < 0 || (ntri > 0 && !tri)) return -6;
+  if (M <= 0) return -8;
+  constexpr int V = 16 / (int)sizeof(T);
+  const bool aligned = ((((uintptr_t)th) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) == 0;
+  int64_t at = 0;
+  for (int k = 0; k < ntri; ++k) {
+    const int64_t off = tri[2 * k], nb = tri[2 * k + 1];
+    const int64_t len = nb * (int64_t)M * M;
+    if (off < at || nb < 0 || off + len > n) return -6;
+    if (!aligned || M % V != 0 || off % V != 0) return -8;
+    if (off > at) adam_launch<T>(th + at, g + at, m + at, v + at, off - at, step, lr, b1, b2, eps, s);
+    if (nb > 0) {
+      const int64_t pairs = nb * ((M + 1) / 2);
+      const int64_t blocks = std::min<int64_t>((pairs + 3) / 4, 16384);
+      hipLaunchKernelGGL(adam_tri_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, s, th + off, g + off, m + off, v + off,
+                         nb, M, step, lr, b1, b2, eps);
+    }
+    at = off + len;
+  }
+  if (n > at) adam_launch<T>(th + at, g + at, m + at, v + at, n - at, step, lr, b1, b2, eps, s);
+  NMGP_CHECK_LAUNCH();
+  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(1), 0, s, step, (int64_t)1);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
+
 // Element-wise precision conversion (grid-strided): fp32 engines factor their four GP priors in fp64
 // (engine.py), the explicit-inverse projections K12 (K22 + 1e-4 I)^-1 of smooth priors lose ~cond*eps
 // in an fp32 factorization.
@@ -1343,6 +1427,26 @@ NMGP_DSVI_ENTRY(finalize)
 NMGP_DSVI_ENTRY(prefinal)
 NMGP_DSVI_ENTRY(mugrad)
 #undef NMGP_DSVI_ENTRY
+int nmgp_adam_lower_f64(double* th, const double* g, double* m, double* v, int64_t n, const int64_t* tri, int ntri,
+                        int M, int64_t* step, double lr, double b1, double b2, double eps, hipStream_t s) {
+  if (!th) return -1;
+  if (!g) return -2;
+  if (!m) return -3;
+  if (!v) return -4;
+  if (!step) return -9;
+  if (n <= 0) return NMGP_OK;
+  return nmgp::adam_lower<double>(th, g, m, v, n, tri, ntri, M, step, lr, b1, b2, eps, s);
+}
+int nmgp_adam_lower_f32(float* th, const float* g, float* m, float* v, int64_t n, const int64_t* tri, int ntri, int M,
+                        int64_t* step, double lr, double b1, double b2, double eps, hipStream_t s) {
+  if (!th) return -1;
+  if (!g) return -2;
+  if (!m) return -3;
+  if (!v) return -4;
+  if (!step) return -9;
+  if (n <= 0) return NMGP_OK;
+  return nmgp::adam_lower<float>(th, g, m, v, n, tri, ntri, M, step, (float)lr, (float)b1, (float)b2, (float)eps, s);
+}
 int nmgp_adam_f64(double* th, const double* g, double* m, double* v, int64_t n, int64_t* step, double lr,
                   double b1, double b2, double eps, hipStream_t s) {
   if (!th) return -1;

@@ -800,6 +800,7 @@ int64_t nmgp_sizeof_gemm_desc(void) { return (int64_t)sizeof(nmgp_gemm_desc); }
 int64_t nmgp_sizeof_pairwise_desc(void) { return (int64_t)sizeof(nmgp_pairwise_desc); }
 int64_t nmgp_sizeof_pairwise_bwd_desc(void) { return (int64_t)sizeof(nmgp_pairwise_bwd_desc); }
 int64_t nmgp_sizeof_dsvi_args(void) { return (int64_t)sizeof(nmgp_dsvi_args); }
+int64_t nmgp_sizeof_pair_desc(void) { return (int64_t)sizeof(nmgp_pair_desc); }
 
 int nmgp_gemm_grouped_f64(const nmgp_gemm_desc* d, int np, int tt, const int32_t* seg, hipStream_t s) {
   return nmgp::launch_grouped<double>(d, np, tt, seg, s);

@@ -67,6 +67,20 @@ def param_layout(D, M, packed=False, pair_range=None):
     return offs, o
 
 
+def lower_block_ranges(offs):
+    """(offset, blocks) of the parameters that are stacks of M x M blocks used only through their lower triangle
+    (sqrt_W, sqrt_v, sqrt_U: mat2ltri, code/utils.py:68-72), ascending -- hip_ops.adam_lower_'s ranges."""
+    out = []
+    for name in ("sqrt_W", "sqrt_v", "sqrt_U"):
+        o, shp = offs[name]
+        out.append((o, int(np.prod(shp[:-2])) if len(shp) > 2 else 1))
+    return sorted(out)
+
+
+# the triangular-block Adam from this M on (fewer, larger blocks: one dense launch is cheaper below)
+ADAM_LOWER_MIN_M = 512
+
+
 def pair_list(D, pair_range=None):
     i0, i1 = (0, D) if pair_range is None else pair_range
     return [(i, j) for i in range(i0, i1) for j in range(i + 1)]
@@ -136,6 +150,14 @@ class DsviEngine:
         self.WG = e(D, B, M)
         self.WP = e(D, B, M)
         self.Zg = e(D, B, M)            # per-factor P-bar_G products W-hat_d L_d^T (rows of outputs >= d)
+        # round 5: where every output owns few minibatch rows (ECoG: B / D = 4) the per-pair products -- the
+        # quadratic-form factors P L_ij, their P-bar W-hat L_ij^T and the pair L-bar P^T W-hat -- stream each
+        # M x M block once on the pair kernels (csrc/pairs.hip) instead of 64-row MFMA tiles that are ~94 %
+        # padding.  NMGP_PAIR_STREAM=0 keeps them on the grouped kernels (tests' equivalence switch).
+        n_out = (self.pair_range[1] - self.pair_range[0]) if self.pair_range is not None else D
+        self.pair_stream = (self.Q > 0 and B <= 32 * max(1, n_out) and M % 4 == 0 and M <= 1024
+                            and os.environ.get("NMGP_PAIR_STREAM", "1") != "0")
+        self.Zp = e(D, B, M) if self.pair_stream else None   # per-pair P-bar products W-hat_ij L_ij^T, slot j
         # HCP / ECoG shapes (fp32, M >= 512): the D+Q factor products run on the 128x128 f32 MFMA kernel at
         # per-factor offsets (BigBatch) instead of the grouped 64x64 tiles.  NMGP_BIG_SIDE=0 keeps them on the
         # grouped kernel: the only schedule switch left, for tests/test_gpu_engine.py's equivalence check
@@ -417,11 +439,18 @@ class DsviEngine:
             d14.append(g(self.WP, self.P, th, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), flags=L.B_LOWER,
                          offs=(typ * BM, sU + pq(i, j) * MM, slot * BM), row_seg=rseg))
         p["quad"] = G(d14)
+        if self.pair_stream:
+            qp = []
+            for (i, j) in pairs:
+                slot, rseg = (j, i) if not elbo_mode else (i, j)
+                qp.append(((2 if i == j else 1) * BM, sU + pq(i, j) * MM, slot * BM, rseg))
+            pair_quad = H.PairStream("quad", self.P, th, self.WP, qp, seg, M)
+            p["quad"] = H.Seq([G(d14[:D]), pair_quad])
         if not elbo_mode:
             # the pair factors W_P = P_{0,1} L_ij need only the L0 / L1 projections (proj3, side2): they run
             # on side2 beside the Gibbs prior chain; only the latent factors W_G = P_G L_d follow projG
             p["quad_W"] = G(d14[:D])
-            p["quad_P"] = G(d14[D:])
+            p["quad_P"] = pair_quad if self.pair_stream else G(d14[D:])
         if elbo_mode:
             # later Monte-Carlo samples of compute_ELBO: the pair factors W_P = P_{0,1} L_ij do not depend
             # on the sample (the L priors and Sigma_U are fixed within a call) -- only the D latent ones
@@ -451,6 +480,14 @@ class DsviEngine:
         # profiles/r03za_kt_cap_ab.txt.)
         p["bwd_wG"] = G(d17G)
         p["bwd_wP"] = G(d17P) if d17P else None
+        if self.pair_stream:
+            # Z_ij = W-hat_ij L_ij^T into slot j (rows of output i), then P-bar_1 += Z_ii and P-bar_0 += Z_i0 + ...
+            # + Z_i,i-1 in j order (csrc/pairs.hip pair_pbar_reduce)
+            pair_dot = H.PairStream("dot", self.WP, th, self.Zp,
+                                    [(j * BM, sU + pq(i, j) * MM, j * BM, i) for (i, j) in pairs], seg, M)
+            Zp, Pb1, Pb2 = self.Zp, self.Pbar[1], self.Pbar[2]
+            p["bwd_wP"] = H.Seq([pair_dot, lambda s_: H.pair_pbar_reduce(Zp, BM, Pb1, Pb2, M, seg, D, i0, i1, B, M,
+                                                                         s_)])
         d17 = []
         if self.Ylb is not None:
             # round 4: one product per (output i, factor d <= i) over output i's rows into slot (i, d) of Ylb,
@@ -475,12 +512,18 @@ class DsviEngine:
                              offs=(3 * BM, d * B, muW + d * M), k_seg=d, seg_span=D - d))
         for (i, j) in pairs:
             typ = 2 if i == j else 1
-            d17.append(g(gr, self.P, self.WP, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_TRIL, beta=1.0,
-                         offs=(typ * BM, j * BM, sU + pq(i, j) * MM), k_seg=i))
+            if not self.pair_stream:
+                d17.append(g(gr, self.P, self.WP, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_TRIL, beta=1.0,
+                             offs=(typ * BM, j * BM, sU + pq(i, j) * MM), k_seg=i))
             d17.append(g(gr, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1), beta=1.0,
                          offs=(typ * BM, (D + j) * B, muU + pq(i, j) * M), k_seg=i))
+        # pair L-bar on the pair kernel: G_ij(lower) += P_typ[rows of i]^T W-hat_ij (the KL L-bar, this block's
+        # first writer on the same stream, already zeroed the strictly upper part: OUT_TRIL)
+        pair_rank = H.PairStream("rank", self.P, gr, self.WP,
+                                 [((2 if i == j else 1) * BM, sU + pq(i, j) * MM, j * BM, i) for (i, j) in pairs],
+                                 seg, M) if self.pair_stream else None
         if not self.big_side:
-            p["bwd_lbar"] = G(d17)
+            p["bwd_lbar"] = G(d17) if pair_rank is None else H.Seq([G(d17), pair_rank])
         else:
             # the D + Q L-bar products P^T W (k over each factor's row segment) on the 128x128 kernel,
             # the M x 1 mu-bar products stay one grouped launch
@@ -488,10 +531,10 @@ class DsviEngine:
                               [sW + d * MM for d in range(D)], M, M, B, lda=M, ldb=M, a_kcontig=False,
                               b_kcontig=False, flags=L.OUT_TRIL, beta=1.0,
                               kseg=(seg, list(range(D)), [D - d for d in range(D)]))
-            bw_u = H.BigBatch(self.P, self.WP, gr, [(2 if i == j else 1) * BM for (i, j) in pairs],
-                              [j * BM for (i, j) in pairs], [sU + pq(i, j) * MM for (i, j) in pairs], M, M, B,
-                              lda=M, ldb=M, a_kcontig=False, b_kcontig=False, flags=L.OUT_TRIL, beta=1.0,
-                              kseg=(seg, [i for (i, j) in pairs], [1] * len(pairs)))
+            bw_u = pair_rank if pair_rank is not None else H.BigBatch(
+                self.P, self.WP, gr, [(2 if i == j else 1) * BM for (i, j) in pairs], [j * BM for (i, j) in pairs],
+                [sU + pq(i, j) * MM for (i, j) in pairs], M, M, B, lda=M, ldb=M, a_kcontig=False, b_kcontig=False,
+                flags=L.OUT_TRIL, beta=1.0, kseg=(seg, [i for (i, j) in pairs], [1] * len(pairs)))
             mu = G([dd for dd in d17 if dd.n == 1])
             p["bwd_lbar"] = H.Seq([bw_w, bw_u, mu])
         # B3: R_k = Pbar_k Ainv_k (G,0,1) ; Abar_k = Cinv^T diag(delta) Cinv ; KL L-bar

@@ -579,6 +579,46 @@ class BigBatch:
                 "gemm_big_offsets_epi")
 
 
+class PairStream:
+    """One launch of a pair-block streaming product (csrc/pairs.hip) over many problems, descriptors uploaded
+    once: kind "quad" C[r] = A[r] L, "dot" Z[r] = W[r] L^T, "rank" G(lower) += P^T W; problem p uses rows
+    seg[s_p] .. seg[s_p + 1] - 1 and operands at the element offsets (a_off, l_off, c_off) of the bases
+    (a, l, c).  Graph-capturable (no allocation per call)."""
+
+    FNS = {"quad": "nmgp_pair_quad_", "dot": "nmgp_pair_dot_", "rank": "nmgp_pair_rank_"}
+
+    def __init__(self, kind, a, l, c, probs, seg, M):
+        assert kind in self.FNS
+        for t_, nm in ((a, "a"), (l, "l"), (c, "c"), (seg, "seg")):
+            L.require_device(t_, nm)
+        assert a.dtype == l.dtype == c.dtype and seg.dtype == torch.int32
+        self.kind, self.a, self.l, self.c, self.seg, self.M = kind, a, l, c, seg, int(M)
+        self.dtype = a.dtype
+        arr = (L.PairDesc * max(1, len(probs)))()
+        for i, (ao, lo, co, s_) in enumerate(probs):
+            arr[i].a_off, arr[i].l_off, arr[i].c_off, arr[i].seg = int(ao), int(lo), int(co), int(s_)
+        self.n = len(probs)
+        self.dev = torch.frombuffer(bytearray(bytes(memoryview(arr).cast("B"))), dtype=torch.uint8).to(a.device)
+
+    def __call__(self, stream=None):
+        if self.n == 0:
+            return
+        s = stream if stream is not None else L.stream_handle()
+        vp = ctypes.c_void_p
+        fn = getattr(L.lib(), self.FNS[self.kind] + _sfx(self.dtype))
+        L.check(fn(vp(self.a.data_ptr()), vp(self.l.data_ptr()), vp(self.c.data_ptr()), vp(self.dev.data_ptr()),
+                   self.n, vp(self.seg.data_ptr()), self.M, s), "pair_" + self.kind)
+
+
+def pair_pbar_reduce(Z, sZ, P0, P1, ldp, seg, D, i0, i1, B, M, stream=None):
+    """P1[r] += Z_i[r], P0[r] += Z_0[r] + ... + Z_{i-1}[r] for every row r of output i, i0 <= i < i1."""
+    s = stream if stream is not None else L.stream_handle()
+    vp = ctypes.c_void_p
+    fn = getattr(L.lib(), "nmgp_pair_pbar_reduce_" + _sfx(Z.dtype))
+    L.check(fn(vp(Z.data_ptr()), int(sZ), vp(P0.data_ptr()), vp(P1.data_ptr()), int(ldp), vp(seg.data_ptr()), int(D),
+               int(i0), int(i1), int(B), int(M), s), "pair_pbar_reduce")
+
+
 class Seq:
     """Launch callables one after another on the same stream (a composite schedule item)."""
 
@@ -899,6 +939,16 @@ def adam_(theta, grad, m, v, step, lr, betas=(0.9, 0.999), eps=1e-8):
     L.check(fn(ctypes.c_void_p(theta.data_ptr()), ctypes.c_void_p(grad.data_ptr()), ctypes.c_void_p(m.data_ptr()),
                ctypes.c_void_p(v.data_ptr()), theta.numel(), ctypes.c_void_p(step.data_ptr()), float(lr),
                float(betas[0]), float(betas[1]), float(eps), L.stream_handle()), "adam")
+
+
+def adam_lower_(theta, grad, m, v, step, lr, tri, M, betas=(0.9, 0.999), eps=1e-8):
+    """adam_ with the ranges `tri` = [(offset, blocks), ...] of the flat vector treated as lower-triangular
+    M x M blocks (only their lower-triangle vectors are read / written; bit-identical results)."""
+    fn = getattr(L.lib(), "nmgp_adam_lower_" + _sfx(theta.dtype))
+    arr = (ctypes.c_int64 * max(1, 2 * len(tri)))(*[int(x) for ab in tri for x in ab])
+    L.check(fn(ctypes.c_void_p(theta.data_ptr()), ctypes.c_void_p(grad.data_ptr()), ctypes.c_void_p(m.data_ptr()),
+               ctypes.c_void_p(v.data_ptr()), theta.numel(), arr, len(tri), int(M), ctypes.c_void_p(step.data_ptr()),
+               float(lr), float(betas[0]), float(betas[1]), float(eps), L.stream_handle()), "adam_lower")
 
 
 def normal_(out, seed, counter=None, offset=0):

@@ -23,7 +23,7 @@ from torch.utils.data import DataLoader, Dataset
 from . import _lib as Lb
 from . import distributed as DD
 from . import hip_ops as H
-from .engine import DsviEngine, HYPER_NAMES, PARAM_NAMES, param_layout
+from .engine import ADAM_LOWER_MIN_M, DsviEngine, HYPER_NAMES, PARAM_NAMES, lower_block_ranges, param_layout
 from .utils import TensorType, tridiagonal_jitter  # noqa: F401  (re-exported like the reference)
 
 F64 = torch.float64
@@ -600,9 +600,14 @@ class DsviTrainer:
         upd.replay()
 
     def update(self):
-        """torch.optim.Adam update of the flat parameter vector (one HIP launch)."""
+        """torch.optim.Adam update of the flat parameter vector (one HIP launch; from M = 512 on the sqrt blocks'
+        lower triangles only, nmgp_adam_lower: their upper triangles never move)."""
         mdl = self.model
-        H.adam_(mdl._theta, mdl._grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps)
+        if mdl.M >= ADAM_LOWER_MIN_M:
+            H.adam_lower_(mdl._theta, mdl._grad, self.m, self.v, self.step_count, self.lr,
+                          lower_block_ranges(mdl._offs), mdl.M, self.betas, self.eps)
+        else:
+            H.adam_(mdl._theta, mdl._grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps)
 
     def step(self, eng, noise=None):
         """One DSVI iteration on the batch already loaded in `eng`; returns the device loss scalar."""

@@ -34,7 +34,8 @@ import torch
 
 from . import distributed as DD
 from . import hip_ops as H
-from .engine import DsviEngine, param_layout, pair_window, PARAM_NAMES, HYPER_NAMES
+from .engine import (ADAM_LOWER_MIN_M, DsviEngine, lower_block_ranges, param_layout, pair_window, PARAM_NAMES,
+                     HYPER_NAMES)
 
 
 def pair_shard_ranges(D, world):
@@ -229,7 +230,11 @@ class PairShard:
         return loss[0]
 
     def update(self):
-        H.adam_(self.theta, self.grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps)
+        if self.engine.M >= ADAM_LOWER_MIN_M:        # the sqrt blocks' lower triangles only (nmgp_adam_lower)
+            H.adam_lower_(self.theta, self.grad, self.m, self.v, self.step_count, self.lr,
+                          lower_block_ranges(self.engine.offs), self.engine.M, self.betas, self.eps)
+        else:
+            H.adam_(self.theta, self.grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps)
 
     def capture(self):
         """Capture the rank-local step (gather + noise + forward / backward) and the Adam update as two HIP

@@ -44,6 +44,7 @@ int64_t nmgp_sizeof_gemm_desc(void);
 int64_t nmgp_sizeof_pairwise_desc(void);
 int64_t nmgp_sizeof_pairwise_bwd_desc(void);
 int64_t nmgp_sizeof_dsvi_args(void);
+int64_t nmgp_sizeof_pair_desc(void);
 
 /* ------------------------------------------------------------------ grouped GEMM (MFMA)
  * C(i,j) = alpha * sum_k op(A)(i,k) * s(k) * op(B)(k,j) + beta*C(i,j) + gamma*rs(i)*E(i,j)
@@ -403,6 +404,16 @@ int nmgp_adam_f64(double* theta, const double* grad, double* m, double* v, int64
                   int64_t* step, double lr, double beta1, double beta2, double eps, hipStream_t stream);
 int nmgp_adam_f32(float* theta, const float* grad, float* m, float* v, int64_t n,
                   int64_t* step, double lr, double beta1, double beta2, double eps, hipStream_t stream);
+/* The same update where the ranges tri[2k] .. tri[2k] + tri[2k+1] M^2 of the vector are lower-triangular M x M
+ * blocks (sqrt_W, sqrt_v, sqrt_U: their strictly upper triangles never receive a gradient, code/utils.py:68-72 --
+ * torch's Adam leaves them unchanged): only the 16-byte vectors holding lower-triangle elements are read and
+ * written there (bit-identical to nmgp_adam_*); ranges ascending and disjoint, 16-byte aligned, M % (16 / size) == 0.
+ * tri is a HOST array of ntri (offset, blocks) pairs.  One step-counter increment.                          */
+int nmgp_adam_lower_f64(double* theta, const double* grad, double* m, double* v, int64_t n, const int64_t* tri,
+                        int ntri, int M, int64_t* step, double lr, double beta1, double beta2, double eps,
+                        hipStream_t stream);
+int nmgp_adam_lower_f32(float* theta, const float* grad, float* m, float* v, int64_t n, const int64_t* tri, int ntri,
+                        int M, int64_t* step, double lr, double beta1, double beta2, double eps, hipStream_t stream);
 /* Counter-based Philox4x32-10 standard normals: out[i] = N(0,1) for stream (seed, *counter + i) */
 int nmgp_normal_f64(double* out, int64_t n, uint64_t seed, const int64_t* counter, int64_t offset,
                     hipStream_t stream);
@@ -421,6 +432,41 @@ int nmgp_pbar_reduce_f64(const double* Z, int64_t sZ, double* P, int64_t ldp, co
                          hipStream_t stream);
 int nmgp_pbar_reduce_f32(const float* Z, int64_t sZ, float* P, int64_t ldp, const int32_t* seg, int D, int B, int M,
                          hipStream_t stream);
+/* ------------------------------------------------------------------ pair-block streaming products (round 5)
+ * The per-pair products of the DSVI step when each output owns few minibatch rows (ECoG: ~4 of B = 512 per
+ * output, Q = 8256 pairs of M = 1024): one problem per coefficient pair (i, j), rows r in [seg[s], seg[s+1]).
+ * Each streams its M x M lower-triangular block once (HBM-bound) with the rows' operands on chip; row r of an
+ * operand at base + offset + r * M (row stride M), blocks row-major with leading dimension M.
+ *   quad : C[r] = A[r] L              (A at a_off, L at l_off, C at c_off)  -- code/utils.py:115-120 (MGP_d),
+ *                                      the quadratic-form factors W = P L_ij of code/nmgp_dsvi.py:227-237
+ *   dot  : Z[r] = W[r] L^T            (W at a_off, L at l_off, Z at c_off)  -- their P-bar (autograd)
+ *   rank : G[k][c] += sum_r P[r][k] W[r][c] for c <= k  (P at a_off, G at l_off, W at c_off; the strictly
+ *          upper part of G is not touched)                                -- the pair's L-bar (autograd)
+ *   pair_pbar_reduce: row r of output i (i0 <= i < i1): P1[r] += Z_i[r], P0[r] += Z_0[r] + ... + Z_{i-1}[r]
+ *          in j order (Z_j at Z + j sZ) -- the L1 / L0 prior P-bars of code/nmgp_dsvi.py:227-237
+ * M must be a multiple of 4 (f32) / 2 (f64); quad needs M <= 2048 (f32) / 3072 (f64), dot and rank M <= 1024.
+ * Deterministic (fixed summation order).  0 or -(argument index).                                       */
+typedef struct nmgp_pair_desc {
+  int64_t a_off, l_off, c_off;   /* element offsets of the three operands */
+  int32_t seg;                   /* segment index s: the problem's rows are seg[s] .. seg[s+1]-1 */
+  int32_t pad;
+} nmgp_pair_desc;
+int nmgp_pair_quad_f64(const double* A, const double* L, double* C, const nmgp_pair_desc* descs, int nprob,
+                       const int32_t* seg, int M, hipStream_t stream);
+int nmgp_pair_quad_f32(const float* A, const float* L, float* C, const nmgp_pair_desc* descs, int nprob,
+                       const int32_t* seg, int M, hipStream_t stream);
+int nmgp_pair_dot_f64(const double* W, const double* L, double* Z, const nmgp_pair_desc* descs, int nprob,
+                      const int32_t* seg, int M, hipStream_t stream);
+int nmgp_pair_dot_f32(const float* W, const float* L, float* Z, const nmgp_pair_desc* descs, int nprob,
+                      const int32_t* seg, int M, hipStream_t stream);
+int nmgp_pair_rank_f64(const double* P, double* G, const double* W, const nmgp_pair_desc* descs, int nprob,
+                       const int32_t* seg, int M, hipStream_t stream);
+int nmgp_pair_rank_f32(const float* P, float* G, const float* W, const nmgp_pair_desc* descs, int nprob,
+                       const int32_t* seg, int M, hipStream_t stream);
+int nmgp_pair_pbar_reduce_f64(const double* Z, int64_t sZ, double* P0, double* P1, int64_t ldp, const int32_t* seg,
+                              int D, int i0, int i1, int B, int M, hipStream_t stream);
+int nmgp_pair_pbar_reduce_f32(const float* Z, int64_t sZ, float* P0, float* P1, int64_t ldp, const int32_t* seg,
+                              int D, int i0, int i1, int B, int M, hipStream_t stream);
 /* L-bar / mu-bar of the latent factors in the DSVI backward (autograd of code/nmgp_dsvi.py:198-215, W = mu + L eps
  * and MGP_d's L-products): factor d's gradient collects Y_{i,d} = P_G[rows of i]^T W-hat_d[rows of i] over outputs
  * i = d .. D-1.  Slot (i, d) is Y + (first(d) + i - d) * sY, first(d) = sum_{d' < d} (D - d'): an M x M matrix, then an

@@ -230,6 +230,40 @@ def test_fp32_big_side_products_match_grouped(monkeypatch):
     assert _rel(res[0][1], res[1][1]) < 1e-3
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_pair_stream_products_match_grouped(monkeypatch, dtype):
+    """Few rows per output (D = 16 outputs, 4 rows each on average, M = 512): the per-pair quadratic-form factors,
+    their P-bar and the pair L-bar on the pair streaming kernels (csrc/pairs.hip) vs the grouped / batched MFMA
+    products (NMGP_PAIR_STREAM=0): same loss and gradient within rounding (fp32: the 128x128 batched path with
+    big_side; fp64: the grouped path)."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP
+    rng = np.random.default_rng(5)
+    D, M = 16, 512
+    n = [int(v) for v in rng.integers(0, 9, D)]
+    n[3] = 0
+    n[7] = 13
+    X = [np.sort(rng.uniform(0, 1, k)).reshape(-1, 1) for k in n]
+    Y = [np.sin(6 * x + d) + 0.3 * rng.standard_normal(x.shape) for d, x in enumerate(X)]
+    res = []
+    for ps in ("1", "0"):
+        monkeypatch.setenv("NMGP_PAIR_STREAM", ps)
+        model = NMGP(number_observations=10 * sum(n), dim_outputs=D, Z=np.linspace(0, 1, M), seed=22,
+                     device="cuda:0", noise="device", dtype=dtype, pair_layout="packed")
+        for k in ["length_scales_tildeell_log", "length_scales_L0_log", "length_scales_L1_log"]:
+            getattr(model, k).data.fill_(float(np.log(3.0 / M)))
+        loss = model(X, Y)
+        loss.backward()
+        torch.cuda.synchronize()
+        assert model.engine(sum(n)).pair_stream == (ps == "1")
+        res.append((float(loss), torch.cat([p.grad.reshape(-1).double() for p in model.parameters()]).cpu()))
+    lt, gt = (1e-4, 1e-3) if dtype == torch.float32 else (1e-12, 1e-10)
+    print(f"PAIR_STREAM {dtype}: loss rel {abs(res[0][0] - res[1][0]) / abs(res[1][0]):.3e}  "
+          f"grad rel {_rel(res[0][1], res[1][1]):.3e}")
+    assert np.isfinite(res[0][0])
+    assert res[0][0] == pytest.approx(res[1][0], rel=lt)
+    assert _rel(res[0][1], res[1][1]) < gt
+
+
 def test_step_begin_matches_separate_launches():
     """nmgp_step_begin (one launch) == batch gather + Philox noise + noise-counter advance + grad
     zeroing as separate launches: bit-identical minibatch, segment table, noise, counters."""
@@ -435,7 +469,10 @@ def test_index_argument_any_order_matches_oracle():
 
 
 RAGGED = [("mid_forward", [5, 0, 7]), ("mid_forward", [0, 9, 3]), ("mid_forward", [40, 1, 0]),
-          ("pm25_forward", [120, 0, 95, 1, 64]), ("hcp_like_forward", [60, 0, 1, 45, 0, 30, 22, 12])]
+          ("pm25_forward", [120, 0, 95, 1, 64]), ("hcp_like_forward", [60, 0, 1, 45, 0, 30, 22, 12]),
+          # few rows per output (B / D <= 32): the per-pair products run on the pair streaming kernels
+          # (csrc/pairs.hip), incl. an empty output and outputs with more rows than one pass holds (RB = 4 / 8)
+          ("hcp_like_forward", [3, 0, 1, 8, 9, 4, 2, 5])]
 RAGGED_DM = {"mid_forward": (3, 64), "pm25_forward": (5, 256), "hcp_like_forward": (8, 512)}
 
 
@@ -469,7 +506,7 @@ def _ragged_run(case, sizes, dtype):
     return eng, lerr, whole
 
 
-@pytest.mark.parametrize("case,sizes", RAGGED[:4] + [RAGGED[4]])
+@pytest.mark.parametrize("case,sizes", RAGGED)
 def test_ragged_minibatch_with_empty_outputs_matches_oracle(case, sizes):
     """Minibatches whose outputs have very different row counts, some none at all (the DataLoader draw of
     code/nmgp_dsvi.py:829-837 can leave an output empty): every row- and k-segmented product then runs on empty
@@ -481,7 +518,7 @@ def test_ragged_minibatch_with_empty_outputs_matches_oracle(case, sizes):
     assert lerr <= SURVEY_FP64_LOSS and whole <= SURVEY_FP64_GRAD, (lerr, whole)
 
 
-@pytest.mark.parametrize("case,sizes", [RAGGED[0], RAGGED[2], RAGGED[4]])
+@pytest.mark.parametrize("case,sizes", [RAGGED[0], RAGGED[2], RAGGED[4], RAGGED[5]])
 def test_fp32_ragged_minibatch_with_empty_outputs(case, sizes):
     """The fp32 engine on the same ragged minibatches (M = 512: the 128x128 batched factor products with
     per-problem k segments, several of them empty) at SURVEY's fp32 gates: loss 1e-3, whole gradient 2e-2."""

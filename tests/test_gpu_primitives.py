@@ -1024,3 +1024,99 @@ def test_hip_graph_external_event_node_fires_mid_replay(ops):
     o = out.cpu()
     assert torch.equal(o[0], torch.ones(3, dtype=F64)), o
     assert torch.equal(o[1], torch.zeros(3, dtype=F64)), o
+
+
+@pytest.mark.parametrize("dt", [F64, torch.float32])
+@pytest.mark.parametrize("M", [1024, 256, 68])
+def test_pair_streaming_products_vs_torch(ops, dt, M):
+    """csrc/pairs.hip (the per-pair products when every output owns few minibatch rows, ECoG shape): quad
+    C[r] = A[r] tril(L), dot Z[r] = W[r] tril(L)^T, rank G += tril(P^T W) (strictly upper part of G untouched),
+    and the P-bar reduction, against torch on ragged segments -- empty, one row, RB, RB + 1 and 3 RB + 2 rows (the
+    chunked path) -- with the upper triangles of L holding junk (mat2ltri ignores them, code/utils.py:68-72)."""
+    import torch as T
+    g = T.Generator().manual_seed(M)
+    sizes = [3, 0, 1, 8, 9, 4, 26, 2]
+    D, B = len(sizes), sum(sizes)
+    seg = T.tensor(np.concatenate([[0], np.cumsum(sizes)]), dtype=T.int32)
+    pairs = [(i, j) for i in range(D) for j in range(i + 1)]
+    Q = len(pairs)
+    Lb = T.randn(Q, M, M, generator=g, dtype=F64)                    # upper parts junk on purpose
+    A = T.randn(3, B, M, generator=g, dtype=F64)                     # P_typ rows
+    Wp = T.randn(D, B, M, generator=g, dtype=F64)                    # W-hat slots
+    G0 = T.randn(Q, M, M, generator=g, dtype=F64)
+    tol = 1e-12 if dt == F64 else 3e-5
+    dev = lambda t: t.to(dt).to(DEV).contiguous()
+    Ld, Ad, Wd, Gd, segd = dev(Lb), dev(A), dev(Wp), dev(G0), seg.to(DEV)
+    C = T.zeros(D, B, M, dtype=dt, device=DEV)
+    Z = T.zeros(D, B, M, dtype=dt, device=DEV)
+    BM, MM = B * M, M * M
+    typ = lambda i, j: 2 if i == j else 1
+    q = [(typ(i, j) * BM, p * MM, j * BM, i) for p, (i, j) in enumerate(pairs)]
+    ops.PairStream("quad", Ad, Ld, C, q, segd, M)()
+    ops.PairStream("dot", Wd, Ld, Z, [(j * BM, p * MM, j * BM, i) for p, (i, j) in enumerate(pairs)], segd, M)()
+    ops.PairStream("rank", Ad, Gd, Wd, [(typ(i, j) * BM, p * MM, j * BM, i) for p, (i, j) in enumerate(pairs)],
+                   segd, M)()
+    torch.cuda.synchronize()
+    C, Z, Gd = C.double().cpu(), Z.double().cpu(), Gd.double().cpu()
+    Lr, Ar, Wr, G0r = Lb.to(dt).double(), A.to(dt).double(), Wp.to(dt).double(), G0.to(dt).double()
+    Gref = G0r.clone()
+    for p, (i, j) in enumerate(pairs):
+        r = slice(int(seg[i]), int(seg[i + 1]))
+        Lt = T.tril(Lr[p])
+        Cref = Ar[typ(i, j), r] @ Lt
+        Zref = Wr[j, r] @ Lt.t()
+        Gref[p] += T.tril(Ar[typ(i, j), r].t() @ Wr[j, r])
+        if sizes[i]:
+            assert rel(C[j, r], Cref) < tol, (p, i, j)
+            assert rel(Z[j, r], Zref) < tol, (p, i, j)
+    assert rel(Gd, Gref) < tol
+    up = T.triu(T.ones(M, M, dtype=T.bool), 1)
+    assert T.equal(Gd[:, up], G0r[:, up])                            # strictly upper part untouched
+    # P-bar reduction: P1[r] += Z_i[r], P0[r] += sum_{j < i} Z_j[r] (outputs 2..6 only)
+    P = T.randn(4, B, M, generator=g, dtype=F64).to(dt).to(DEV)
+    P0 = P.double().cpu()
+    Zd = Z.to(dt).to(DEV).contiguous()
+    ops.pair_pbar_reduce(Zd, BM, P[1], P[2], M, segd, D, 2, 7, B, M)
+    torch.cuda.synchronize()
+    ref = P0.clone()
+    Zr = Zd.double().cpu()
+    for i in range(2, 7):
+        r = slice(int(seg[i]), int(seg[i + 1]))
+        ref[2, r] += Zr[i, r]
+        for j in range(i):
+            ref[1, r] += Zr[j, r]
+    assert rel(P.double().cpu(), ref) < tol
+    assert T.equal(P.double().cpu()[:, :int(seg[2])], P0[:, :int(seg[2])])    # outputs outside [2, 7) untouched
+
+
+@pytest.mark.parametrize("dt", [F64, torch.float32])
+def test_adam_lower_matches_dense_adam(ops, dt):
+    """nmgp_adam_lower (only the lower-triangle vectors of the sqrt blocks, code/utils.py:68-72's mat2ltri) equals
+    the dense nmgp_adam bit for bit over several steps, with gradients that are zero above each block's diagonal
+    (as the model's are) and dense ranges before, between and after the blocks; the step counter advances once."""
+    g = torch.Generator().manual_seed(9)
+    M = 24
+    ranges = [(8, 2), (8 + 2 * M * M + 4, 1), (8 + 3 * M * M + 4 + 12, 3)]     # (offset, blocks), 16-byte aligned
+    n = ranges[-1][0] + 3 * M * M + 20
+    th0 = torch.randn(n, generator=g, dtype=F64)
+    up = torch.triu(torch.ones(M, M, dtype=torch.bool), 1)
+    outs = []
+    for lower in (False, True):
+        th, m, v = th0.to(dt).to(DEV), torch.zeros(n, dtype=dt, device=DEV), torch.zeros(n, dtype=dt, device=DEV)
+        step = torch.zeros(1, dtype=torch.int64, device=DEV)
+        gg = torch.Generator().manual_seed(10)
+        for _ in range(3):
+            gr = torch.randn(n, generator=gg, dtype=F64)
+            for o, nb in ranges:
+                blk = gr[o:o + nb * M * M].view(nb, M, M)
+                blk[:, up] = 0.0
+            gr = gr.to(dt).to(DEV)
+            if lower:
+                ops.adam_lower_(th, gr, m, v, step, 0.01, ranges, M)
+            else:
+                ops.adam_(th, gr, m, v, step, 0.01)
+        torch.cuda.synchronize()
+        outs.append((th.cpu(), m.cpu(), v.cpu(), int(step.item())))
+    for a, b in zip(outs[0][:3], outs[1][:3]):
+        assert torch.equal(a, b)
+    assert outs[0][3] == outs[1][3] == 3
