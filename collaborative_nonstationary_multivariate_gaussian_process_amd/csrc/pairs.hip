@@ -43,20 +43,15 @@ template <typename T, int V> __device__ inline void vmask(T (&v)[V], int c0, int
   for (int e = 0; e < V; ++e) v[e] = keep_if(v[e], c0 + e <= kmax);
 }
 
-// streamed once (L, the gradient blocks): nontemporal, so the re-read operands (A, W, P) stay in L2
-template <typename T, int V> __device__ inline void vload(T (&v)[V], const T* p) {
+// 16 bytes through a buffer resource: an offset past the resource's extent (0x80000000) reads zeros, so a
+// masked-off load needs no branch (a load under a runtime condition is sunk into its own exec-masked branch
+// with a full wait, serialising the loads that should be in flight together)
+template <typename T, int V> __device__ inline void vload_b(T (&v)[V], __amdgpu_buffer_rsrc_t r, uint32_t off) {
   typedef T vec_t __attribute__((ext_vector_type(V)));
-  const vec_t x = __builtin_nontemporal_load((const vec_t*)p);
+  const vec_t x = __builtin_bit_cast(vec_t, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 #pragma unroll
   for (int e = 0; e < V; ++e) v[e] = x[e];
 }
-template <typename T, int V> __device__ inline void vload_c(T (&v)[V], const T* p) {
-  typedef T vec_t __attribute__((ext_vector_type(V)));
-  const vec_t x = *(const vec_t*)p;
-#pragma unroll
-  for (int e = 0; e < V; ++e) v[e] = x[e];
-}
-
 // ------------------------------------------------------------------------------------------------ quad
 // grid (problems, column blocks of 64 V columns).  Lane l of every wave owns columns kstart + l V .. + V - 1;
 // wave w takes the rows k = kstart + w + 4 i of L (k >= the block's first column: rows above contribute 0).
@@ -76,7 +71,8 @@ __global__ __launch_bounds__(PT) void pair_quad_kernel(const T* __restrict__ A, 
   T* red = sA + (size_t)nk * RB;           // 4 x RB x CB: wave partials
   const int c0 = kstart + lane * V;
   const bool colok = c0 < M;
-  const T* Lp = L + d.l_off + c0;
+  const __amdgpu_buffer_rsrc_t rL = make_rsrc(L + d.l_off, (int64_t)M * M * (int64_t)sizeof(T));
+  const uint32_t lc = colok ? (uint32_t)(c0 * sizeof(T)) : 0x80000000u;   // (a column block past M reads zeros)
   for (int rc = 0; rc < R; rc += RB) {
     const int Rc = min(RB, R - rc);
     __syncthreads();                       // the previous chunk's readers are done
@@ -102,30 +98,17 @@ __global__ __launch_bounds__(PT) void pair_quad_kernel(const T* __restrict__ A, 
       }
     };
     int k = kstart + w;
-    for (; k + 12 < M; k += 16) {          // four rows of this wave in flight
-      T l0[V], l1[V], l2[V], l3[V];
-      if (colok) {
-        vload<T, V>(l0, Lp + (int64_t)k * M);
-        vload<T, V>(l1, Lp + (int64_t)(k + 4) * M);
-        vload<T, V>(l2, Lp + (int64_t)(k + 8) * M);
-        vload<T, V>(l3, Lp + (int64_t)(k + 12) * M);
-      } else {
+    for (; k + 28 < M; k += 32) {          // eight rows of this wave in flight
+      T l[8][V];
 #pragma unroll
-        for (int e = 0; e < V; ++e) l0[e] = l1[e] = l2[e] = l3[e] = (T)0;
-      }
-      row(k, l0);
-      row(k + 4, l1);
-      row(k + 8, l2);
-      row(k + 12, l3);
+      for (int u = 0; u < 8; ++u)
+        vload_b<T, V>(l[u], rL, colok ? lc + (uint32_t)((int64_t)(k + 4 * u) * M * sizeof(T)) : lc);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) row(k + 4 * u, l[u]);
     }
     for (; k < M; k += 4) {
       T l0[V];
-      if (colok) {
-        vload<T, V>(l0, Lp + (int64_t)k * M);
-      } else {
-#pragma unroll
-        for (int e = 0; e < V; ++e) l0[e] = (T)0;
-      }
+      vload_b<T, V>(l0, rL, colok ? lc + (uint32_t)((int64_t)k * M * sizeof(T)) : lc);
       row(k, l0);
     }
 #pragma unroll
@@ -150,20 +133,13 @@ template <typename T, int NCH>
 __device__ inline void load_w(T (&wv)[PairCfg<T>::RB][NCH][PairCfg<T>::V], const T* W, int64_t off, int r0, int rc,
                               int Rc, int M, int lane) {
   constexpr int V = PairCfg<T>::V, RB = PairCfg<T>::RB;
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(W + off + (int64_t)(r0 + rc) * M, (int64_t)Rc * M * (int64_t)sizeof(T));
 #pragma unroll
   for (int rr = 0; rr < RB; ++rr)
 #pragma unroll
     for (int j = 0; j < NCH; ++j) {
       const int k0 = j * 64 * V + lane * V;
-      if (rr < Rc && k0 < M) {
-        T v[V];
-        vload_c<T, V>(v, W + off + (int64_t)(r0 + rc + rr) * M + k0);
-#pragma unroll
-        for (int e = 0; e < V; ++e) wv[rr][j][e] = v[e];
-      } else {
-#pragma unroll
-        for (int e = 0; e < V; ++e) wv[rr][j][e] = (T)0;
-      }
+      vload_b<T, V>(wv[rr][j], rW, (rr < Rc && k0 < M) ? (uint32_t)(((int64_t)rr * M + k0) * sizeof(T)) : 0x80000000u);
     }
 }
 
@@ -180,7 +156,7 @@ __global__ __launch_bounds__(PT) void pair_dot_kernel(const T* __restrict__ W, c
   const int base = blockIdx.y * PROWS;
   if (R <= 0 || base >= M) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const T* Lb = L + d.l_off + lane * V;
+  const __amdgpu_buffer_rsrc_t rL = make_rsrc(L + d.l_off, (int64_t)M * M * (int64_t)sizeof(T));
   for (int rc = 0; rc < R; rc += RB) {
     const int Rc = min(RB, R - rc);
     T wv[RB][NCH][V];
@@ -188,36 +164,40 @@ __global__ __launch_bounds__(PT) void pair_dot_kernel(const T* __restrict__ W, c
     T res[RB];
 #pragma unroll
     for (int rr = 0; rr < RB; ++rr) res[rr] = (T)0;
-    for (int i = 0; i < PROWS / 4; ++i) {
-      const int c = base + w + 4 * i;
-      if (c >= M) break;
-      const T* Lc = Lb + (int64_t)c * M;
-      T acc[RB];
+    // two rows of this wave per iteration (all of both rows' loads in flight together)
+    for (int i = 0; i < PROWS / 4; i += 2) {
+      T l[2][NCH][V];
+      int nj[2];
 #pragma unroll
-      for (int rr = 0; rr < RB; ++rr) acc[rr] = (T)0;
-      const int nj = c / CW + 1;           // chunks that hold columns <= c
-      T l[NCH][V];
+      for (int h = 0; h < 2; ++h) {
+        const int c = base + w + 4 * (i + h);                  // (a row past M reads zeros, unused)
+        nj[h] = c / CW + 1;                                    // chunks that hold columns <= c
 #pragma unroll
-      for (int j = 0; j < NCH; ++j) {      // all of the row's loads first
-        if (j < nj && j * CW + lane * V < M) {
-          vload<T, V>(l[j], Lc + j * CW);
-        } else {
-#pragma unroll
-          for (int e = 0; e < V; ++e) l[j][e] = (T)0;
+        for (int j = 0; j < NCH; ++j) {
+          const int k0 = j * CW + lane * V;
+          const bool ok = j < nj[h] && k0 < M && c < M;
+          vload_b<T, V>(l[h][j], rL, ok ? (uint32_t)(((int64_t)c * M + k0) * sizeof(T)) : 0x80000000u);
         }
       }
 #pragma unroll
-      for (int j = 0; j < NCH; ++j) {
-        if (j == nj - 1) vmask<T, V>(l[j], j * CW + lane * V, c);
+      for (int h = 0; h < 2; ++h) {
+        const int c = base + w + 4 * (i + h);
+        T acc[RB];
 #pragma unroll
-        for (int rr = 0; rr < RB; ++rr)
+        for (int rr = 0; rr < RB; ++rr) acc[rr] = (T)0;
 #pragma unroll
-          for (int e = 0; e < V; ++e) acc[rr] = fma(l[j][e], wv[rr][j][e], acc[rr]);
-      }
+        for (int j = 0; j < NCH; ++j) {
+          if (j == nj[h] - 1) vmask<T, V>(l[h][j], j * CW + lane * V, c);
 #pragma unroll
-      for (int rr = 0; rr < RB; ++rr) {
-        const T s = wave_sum(acc[rr]);
-        res[rr] = lane == i ? s : res[rr];
+          for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+            for (int e = 0; e < V; ++e) acc[rr] = fma(l[h][j][e], wv[rr][j][e], acc[rr]);
+        }
+#pragma unroll
+        for (int rr = 0; rr < RB; ++rr) {
+          const T sm = wave_sum(acc[rr]);
+          res[rr] = lane == i + h ? sm : res[rr];
+        }
       }
     }
     const int c = base + w + 4 * lane;
@@ -244,6 +224,7 @@ __global__ __launch_bounds__(PT) void pair_rank_kernel(const T* __restrict__ P, 
   if (R <= 0 || base >= M) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   T* Gb = G + d.l_off + lane * V;
+  const __amdgpu_buffer_rsrc_t rG = make_rsrc(G + d.l_off, (int64_t)M * M * (int64_t)sizeof(T));
   for (int rc = 0; rc < R; rc += RB) {
     const int Rc = min(RB, R - rc);
     __syncthreads();
@@ -254,45 +235,52 @@ __global__ __launch_bounds__(PT) void pair_rank_kernel(const T* __restrict__ P, 
     T wv[RB][NCH][V];
     load_w<T, NCH>(wv, W, d.c_off, r0, rc, Rc, M, lane);
     __syncthreads();
-    for (int i = w; i < PROWS; i += 4) {
-      const int k = base + i;
-      if (k >= M) break;
-      T coef[RB];
+    // two rows of this wave per iteration: both rows' gradient loads in flight together
+    for (int i = w; i < PROWS; i += 8) {
+      T g[2][NCH][V];
+      int nj[2], kk[2];
 #pragma unroll
-      for (int rr = 0; rr < RB; ++rr) coef[rr] = sP[i][rr];
-      T* Gk = Gb + (int64_t)k * M;
-      const int nj = k / CW + 1;
-      T g[NCH][V];
+      for (int h = 0; h < 2; ++h) {
+        kk[h] = base + i + 4 * h;
+        const int k = kk[h];
+        nj[h] = k < M ? k / CW + 1 : 0;
 #pragma unroll
-      for (int j = 0; j < NCH; ++j) {
-        if (j < nj && j * CW + lane * V < M) {
-          vload<T, V>(g[j], Gk + j * CW);
-        } else {
-#pragma unroll
-          for (int e = 0; e < V; ++e) g[j][e] = (T)0;
+        for (int j = 0; j < NCH; ++j) {
+          const int c0 = j * CW + lane * V;
+          const bool ok = j < nj[h] && c0 < M;
+          vload_b<T, V>(g[h][j], rG, ok ? (uint32_t)(((int64_t)k * M + c0) * sizeof(T)) : 0x80000000u);
         }
       }
 #pragma unroll
-      for (int j = 0; j < NCH; ++j) {
-        const int c0 = j * CW + lane * V;
-        if (j < nj && c0 < M) {
+      for (int h = 0; h < 2; ++h) {
+        const int k = kk[h];
+        if (k >= M) continue;
+        T coef[RB];
 #pragma unroll
-          for (int e = 0; e < V; ++e) {
-            T s = g[j][e];
+        for (int rr = 0; rr < RB; ++rr) coef[rr] = sP[i + 4 * h][rr];
+        T* Gk = Gb + (int64_t)k * M;
 #pragma unroll
-            for (int rr = 0; rr < RB; ++rr) s = fma(coef[rr], wv[rr][j][e], s);
-            g[j][e] = s;
-          }
-          if (c0 + V - 1 <= k) {
-            typedef T vec_t __attribute__((ext_vector_type(V)));
-            vec_t x;
+        for (int j = 0; j < NCH; ++j) {
+          const int c0 = j * CW + lane * V;
+          if (j < nj[h] && c0 < M) {
 #pragma unroll
-            for (int e = 0; e < V; ++e) x[e] = g[j][e];
-            __builtin_nontemporal_store(x, (vec_t*)(Gk + j * CW));
-          } else {
+            for (int e = 0; e < V; ++e) {
+              T sacc = g[h][j][e];
 #pragma unroll
-            for (int e = 0; e < V; ++e)
-              if (c0 + e <= k) Gk[j * CW + e] = g[j][e];
+              for (int rr = 0; rr < RB; ++rr) sacc = fma(coef[rr], wv[rr][j][e], sacc);
+              g[h][j][e] = sacc;
+            }
+            if (c0 + V - 1 <= k) {
+              typedef T vec_t __attribute__((ext_vector_type(V)));
+              vec_t x;
+#pragma unroll
+              for (int e = 0; e < V; ++e) x[e] = g[h][j][e];
+              __builtin_nontemporal_store(x, (vec_t*)(Gk + j * CW));
+            } else {
+#pragma unroll
+              for (int e = 0; e < V; ++e)
+                if (c0 + e <= k) Gk[j * CW + e] = g[h][j][e];
+            }
           }
         }
       }

@@ -1,7 +1,7 @@
 """Per-kernel breakdown of graph-replayed training steps from a rocprofv3 kernel-trace CSV (tools/train_trace.sh).
-The timed steps are the last `steps` Adam launches of the trace (bench.graph_train's JSON says how many);
-each kernel's busy time inside [end of the Adam before them, end of the last Adam] is summed and divided by
-the step count (kernels on concurrent streams overlap, so the busy times can add up to more than the wall).
+The timed steps are the last `steps` graphed steps of the trace (bench.graph_train's JSON says how many): each
+kernel's busy time inside [start of the first timed step's step_begin launch, end of the last step's Adam counter
+increment] is summed and divided by the step count (kernels on concurrent streams overlap, so the busy times can add up to more than the wall).
 usage: python tools/train_summary.py <run_kernel_trace.csv> <train_leg.json> <out.json>"""
 import collections
 import csv
@@ -23,8 +23,12 @@ def main():
     leg = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
     steps = int(leg["steps"])
     rows.sort(key=lambda x: int(x["Start_Timestamp"]))
-    adam = [x for x in rows if "adam_kernel" in x["Kernel_Name"]]
-    t0, t1 = int(adam[-steps - 1]["End_Timestamp"]), int(adam[-1]["End_Timestamp"])
+    # step window: from the start of the step_begin launch (minibatch gather + noise: once per graphed step) of the
+    # first timed step to the end of the last Adam step-counter increment (the step's last launch; the Adam itself
+    # is one or several launches, nmgp_adam / nmgp_adam_lower)
+    begin = [x for x in rows if "step_begin_kernel" in x["Kernel_Name"]]
+    ctr = [x for x in rows if "counter_add_kernel" in x["Kernel_Name"]]
+    t0, t1 = int(begin[-steps]["Start_Timestamp"]), int(ctr[-1]["End_Timestamp"])
     busy = collections.defaultdict(float)
     calls = collections.Counter()
     for x in rows:
