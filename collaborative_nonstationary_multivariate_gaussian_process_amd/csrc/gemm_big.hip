@@ -20,6 +20,7 @@
 //     tiles (shared A rows stay in one L2); batched problems rotate the tile index per problem so no XCD
 //     gets the same (for triangular operands: the longest-k) tile row of every problem.
 #include "common.hpp"
+#include "potrf_parts.hpp"   // ps_* row-panel helpers (shared with chol.hip's fused leaf + step kernel)
 
 namespace nmgp {
 
@@ -627,65 +628,6 @@ __global__ __launch_bounds__(256, 2) void potrf_step_kernel(PotrfStepArgs pa) {
 // publish by counting on flag[0]; every workgroup then reads them back (sc1) for
 // A(rows, block column j+1) -= L_i L_0^T.  In place: the four waves read all of their rows before the
 // barrier that precedes the stores.
-constexpr int PS_NV = 32;
-
-template <int RB>
-__device__ __forceinline__ void ps_load_rows(float (&v)[RB][PS_NV], __amdgpu_buffer_rsrc_t r, int64_t row0,
-                                             int64_t ld, int nrows, bool sc1) {
-  const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
-#pragma unroll
-  for (int bi = 0; bi < RB; ++bi) {
-    const int64_t row = row0 + 16 * bi + li;
-    const uint32_t off = row < nrows ? (uint32_t)((row * ld + PS_NV * g) * 4) : 0x80000000u;
-#pragma unroll
-    for (int q = 0; q < PS_NV / 4; ++q) {
-      const u32x4g u = sc1 ? __builtin_amdgcn_raw_buffer_load_b128(r, off, 16 * q, 16)
-                           : __builtin_amdgcn_raw_buffer_load_b128(r, off, 16 * q, 0);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[bi][4 * q + e] = __uint_as_float(u[e]);
-    }
-  }
-}
-
-template <int RA>
-__device__ __forceinline__ void ps_mma(const float (&a)[RA][PS_NV], const float (&b)[2][PS_NV],
-                                       f32x4 (&acc)[RA][2]) {
-#pragma unroll
-  for (int s = 0; s < PS_NV; ++s)
-#pragma unroll
-    for (int q = 0; q < 2 * RA; ++q)
-      acc[q >> 1][q & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q >> 1][s], b[q & 1][s], acc[q >> 1][q & 1], 0, 0, 0);
-}
-
-// lookahead target of this workgroup's rows (prefetched: its other writers finished before the launch)
-template <int RB>
-__device__ __forceinline__ void ps_load_c(__amdgpu_buffer_rsrc_t rC, int i0, int64_t lda, int m, int c1,
-                                          f32x4 (&cv)[RB][2], uint32_t (&coff)[RB][2][4]) {
-  const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#pragma unroll
-  for (int q = 0; q < 2 * RB; ++q)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = i0 + 16 * (q >> 1) + 4 * g + r, j = 32 * w + 16 * (q & 1) + li;
-      coff[q >> 1][q & 1][r] = (i < m && j < c1) ? (uint32_t)(((int64_t)i * lda + j) * 4) : 0x80000000u;
-      cv[q >> 1][q & 1][r] =
-          __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rC, coff[q >> 1][q & 1][r], 0, 0));
-    }
-}
-
-template <int RB>
-__device__ __forceinline__ void ps_store_c(__amdgpu_buffer_rsrc_t rC, const f32x4 (&cv)[RB][2],
-                                           const uint32_t (&coff)[RB][2][4], const f32x4 (&acc)[RB][2]) {
-#pragma unroll
-  for (int q = 0; q < 2 * RB; ++q)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (coff[q >> 1][q & 1][r] != 0x80000000u)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cv[q >> 1][q & 1][r] - acc[q >> 1][q & 1][r]), rC,
-                                              coff[q >> 1][q & 1][r], 0, 0);
-}
-
 template <int RB>
 __global__ __launch_bounds__(256) void potrf_step32_kernel(PotrfStepArgs pa) {
   constexpr int ROWS = 16 * RB;
@@ -707,7 +649,7 @@ __global__ __launch_bounds__(256) void potrf_step32_kernel(PotrfStepArgs pa) {
   ps_load_rows<2>(b, rX, 32 * w, 128, pa.nb, false);
   f32x4 cv[RB][2];
   uint32_t coff[RB][2][4];
-  ps_load_c<RB>(rC, i0, pa.lda, pa.n2, pa.c1, cv, coff);   // behind the operands: overlaps the panel product
+  ps_load_c<RB>(rC, i0, pa.lda, pa.n2, pa.c1, cv, coff, w);   // behind the operands: overlaps the panel product
 #pragma unroll
   for (int bj = 0; bj < 2; ++bj)
 #pragma unroll
@@ -788,7 +730,7 @@ __global__ __launch_bounds__(256) void potrf_strip32_kernel(const float* L, floa
   ps_load_rows<2>(b, rL, 32 * w, lda, c1, false);
   f32x4 cv[RB][2];
   uint32_t coff[RB][2][4];
-  ps_load_c<RB>(rC, i0, lda, m, c1, cv, coff);
+  ps_load_c<RB>(rC, i0, lda, m, c1, cv, coff, w);
   ps_mma<RB>(a, b, acc);
   ps_store_c<RB>(rC, cv, coff, acc);
 }

@@ -499,7 +499,7 @@ def test_gemm_big_stream_k(ops, kind, n, k):
         assert rel(outs[0], ref) < 2e-6 and rel(C1, ref) < 2e-6
 
 
-@pytest.mark.parametrize("n", [130, 300, 1000, 2048, 4096])
+@pytest.mark.parametrize("n", [130, 300, 640, 1000, 2048, 4096, 4160])
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64])
 def test_potrf_blocked(ops, n, dt):
     # large single-matrix blocked Cholesky with lookahead (stress path): fp64-accurate residual,
@@ -531,11 +531,12 @@ def test_potrf_blocked(ops, n, dt):
     assert torch.equal(G, W)
 
 
-def test_potrf_blocked_not_pd(ops):
-    # first failing pivot reported as a global 1-based column, inside a later block
+@pytest.mark.parametrize("dt", [torch.float64, torch.float32])
+def test_potrf_blocked_not_pd(ops, dt):
+    # first failing pivot reported as a global 1-based column, inside a later block (f32: a fused block step)
     A = _spd(400, 1, 3)[0]
     A[333, 333] = -50.0
-    W = A.to(DEV).contiguous()
+    W = A.to(dt).to(DEV).contiguous()
     info = ops.potrf_blocked_(W)
     ref = torch.linalg.cholesky_ex(A).info
     assert int(info.item()) == int(ref.item()) == 334
