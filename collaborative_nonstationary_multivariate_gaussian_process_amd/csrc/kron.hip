@@ -46,7 +46,7 @@ static int kron_product(const T* t1, int64_t r1, int64_t c1, const T* t2, int64_
 }
 
 // Fused Kronecker mat-vec for small P2 (the legacy likelihood: B is P x P over a few outputs, K is N x N).
-// One workgroup owns KMV_ROWS consecutive rows n of K and its 256 threads walk those rows together in
+// One workgroup owns KMV_ROWS (4) consecutive rows n of K and its 256 threads walk those rows together in
 // 16-byte loads (thread t takes vectors t, t + 256, ... of every row), two iterations in flight: per thread
 // 2 x KMV_ROWS nontemporal K loads (K is streamed exactly once and must not evict y from L2) against P2 y
 // loads shared by the KMV_ROWS rows.  Per thread KMV_ROWS x P2 partial sums of
@@ -54,10 +54,11 @@ static int kron_product(const T* t1, int64_t r1, int64_t c1, const T* t2, int64_
 // are added in wave order through LDS (deterministic), and the second GEMM out[p N1 + n] = sum_m B[p,m]
 // work[n,m] runs on the threads of the block.  P2 is a template parameter so the accumulators are exactly
 // KMV_ROWS x P2 registers.  Bound: HBM, N1 N2 s bytes of K (+ y, B, out: P2 N2 + P1 P2 + P1 N1 elements).
-// Round 5: the round-4 form (one wave per 4 rows, P2 up to 8 in a fixed-size accumulator, one iteration in
+// 4 rows per workgroup: 2048 workgroups of <= 128 VGPRs fill the 1024 slots (occupancy 4) in two even rounds
+// (8 rows: 1024 workgroups at occupancy 3, 1.33 rounds, 94-98 us against 92-96 us).  Round 5: the round-4 form (one wave per 4 rows, P2 up to 8 in a fixed-size accumulator, one iteration in
 // flight, 512 workgroups) streamed K at 2.6 TB/s.
 constexpr int KMV_MAXP = 8;   // P2 limit of the fused path
-constexpr int KMV_ROWS = 8;   // rows of K per workgroup
+constexpr int KMV_ROWS = 4;   // rows of K per workgroup
 
 template <typename T, int V, int P2>
 __global__ __launch_bounds__(256) void kron_mv_kernel(const T* __restrict__ B, int P1, const T* __restrict__ K, int N1,
