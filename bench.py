@@ -711,6 +711,8 @@ def main():
     ap.add_argument("--no-kron", action="store_true", help="skip the Kronecker mat-vec leg")
     ap.add_argument("--pair-D", type=int, default=128, help="channels of the pair-sharded leg (default: ECoG-full 128)")
     ap.add_argument("--elbo-D", type=int, default=128, help="channels of the ELBO leg (default: ECoG-full 128)")
+    ap.add_argument("--dp-allreduce", choices=["auto", "bucketed", "flat"], default="auto",
+                    help="N > 1 gradient all-reduce: bucketed + overlapped (from 64 MB of gradient with auto) or flat")
     args = ap.parse_args()
 
     # --gpus N is honoured before anything touches the GPU: without a launcher, N > 1 re-runs this
@@ -773,11 +775,13 @@ def main():
     if world > 1:
         dist.broadcast(model._theta, 0)
     graph = None
+    dp_bucketed = False
     if not args.eager:
         if world > 1:
             # gradient graph (with an external event node where the sqrt_W / sqrt_U rows are final) and the
             # 1/world + Adam graph; the bucketed RCCL all-reduce between them overlaps the backward's tail
-            graph = trainer.capture_dp(eng, world)[0]
+            graph = trainer.capture_dp(eng, world, mode=args.dp_allreduce)[0]
+            dp_bucketed = trainer.dp_bucketed(args.dp_allreduce)
         else:
             graph = trainer.capture(eng, include_update=True)
 
@@ -1003,7 +1007,13 @@ def main():
                "config": {"workload": "PM2.5-shaped synthetic DSVI step (BASELINE.json configs[1])",
                           "D_outputs": D, "M_inducing": M, "minibatch_rows": B, "N_observations": D * N_LOC,
                           "global_batch": B * world, "parallelism": f"dp{world}" if world > 1 else "single",
-                          "hip_graph": used_graph},
+                          "hip_graph": used_graph,
+                          "dp_allreduce": (("bucketed: the sqrt_W / sqrt_U rows on a communication stream from the step "
+                                            "graph's external lbar_done node (overlapping the backward's tail), the "
+                                            "remainder after it; then the 1/N + Adam graph" if dp_bucketed else
+                                            "flat: one all-reduce of the whole gradient between the gradient graph and "
+                                            "the 1/N + Adam graph") if used_graph else
+                                           "eager: bucketed, hooked on lbar_done") if world > 1 else None},
                "roofline": roofline, "cpu_baseline": cpu, "cholesky": chol, "cholesky_stress": stress,
                "kron_mv": kron,
                "elbo_sample_sharded": elbo,

@@ -560,31 +560,49 @@ class DsviTrainer:
             self._comm = torch.cuda.Stream(device=self.model.device_)
         return self._comm
 
-    def capture_dp(self, eng, world):
-        """The data-parallel step as two graphs around an overlapped, bucketed all-reduce (dp_graph_step):
-        the gradient graph of `eng` with an EXTERNAL event node at "lbar_done" (hip_ops.ExtEvent: the point
-        after which the sqrt_W / sqrt_U gradient rows are final), and the update graph (1/world + Adam)."""
-        if "lbar_done" not in getattr(eng, "ext_events", {}):
+    # gradients from this size on take the bucketed, overlapped all-reduce (below: one flat all-reduce after the
+    # graph -- PM2.5's 16 MB in five collectives cost more in per-collective latency than the overlap hides)
+    DP_BUCKET_MIN_BYTES = 64 << 20
+
+    def dp_bucketed(self, mode="auto"):
+        if mode not in ("auto", "bucketed", "flat"):
+            raise ValueError(f"dp all-reduce mode {mode!r}")
+        g = self.model._grad
+        return mode == "bucketed" or (mode == "auto" and g.numel() * g.element_size() >= self.DP_BUCKET_MIN_BYTES)
+
+    def capture_dp(self, eng, world, mode="auto"):
+        """The data-parallel step as two graphs around the gradient all-reduce (dp_graph_step): the gradient graph
+        of `eng` and the update graph (1/world + Adam).  Bucketed (mode "bucketed", or "auto" from 64 MB of
+        gradient): the gradient graph carries an EXTERNAL event node at "lbar_done" (hip_ops.ExtEvent: the point
+        after which the sqrt_W / sqrt_U gradient rows are final) for the overlapped all-reduce; "flat": one
+        all-reduce of the whole vector after the graph."""
+        bucketed = self.dp_bucketed(mode)
+        if bucketed and "lbar_done" not in getattr(eng, "ext_events", {}):
             eng.ext_events = {"lbar_done": H.ExtEvent()}
         g = self.capture(eng, include_update=False)
         if not hasattr(self, "_dp_graphs"):
             self._dp_graphs = {}
-        self._dp_graphs[id(eng)] = (g, eng.ext_events["lbar_done"], self.capture_update(world))
+        self._dp_graphs[id(eng)] = (g, eng.ext_events["lbar_done"] if bucketed else None, self.capture_update(world))
         return self._dp_graphs[id(eng)]
 
     def dp_graph_step(self, eng, group=None):
         """One data-parallel step on the graph path (SURVEY §8e axis 2; the reference's loss.backward();
-        optimizer.step(), code/nmgp_dsvi.py:847-854, with the gradient average between them):
+        optimizer.step(), code/nmgp_dsvi.py:847-854, with the gradient average between them).  Bucketed:
           main:  replay the gradient graph ........................ | wait comm | replay 1/world + Adam
           comm:  wait for the graph's lbar_done node -> all-reduce(sqrt_W, sqrt_U rows)
                  wait for the graph's end -> all-reduce(the small remainder)
         The sqrt rows' all-reduce runs while the graph's remaining backward (R, prior adjoints, t and v chains,
-        finalize: none of them touches those rows) still runs.  Sums are element-wise those of one flat
-        all-reduce, so the result equals the flat path bit for bit."""
+        finalize: none of them touches those rows) still runs.  Flat: replay, one all-reduce, replay.  Sums are
+        element-wise those of one flat all-reduce (bit-identical at two ranks)."""
         mdl = self.model
         rank, world = DD.world_info(group)
         dpg = getattr(self, "_dp_graphs", {}).get(id(eng))
         g, ev, upd = dpg if dpg is not None else self.capture_dp(eng, world)
+        if ev is None:
+            g.replay()
+            DD.allreduce_sum_(mdl._grad, group)
+            upd.replay()
+            return
         main = torch.cuda.current_stream(mdl.device_)
         comm = self._comm_stream()
         big, small = DD.grad_buckets(mdl._offs, mdl._grad)

@@ -187,7 +187,7 @@ def _dp_graph_bucketed_vs_flat(rank):
         eng = model.engine(sum(sizes))
         eng.load_batch(x, y, sizes)
         if bucketed:
-            tr.capture_dp(eng, WORLD)
+            tr.capture_dp(eng, WORLD, mode="bucketed")
         else:
             gg, upd = tr.capture(eng, include_update=False), tr.capture_update(WORLD)
         for _ in range(4):
