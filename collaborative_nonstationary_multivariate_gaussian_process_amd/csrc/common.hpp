@@ -44,6 +44,16 @@ template <> struct Mfma<float> {
 // Raw buffer resources: loads past num_records return 0 (checked per dword), so a buffer load is a
 // bounds-checked load without a branch.  aux 16 = sc1 (bypass this CU's L1 on loads; write through
 // on stores) for data handed between workgroups inside a launch.
+// A value every lane of the wave holds (e.g. loaded from a per-problem table at a wave-uniform index) moved to
+// SGPRs: a buffer resource built from a VGPR base makes the compiler wrap every buffer load in a waterfall loop
+// (readfirstlane, compare, exec save / restore, and a vmcnt(0) wait per load where the loop carries its result).
+__device__ inline int64_t uniform64(int64_t v) {
+  const uint64_t u = (uint64_t)v;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ inline int uniform32(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ inline __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t nbytes) {
   const int32_t nr = (int32_t)(nbytes <= 0 ? 0 : (nbytes > 0x7fffffffLL ? 0x7fffffffLL : nbytes));
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nr, 0x00020000);

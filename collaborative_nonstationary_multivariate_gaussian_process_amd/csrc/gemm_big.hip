@@ -90,9 +90,9 @@ __device__ inline void tile_coords(const BigGemmArgs& g, int tile, int& tm, int&
 }
 
 // Structurally nonzero k range of a tile (triangular operands), in whole k-tiles from kbeg.
-__device__ inline void tile_krange(const BigGemmArgs& g, int i0, int j0, int& kbeg, int& kend) {
+__device__ inline void tile_krange(const BigGemmArgs& g, int K, int i0, int j0, int& kbeg, int& kend) {
   kbeg = 0;
-  kend = g.k;
+  kend = K;
   if (g.flags & NMGP_A_LOWER) kend = min(kend, i0 + BBM);
   if (g.flags & NMGP_B_UPPER) kend = min(kend, j0 + BBN);
   if (g.flags & NMGP_B_LOWER) kbeg = max(kbeg, j0);
@@ -102,22 +102,25 @@ __device__ inline void tile_krange(const BigGemmArgs& g, int i0, int j0, int& kb
 
 // acc += A[i0:i0+128, kt0:kt1] op(B)[kt0:kt1, j0:j0+128] (kend bounds the masks).  AK / BK: operand
 // layouts (k-contiguous or not) as compile-time variants, so each kernel carries one loader per operand.
+// K / koff: the problem's k extent and first k (per-problem segment variants; g.k and g.koff otherwise) -- kept out of
+// the argument struct so the kernel never writes it (a written copy lives in scratch and every operand address
+// derived from it becomes a per-lane value).
 template <bool AK, bool BK, int MODE, int AUX = 0>
-__device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, float* big_smem, int64_t bat, int i0, int j0,
-                                             int kend, int kt0, int kt1, f32x16 (&acc)[2][2]) {
+__device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int koff, float* big_smem, int64_t bat,
+                                             int i0, int j0, int kend, int kt0, int kt1, f32x16 (&acc)[2][2]) {
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = w >> 1, wc = w & 1;
   const int fl = g.flags;
   const bool aLo = fl & NMGP_A_LOWER, aUp = fl & NMGP_A_UPPER, bUp = fl & NMGP_B_UPPER, bLo = fl & NMGP_B_LOWER;
-  const float* Ab = g.A + (MODE ? g.offA[bat] : bat * g.sAb) + (AK ? (int64_t)g.koff : (int64_t)g.koff * g.lda);
-  const float* Bb = g.B + (MODE ? g.offB[bat] : bat * g.sBb) + (BK ? (int64_t)g.koff : (int64_t)g.koff * g.ldb);
+  const float* Ab = g.A + (MODE ? uniform64(g.offA[bat]) : bat * g.sAb) + (AK ? (int64_t)koff : (int64_t)koff * g.lda);
+  const float* Bb = g.B + (MODE ? uniform64(g.offB[bat]) : bat * g.sBb) + (BK ? (int64_t)koff : (int64_t)koff * g.ldb);
   const __amdgpu_buffer_rsrc_t rA =
-      AK ? make_rsrc(Ab, ((int64_t)(g.m - 1) * g.lda + g.k) * 4)
-                  : make_rsrc(Ab, ((int64_t)(g.k - 1) * g.lda + g.m) * 4);
+      AK ? make_rsrc(Ab, ((int64_t)(g.m - 1) * g.lda + K) * 4)
+                  : make_rsrc(Ab, ((int64_t)(K - 1) * g.lda + g.m) * 4);
   const __amdgpu_buffer_rsrc_t rB =
-      BK ? make_rsrc(Bb, ((int64_t)(g.n - 1) * g.ldb + g.k) * 4)
-                  : make_rsrc(Bb, ((int64_t)(g.k - 1) * g.ldb + g.n) * 4);
+      BK ? make_rsrc(Bb, ((int64_t)(g.n - 1) * g.ldb + K) * 4)
+                  : make_rsrc(Bb, ((int64_t)(K - 1) * g.ldb + g.n) * 4);
 
   // loader maps: k-contiguous A / B: row t>>3 (+32q), k 4*(t&7)
   const int lr = t >> 3, lk = (t & 7) * 4;
@@ -268,7 +271,7 @@ __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S,
   __shared__ int s_last;
   const int t = threadIdx.x;
   {
-    const __amdgpu_buffer_rsrc_t rws = make_rsrc(g.ws + (int64_t)slot_of(me) * BSLOT, (int64_t)BSLOT * 4);
+    const __amdgpu_buffer_rsrc_t rws = make_rsrc(g.ws + uniform64(slot_of(me)) * BSLOT, (int64_t)BSLOT * 4);
     const uint32_t off = (uint32_t)(t * 64 * 4);
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -307,7 +310,7 @@ __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S,
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         if (c >= S) continue;
-        const __amdgpu_buffer_rsrc_t rws = make_rsrc(g.ws + (int64_t)slot_of(c) * BSLOT, (int64_t)BSLOT * 4);
+        const __amdgpu_buffer_rsrc_t rws = make_rsrc(g.ws + uniform64(slot_of(c)) * BSLOT, (int64_t)BSLOT * 4);
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -347,7 +350,7 @@ __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S,
         for (int b = 0; b < 2; ++b) sum[a][b] += acc[a][b];
       continue;
     }
-    const __amdgpu_buffer_rsrc_t rws = make_rsrc(g.ws + (int64_t)slot_of(c) * BSLOT, (int64_t)BSLOT * 4);
+    const __amdgpu_buffer_rsrc_t rws = make_rsrc(g.ws + uniform64(slot_of(c)) * BSLOT, (int64_t)BSLOT * 4);
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -374,12 +377,12 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, 
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = w >> 1, wc = w & 1;
   constexpr bool EPI = MODE == 2;
-  float* Cb = g.C + (MODE ? g.offC[bat] : bat * g.sCb);
+  float* Cb = g.C + (MODE ? uniform64(g.offC[bat]) : bat * g.sCb);
   const bool lower = g.flags & NMGP_OUT_LOWER;
   const bool tril = MODE && (g.flags & NMGP_OUT_TRIL);
   const bool eLo = g.flags & NMGP_EPI_E_LOWER;
-  const float* Eb = EPI ? g.E + (g.offE ? g.offE[bat] : 0) : nullptr;
-  const float* rs = EPI ? g.RS + (g.offRS ? g.offRS[bat] : 0) : nullptr;
+  const float* Eb = EPI ? g.E + (g.offE ? uniform64(g.offE[bat]) : 0) : nullptr;
+  const float* rs = EPI ? g.RS + (g.offRS ? uniform64(g.offRS[bat]) : 0) : nullptr;
   // with beta != 0 all 64 C values of the thread are loaded before the first store: one memory round trip per
   // tile (per accumulator block, the compiler kept 4 dependent load -> store rounds: 6.4 us of a 36 us k = 512
   // tile, tools/big_trace.hip)
@@ -436,7 +439,7 @@ __device__ inline void zero_acc(f32x16 (&acc)[2][2]) {
 }
 
 template <bool AK, bool BK, int MODE>
-__global__ __launch_bounds__(256, 2) void gemm_big_kernel(BigGemmArgs g) {
+__global__ __launch_bounds__(256, 2) void gemm_big_kernel(const BigGemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) float big_smem[];
   BIG_STAMP(0);
   // XCD-aware block order: hardware places block b on XCD b % 8; give each XCD a contiguous run
@@ -456,12 +459,13 @@ __global__ __launch_bounds__(256, 2) void gemm_big_kernel(BigGemmArgs g) {
   }
   const int64_t bat = blockIdx.y;
   f32x16 acc[2][2];
+  int K = g.k, koff = g.koff;
   if constexpr (MODE != 0) {
     if (g.kseg != nullptr) {
-      const int s0 = g.kseg[bat];
-      const int k0 = g.seg[s0], k1 = g.seg[s0 + g.kspan[bat]];
-      g.k = max(0, k1 - k0);
-      g.koff = k0;
+      const int s0 = uniform32(g.kseg[bat]);
+      const int k0 = uniform32(g.seg[s0]), k1 = uniform32(g.seg[s0 + uniform32(g.kspan[bat])]);
+      K = max(0, k1 - k0);
+      koff = k0;
     }
   }
 
@@ -472,7 +476,7 @@ __global__ __launch_bounds__(256, 2) void gemm_big_kernel(BigGemmArgs g) {
   // finished by the last of its contributors, summing partials in k order (deterministic).
   const bool sk = g.streamk;
   const int S = g.ksplit;
-  const int nkt_u = (g.k + BBK - 1) / BBK;
+  const int nkt_u = (K + BBK - 1) / BBK;
   const int64_t I = (int64_t)g.tiles * nkt_u, G = nb;
   auto lo = [&](int64_t w) { return (w * I) / G; };
   auto wg_of = [&](int64_t i) { return (int)(((i + 1) * G - 1) / I); };
@@ -485,9 +489,9 @@ __global__ __launch_bounds__(256, 2) void gemm_big_kernel(BigGemmArgs g) {
       tile = (int)(it / nkt_u);
       const int ka = (int)(it - (int64_t)tile * nkt_u);
       const int kb = (int)min((int64_t)nkt_u, (int64_t)ka + (end - it));
-      kend = g.k;
+      kend = K;
       kt0 = ka * BBK;
-      kt1 = min(g.k, kb * BBK);
+      kt1 = min(K, kb * BBK);
       step = kb - ka;
       if (ka > 0 || kb < nkt_u) {
         c0 = wg_of((int64_t)tile * nkt_u);
@@ -499,7 +503,7 @@ __global__ __launch_bounds__(256, 2) void gemm_big_kernel(BigGemmArgs g) {
       const int split = bid - tile * S;
       int tm0, tn0, kbeg;
       tile_coords(g, tile, tm0, tn0);
-      tile_krange(g, tm0 * BBM, tn0 * BBN, kbeg, kend);
+      tile_krange(g, K, tm0 * BBM, tn0 * BBN, kbeg, kend);
       // a tile wholly above the diagonal of an OUT_TRIL output (offsets variants) is stored as zeros:
       // no operand loads or MFMAs (the L-bar products over the minibatch rows have long k ranges)
       if (MODE != 0 && (g.flags & NMGP_OUT_TRIL) && tn0 * BBN > tm0 * BBM + BBM - 1) kend = kbeg;
@@ -515,7 +519,7 @@ __global__ __launch_bounds__(256, 2) void gemm_big_kernel(BigGemmArgs g) {
     tile_coords(g, tile, tm, tn);
     const int i0 = tm * BBM, j0 = tn * BBN;
     zero_acc(acc);
-    big_mainloop<AK, BK, MODE>(g, big_smem, bat, i0, j0, kend, kt0, kt1, acc);
+    big_mainloop<AK, BK, MODE>(g, K, koff, big_smem, bat, i0, j0, kend, kt0, kt1, acc);
     BIG_STAMP(2);
     bool store = true;
     if (nparts > 1) {
@@ -569,7 +573,7 @@ __global__ __launch_bounds__(256, 2) void potrf_step_kernel(PotrfStepArgs pa) {
   g.A = pa.P; g.lda = pa.lda; g.B = pa.X; g.ldb = 128; g.C = pa.P; g.sCi = pa.lda; g.sCj = 1;
   g.m = pa.n2; g.n = pa.nb; g.k = pa.nb; g.flags = NMGP_B_UPPER; g.alpha = 1.0f; g.beta = 0.0f;
   zero_acc(acc);
-  big_mainloop<true, true, 0>(g, big_smem, 0, i0, 0, pa.nb, 0, pa.nb, acc);
+  big_mainloop<true, true, 0>(g, g.k, 0, big_smem, 0, i0, 0, pa.nb, 0, pa.nb, acc);
   {
     const __amdgpu_buffer_rsrc_t rC = make_rsrc(pa.P, ((int64_t)(pa.n2 - 1) * pa.lda + pa.nb) * 4);
 #pragma unroll
@@ -607,7 +611,7 @@ __global__ __launch_bounds__(256, 2) void potrf_step_kernel(PotrfStepArgs pa) {
   g2.A = pa.P; g2.lda = pa.lda; g2.B = pa.P; g2.ldb = pa.lda; g2.C = pa.C; g2.sCi = pa.lda; g2.sCj = 1;
   g2.m = pa.n2; g2.n = pa.c1; g2.k = pa.nb; g2.flags = 0; g2.alpha = -1.0f; g2.beta = 1.0f;
   zero_acc(acc);
-  big_mainloop<true, true, 0, 16>(g2, big_smem, 0, i0, 0, pa.nb, 0, pa.nb, acc);
+  big_mainloop<true, true, 0, 16>(g2, g2.k, 0, big_smem, 0, i0, 0, pa.nb, 0, pa.nb, acc);
   if (t == 0) {
     const int old = __hip_atomic_fetch_add(pa.flag + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old == (int)gridDim.x - 1) {   // every reader is past its loads of L_0: re-arm for the next launch

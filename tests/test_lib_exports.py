@@ -28,3 +28,16 @@ def test_every_header_symbol_is_exported_and_bound():
     for name in declared:
         assert hasattr(lib, name), name
         assert name in L.exported_symbols(), f"{name} has no ctypes signature"
+
+
+def test_no_waterfall_buffer_loops_in_device_code():
+    """Every buffer resource in the HIP kernels is built from wave-uniform values: no kernel's device assembly
+    wraps a buffer access in a readfirstlane waterfall loop (round 5: the batched factor products built their
+    operand resources from per-problem offsets read as per-lane values -- 112 such loops per kernel)."""
+    import shutil
+    import sys as _sys
+    if shutil.which("/opt/rocm/bin/hipcc") is None:
+        pytest.skip("no hipcc")
+    _sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
+    import isa_check
+    assert isa_check.main() == {}

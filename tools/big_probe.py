@@ -1,73 +1,74 @@
-"""gemm_big_kernel (128x128 f32 MFMA, gemm_big.hip) on the shapes of the stress potrf's k = 512 updates, GPU box.
+"""Isolated timings of the ECoG-shaped batched factor products on gemm_big_kernel (HIP events, one stream).
 
-Every case reads L from the first 512 columns of a 4096 x 4096 row-major matrix (lda = 4096) and updates a
-lower / tall-lower block of it, as potrf_two_level_f32 does: C -= L_a L_b^T.  Timed per launch as the mean of
-a graph-replayed run of `reps` launches, with the split-K workspace (the library's automatic split / stream-K)
-and without it (one workgroup per tile).  Algorithmic flops: 2 * (stored elements) * k.
-usage: python tools/big_probe.py [--reps R]"""
+  python tools/big_probe.py [--nf 1024] [--M 1024] [--reps 5]
+
+Variants: the three products of the training step (syrk_side, xs_side, kl_lbar as engine.py builds them) and
+ablations of kl_lbar (no epilogue; k-contiguous A and/or B -- wrong values, same masks and tile ranges) that
+separate the epilogue's cost from the transposed-operand staging.  Prints one JSON line per variant.
+"""
 import argparse
-import ctypes
 import json
 import os
 import sys
 
-import torch
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from collaborative_nonstationary_multivariate_gaussian_process_amd import hip_ops as H  # noqa: E402
+import torch  # noqa: E402
+
 from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L  # noqa: E402
-
-PEAK = 157.3
-N = 4096
+from collaborative_nonstationary_multivariate_gaussian_process_amd import hip_ops as H  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--reps", type=int, default=20)
-    args = ap.parse_args()
-    dev = torch.device("cuda", 0)
+    ap.add_argument("--nf", type=int, default=1024)
+    ap.add_argument("--M", type=int, default=1024)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    M, nf = a.M, a.nf
+    MM = M * M
     g = torch.Generator(device=dev).manual_seed(0)
-    A = (torch.rand(N, N, generator=g, device=dev) * 2 - 1) * 1e-3
-    ws = H.big_workspace(dev, L.lib().nmgp_gemm_big_workspace_size())
-    lib = L.lib()
-    # (name, row0 of C, col0 of C, m, n, k): C = A[row0:row0+m, col0:col0+n], L rows = same rows, k columns 0..k
-    cases = [("np_first", 512, 512, 3584, 128, 512), ("np_rest", 640, 640, 3456, 384, 512),
-             ("far_full_p0", 1024, 1024, 3072, 3072, 512), ("far_piece_p0", 1024, 1024, 3072, 640, 512),
-             ("far_full_p3", 2560, 2560, 1536, 1536, 512), ("tile1", 3968, 3968, 128, 128, 512),
-             ("far_full_k1024", 2048, 2048, 2048, 2048, 1024), ("syrk_k128", 256, 256, 3840, 3840, 128)]
-    for name, r0, c0, m, n, k in cases:
-        for split in (True, False):
-            Lp = A[r0:, :k]
-            Lb = A[c0:, :k]
-            C = A[r0:, c0:]
-
-            def body():
-                rc = lib.nmgp_gemm_big_f32(ctypes.c_void_p(Lp.data_ptr()), N, ctypes.c_void_p(Lb.data_ptr()), N, 1,
-                                           ctypes.c_void_p(C.data_ptr()), N, 1, m, n, k, L.OUT_LOWER, -1.0, 1.0, 0, 0,
-                                           0, 1, ctypes.c_void_p(ws.data_ptr()) if split else None,
-                                           L.stream_handle())
-                L.check(rc, "gemm_big")
-            body()
-            torch.cuda.synchronize()
-            gr = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gr):
-                for _ in range(args.reps):
-                    body()
-            gr.replay()
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            best = 1e9
-            for _ in range(3):
-                e0.record()
-                gr.replay()
-                e1.record()
-                torch.cuda.synchronize()
-                best = min(best, e0.elapsed_time(e1) / args.reps)
-            tri = min(m, n)
-            elems = tri * (tri + 1) // 2 + (m - tri) * n
-            tf = 2.0 * elems * k / (best * 1e-3) / 1e12
-            print(json.dumps({"case": name, "m": m, "n": n, "k": k, "split": split, "us": round(best * 1e3, 2),
-                              "tflops": round(tf, 2), "frac": round(tf / PEAK, 4)}), flush=True)
+    mk = lambda: torch.randn(nf * MM, device=dev, generator=g) * 0.01
+    th, Cinv, Xs, gr, Af = mk(), mk(), mk(), mk(), mk()
+    rs = torch.rand(nf * M, device=dev, generator=g)
+    offs = [f * MM for f in range(nf)]
+    roffs = [f * M for f in range(nf)]
+    BB = H.BigBatch
+    base = dict(lda=M, ldb=M)
+    lb = L.A_UPPER | L.B_LOWER | L.OUT_TRIL
+    epi = (th, offs, (M, 1), rs, roffs, 1.0)
+    v = {
+        "syrk_side": BB(th, th, Af, offs, offs, offs, M, M, M, b_kcontig=True,
+                        flags=L.A_LOWER | L.B_UPPER | L.OUT_LOWER, diag_add=1e-4, **base),
+        "xs_side": BB(Cinv, th, Xs, offs, offs, offs, M, M, M, b_kcontig=False,
+                      flags=L.A_LOWER | L.B_LOWER | L.OUT_TRIL, **base),
+        "kl_lbar": BB(Cinv, Xs, gr, offs, offs, offs, M, M, M, a_kcontig=False, b_kcontig=False,
+                      flags=lb | L.EPI_E_LOWER, alpha=-1.0, beta=1.0, epi=epi, **base),
+        "kl_lbar_noepi_beta1": BB(Cinv, Xs, gr, offs, offs, offs, M, M, M, a_kcontig=False, b_kcontig=False,
+                                  flags=lb, alpha=-1.0, beta=1.0, **base),
+        "kl_lbar_noepi_beta0": BB(Cinv, Xs, gr, offs, offs, offs, M, M, M, a_kcontig=False, b_kcontig=False,
+                                  flags=lb, alpha=-1.0, beta=0.0, **base),
+        "kl_lbar_ak_beta0": BB(Cinv, Xs, gr, offs, offs, offs, M, M, M, a_kcontig=True, b_kcontig=False,
+                               flags=lb, alpha=-1.0, beta=0.0, **base),
+        "kl_lbar_ak_bk_beta0": BB(Cinv, Xs, gr, offs, offs, offs, M, M, M, a_kcontig=True, b_kcontig=True,
+                                  flags=lb, alpha=-1.0, beta=0.0, **base),
+    }
+    st = torch.cuda.current_stream()
+    for name, bb in v.items():
+        macs = bb.macs()
+        bb()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(a.reps):
+            bb()
+        e1.record(st)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / a.reps
+        print(json.dumps({"variant": name, "nf": nf, "M": M, "ms": round(ms, 3), "tflop": round(2 * macs / 1e12, 4),
+                          "tflops": round(2 * macs / ms / 1e9, 2), "ms_per_8384": round(ms * 8384 / nf, 2)}),
+              flush=True)
 
 
 if __name__ == "__main__":
