@@ -1679,12 +1679,15 @@ static int chol_inv_rec_big(float* A, int n, int64_t lda, int64_t sA, float* X, 
     return rc;
   if ((rc = block_copy<float>(nullptr, 0, 0, A + n1, lda, sA, n1, n2, batch, s)) != NMGP_OK) return rc;   // L12 = 0
   if ((rc = chol_inv_rec_big(A22, n2, lda, sA, X22, ldx, sX, batch, info, s, col_off + n1, ws)) != NMGP_OK) return rc;
-  // T = L21 X11 (op(B)(k,j) = X11[k][j], lower), stored transposed in X12;  X21 = -X22 T
-  if ((rc = gemm_big_f32(A21, lda, X, ldx, 0, X12, 1, ldx, n2, n1, n1, NMGP_B_LOWER, 1.f, 0.f, sA, sX, sX, nb, ws,
-                         s)) != NMGP_OK)
+  // T = L21 X11 (op(B)(k,j) = X11[k][j], lower) staged in X12;  X21 = -X22 T.  With n1 == n2 (every level of the
+  // power-of-two shapes) T fits X12 row-major: coalesced stores, and the second product reads it k-row-wise (the
+  // non-k-contiguous operand path stages as fast as the k-contiguous one).  Otherwise T is stored transposed.
+  const bool t_rows = n1 == n2;
+  if ((rc = gemm_big_f32(A21, lda, X, ldx, 0, X12, t_rows ? ldx : 1, t_rows ? 1 : ldx, n2, n1, n1, NMGP_B_LOWER, 1.f,
+                         0.f, sA, sX, sX, nb, ws, s)) != NMGP_OK)
     return rc;
-  if ((rc = gemm_big_f32(X22, ldx, X12, ldx, 1, X21, ldx, 1, n2, n1, n2, NMGP_A_LOWER, -1.f, 0.f, sX, sX, sX, nb, ws,
-                         s)) != NMGP_OK)
+  if ((rc = gemm_big_f32(X22, ldx, X12, ldx, t_rows ? 0 : 1, X21, ldx, 1, n2, n1, n2, NMGP_A_LOWER, -1.f, 0.f, sX, sX,
+                         sX, nb, ws, s)) != NMGP_OK)
     return rc;
   return block_copy<float>(nullptr, 0, 0, X12, ldx, sX, n1, n2, batch, s);   // X12 = 0
 }

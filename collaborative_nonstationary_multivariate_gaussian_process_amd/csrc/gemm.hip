@@ -628,13 +628,68 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, const nmgp_gemm_
     }
   }
 
+  // The thread's 16 outputs.  C (beta != 0) and the epilogue operand rs(i) E(i, j) are read for all 16 before the
+  // first store, as branch-free buffer loads (an element that is not read takes an out-of-range offset and reads
+  // 0): emit() per element waited on each C / E load before its store and the next load (16-32 dependent round
+  // trips per tile).  Spans of 2 GiB or more keep the per-element form.
+  const int64_t sz = (int64_t)sizeof(T);
+  const int64_t extC = ((r0 + m - 1) * d.sC_i + (int64_t)(n - 1) * d.sC_j + 1) * sz;
+  const int64_t extE = (flags & NMGP_EPI) ? ((r0 + m - 1) * d.sE_i + (int64_t)(n - 1) * d.sE_j + 1) * sz : 0;
+  if (extC < 0x7fffffffLL && extE < 0x7fffffffLL && d.sC_i >= 0 && d.sC_j >= 0) {
+    const bool ldc = beta != (T)0, epi = (flags & NMGP_EPI) != 0;
+    const __amdgpu_buffer_rsrc_t rC = make_rsrc(d.C, extC);
+    const __amdgpu_buffer_rsrc_t rE = make_rsrc(epi ? d.epi_E : d.C, extE);
+    const __amdgpu_buffer_rsrc_t rR = make_rsrc(epi && rsp ? (const void*)d.epi_rs : d.C, epi && rsp ? (r0 + m) * sz : 0);
+    // raw values only in the load loop (arithmetic and flag tests there made the compiler wait on each load)
+    T cv[16], ev[16], rv[8];
+    const uint32_t oob = 0x80000000u;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const acc_t& acc = q == 0 ? acc00 : q == 1 ? acc01 : q == 2 ? acc10 : acc11;
-    const int mi = q >> 1, ni = q & 1;
+    for (int q = 0; q < 4; ++q) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      emit(i0 + wr * 32 + mi * 16 + Mfma<T>::row(lane, r), j0 + wc * 32 + ni * 16 + (lane & 15), acc[r]);
+      for (int r = 0; r < 4; ++r) {
+        const int gi = i0 + wr * 32 + (q >> 1) * 16 + Mfma<T>::row(lane, r), gj = j0 + wc * 32 + (q & 1) * 16 + (lane & 15);
+        const bool upper = gj > gi;
+        const bool rd = gi < m && gj < n && !(upper && (flags & (NMGP_OUT_LOWER | NMGP_OUT_TRIL)));
+        const bool rde = epi && rd && !((flags & NMGP_EPI_E_LOWER) && upper);
+        cv[4 * q + r] = bload<T>(rC, ldc && rd ? (uint32_t)(((r0 + gi) * d.sC_i + (int64_t)gj * d.sC_j) * sz) : oob);
+        ev[4 * q + r] = bload<T>(rE, rde ? (uint32_t)(((r0 + gi) * d.sE_i + (int64_t)gj * d.sE_j) * sz) : oob);
+        if ((q & 1) == 0) rv[4 * (q >> 1) + r] = bload<T>(rR, gi < m ? (uint32_t)((r0 + gi) * sz) : oob);
+      }
+    }
+    const T rsgn = (flags & NMGP_EPI_RS_NEG) ? (T)-1 : (T)1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const acc_t& acc = q == 0 ? acc00 : q == 1 ? acc01 : q == 2 ? acc10 : acc11;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = i0 + wr * 32 + (q >> 1) * 16 + Mfma<T>::row(lane, r), gj = j0 + wc * 32 + (q & 1) * 16 + (lane & 15);
+        if (gi >= m || gj >= n) continue;
+        const bool upper = gj > gi;
+        if (upper && (flags & NMGP_OUT_LOWER)) continue;
+        T val;
+        if (upper && (flags & NMGP_OUT_TRIL)) {
+          val = 0;
+        } else {
+          val = alpha * acc[r];
+          if (ldc) val += beta * cv[4 * q + r];
+          if (epi) {
+            const T rs = (rsp ? rv[4 * (q >> 1) + r] : (T)1) * rsgn;
+            val += gamma * rs * ev[4 * q + r];
+          }
+          if ((flags & NMGP_DIAG_ADD) && gi == gj) val += dadd;
+        }
+        C[(r0 + gi) * d.sC_i + (int64_t)gj * d.sC_j] = val;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const acc_t& acc = q == 0 ? acc00 : q == 1 ? acc01 : q == 2 ? acc10 : acc11;
+      const int mi = q >> 1, ni = q & 1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        emit(i0 + wr * 32 + mi * 16 + Mfma<T>::row(lane, r), j0 + wc * 32 + ni * 16 + (lane & 15), acc[r]);
+    }
   }
   GEMM_STAMP(71);
   GEMM_STAMPB(3);

@@ -124,9 +124,10 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
 
   // loader maps: k-contiguous A / B: row t>>3 (+32q), k 4*(t&7)
   const int lr = t >> 3, lk = (t & 7) * 4;
-  // i-contiguous A / j-contiguous B: k = (t & 7) + 8q, i or j = 4 (t >> 3): each k row is read as 128
-  // contiguous bytes by 8 lanes, and the transposed LDS writes of consecutive lanes hit consecutive
-  // banks (2-way at most; a k = t >> 5 map put 8 lanes on one bank)
+  // i-contiguous A / j-contiguous B: k = 4 (t & 7) + q, i or j = 4 (t >> 3) + e: each k row is read as 128
+  // contiguous bytes by 8 lanes, and the thread's 4 x 4 block (k rows q, columns e) is transposed in registers
+  // so the LDS image [i][k] is written with one 16-byte store per i -- the k-contiguous operands' store pattern
+  // (16 single-float transposed stores per operand before: a both-transposed product ran at half the MFMA rate)
   const int jr = t & 7, jc = (t >> 3) * 4;
   float4 ra[4], rb[4];
 
@@ -140,7 +141,7 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
     } else {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int64_t kr = kt + jr + 8 * q;
+        const int64_t kr = kt + 4 * jr + q;
         ra[q] = ld4<AUX>(rA, (uint32_t)((kr * g.lda + i0 + jc) * 4));
       }
     }
@@ -153,7 +154,7 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
     } else {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int64_t kr = kt + jr + 8 * q;
+        const int64_t kr = kt + 4 * jr + q;
         rb[q] = ld4<AUX>(rB, (uint32_t)((kr * g.ldb + j0 + jc) * 4));
       }
     }
@@ -175,7 +176,7 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
             a[e] = keep_if(a[e], kk < kend && (!aLo || kk <= i) && (!aUp || kk >= i));
           }
         } else {
-          const int kk = kt + jr + 8 * q;
+          const int kk = kt + 4 * jr + q;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int i = i0 + jc + e;
@@ -191,7 +192,7 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
             b[e] = keep_if(b[e], kk < kend && (!bUp || kk <= j) && (!bLo || kk >= j));
           }
         } else {
-          const int kk = kt + jr + 8 * q;
+          const int kk = kt + 4 * jr + q;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int j = j0 + jc + e;
@@ -207,22 +208,16 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
       for (int q = 0; q < 4; ++q) *(float4*)&As[(lr + 32 * q) * BP + lk] = ra[q];
     } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float* a = (const float*)&ra[q];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) As[(jc + e) * BP + jr + 8 * q] = a[e];
-      }
+      for (int e = 0; e < 4; ++e)
+        *(float4*)&As[(jc + e) * BP + 4 * jr] = make_float4(ra[0][e], ra[1][e], ra[2][e], ra[3][e]);
     }
     if constexpr (BK) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) *(float4*)&Bs[(lr + 32 * q) * BP + lk] = rb[q];
     } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float* b = (const float*)&rb[q];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) Bs[(jc + e) * BP + jr + 8 * q] = b[e];
-      }
+      for (int e = 0; e < 4; ++e)
+        *(float4*)&Bs[(jc + e) * BP + 4 * jr] = make_float4(rb[0][e], rb[1][e], rb[2][e], rb[3][e]);
     }
   };
 
@@ -369,64 +364,85 @@ __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S,
   return true;
 }
 
-// C = alpha * acc + beta * C (+ diag_add, + the KL epilogue) on the stored part of the tile.  The C loads are
-// issued together before any store (the compiler cannot move a C load above a C store it may alias).
-template <int MODE>
-__device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, int i0, int j0, f32x16 (&acc)[2][2]) {
+// One half tile (acc[A][*], 64 x 128) of the epilogue: C and the epilogue operand gamma rs(i) E(i, j) are read
+// before the half's stores, as branch-free buffer loads (an element outside the stored part reads 0 through an
+// out-of-range offset; the host checks that every problem's C and E span < 2 GiB).  With per-element guards each
+// load sat in its own branch and was waited on before the next, and E, read in the store loop, waited on every
+// store before it (64 dependent round trips per tile in the KL L-bar product, the ECoG step's longest launch).
+// E must not alias C.  A is a template parameter so every accumulator index is a constant.
+template <int MODE, int A>
+__device__ __forceinline__ void big_epi_half(const BigGemmArgs& g, float* Cb, __amdgpu_buffer_rsrc_t rCb,
+                                             __amdgpu_buffer_rsrc_t rEb, __amdgpu_buffer_rsrc_t rRS, int i0, int j0,
+                                             const f32x16 (&acc)[2][2]) {
+  constexpr bool EPI = MODE == 2;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = w >> 1, wc = w & 1;
-  constexpr bool EPI = MODE == 2;
-  float* Cb = g.C + (MODE ? uniform64(g.offC[bat]) : bat * g.sCb);
   const bool lower = g.flags & NMGP_OUT_LOWER;
   const bool tril = MODE && (g.flags & NMGP_OUT_TRIL);
   const bool eLo = g.flags & NMGP_EPI_E_LOWER;
-  const float* Eb = EPI ? g.E + (g.offE ? uniform64(g.offE[bat]) : 0) : nullptr;
-  const float* rs = EPI ? g.RS + (g.offRS ? uniform64(g.offRS[bat]) : 0) : nullptr;
-  // with beta != 0 all 64 C values of the thread are loaded before the first store: one memory round trip per
-  // tile (per accumulator block, the compiler kept 4 dependent load -> store rounds: 6.4 us of a 36 us k = 512
-  // tile, tools/big_trace.hip)
-  f32x16 cv[2][2];
-  if (g.beta != 0.0f) {
+  const bool ldc = g.beta != 0.0f;
+  const int ib = i0 + 64 * wr + 32 * A + 4 * (lane >> 5);
+  f32x16 cv[2], ev[2];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+  for (int b = 0; b < 2; ++b) {
+    const int j = j0 + 64 * wc + 32 * b + (lane & 31);
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int ib = i0 + 64 * wr + 32 * a + 4 * (lane >> 5);
-        const int j = j0 + 64 * wc + 32 * b + (lane & 31);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int i = ib + (r & 3) + 8 * (r >> 2);
-          // (elements that OUT_TRIL zeroes are not read: a third of C's traffic in the batched L-bar forms)
-          const bool ok = i < g.m && j < g.n && (!lower || j <= i) && !(tril && j > i);
-          cv[a][b][r] = ok ? __builtin_nontemporal_load(Cb + (int64_t)i * g.sCi + (int64_t)j * g.sCj) : 0.0f;
-        }
-      }
-  }
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int ib = i0 + 64 * wr + 32 * a + 4 * (lane >> 5);
-      const int j = j0 + 64 * wc + 32 * b + (lane & 31);
-      f32x16 v = acc[a][b] * g.alpha;
-      if (g.beta != 0.0f) v += g.beta * cv[a][b];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int i = ib + (r & 3) + 8 * (r >> 2);
-        if (i < g.m && j < g.n && (!lower || j <= i)) {
-          float x = v[r];
-          if constexpr (MODE == 1) {
-            if (i == j) x += g.diag_add;
-          }
-          if constexpr (EPI) {
-            if (!(eLo && j > i)) x += g.gamma * rs[i] * Eb[(int64_t)i * g.sEi + (int64_t)j * g.sEj];
-          }
-          if (tril && j > i) x = 0.0f;
-          Cb[(int64_t)i * g.sCi + (int64_t)j * g.sCj] = x;
-        }
+    for (int r = 0; r < 16; ++r) {
+      const int i = ib + (r & 3) + 8 * (r >> 2);
+      // (elements that OUT_TRIL zeroes are not read: a third of C's traffic in the batched L-bar forms)
+      const bool ok = i < g.m && j < g.n && (!lower || j <= i) && !(tril && j > i);
+      cv[b][r] = ldc ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                           rCb, ok ? (uint32_t)(((int64_t)i * g.sCi + (int64_t)j * g.sCj) * 4) : 0x80000000u, 0, 0))
+                     : 0.0f;
+      if constexpr (EPI) {
+        const bool oke = ok && !(eLo && j > i);
+        const float e = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+            rEb, oke ? (uint32_t)(((int64_t)i * g.sEi + (int64_t)j * g.sEj) * 4) : 0x80000000u, 0, 0));
+        const float rv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+            rRS, i < g.m ? (uint32_t)(i * 4) : 0x80000000u, 0, 0));
+        ev[b][r] = g.gamma * rv * e;
+      } else {
+        ev[b][r] = 0.0f;
       }
     }
+  }
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int j = j0 + 64 * wc + 32 * b + (lane & 31);
+    f32x16 v = acc[A][b] * g.alpha;
+    if (ldc) v += g.beta * cv[b];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = ib + (r & 3) + 8 * (r >> 2);
+      if (i < g.m && j < g.n && (!lower || j <= i)) {
+        float x = v[r];
+        if constexpr (MODE == 1) {
+          if (i == j) x += g.diag_add;
+        }
+        if constexpr (EPI) {
+          if (!(eLo && j > i)) x += ev[b][r];
+        }
+        if (tril && j > i) x = 0.0f;
+        Cb[(int64_t)i * g.sCi + (int64_t)j * g.sCj] = x;
+      }
+    }
+  }
+}
+
+// C = alpha * acc + beta * C (+ diag_add, + the KL epilogue) on the stored part of the tile.
+template <int MODE>
+__device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, int i0, int j0, f32x16 (&acc)[2][2]) {
+  constexpr bool EPI = MODE == 2;
+  float* Cb = g.C + (MODE ? uniform64(g.offC[bat]) : bat * g.sCb);
+  const float* Eb = EPI ? g.E + (g.offE ? uniform64(g.offE[bat]) : 0) : nullptr;
+  const float* rs = EPI ? g.RS + (g.offRS ? uniform64(g.offRS[bat]) : 0) : nullptr;
+  const __amdgpu_buffer_rsrc_t rCb = make_rsrc(Cb, ((int64_t)(g.m - 1) * g.sCi + (int64_t)(g.n - 1) * g.sCj + 1) * 4);
+  const __amdgpu_buffer_rsrc_t rEb =
+      make_rsrc(EPI ? Eb : Cb, EPI ? ((int64_t)(g.m - 1) * g.sEi + (int64_t)(g.n - 1) * g.sEj + 1) * 4 : 0);
+  const __amdgpu_buffer_rsrc_t rRS = make_rsrc(EPI ? rs : Cb, EPI ? (int64_t)g.m * 4 : 0);
+  big_epi_half<MODE, 0>(g, Cb, rCb, rEb, rRS, i0, j0, acc);
+  big_epi_half<MODE, 1>(g, Cb, rCb, rEb, rRS, i0, j0, acc);
 }
 
 __device__ inline void zero_acc(f32x16 (&acc)[2][2]) {
@@ -814,6 +830,16 @@ static int gemm_big_f32_ex(const float* A, int64_t lda, const float* B, int64_t 
   g.seg = ep.seg; g.kseg = ep.kseg; g.kspan = ep.kspan; g.koff = 0;
   if (ep.kseg != nullptr && (offA == nullptr || ep.seg == nullptr || ep.kspan == nullptr)) return -1;
   if ((flags & NMGP_EPI) && (ep.E == nullptr || ep.RS == nullptr)) return -1;
+  {
+    // 32-bit buffer offsets: every problem's operand, output and epilogue spans stay below 2 GiB
+    const int64_t lim = 0x7fffffffLL;
+    const int64_t spanA = ep.a_kcontig ? (int64_t)(m - 1) * lda + k : (int64_t)(k - 1) * lda + m;
+    const int64_t spanB = b_kcontig ? (int64_t)(n - 1) * ldb + k : (int64_t)(k - 1) * ldb + n;
+    const int64_t spanC = (int64_t)(m - 1) * sCi + (int64_t)(n - 1) * sCj + 1;
+    const int64_t spanE = (flags & NMGP_EPI) ? (int64_t)(m - 1) * ep.sEi + (int64_t)(n - 1) * ep.sEj + 1 : 0;
+    if (spanA * 4 >= lim || spanB * 4 >= lim || spanC * 4 >= lim || spanE * 4 >= lim || sCi < 0 || sCj < 0)
+      return -1;
+  }
   g.lda = lda; g.ldb = ldb; g.sCi = sCi; g.sCj = sCj;
   g.sAb = sAb; g.sBb = sBb; g.sCb = sCb;
   g.m = m; g.n = n; g.k = k; g.flags = flags; g.b_kcontig = b_kcontig;
