@@ -838,7 +838,7 @@ static int gemm_big_f32_ex(const float* A, int64_t lda, const float* B, int64_t 
     const int64_t spanC = (int64_t)(m - 1) * sCi + (int64_t)(n - 1) * sCj + 1;
     const int64_t spanE = (flags & NMGP_EPI) ? (int64_t)(m - 1) * ep.sEi + (int64_t)(n - 1) * ep.sEj + 1 : 0;
     if (spanA * 4 >= lim || spanB * 4 >= lim || spanC * 4 >= lim || spanE * 4 >= lim || sCi < 0 || sCj < 0)
-      return -1;
+      return -40;
   }
   g.lda = lda; g.ldb = ldb; g.sCi = sCi; g.sCj = sCj;
   g.sAb = sAb; g.sBb = sBb; g.sCb = sCb;

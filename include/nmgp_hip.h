@@ -229,7 +229,10 @@ int nmgp_gemm_big_offsets_f32(const float* A, int64_t lda, const float* B, int64
  * -C^-T (C^-1 L) + diag(1/C_ii^2) L (code/utils.py:339-351 and its autograd), for all D + Q + 1
  * factors in one launch.  kseg != NULL: problem b sums k over [seg[kseg[b]], seg[kseg[b] + kspan[b]])
  * of the device segment table (A and B advanced to that k), the rows of the outputs it covers -- the
- * L-bar products P^T W of the quadratic forms (code/nmgp_dsvi.py:227-258 and their autograd).    */
+ * L-bar products P^T W of the quadratic forms (code/nmgp_dsvi.py:227-258 and their autograd).
+ * All nmgp_gemm_big_* forms: every problem's A, B, C and E span must stay below 2 GiB (32-bit buffer
+ * offsets; -40 otherwise), output strides are non-negative, and E must not alias C (a tile's C and E
+ * values are read before its stores).                                                               */
 int nmgp_gemm_big_offsets_epi_f32(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb,
                                   int b_kcontig, float* C, int64_t sCi, int64_t sCj, int m, int n, int k, int flags,
                                   double alpha, double beta, double diag_add, const int64_t* offA,

@@ -41,3 +41,18 @@ def test_no_waterfall_buffer_loops_in_device_code():
     _sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
     import isa_check
     assert isa_check.main() == {}
+
+
+def test_gemm_big_rejects_spans_past_32bit_offsets():
+    """The 128x128 f32 GEMM addresses operands, outputs and the epilogue operand through 32-bit buffer offsets: a
+    problem whose A / B / C span reaches 2 GiB is refused (-40) before anything is launched (no GPU needed)."""
+    lib = L.lib()
+    vp = ctypes.c_void_p
+    fake = vp(0x1000)
+    f = lib.nmgp_gemm_big_f32
+    # A: 4 rows at lda = 2^29 floats -> span 3 * 2^31 bytes
+    rc = f(fake, 1 << 29, fake, 64, 1, fake, 64, 1, 4, 64, 64, 0, 1.0, 0.0, 0, 0, 0, 1, None, None)
+    assert rc == -40
+    # C: row stride 2^29 floats
+    rc = f(fake, 64, fake, 64, 1, fake, 1 << 29, 1, 4, 64, 64, 0, 1.0, 0.0, 0, 0, 0, 1, None, None)
+    assert rc == -40
