@@ -445,6 +445,112 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, 
   big_epi_half<MODE, 1>(g, Cb, rCb, rEb, rRS, i0, j0, acc);
 }
 
+// Row-vector epilogue through LDS (row-contiguous C, and E, 16-byte aligned): the accumulators (each lane holds 16
+// values of ONE column) go to a 128 x 128 LDS image, then every thread owns 16 four-column row chunks -- a wave
+// stores two 512-byte row segments per instruction (global_store_dwordx4) instead of 64 single floats per thread,
+// and reads C / E the same way, all 16 chunks' loads before the first store.  The per-workgroup phase trace of the
+// batched ECoG products (tools/big_trace_batch.hip) had the single-float epilogue at 13.3-13.5 us of a 43-65 us
+// tile.  Same arithmetic, element by element, as big_epi_half.
+constexpr int BCP = 136;   // LDS pitch of the C image (floats): lanes 32..63 of a column write land 32 banks over
+template <int MODE>
+__device__ __forceinline__ void big_epilogue_rows(const BigGemmArgs& g, float* Cb, const float* Eb, const float* rs,
+                                                  int i0, int j0, const f32x16 (&acc)[2][2], float* sm) {
+  constexpr bool EPI = MODE == 2;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 1, wc = w & 1;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        sm[(64 * wr + 32 * a + 4 * (lane >> 5) + (r & 3) + 8 * (r >> 2)) * BCP + 64 * wc + 32 * b + (lane & 31)] =
+            acc[a][b][r];
+  __syncthreads();
+  // the scalar arguments the chunk loop uses, read once (left in the argument struct, several were spilled and
+  // re-read from scratch per chunk)
+  const int gm = g.m, gn = g.n;
+  const int64_t sCi = g.sCi, sEi = EPI ? g.sEi : 0;
+  const float alpha = g.alpha, beta = g.beta, dadd = g.diag_add, gamma = EPI ? g.gamma : 0.0f;
+  const bool lower = g.flags & NMGP_OUT_LOWER;
+  const bool tril = MODE && (g.flags & NMGP_OUT_TRIL);
+  const bool eLo = g.flags & NMGP_EPI_E_LOWER;
+  const bool ldc = beta != 0.0f;
+  const int c4 = (t & 31) * 4, rb = t >> 5;
+  const int j = j0 + c4;
+  // (the pointers are wave-uniform; said explicitly, or the compiler may keep one in VGPRs and wrap every buffer
+  // access in a waterfall loop)
+  Cb = (float*)uniform64((int64_t)Cb);
+  if constexpr (EPI) {
+    Eb = (const float*)uniform64((int64_t)Eb);
+    rs = (const float*)uniform64((int64_t)rs);
+  }
+  const __amdgpu_buffer_rsrc_t rC = make_rsrc(Cb, ((int64_t)(gm - 1) * sCi + gn) * 4);
+  const __amdgpu_buffer_rsrc_t rE = make_rsrc(EPI ? Eb : Cb, EPI ? ((int64_t)(gm - 1) * sEi + gn) * 4 : 0);
+  const __amdgpu_buffer_rsrc_t rR = make_rsrc(EPI ? rs : Cb, EPI ? (int64_t)gm * 4 : 0);
+  constexpr uint32_t oob = 0x80000000u;
+  // 16 chunks per thread in two halves of 8 (loads of a half in flight together)
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float4 cv[8], ev[8];
+    float rv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = i0 + rb + 8 * (8 * h + q);
+      // a chunk is read when any of its elements keeps a computed value (not wholly above an OUT_LOWER / OUT_TRIL
+      // diagonal, inside the matrix); out-of-range columns read 0 through the resource bound
+      const bool rd = i < gm && j < gn && !((lower || tril) && j > i);
+      cv[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rC, ldc && rd ? (uint32_t)(((int64_t)i * sCi + j) * 4) : oob, 0, 0));
+      if constexpr (EPI) {
+        ev[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               rE, rd && !(eLo && j > i) ? (uint32_t)(((int64_t)i * sEi + j) * 4) : oob,
+                                               0, 0));
+        rv[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rR, rd ? (uint32_t)(i * 4) : oob, 0, 0));
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int row = rb + 8 * (8 * h + q);
+      const int i = i0 + row;
+      if (i >= gm || j >= gn) continue;
+      if (lower && j > i) continue;                 // wholly above the diagonal: nothing stored
+      const float4 av = *(const float4*)&sm[row * BCP + c4];
+      float x[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int jj = j + e;
+        float v = ((const float*)&av)[e] * alpha;
+        if (ldc) v += beta * ((const float*)&cv[q])[e];
+        if constexpr (MODE == 1) {
+          if (i == jj) v += dadd;
+        }
+        if constexpr (EPI) {
+          if (!(eLo && jj > i)) v += gamma * rv[q] * ((const float*)&ev[q])[e];
+        }
+        if (tril && jj > i) v = 0.0f;
+        x[e] = v;
+      }
+      const uint32_t off = (uint32_t)(((int64_t)i * sCi + j) * 4);
+      if (j + 3 < gn && !(lower && j + 3 > i)) {
+        u32x4g v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = __float_as_uint(x[e]);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rC, off, 0, 0);
+      } else {
+        // a chunk across the matrix edge or an OUT_LOWER diagonal: the elements that are not stored take an
+        // out-of-range offset (buffer stores past the resource are dropped)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x[e]), rC,
+                                                j + e < gn && !(lower && j + e > i) ? off + 4 * e : oob, 0, 0);
+      }
+    }
+  }
+  __syncthreads();   // the LDS image is the next tile's staging buffer (stream-K workgroups run several tiles)
+}
+
 __device__ inline void zero_acc(f32x16 (&acc)[2][2]) {
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -549,7 +655,19 @@ __global__ __launch_bounds__(256, 2) void gemm_big_kernel(const BigGemmArgs g) {
       store = big_combine(g, me, nparts, ctr, slot_of, acc);
     }
     BIG_STAMP(3);
-    if (store) big_epilogue<MODE>(g, bat, i0, j0, acc);
+    if (store) {
+      // row-vector epilogue when C (and E) rows are contiguous and 16-byte aligned (every engine product)
+      constexpr bool EPI = MODE == 2;
+      float* Cb = g.C + (MODE ? uniform64(g.offC[bat]) : bat * g.sCb);
+      const float* Eb = EPI ? g.E + (g.offE ? uniform64(g.offE[bat]) : 0) : nullptr;
+      const float* rsb = EPI ? g.RS + (g.offRS ? uniform64(g.offRS[bat]) : 0) : nullptr;
+      const bool rows = g.sCj == 1 && (g.sCi & 3) == 0 && (((uintptr_t)Cb) & 15) == 0 &&
+                        (!EPI || (g.sEj == 1 && (g.sEi & 3) == 0 && (((uintptr_t)Eb) & 15) == 0));
+      if (rows)
+        big_epilogue_rows<MODE>(g, Cb, Eb, rsb, i0, j0, acc, big_smem);
+      else
+        big_epilogue<MODE>(g, bat, i0, j0, acc);
+    }
     it += step;
   }
 #ifdef NMGP_BIG_TRACE
