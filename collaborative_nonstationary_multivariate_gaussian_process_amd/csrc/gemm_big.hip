@@ -129,6 +129,11 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
   // so the LDS image [i][k] is written with one 16-byte store per i -- the k-contiguous operands' store pattern
   // (16 single-float transposed stores per operand before: a both-transposed product ran at half the MFMA rate)
   const int jr = t & 7, jc = (t >> 3) * 4;
+  // k row of load q: 4 jr + q (LDS slot 4 jr + q holds k 4 jr + q, the k-contiguous operands' order); with BOTH
+  // operands k-strided the slots may hold any common permutation of k, and load q takes k = 8 q + jr instead, so
+  // one wave instruction covers 8 consecutive k rows (4 KB apart) rather than rows 16 KB apart
+  constexpr bool KPERM = !AK && !BK;
+  auto krow = [&](int q) { return KPERM ? 8 * q + jr : 4 * jr + q; };
   float4 ra[4], rb[4];
 
   auto load = [&](int kt) {
@@ -141,7 +146,7 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
     } else {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int64_t kr = kt + 4 * jr + q;
+        const int64_t kr = kt + krow(q);
         ra[q] = ld4<AUX>(rA, (uint32_t)((kr * g.lda + i0 + jc) * 4));
       }
     }
@@ -154,7 +159,7 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
     } else {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int64_t kr = kt + 4 * jr + q;
+        const int64_t kr = kt + krow(q);
         rb[q] = ld4<AUX>(rB, (uint32_t)((kr * g.ldb + j0 + jc) * 4));
       }
     }
@@ -176,7 +181,7 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
             a[e] = keep_if(a[e], kk < kend && (!aLo || kk <= i) && (!aUp || kk >= i));
           }
         } else {
-          const int kk = kt + 4 * jr + q;
+          const int kk = kt + krow(q);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int i = i0 + jc + e;
@@ -192,7 +197,7 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
             b[e] = keep_if(b[e], kk < kend && (!bUp || kk <= j) && (!bLo || kk >= j));
           }
         } else {
-          const int kk = kt + 4 * jr + q;
+          const int kk = kt + krow(q);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int j = j0 + jc + e;

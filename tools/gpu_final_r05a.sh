@@ -1,10 +1,11 @@
 #!/bin/bash
 # Round-5 final evidence, part A: the whole GPU suite and smoke on the final code.
 set -e
+TAG=${1:-r05z}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r05z_gpu_tests.log 2>&1 || { tail -40 gpurun_out/r05z_gpu_tests.log; exit 1; }
-tail -3 gpurun_out/r05z_gpu_tests.log
-timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r05z_smoke.log 2>&1
-tail -1 gpurun_out/r05z_smoke.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_gpu_tests.log 2>&1 || { tail -40 gpurun_out/${TAG}_gpu_tests.log; exit 1; }
+tail -3 gpurun_out/${TAG}_gpu_tests.log
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/${TAG}_smoke.log 2>&1
+tail -1 gpurun_out/${TAG}_smoke.log
