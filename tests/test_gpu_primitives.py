@@ -590,6 +590,47 @@ def test_gemm_big_offsets_batch(ops):
         assert rel(got, ref) < 2e-6 and torch.all(got[~lo] == 0)
 
 
+def test_gemm_big_row_epilogue_edges(ops):
+    # the row-vector epilogue (row-contiguous, 16-byte aligned C and E): n = 130 leaves a partial 4-column chunk at
+    # the right edge, OUT_LOWER chunks straddle the diagonal, beta = 1 and the E term read 16-byte chunks; the
+    # row pitch 132 keeps the rows aligned.  Compared with fp64 torch element by element, masked parts untouched.
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L
+    g = torch.Generator().manual_seed(41)
+    M, LD, nb = 130, 132, 3
+    pool = torch.randn(nb * M * M, generator=g)
+    P = pool.to(DEV)
+    offs = [b * M * M for b in range(nb)]
+    C0 = torch.randn(nb, M, LD, generator=g)
+    C = C0.clone().to(DEV)
+    cs = [b * M * LD for b in range(nb)]
+    syrk = ops.BigBatch(P, P, C, offs, offs, cs, M, M, M, lda=M, ldb=M, b_kcontig=True, sC=(LD, 1),
+                        flags=L.A_LOWER | L.B_UPPER | L.OUT_LOWER, beta=1.0, diag_add=0.5)
+    syrk()
+    lo = torch.tril(torch.ones(M, M, dtype=torch.bool))
+    for b, o in enumerate(offs):
+        S = torch.tril(pool[o:o + M * M].reshape(M, M).double())
+        ref = S @ S.t() + C0[b, :, :M].double() + 0.5 * torch.eye(M, dtype=F64)
+        got = C[b].cpu()
+        assert rel(got[:, :M][lo], ref[lo]) < 2e-6
+        assert torch.equal(got[:, :M][~lo], C0[b, :, :M][~lo]) and torch.equal(got[:, M:], C0[b, :, M:])
+    E = torch.randn(nb, M, LD, generator=g)
+    Ed = E.to(DEV)
+    RS = torch.randn(nb * M, generator=g).to(DEV)
+    G0 = torch.randn(nb, M, LD, generator=g)
+    G = G0.clone().to(DEV)
+    kl = ops.BigBatch(P, P, G, offs, offs, cs, M, M, M, lda=M, ldb=M, a_kcontig=False, b_kcontig=False, sC=(LD, 1),
+                      flags=L.A_UPPER | L.B_LOWER | L.OUT_TRIL | L.EPI_E_LOWER, alpha=-1.0, beta=1.0,
+                      epi=(Ed, cs, (LD, 1), RS, [b * M for b in range(nb)], 2.0))
+    kl()
+    for b, o in enumerate(offs):
+        A = torch.tril(pool[o:o + M * M].reshape(M, M).double())
+        rs = RS.cpu().double()[b * M:(b + 1) * M]
+        ref = torch.tril(-A.t() @ A + G0[b, :, :M].double() + 2.0 * rs[:, None] * torch.tril(E[b, :, :M].double()))
+        got = G[b].cpu()
+        assert rel(got[:, :M], ref) < 2e-6 and torch.all(got[:, :M][~lo] == 0)
+        assert torch.equal(got[:, M:], G0[b, :, M:])
+
+
 def test_gemm_big_kseg_batch(ops):
     # per-problem k ranges from a device segment table (L-bar products P^T W over each factor's rows),
     # transposed operands, OUT_TRIL + beta accumulate; an empty segment leaves C (lower) unchanged
