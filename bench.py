@@ -406,6 +406,7 @@ def train_roofline(eng, cfg):
         fams["gemm_big_kernel"][0] += (kf1 - kf0) * 2.0 * H.chol_inv_rec_macs(eng.M) / 1e9
         fams["gemm_big_kernel"][1].append("chol_side (recursive factor + inverse GEMMs)")
     src, d, stale = matched_profile(f"r*_{cfg}_train_kernels.json")
+    tsrc, td, tstale = matched_profile(f"r*_{cfg}_train_traffic.json")
     busy = {}
     if d is not None:
         for r in d["kernels"]:
@@ -428,6 +429,13 @@ def train_roofline(eng, cfg):
                       "profile_share_of_busy": round(share, 4), "achieved": round(ach, 3),
                       "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "source": src, "stale": stale,
                       "timing": "rocprofv3 --kernel-trace busy time of the family per graphed step"})
+        if tsrc is not None and fam in td.get("families", {}):
+            # HBM traffic of the family per step from the FETCH / WRITE PMC passes (tools/train_pmc.sh)
+            tb = td["families"][fam]["traffic_bytes_per_step"]
+            e.update({"traffic": tb, "traffic_unit": "bytes/step (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                      "traffic_source": tsrc, "traffic_stale": tstale})
+            if fam in busy:
+                e["traffic_GBs_over_busy_time"] = round(tb / (busy[fam][0] * 1e-3) / 1e9, 1)
         lines[fam] = e
     top = max(lines, key=lambda f: busy.get(f, [0.0])[0]) if busy else "gemm_big_kernel"
     out = dict(lines[top])
