@@ -105,12 +105,18 @@ __device__ inline void tile_krange(const BigGemmArgs& g, int K, int i0, int j0, 
 // K / koff: the problem's k extent and first k (per-problem segment variants; g.k and g.koff otherwise) -- kept out of
 // the argument struct so the kernel never writes it (a written copy lives in scratch and every operand address
 // derived from it becomes a per-lane value).
-template <bool AK, bool BK, int MODE, int AUX = 0>
+// NB: 32-column accumulator blocks per wave -- 2: 4 waves (256 threads) of 64 x 64; 1: 8 waves (512 threads) of
+// 64 x 32, the tile's columns split over 4 wave columns (two workgroups per CU then hold 4 waves per SIMD: a CU
+// whose other workgroup is in its prologue / epilogue still has two waves per SIMD issuing MFMAs).
+template <bool AK, bool BK, int MODE, int AUX = 0, int NB = 2>
 __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int koff, float* big_smem, int64_t bat,
-                                             int i0, int j0, int kend, int kt0, int kt1, f32x16 (&acc)[2][2]) {
+                                             int i0, int j0, int kend, int kt0, int kt1, f32x16 (&acc)[2][NB]) {
+  constexpr int NT = 512 / NB;                 // threads
+  constexpr int NQ = 1024 / NT;                // 16-byte operand loads per thread and operand (4 or 2)
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wr = w >> 1, wc = w & 1;
+  // wave grid 2 x (4 / NB): rows 64 wr8, columns 32 NB wc8
+  const int wr8 = NB == 1 ? (w >> 2) : (w >> 1), wc8 = NB == 1 ? (w & 3) : (w & 1);
   const int fl = g.flags;
   const bool aLo = fl & NMGP_A_LOWER, aUp = fl & NMGP_A_UPPER, bUp = fl & NMGP_B_UPPER, bLo = fl & NMGP_B_LOWER;
   const float* Ab = g.A + (MODE ? uniform64(g.offA[bat]) : bat * g.sAb) + (AK ? (int64_t)koff : (int64_t)koff * g.lda);
@@ -122,7 +128,7 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
       BK ? make_rsrc(Bb, ((int64_t)(g.n - 1) * g.ldb + K) * 4)
                   : make_rsrc(Bb, ((int64_t)(K - 1) * g.ldb + g.n) * 4);
 
-  // loader maps: k-contiguous A / B: row t>>3 (+32q), k 4*(t&7)
+  // loader maps: k-contiguous A / B: row t>>3 (+ NT/8 q), k 4*(t&7)
   const int lr = t >> 3, lk = (t & 7) * 4;
   // i-contiguous A / j-contiguous B: k = 4 (t & 7) + q, i or j = 4 (t >> 3) + e: each k row is read as 128
   // contiguous bytes by 8 lanes, and the thread's 4 x 4 block (k rows q, columns e) is transposed in registers
@@ -133,34 +139,38 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
   // operands k-strided the slots may hold any common permutation of k, and load q takes k = 8 q + jr instead, so
   // one wave instruction covers 8 consecutive k rows (4 KB apart) rather than rows 16 KB apart
   constexpr bool KPERM = !AK && !BK;
-  auto krow = [&](int q) { return KPERM ? 8 * q + jr : 4 * jr + q; };
-  float4 ra[4], rb[4];
+  // 8 waves: two k rows per thread, k = 2 (t >> 5) + q, i or j = 4 (t & 31) + e -- a wave instruction reads two
+  // 512-byte k-row segments; the 2 x 4 block goes to LDS as four 8-byte stores (slot = k: the k-contiguous order)
+  const int ic8 = (t & 31) * 4, kg8 = (t >> 5) * 2;
+  auto krow = [&](int q) { return NB == 1 ? kg8 + q : (KPERM ? 8 * q + jr : 4 * jr + q); };
+  const int jcx = NB == 1 ? ic8 : jc;
+  float4 ra[NQ], rb[NQ];
 
   auto load = [&](int kt) {
     if constexpr (AK) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int64_t row = i0 + lr + 32 * q;
+      for (int q = 0; q < NQ; ++q) {
+        const int64_t row = i0 + lr + (NT / 8) * q;
         ra[q] = ld4<AUX>(rA, (uint32_t)((row * g.lda + kt + lk) * 4));
       }
     } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < NQ; ++q) {
         const int64_t kr = kt + krow(q);
-        ra[q] = ld4<AUX>(rA, (uint32_t)((kr * g.lda + i0 + jc) * 4));
+        ra[q] = ld4<AUX>(rA, (uint32_t)((kr * g.lda + i0 + jcx) * 4));
       }
     }
     if constexpr (BK) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int64_t row = j0 + lr + 32 * q;
+      for (int q = 0; q < NQ; ++q) {
+        const int64_t row = j0 + lr + (NT / 8) * q;
         rb[q] = ld4<AUX>(rB, (uint32_t)((row * g.ldb + kt + lk) * 4));
       }
     } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < NQ; ++q) {
         const int64_t kr = kt + krow(q);
-        rb[q] = ld4<AUX>(rB, (uint32_t)((kr * g.ldb + j0 + jc) * 4));
+        rb[q] = ld4<AUX>(rB, (uint32_t)((kr * g.ldb + j0 + jcx) * 4));
       }
     }
   };
@@ -171,10 +181,10 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
                       (bLo && kt < j0 + BBN - 1) || (aUp && kt < i0 + BBM - 1);
     if (need) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < NQ; ++q) {
         float* a = (float*)&ra[q];
         if constexpr (AK) {
-          const int i = i0 + lr + 32 * q;
+          const int i = i0 + lr + (NT / 8) * q;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int kk = kt + lk + e;
@@ -184,13 +194,13 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
           const int kk = kt + krow(q);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const int i = i0 + jc + e;
+            const int i = i0 + jcx + e;
             a[e] = keep_if(a[e], kk < kend && (!aLo || kk <= i) && (!aUp || kk >= i));
           }
         }
         float* b = (float*)&rb[q];
         if constexpr (BK) {
-          const int j = j0 + lr + 32 * q;
+          const int j = j0 + lr + (NT / 8) * q;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int kk = kt + lk + e;
@@ -200,7 +210,7 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
           const int kk = kt + krow(q);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const int j = j0 + jc + e;
+            const int j = j0 + jcx + e;
             b[e] = keep_if(b[e], kk < kend && (!bUp || kk <= j) && (!bLo || kk >= j));
           }
         }
@@ -210,7 +220,10 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
     float* Bs = st + BBM * BP;
     if constexpr (AK) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) *(float4*)&As[(lr + 32 * q) * BP + lk] = ra[q];
+      for (int q = 0; q < NQ; ++q) *(float4*)&As[(lr + (NT / 8) * q) * BP + lk] = ra[q];
+    } else if constexpr (NB == 1) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) *(float2*)&As[(ic8 + e) * BP + kg8] = make_float2(ra[0][e], ra[1][e]);
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
@@ -218,7 +231,10 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
     }
     if constexpr (BK) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) *(float4*)&Bs[(lr + 32 * q) * BP + lk] = rb[q];
+      for (int q = 0; q < NQ; ++q) *(float4*)&Bs[(lr + (NT / 8) * q) * BP + lk] = rb[q];
+    } else if constexpr (NB == 1) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) *(float2*)&Bs[(ic8 + e) * BP + kg8] = make_float2(rb[0][e], rb[1][e]);
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
@@ -238,22 +254,25 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
       if (more) load(kt + BBK);
       const float* As = big_smem + st * BSTAGE;
       const float* Bs = As + BBM * BP;
-      float4 fa[2][4], fb[2][4];
+      float4 fa[2][4], fb[NB][4];
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
+      for (int c = 0; c < 4; ++c) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          fa[h][c] = *(const float4*)&As[(64 * wr + 32 * h + rl) * BP + ko + 4 * c];
-          fb[h][c] = *(const float4*)&Bs[(64 * wc + 32 * h + rl) * BP + ko + 4 * c];
-        }
+        for (int h = 0; h < 2; ++h) fa[h][c] = *(const float4*)&As[(64 * wr8 + 32 * h + rl) * BP + ko + 4 * c];
+#pragma unroll
+        for (int h = 0; h < NB; ++h)
+          fb[h][c] = *(const float4*)&Bs[(32 * NB * wc8 + 32 * h + rl) * BP + ko + 4 * c];
+      }
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
-        const float a0 = ((const float*)&fa[0][s >> 2])[s & 3], a1 = ((const float*)&fa[1][s >> 2])[s & 3];
-        const float b0 = ((const float*)&fb[0][s >> 2])[s & 3], b1 = ((const float*)&fb[1][s >> 2])[s & 3];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float av = ((const float*)&fa[h][s >> 2])[s & 3];
+#pragma unroll
+          for (int b = 0; b < NB; ++b)
+            acc[h][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, ((const float*)&fb[b][s >> 2])[s & 3], acc[h][b], 0,
+                                                             0, 0);
+        }
       }
       if (more) store_lds(big_smem + (st ^ 1) * BSTAGE, kt + BBK);
       lds_barrier();
@@ -265,18 +284,19 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
 // Publish this workgroup's partial tile (slot `mine`) write-through, count arrivals on `ctr`;
 // the last of the `S` contributors sums all partials in contributor order (its own from
 // registers) into acc and returns true.  slot_of(c) gives contributor c's slot.
-template <typename SlotOf>
+template <int NB = 2, typename SlotOf>
 __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S, int32_t* ctr, SlotOf slot_of,
-                                            f32x16 (&acc)[2][2]) {
+                                            f32x16 (&acc)[2][NB]) {
   __shared__ int s_last;
   const int t = threadIdx.x;
+  constexpr int PT = 32 * NB;                // partial values per thread (a tile's 16384 over the workgroup)
   {
     const __amdgpu_buffer_rsrc_t rws = make_rsrc(g.ws + uniform64(slot_of(me)) * BSLOT, (int64_t)BSLOT * 4);
-    const uint32_t off = (uint32_t)(t * 64 * 4);
+    const uint32_t off = (uint32_t)(t * PT * 4);
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           u32x4g v;
@@ -284,7 +304,7 @@ __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S,
           v[1] = __float_as_uint(acc[a][b][4 * q + 1]);
           v[2] = __float_as_uint(acc[a][b][4 * q + 2]);
           v[3] = __float_as_uint(acc[a][b][4 * q + 3]);
-          __builtin_amdgcn_raw_buffer_store_b128(v, rws, off + ((a * 2 + b) * 4 + q) * 16, 0, 16 /* sc1 */);
+          __builtin_amdgcn_raw_buffer_store_b128(v, rws, off + ((a * NB + b) * 4 + q) * 16, 0, 16 /* sc1 */);
         }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -300,25 +320,25 @@ __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S,
   __syncthreads();   // s_last is reused by the next tile of a stream-K workgroup
   if (!last) return false;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const uint32_t off = (uint32_t)(t * 64 * 4);
+  const uint32_t off = (uint32_t)(t * PT * 4);
   if (S <= 4) {
     // per half-tile (acc[a][*]) all S partials -- this workgroup's own as stored above -- are loaded at once and
     // then summed in contributor order: two memory round trips instead of S - 1 (the same sums, bit for bit)
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
-      u32x4g v[4][8];
+      u32x4g v[4][4 * NB];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         if (c >= S) continue;
         const __amdgpu_buffer_rsrc_t rws = make_rsrc(g.ws + uniform64(slot_of(c)) * BSLOT, (int64_t)BSLOT * 4);
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < NB; ++b)
 #pragma unroll
           for (int q = 0; q < 4; ++q)
-            v[c][b * 4 + q] = __builtin_amdgcn_raw_buffer_load_b128(rws, off + ((a * 2 + b) * 4 + q) * 16, 0, 16);
+            v[c][b * 4 + q] = __builtin_amdgcn_raw_buffer_load_b128(rws, off + ((a * NB + b) * 4 + q) * 16, 0, 16);
       }
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
+      for (int b = 0; b < NB; ++b) {
         f32x16 sum;
 #pragma unroll
         for (int r = 0; r < 16; ++r) sum[r] = 0.0f;
@@ -335,11 +355,11 @@ __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S,
     }
     return true;
   }
-  f32x16 sum[2][2];
+  f32x16 sum[2][NB];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < NB; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) sum[a][b][r] = 0.0f;
   for (int c = 0; c < S; ++c) {
@@ -347,17 +367,17 @@ __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S,
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) sum[a][b] += acc[a][b];
+        for (int b = 0; b < NB; ++b) sum[a][b] += acc[a][b];
       continue;
     }
     const __amdgpu_buffer_rsrc_t rws = make_rsrc(g.ws + uniform64(slot_of(c)) * BSLOT, (int64_t)BSLOT * 4);
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const u32x4g v = __builtin_amdgcn_raw_buffer_load_b128(rws, off + ((a * 2 + b) * 4 + q) * 16, 0, 16);
+          const u32x4g v = __builtin_amdgcn_raw_buffer_load_b128(rws, off + ((a * NB + b) * 4 + q) * 16, 0, 16);
 #pragma unroll
           for (int e = 0; e < 4; ++e) sum[a][b][4 * q + e] += __uint_as_float(v[e]);
         }
@@ -365,7 +385,7 @@ __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S,
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = sum[a][b];
+    for (int b = 0; b < NB; ++b) acc[a][b] = sum[a][b];
   return true;
 }
 
@@ -375,14 +395,14 @@ __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S,
 // load sat in its own branch and was waited on before the next, and E, read in the store loop, waited on every
 // store before it (64 dependent round trips per tile in the KL L-bar product, the ECoG step's longest launch).
 // E must not alias C.  A is a template parameter so every accumulator index is a constant.
-template <int MODE, int A>
+template <int MODE, int A, int NB = 2>
 __device__ __forceinline__ void big_epi_half(const BigGemmArgs& g, float* Cb, __amdgpu_buffer_rsrc_t rCb,
                                              __amdgpu_buffer_rsrc_t rEb, __amdgpu_buffer_rsrc_t rRS, int i0, int j0,
-                                             const f32x16 (&acc)[2][2]) {
+                                             const f32x16 (&acc)[2][NB]) {
   constexpr bool EPI = MODE == 2;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wr = w >> 1, wc = w & 1;
+  const int wr = NB == 1 ? (w >> 2) : (w >> 1), wc = NB == 1 ? (w & 3) : (w & 1);
   const bool lower = g.flags & NMGP_OUT_LOWER;
   const bool tril = MODE && (g.flags & NMGP_OUT_TRIL);
   const bool eLo = g.flags & NMGP_EPI_E_LOWER;
@@ -390,8 +410,8 @@ __device__ __forceinline__ void big_epi_half(const BigGemmArgs& g, float* Cb, __
   const int ib = i0 + 64 * wr + 32 * A + 4 * (lane >> 5);
   f32x16 cv[2], ev[2];
 #pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    const int j = j0 + 64 * wc + 32 * b + (lane & 31);
+  for (int b = 0; b < NB; ++b) {
+    const int j = j0 + 32 * NB * wc + 32 * b + (lane & 31);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int i = ib + (r & 3) + 8 * (r >> 2);
@@ -413,8 +433,8 @@ __device__ __forceinline__ void big_epi_half(const BigGemmArgs& g, float* Cb, __
     }
   }
 #pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    const int j = j0 + 64 * wc + 32 * b + (lane & 31);
+  for (int b = 0; b < NB; ++b) {
+    const int j = j0 + 32 * NB * wc + 32 * b + (lane & 31);
     f32x16 v = acc[A][b] * g.alpha;
     if (ldc) v += g.beta * cv[b];
 #pragma unroll
@@ -436,8 +456,8 @@ __device__ __forceinline__ void big_epi_half(const BigGemmArgs& g, float* Cb, __
 }
 
 // C = alpha * acc + beta * C (+ diag_add, + the KL epilogue) on the stored part of the tile.
-template <int MODE>
-__device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, int i0, int j0, f32x16 (&acc)[2][2]) {
+template <int MODE, int NB = 2>
+__device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, int i0, int j0, f32x16 (&acc)[2][NB]) {
   constexpr bool EPI = MODE == 2;
   float* Cb = g.C + (MODE ? uniform64(g.offC[bat]) : bat * g.sCb);
   const float* Eb = EPI ? g.E + (g.offE ? uniform64(g.offE[bat]) : 0) : nullptr;
@@ -446,8 +466,8 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, 
   const __amdgpu_buffer_rsrc_t rEb =
       make_rsrc(EPI ? Eb : Cb, EPI ? ((int64_t)(g.m - 1) * g.sEi + (int64_t)(g.n - 1) * g.sEj + 1) * 4 : 0);
   const __amdgpu_buffer_rsrc_t rRS = make_rsrc(EPI ? rs : Cb, EPI ? (int64_t)g.m * 4 : 0);
-  big_epi_half<MODE, 0>(g, Cb, rCb, rEb, rRS, i0, j0, acc);
-  big_epi_half<MODE, 1>(g, Cb, rCb, rEb, rRS, i0, j0, acc);
+  big_epi_half<MODE, 0, NB>(g, Cb, rCb, rEb, rRS, i0, j0, acc);
+  big_epi_half<MODE, 1, NB>(g, Cb, rCb, rEb, rRS, i0, j0, acc);
 }
 
 // Row-vector epilogue through LDS (row-contiguous C, and E, 16-byte aligned): the accumulators (each lane holds 16
@@ -457,20 +477,20 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, 
 // batched ECoG products (tools/big_trace_batch.hip) had the single-float epilogue at 13.3-13.5 us of a 43-65 us
 // tile.  Same arithmetic, element by element, as big_epi_half.
 constexpr int BCP = 136;   // LDS pitch of the C image (floats): lanes 32..63 of a column write land 32 banks over
-template <int MODE>
+template <int MODE, int NB = 2>
 __device__ __forceinline__ void big_epilogue_rows(const BigGemmArgs& g, float* Cb, const float* Eb, const float* rs,
-                                                  int i0, int j0, const f32x16 (&acc)[2][2], float* sm) {
+                                                  int i0, int j0, const f32x16 (&acc)[2][NB], float* sm) {
   constexpr bool EPI = MODE == 2;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wr = w >> 1, wc = w & 1;
+  const int wr = NB == 1 ? (w >> 2) : (w >> 1), wc = NB == 1 ? (w & 3) : (w & 1);
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < NB; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        sm[(64 * wr + 32 * a + 4 * (lane >> 5) + (r & 3) + 8 * (r >> 2)) * BCP + 64 * wc + 32 * b + (lane & 31)] =
+        sm[(64 * wr + 32 * a + 4 * (lane >> 5) + (r & 3) + 8 * (r >> 2)) * BCP + 32 * NB * wc + 32 * b + (lane & 31)] =
             acc[a][b][r];
   __syncthreads();
   // the scalar arguments the chunk loop uses, read once (left in the argument struct, several were spilled and
@@ -482,7 +502,8 @@ __device__ __forceinline__ void big_epilogue_rows(const BigGemmArgs& g, float* C
   const bool tril = MODE && (g.flags & NMGP_OUT_TRIL);
   const bool eLo = g.flags & NMGP_EPI_E_LOWER;
   const bool ldc = beta != 0.0f;
-  const int c4 = (t & 31) * 4, rb = t >> 5;
+  const int c4 = (t & 31) * 4, rb = t >> 5;   // row rb + RS (RQ h + q): RS = threads / 32 rows apart
+  constexpr int RS = 16 / NB, RQ = 4 * NB;
   const int j = j0 + c4;
   // (the pointers are wave-uniform; said explicitly, or the compiler may keep one in VGPRs and wrap every buffer
   // access in a waterfall loop)
@@ -498,11 +519,11 @@ __device__ __forceinline__ void big_epilogue_rows(const BigGemmArgs& g, float* C
   // 16 chunks per thread in two halves of 8 (loads of a half in flight together)
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    float4 cv[8], ev[8];
-    float rv[8];
+    float4 cv[RQ], ev[RQ];
+    float rv[RQ];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int i = i0 + rb + 8 * (8 * h + q);
+    for (int q = 0; q < RQ; ++q) {
+      const int i = i0 + rb + RS * (RQ * h + q);
       // a chunk is read when any of its elements keeps a computed value (not wholly above an OUT_LOWER / OUT_TRIL
       // diagonal, inside the matrix); out-of-range columns read 0 through the resource bound
       const bool rd = i < gm && j < gn && !((lower || tril) && j > i);
@@ -516,8 +537,8 @@ __device__ __forceinline__ void big_epilogue_rows(const BigGemmArgs& g, float* C
       }
     }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int row = rb + 8 * (8 * h + q);
+    for (int q = 0; q < RQ; ++q) {
+      const int row = rb + RS * (RQ * h + q);
       const int i = i0 + row;
       if (i >= gm || j >= gn) continue;
       if (lower && j > i) continue;                 // wholly above the diagonal: nothing stored
@@ -556,17 +577,19 @@ __device__ __forceinline__ void big_epilogue_rows(const BigGemmArgs& g, float* C
   __syncthreads();   // the LDS image is the next tile's staging buffer (stream-K workgroups run several tiles)
 }
 
-__device__ inline void zero_acc(f32x16 (&acc)[2][2]) {
+template <int NB = 2>
+__device__ inline void zero_acc(f32x16 (&acc)[2][NB]) {
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < NB; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
 }
 
-template <bool AK, bool BK, int MODE>
-__global__ __launch_bounds__(256, 2) void gemm_big_kernel(const BigGemmArgs g) {
+template <bool AK, bool BK, int MODE, int NB>
+// second argument: waves per SIMD (two workgroups per CU: 2 with 4 waves, 4 with 8 waves -- 128 VGPRs)
+__global__ __launch_bounds__(512 / NB, 4 / NB) void gemm_big_kernel(const BigGemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) float big_smem[];
   BIG_STAMP(0);
   // XCD-aware block order: hardware places block b on XCD b % 8; give each XCD a contiguous run
@@ -585,7 +608,7 @@ __global__ __launch_bounds__(256, 2) void gemm_big_kernel(const BigGemmArgs g) {
     bid = (int)(((int64_t)bid + 9LL * blockIdx.y) % nb);
   }
   const int64_t bat = blockIdx.y;
-  f32x16 acc[2][2];
+  f32x16 acc[2][NB];
   int K = g.k, koff = g.koff;
   if constexpr (MODE != 0) {
     if (g.kseg != nullptr) {
@@ -646,7 +669,7 @@ __global__ __launch_bounds__(256, 2) void gemm_big_kernel(const BigGemmArgs g) {
     tile_coords(g, tile, tm, tn);
     const int i0 = tm * BBM, j0 = tn * BBN;
     zero_acc(acc);
-    big_mainloop<AK, BK, MODE>(g, K, koff, big_smem, bat, i0, j0, kend, kt0, kt1, acc);
+    big_mainloop<AK, BK, MODE, 0, NB>(g, K, koff, big_smem, bat, i0, j0, kend, kt0, kt1, acc);
     BIG_STAMP(2);
     bool store = true;
     if (nparts > 1) {
@@ -910,6 +933,12 @@ int potrf_step_f32(float* P, float* C, const float* X, int64_t lda, int n2, int 
   return NMGP_OK;
 }
 
+// Accumulator column blocks per wave of the gemm_big_kernel launches: 1 = 8 waves (512 threads) per 128 x 128 tile,
+// 64 x 32 per wave (tools/big8_probe.hip: the batched SYRK 4-11 % faster than 4 waves of 64 x 64, bit-identical;
+// ECoG step 0.333 -> 0.328 s, profiles/r05aa_*).  Products with BOTH operands k-strided (the KL L-bar) keep 4 waves:
+// their 8-wave form spills in the staging and measured 9 % slower.
+constexpr int kBigNB = 1;
+
 // Partial slots the split-K path may use per call (workspace = slots * 64 KB + counters).
 constexpr int kBigSlots = 1024;
 size_t gemm_big_ws_bytes() { return (size_t)kBigSlots * BSLOT * sizeof(float) + (size_t)kBigSlots * sizeof(int32_t); }
@@ -994,38 +1023,38 @@ static int gemm_big_f32_ex(const float* A, int64_t lda, const float* B, int64_t 
   const size_t lds = 2 * BSTAGE * sizeof(float);
   const dim3 gd(sk ? (unsigned)P : (unsigned)(g.tiles * S), (unsigned)batch);
   const bool epi = flags & NMGP_EPI;
-  auto go = [&](auto kern) {
+  auto go = [&](auto kern, int nb) {
     static bool attr = false;   // one per instantiation
     if (!attr) {
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr = true;
     }
-    hipLaunchKernelGGL(kern, gd, dim3(256), lds, s, g);
+    hipLaunchKernelGGL(kern, gd, dim3(512 / nb), lds, s, g);
   };
   const bool offs = offA != nullptr;
   if (offs && (offB == nullptr || offC == nullptr)) return -1;
   if (!offs && (diag_add != 0.0f || (flags & NMGP_OUT_TRIL))) return -1;   // those live in the offsets variants
   if (epi) {
     if (!offs || g.a_kcontig || g.b_kcontig) return -1;   // only the KL L-bar form (both operands transposed)
-    go(gemm_big_kernel<false, false, 2>);
+    go(gemm_big_kernel<false, false, 2, 2>, 2);
   } else if (offs) {
     if (g.a_kcontig && g.b_kcontig)
-      go(gemm_big_kernel<true, true, 1>);
+      go(gemm_big_kernel<true, true, 1, kBigNB>, kBigNB);
     else if (g.a_kcontig)
-      go(gemm_big_kernel<true, false, 1>);
+      go(gemm_big_kernel<true, false, 1, kBigNB>, kBigNB);
     else if (g.b_kcontig)
-      go(gemm_big_kernel<false, true, 1>);
+      go(gemm_big_kernel<false, true, 1, kBigNB>, kBigNB);
     else
-      go(gemm_big_kernel<false, false, 1>);
+      go(gemm_big_kernel<false, false, 1, 2>, 2);
   } else {
     if (g.a_kcontig && g.b_kcontig)
-      go(gemm_big_kernel<true, true, 0>);
+      go(gemm_big_kernel<true, true, 0, kBigNB>, kBigNB);
     else if (g.a_kcontig)
-      go(gemm_big_kernel<true, false, 0>);
+      go(gemm_big_kernel<true, false, 0, kBigNB>, kBigNB);
     else if (g.b_kcontig)
-      go(gemm_big_kernel<false, true, 0>);
+      go(gemm_big_kernel<false, true, 0, kBigNB>, kBigNB);
     else
-      go(gemm_big_kernel<false, false, 0>);
+      go(gemm_big_kernel<false, false, 0, 2>, 2);
   }
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;

@@ -15,6 +15,8 @@ python3 tools/mfma_summary.py $(find gpurun_out/syrkin/stress -name "*counter_co
 python3 tools/mfma_summary.py $(find gpurun_out/syrkin/ecog -name "*counter_collection.csv") gpurun_out/${TAG}_ecog_step_mfma_util.json --by-grid > /dev/null
 bash tools/stress_hbm.sh $TAG
 bash tools/train_trace.sh $TAG
+bash tools/train_pmc.sh $TAG
+cp gpurun_out/${TAG}_hcp_train_traffic.json gpurun_out/${TAG}_ecog_train_traffic.json profiles/
 cp gpurun_out/${TAG}_pm25_bench_summary.json gpurun_out/${TAG}_pm25_bench_kernel_stats.csv gpurun_out/${TAG}_pm25_mfma.json \
    gpurun_out/${TAG}_stress_potrf_mfma_util.json gpurun_out/${TAG}_ecog_step_mfma_util.json gpurun_out/${TAG}_stress_potrf_hbm.json \
    gpurun_out/${TAG}_hcp_train_kernels.json gpurun_out/${TAG}_ecog_train_kernels.json profiles/
