@@ -230,11 +230,13 @@ def _stress_hbm(potrf_ms):
 
 
 # ECoG batched recursive Cholesky of the 8384 M = 1024 variational factors (chol.hip chol_inv_rec_big): its trailing
-# SYRKs A22 -= L21 L21^T per recursion level, identified by grid (threads = 256 x lower tiles x 8384 factors)
+# SYRKs A22 -= L21 L21^T per recursion level, identified by grid (threads = 256 x lower tiles x 8384 factors, or
+# twice that for the 8-wave tiles)
 ECOG_SYRK_LEVELS = [("top, n2 = 512, k = 512 (10 lower tiles)", 21463040, 1.0),
                     ("level 2, n2 = 256, k = 256 (3 lower tiles)", 6438912, 1.0),
-                    # one-tile k = 128 products share a grid: SYRK, L21 panel and the inverse product, equal shapes
-                    ("level 3, n2 = 128, k = 128 (1 tile; 1 of the 3 one-tile products of the grid)", 2146304, 1 / 3.)]
+                    # one-tile k = 128 products of this template share a grid: the L21 panel and the SYRK, equal
+                    # shapes (the inverse product X21 = -X22 T reads T row-major since round 5: another template)
+                    ("level 3, n2 = 128, k = 128 (1 tile; 1 of the 2 one-tile products of the grid)", 2146304, 1 / 2.)]
 
 
 def _ecog_syrk_pmc():
@@ -247,8 +249,9 @@ def _ecog_syrk_pmc():
         return None
     lev = []
     for label, grid, share in ECOG_SYRK_LEVELS:
-        rs = [r for r in d["rows"] if r["kernel"].startswith("void nmgp::gemm_big_kernel<true, true, 0>")
-              and r["grid_threads"] == grid]
+        # (4-wave launches: 256 threads per tile, 8-wave launches from round 5: 512)
+        rs = [r for r in d["rows"] if r["kernel"].startswith("void nmgp::gemm_big_kernel<true, true, 0")
+              and r["grid_threads"] in (grid, 2 * grid)]
         if rs:
             us = sum(r["avg_us"] * r["dispatches"] for r in rs)
             lev.append({"level": label, "us_total": round(us * share, 1),
