@@ -257,7 +257,22 @@ def _ecog_syrk_pmc():
             lev.append({"level": label, "us_total": round(us * share, 1),
                         "mfma_busy": round(sum(r["mfma_util"] * r["avg_us"] * r["dispatches"] for r in rs) / us, 4)})
     if not lev:
-        return None
+        # persistent batched launches (round 5) share one grid (2 workgroups per CU) whatever the level, so the
+        # levels cannot be told apart by grid: report the time-weighted MFMA-busy over every launch of the
+        # recursion's k-contiguous template -- the trailing SYRKs AND the L21 panel products of all levels
+        rs = [r for r in d["rows"] if r["kernel"].startswith("void nmgp::gemm_big_kernel<true, true, 0")]
+        if not rs:
+            return None
+        us = sum(r["avg_us"] * r["dispatches"] for r in rs)
+        busy = round(sum(r["mfma_util"] * r["avg_us"] * r["dispatches"] for r in rs) / us, 4)
+        return {"kernel": "gemm_big_kernel (batched trailing SYRKs A22 -= L21 L21^T and L21 panels of the recursive "
+                          "Cholesky of 8384 M=1024 factors, persistent launches)",
+                "mfma_busy_time_weighted": busy, "mfma_busy_all_levels_time_weighted": busy,
+                "mfma_busy_top_level_k512": None,
+                "levels": [{"level": "all levels, SYRK + L21 panel launches (one grid for every level)",
+                            "us_total": round(us, 1), "mfma_busy": busy,
+                            "dispatches": sum(r["dispatches"] for r in rs)}],
+                "source": src, "stale": stale}
     w = sum(x["us_total"] for x in lev)
     return {"kernel": "gemm_big_kernel (batched trailing SYRK A22 -= L21 L21^T of 8384 M=1024 factors)",
             "mfma_busy_time_weighted": lev[0]["mfma_busy"], "mfma_busy_top_level_k512": lev[0]["mfma_busy"],

@@ -61,6 +61,9 @@ struct BigGemmArgs {
   int koff;
   int ksplit;
   int streamk;              // 1: stream-K partition over a persistent grid (batch 1, uniform k)
+  int persist;              // batched, one pass per tile: workgroup x runs work items x, x + G, ... of the
+                            // (tile, problem) space, problem-major (item w: problem w % batch, tile w / batch)
+  int batch, total;         // (persist) problems and work items
   float* ws; int32_t* counters;
 };
 
@@ -607,8 +610,15 @@ __global__ __launch_bounds__(512 / NB, 4 / NB) void gemm_big_kernel(const BigGem
     // M = 1024).  Rotating the tile index by 9 per problem walks each XCD over all tile columns instead.
     bid = (int)(((int64_t)bid + 9LL * blockIdx.y) % nb);
   }
-  const int64_t bat = blockIdx.y;
   f32x16 acc[2][NB];
+  // persistent batched grid (measured on the batched SYRK, tools/big8p_probe.hip: 2.70-2.99 -> 2.25-2.37 ms, the
+  // same results bit for bit): a fixed set of co-resident workgroups walks the work items instead of one
+  // workgroup per (tile, problem) -- no per-workgroup launch / LDS allocation per tile and no tail of ragged
+  // triangular tiles at the end of the grid
+  const int wstep = g.persist ? (int)gridDim.x : 1;
+  for (int wi = g.persist ? (int)blockIdx.x : 0; wi < (g.persist ? g.total : 1); wi += wstep) {
+  const int64_t bat = g.persist ? (int64_t)(wi % g.batch) : (int64_t)blockIdx.y;
+  const int bidw = g.persist ? wi / g.batch : bid;
   int K = g.k, koff = g.koff;
   if constexpr (MODE != 0) {
     if (g.kseg != nullptr) {
@@ -649,8 +659,8 @@ __global__ __launch_bounds__(512 / NB, 4 / NB) void gemm_big_kernel(const BigGem
         me = bid - c0;
       }
     } else {
-      tile = bid / S;
-      const int split = bid - tile * S;
+      tile = bidw / S;
+      const int split = bidw - tile * S;
       int tm0, tn0, kbeg;
       tile_coords(g, tile, tm0, tn0);
       tile_krange(g, K, tm0 * BBM, tn0 * BBN, kbeg, kend);
@@ -698,6 +708,7 @@ __global__ __launch_bounds__(512 / NB, 4 / NB) void gemm_big_kernel(const BigGem
     }
     it += step;
   }
+  }   // persistent work items
 #ifdef NMGP_BIG_TRACE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   BIG_STAMP(4);
@@ -1018,10 +1029,14 @@ static int gemm_big_f32_ex(const float* A, int64_t lda, const float* B, int64_t 
   }
   g.ksplit = S;
   g.streamk = sk;
+  g.batch = batch;
+  g.total = (int)min(total, (int64_t)0x7fffffff);
+  g.persist = (!sk && S == 1 && batch > 1) ? 1 : 0;
   g.ws = (float*)ws;
   g.counters = ws ? (int32_t*)((char*)ws + (size_t)kBigSlots * BSLOT * sizeof(float)) : nullptr;
   const size_t lds = 2 * BSTAGE * sizeof(float);
-  const dim3 gd(sk ? (unsigned)P : (unsigned)(g.tiles * S), (unsigned)batch);
+  const dim3 gd = g.persist ? dim3((unsigned)min((int64_t)P, total), 1u)
+                             : dim3(sk ? (unsigned)P : (unsigned)(g.tiles * S), (unsigned)batch);
   const bool epi = flags & NMGP_EPI;
   auto go = [&](auto kern, int nb) {
     static bool attr = false;   // one per instantiation

@@ -6,7 +6,9 @@
 //   syrk:    Sigma = L L^T + j I          (A_LOWER | B_UPPER | OUT_LOWER, both operands k-contiguous)
 //   kl_lbar: G = -C^-T Xs + rs(i) E(i, j) (A_UPPER | B_LOWER | OUT_TRIL | EPI, both operands k-strided, beta 1)
 // Per workgroup (100 MHz wall clock): prologue (first k-tile in LDS), main loop, epilogue -- medians, and the
-// main loop's time per 32-deep k-tile (sum over workgroups / sum of their k-tiles).
+// main loop's time per 32-deep k-tile (sum over workgroups / sum of their k-tiles).  (Since the batched launches
+// became persistent the stamps of a workgroup are those of its LAST work item: the per-k-tile figure no longer
+// normalises correctly; the profiles r05t / r05u / r05aa predate that change.)
 #include "gemm_big.hip"
 
 #include <algorithm>
