@@ -738,7 +738,7 @@ def main():
     ap.add_argument("--pair-D", type=int, default=128, help="channels of the pair-sharded leg (default: ECoG-full 128)")
     ap.add_argument("--elbo-D", type=int, default=128, help="channels of the ELBO leg (default: ECoG-full 128)")
     ap.add_argument("--dp-allreduce", choices=["auto", "bucketed", "flat"], default="auto",
-                    help="N > 1 gradient all-reduce: bucketed + overlapped (from 64 MB of gradient with auto) or flat")
+                    help="N > 1 gradient all-reduce: flat (auto: DsviTrainer.DP_BUCKET_MIN_BYTES unset) or bucketed + overlapped")
     args = ap.parse_args()
 
     # --gpus N is honoured before anything touches the GPU: without a launcher, N > 1 re-runs this

@@ -635,7 +635,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, const nmgp_gemm_
   const int64_t sz = (int64_t)sizeof(T);
   const int64_t extC = ((r0 + m - 1) * d.sC_i + (int64_t)(n - 1) * d.sC_j + 1) * sz;
   const int64_t extE = (flags & NMGP_EPI) ? ((r0 + m - 1) * d.sE_i + (int64_t)(n - 1) * d.sE_j + 1) * sz : 0;
-  if (extC < 0x7fffffffLL && extE < 0x7fffffffLL && d.sC_i >= 0 && d.sC_j >= 0) {
+  // (negative strides take emit(): a negative extent would build a 0-record resource that reads every element as 0)
+  if (extC < 0x7fffffffLL && extE < 0x7fffffffLL && d.sC_i >= 0 && d.sC_j >= 0 &&
+      (!(flags & NMGP_EPI) || (d.sE_i >= 0 && d.sE_j >= 0))) {
     const bool ldc = beta != (T)0, epi = (flags & NMGP_EPI) != 0;
     const __amdgpu_buffer_rsrc_t rC = make_rsrc(d.C, extC);
     const __amdgpu_buffer_rsrc_t rE = make_rsrc(epi ? d.epi_E : d.C, extE);

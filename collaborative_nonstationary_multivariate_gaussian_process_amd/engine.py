@@ -81,6 +81,14 @@ def lower_block_ranges(offs):
 ADAM_LOWER_MIN_M = 512
 
 
+def use_adam_lower(M, dtype, offs):
+    """nmgp_adam_lower walks 16-byte vectors of each block row: it needs M and every block range's offset to be
+    multiples of 16 / element size (the C side returns -8 otherwise, csrc/dsvi.hip adam_lower).  Shapes that are
+    not (fp32 M % 4 != 0, fp64 odd M) keep the dense update."""
+    V = 16 // torch.empty((), dtype=dtype).element_size()
+    return M >= ADAM_LOWER_MIN_M and M % V == 0 and all(o % V == 0 for o, _ in lower_block_ranges(offs))
+
+
 def pair_list(D, pair_range=None):
     i0, i1 = (0, D) if pair_range is None else pair_range
     return [(i, j) for i in range(i0, i1) for j in range(i + 1)]

@@ -23,7 +23,7 @@ from torch.utils.data import DataLoader, Dataset
 from . import _lib as Lb
 from . import distributed as DD
 from . import hip_ops as H
-from .engine import ADAM_LOWER_MIN_M, DsviEngine, HYPER_NAMES, PARAM_NAMES, lower_block_ranges, param_layout
+from .engine import DsviEngine, use_adam_lower, HYPER_NAMES, PARAM_NAMES, lower_block_ranges, param_layout
 from .utils import TensorType, tridiagonal_jitter  # noqa: F401  (re-exported like the reference)
 
 F64 = torch.float64
@@ -560,15 +560,19 @@ class DsviTrainer:
             self._comm = torch.cuda.Stream(device=self.model.device_)
         return self._comm
 
-    # gradients from this size on take the bucketed, overlapped all-reduce (below: one flat all-reduce after the
-    # graph -- PM2.5's 16 MB in five collectives cost more in per-collective latency than the overlap hides)
-    DP_BUCKET_MIN_BYTES = 64 << 20
+    # "auto" on the graph path = flat (round 6): the bucketed, overlapped all-reduce has one measurement, gloo ranks
+    # sharing one GPU (profiles/r05n_*: 296 ms/step bucketed vs 8.0 flat at N = 2), where gloo stages every bucket
+    # through the host; RCCL over xGMI has not run with N > 1 on this project's hardware, so nothing justifies a size
+    # threshold yet.  Set DP_BUCKET_MIN_BYTES (bytes of gradient) to make "auto" pick the bucketed form from that size
+    # on once a multi-GPU run measures it; "bucketed" forces it.
+    DP_BUCKET_MIN_BYTES = None
 
     def dp_bucketed(self, mode="auto"):
         if mode not in ("auto", "bucketed", "flat"):
             raise ValueError(f"dp all-reduce mode {mode!r}")
         g = self.model._grad
-        return mode == "bucketed" or (mode == "auto" and g.numel() * g.element_size() >= self.DP_BUCKET_MIN_BYTES)
+        thr = self.DP_BUCKET_MIN_BYTES
+        return mode == "bucketed" or (mode == "auto" and thr is not None and g.numel() * g.element_size() >= thr)
 
     def capture_dp(self, eng, world, mode="auto"):
         """The data-parallel step as two graphs around the gradient all-reduce (dp_graph_step): the gradient graph
@@ -582,10 +586,18 @@ class DsviTrainer:
         g = self.capture(eng, include_update=False)
         if not hasattr(self, "_dp_graphs"):
             self._dp_graphs = {}
-        self._dp_graphs[id(eng)] = (g, eng.ext_events["lbar_done"] if bucketed else None, self.capture_update(world))
-        return self._dp_graphs[id(eng)]
+        self._dp_graphs[self._dp_key(eng)] = (g, eng.ext_events["lbar_done"] if bucketed else None,
+                                              self.capture_update(world))
+        return self._dp_graphs[self._dp_key(eng)]
 
-    def dp_graph_step(self, eng, group=None):
+    @staticmethod
+    def _dp_key(eng):
+        # the captured graph holds the bound dataset's buffer pointers: a rebind (the device pipeline's slot
+        # rebuilt after the number of minibatches changed) must recapture, not replay freed buffers
+        ds = getattr(eng, "_dataset", None)
+        return (id(eng),) + (tuple(t.data_ptr() for t in ds) if ds is not None else ())
+
+    def dp_graph_step(self, eng, group=None, graphs=None):
         """One data-parallel step on the graph path (SURVEY §8e axis 2; the reference's loss.backward();
         optimizer.step(), code/nmgp_dsvi.py:847-854, with the gradient average between them).  Bucketed:
           main:  replay the gradient graph ........................ | wait comm | replay 1/world + Adam
@@ -596,7 +608,7 @@ class DsviTrainer:
         element-wise those of one flat all-reduce (bit-identical at two ranks)."""
         mdl = self.model
         rank, world = DD.world_info(group)
-        dpg = getattr(self, "_dp_graphs", {}).get(id(eng))
+        dpg = graphs if graphs is not None else getattr(self, "_dp_graphs", {}).get(self._dp_key(eng))
         g, ev, upd = dpg if dpg is not None else self.capture_dp(eng, world)
         if ev is None:
             g.replay()
@@ -621,7 +633,7 @@ class DsviTrainer:
         """torch.optim.Adam update of the flat parameter vector (one HIP launch; from M = 512 on the sqrt blocks'
         lower triangles only, nmgp_adam_lower: their upper triangles never move)."""
         mdl = self.model
-        if mdl.M >= ADAM_LOWER_MIN_M:
+        if use_adam_lower(mdl.M, mdl._theta.dtype, mdl._offs):
             H.adam_lower_(mdl._theta, mdl._grad, self.m, self.v, self.step_count, self.lr,
                           lower_block_ranges(mdl._offs), mdl.M, self.betas, self.eps)
         else:
@@ -741,7 +753,7 @@ class _DevicePipeline:
                 torch.empty(nb, B, dtype=torch.int32, device=dev), torch.empty(nb, self.D + 1, dtype=torch.int32,
                                                                                 device=dev))
         ctr = eng.bind_dataset(*bufs)
-        sl = {"eng": eng, "bufs": bufs, "ctr": ctr, "graph": None, "nb": nb}
+        sl = {"eng": eng, "bufs": bufs, "ctr": ctr, "graph": None, "dp": None, "nb": nb}
         self.slots[B] = sl
         return sl
 
@@ -784,9 +796,11 @@ class _DevicePipeline:
     def step(self, sl, group=None):
         tr = self.trainer
         if self.use_graph and self.world > 1:
-            # data parallel on the graph path: gradient graph, bucketed all-reduce overlapped with its tail
-            # (the sqrt rows from the graph's lbar_done node on), update graph
-            tr.dp_graph_step(sl["eng"], group)
+            # data parallel on the graph path: gradient graph, all-reduce (flat by default; bucketed and overlapped
+            # with the graph's tail from its lbar_done node when DsviTrainer.dp_bucketed says so), update graph
+            if sl.get("dp") is None:          # kept in the slot: a rebound slot starts without graphs
+                sl["dp"] = tr.capture_dp(sl["eng"], self.world)
+            tr.dp_graph_step(sl["eng"], group, graphs=sl["dp"])
         elif self.use_graph:
             if sl["graph"] is None:
                 sl["graph"] = tr.capture(sl["eng"], include_update=self.include_update)
@@ -822,8 +836,8 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
     """
     rank, world = DD.world_info(group) if distributed else (0, 1)
     if use_graph is None:
-        # device noise: one graph per step; data parallel on the graph path overlaps the bucketed all-reduce
-        # with the backward's tail (DsviTrainer.dp_graph_step), as the eager dp_grad_step does
+        # device noise: one graph per step; data parallel on the graph path: gradient graph, one all-reduce,
+        # 1/world + Adam graph (DsviTrainer.dp_graph_step; the bucketed form on request, DP_BUCKET_MIN_BYTES)
         use_graph = noise == "device"
     if use_graph and noise != "device":
         raise ValueError("use_graph=True needs noise='device' (host RNG cannot be replayed)")
@@ -900,8 +914,7 @@ def inference(X_train_list, Y_train_list, z, batch_size, dim_outputs, hyperpars=
                     trainer.dp_grad_step(eng, group)        # bucketed all-reduce overlapped with the backward
                     trainer.update()
                 else:
-                    # (world > 1: DsviTrainer.dp_graph_step -- gradient graph, bucketed all-reduce overlapped
-                    # with its tail, 1/world + Adam graph)
+                    # (world > 1: DsviTrainer.dp_graph_step -- gradient graph, all-reduce, 1/world + Adam graph)
                     eng = pipe.step(sl, group)
                 losses_dev.append(eng.out[0].clone())
                 ev = torch.cuda.Event(enable_timing=True)

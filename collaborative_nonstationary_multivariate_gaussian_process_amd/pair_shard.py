@@ -34,7 +34,7 @@ import torch
 
 from . import distributed as DD
 from . import hip_ops as H
-from .engine import (ADAM_LOWER_MIN_M, DsviEngine, lower_block_ranges, param_layout, pair_window, PARAM_NAMES,
+from .engine import (DsviEngine, lower_block_ranges, use_adam_lower, param_layout, pair_window, PARAM_NAMES,
                      HYPER_NAMES)
 
 
@@ -230,7 +230,7 @@ class PairShard:
         return loss[0]
 
     def update(self):
-        if self.engine.M >= ADAM_LOWER_MIN_M:        # the sqrt blocks' lower triangles only (nmgp_adam_lower)
+        if use_adam_lower(self.engine.M, self.theta.dtype, self.engine.offs):   # lower triangles only (nmgp_adam_lower)
             H.adam_lower_(self.theta, self.grad, self.m, self.v, self.step_count, self.lr,
                           lower_block_ranges(self.engine.offs), self.engine.M, self.betas, self.eps)
         else:

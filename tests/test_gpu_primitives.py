@@ -657,6 +657,61 @@ def test_gemm_big_kseg_batch(ops):
         assert rel(got, ref) < 2e-6 and torch.all(got[~lo] == 0)
 
 
+def test_gemm_big_persistent_multi_item_walk(ops):
+    # a batched single-pass launch is a grid of 2 x CUs workgroups that walk the (tile, problem) items;
+    # only with items > 2 x CUs does a workgroup run several.  M = 512 (16 tiles per problem) x 72 problems = 1152
+    # items: per-problem kseg k ranges incl. empty ones (OUT_TRIL items with no k-tiles), beta accumulate, and a
+    # rows-epilogue SYRK (OUT_LOWER + diag) handing LDS to the next item.  Bit-identical to the same problems
+    # launched 8 at a time (128 items: one item per workgroup) and within f32 rounding of fp64 torch.
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L
+    g = torch.Generator().manual_seed(51)
+    Bn, M, nprob = 300, 512, 72
+    P = torch.randn(Bn, M, generator=g).to(DEV)
+    W = torch.randn(3, Bn, M, generator=g).to(DEV)
+    seg = torch.tensor([0, 120, 120, 260, 300], dtype=torch.int32, device=DEV)   # segment 1 empty
+    probs = [(b % 4, 1 + (b // 4) % 2 if b % 4 < 3 else 1, b % 3) for b in range(nprob)]
+    probs[5] = (1, 1, 2)                                                          # empty k range
+    C0 = torch.randn(nprob, M, M, generator=g).to(DEV)
+
+    def run(chunk):
+        C = C0.clone()
+        for c0 in range(0, nprob, chunk):
+            pr = probs[c0:c0 + chunk]
+            op = ops.BigBatch(P, W, C, [0] * len(pr), [w * Bn * M for (_, _, w) in pr],
+                              [(c0 + b) * M * M for b in range(len(pr))], M, M, Bn, lda=M, ldb=M, a_kcontig=False,
+                              b_kcontig=False, flags=L.OUT_TRIL, beta=1.0,
+                              kseg=(seg, [s_ for (s_, _, _) in pr], [sp for (_, sp, _) in pr]))
+            op()
+        return C
+    got, ref8 = run(nprob), run(8)
+    assert torch.equal(got, ref8)
+    sc = seg.cpu().tolist()
+    lo = torch.tril(torch.ones(M, M, dtype=torch.bool))
+    for b in (0, 5, 6, 37, nprob - 1):
+        s_, sp, w = probs[b]
+        k0, k1 = sc[s_], sc[s_ + sp]
+        ref = torch.tril(C0[b].cpu().double() + P[k0:k1].cpu().double().t() @ W[w, k0:k1].cpu().double())
+        assert rel(got[b].cpu(), ref) < 2e-6 and torch.all(got[b].cpu()[~lo] == 0)
+    assert torch.equal(got[5].cpu()[lo], C0[5].cpu()[lo])                           # k = 0: C kept
+    # rows-epilogue SYRK items (OUT_LOWER + diag_add), 72 problems of M = 512 at per-problem offsets
+    pool = torch.randn(4 * M * M, generator=g).to(DEV)
+    offs = [(b % 4) * M * M for b in range(nprob)]
+
+    def syrk(chunk):
+        C = torch.full((nprob, M, M), 5.0, device=DEV)
+        for c0 in range(0, nprob, chunk):
+            o = offs[c0:c0 + chunk]
+            ops.BigBatch(pool, pool, C, o, o, [(c0 + b) * M * M for b in range(len(o))], M, M, M, lda=M, ldb=M,
+                         b_kcontig=True, flags=L.A_LOWER | L.B_UPPER | L.OUT_LOWER, diag_add=0.5)()
+        return C
+    s_all, s8 = syrk(nprob), syrk(8)
+    assert torch.equal(s_all, s8)
+    for b in (0, 41, nprob - 1):
+        S = torch.tril(pool[offs[b]:offs[b] + M * M].reshape(M, M).double().cpu())
+        ref = S @ S.t() + 0.5 * torch.eye(M, dtype=F64)
+        assert rel(s_all[b].cpu()[lo], ref[lo]) < 2e-6 and torch.all(s_all[b].cpu()[~lo] == 5.0)
+
+
 def test_chol_inv_blocked_not_pd_reports_global_column(ops):
     A = _spd(400, 2, 9)
     bad = A.clone()

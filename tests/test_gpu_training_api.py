@@ -367,3 +367,29 @@ def test_inference_with_test_lists_rmse_matches_predict_after_training():
         est = predict_Y(model, Xt)
         ref = np.sqrt(np.mean((est[:, None] - np.concatenate(Yt)) ** 2))
         assert float(rmse[-1]) == pytest.approx(float(ref), rel=1e-12)
+
+
+@pytest.mark.parametrize("M,dt", [(514, torch.float32), (513, torch.float64)])
+def test_unaligned_M_trains_with_the_dense_adam(M, dt):
+    """from M = 512 the trainer updated the sqrt blocks with nmgp_adam_lower, which needs M (and every
+    block offset) to be a multiple of 16 / element size -- fp32 M = 514 or fp64 M = 513 raised at the first
+    optimizer step.  Such shapes now take the dense Adam: inference runs and its update equals
+    torch.optim.Adam's first step on the same gradient."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP, DsviTrainer, inference
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.engine import use_adam_lower
+    g, xs, ys = _toy()
+    z = np.linspace(0, 1, M)
+    m = NMGP(200, 2, z, device="cuda:0", noise="device", dtype=dt)
+    assert not use_adam_lower(M, dt, m._offs)
+    tr = DsviTrainer(m, lr=0.01)
+    gen = torch.Generator(device="cuda:0").manual_seed(3)
+    m._grad.copy_(torch.randn(m._grad.shape, generator=gen, device="cuda:0", dtype=dt))
+    ref = m._theta.detach().clone().requires_grad_(True)
+    opt = torch.optim.Adam([ref], lr=0.01)
+    ref.grad = m._grad.clone()
+    opt.step()
+    tr.update()
+    assert _rel(m._theta, ref) < (1e-6 if dt == torch.float32 else 1e-14)
+    model, losses, _ = inference(xs, ys, z, 200, 2, hyperpars=dict(TOY_HYPER), lr=0.005, itnum=2, show_ELBO=False,
+                                 device="cuda:0", noise="device", dtype=dt)
+    assert len(losses) == 2 and all(np.isfinite(losses))
