@@ -72,6 +72,17 @@ class DsviArgs(ctypes.Structure):
                 ("t64", c_vp), ("scal64", c_vp)]
 
 
+class CholTpMat(ctypes.Structure):
+    _fields_ = [("build", c_int), ("rows", c_int), ("hyp", c_vp), ("K12", c_vp), ("T", c_vp), ("P", c_vp)]
+
+
+class CholTpArgs(ctypes.Structure):
+    _fields_ = [("A", c_vp), ("n", c_i64), ("lda", c_i64), ("strideA", c_i64), ("X", c_vp), ("ldx", c_i64),
+                ("strideX", c_i64), ("batch", c_i64), ("info", c_vp), ("jitter", c_dbl), ("Z", c_vp), ("ellZ", c_vp),
+                ("x", c_vp), ("B", c_i64), ("Pt", c_vp), ("Tt", c_vp), ("v", c_vp), ("zt", c_vp), ("hyp_t", c_vp),
+                ("ellX", c_vp), ("var_t", c_vp), ("mats", CholTpMat * 4)]
+
+
 # flags (include/nmgp_hip.h)
 A_LOWER, A_UPPER, B_LOWER, B_UPPER = 1, 2, 4, 8
 OUT_LOWER, OUT_TRIL, KSCALE, EPI, EPI_E_LOWER, DIAG_ADD, EPI_RS_NEG = 16, 32, 64, 128, 256, 512, 1024
@@ -106,6 +117,9 @@ _SIGS = {
     "nmgp_sizeof_pairwise_desc": (c_i64, []),
     "nmgp_sizeof_pairwise_bwd_desc": (c_i64, []),
     "nmgp_sizeof_dsvi_args": (c_i64, []),
+    "nmgp_sizeof_chol_tp_args": (c_i64, []),
+    "nmgp_chol_tp_f64": (c_int, [c_vp, c_vp]),
+    "nmgp_chol_tp_trace": (c_int, [c_vp, c_i64]),
     "nmgp_gemm_grouped_f64": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
     "nmgp_gemm_grouped_f32": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
     "nmgp_gemm_grouped_dyn_f64": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
@@ -221,7 +235,7 @@ def lib():
         f.argtypes = args
     for cls, fn in [(GemmDesc, "nmgp_sizeof_gemm_desc"), (PairwiseDesc, "nmgp_sizeof_pairwise_desc"),
                     (PairwiseBwdDesc, "nmgp_sizeof_pairwise_bwd_desc"), (DsviArgs, "nmgp_sizeof_dsvi_args"),
-                    (PairDesc, "nmgp_sizeof_pair_desc")]:
+                    (PairDesc, "nmgp_sizeof_pair_desc"), (CholTpArgs, "nmgp_sizeof_chol_tp_args")]:
         if ctypes.sizeof(cls) != getattr(L, fn)():
             raise ImportError(f"ABI mismatch: ctypes {cls.__name__} is {ctypes.sizeof(cls)} bytes, "
                               f"library says {getattr(L, fn)()}")

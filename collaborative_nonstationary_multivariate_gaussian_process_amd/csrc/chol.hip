@@ -592,6 +592,65 @@ template <typename T> __device__ inline unsigned long long* ctl_flag(T* Xm, int 
 template <typename T> __device__ inline unsigned long long* ctl_done(T* Xm, int n) {
   return (unsigned long long*)(Xm + (n - 2 * kCtl<T>));
 }
+// fused prior launch (chol_tp_kernel): the inverse workgroup of block-column parity `par` publishes its finished X
+// rows through X(0, n - (4 + par) words) (the four-role kernel's hflag is the third word)
+template <typename T> __device__ inline unsigned long long* ctl_xflag(T* Xm, int n, int par) {
+  return (unsigned long long*)(Xm + (n - (4 + par) * kCtl<T>));
+}
+// ... and, for a built prior, the block columns 1..3 it built for the factor workgroup (par 0: 1 and 3, par 1: 2)
+template <typename T> __device__ inline unsigned long long* ctl_bflag(T* Xm, int n, int par) {
+  return (unsigned long long*)(Xm + (n - (6 + par) * kCtl<T>));
+}
+// the fused launch's extra words, cleared by the last of a matrix's readers
+template <typename T> __device__ inline void tp_clear_words(T* Xm, int n) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    __hip_atomic_store(ctl_xflag(Xm, n, q), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ctl_bflag(Xm, n, q), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// K22 + jitter I element of a prior that the fused launch builds in the factor / update workgroups instead of
+// reading it: the arithmetic of pairwise_kernel (csrc/pairwise.hip) for the same matrix -- RBF
+// s2 exp(-(z_i/ls - z_j/ls)^2 / 2) (code/utils.py:91-94), Gibbs sqrt(2 l_i l_j / S) exp(-(z_i - z_j)^2 / S),
+// S = l_i^2 + l_j^2 (code/utils.py:97-103)
+// phase stamps of the fused launch (tools/chol_tp_probe.py, NMGP_TP_DBG bit 16): 8 words per workgroup, read back
+// with nmgp_chol_tp_trace
+__device__ unsigned long long g_tp_trace[8 * 512];
+#define TP_STAMP(on, k) \
+  if ((on) && threadIdx.x == 0 && blockIdx.x < 512) g_tp_trace[8 * blockIdx.x + (k)] = wall_clock64()
+struct TpBuild {
+  int mode;            // 0: read A, 1: RBF, 2: Gibbs
+  int trace;           // phase stamps (g_tp_trace)
+  double s2, jitter;
+  const double* uz;    // LDS: z_i / ls (RBF) or z_i (Gibbs), staged once per workgroup (tp_stage)
+  const double* ul;    // LDS: ell_Z (Gibbs)
+};
+__device__ inline double tp_k22(const TpBuild& b, int i, int j) {
+  double k;
+  const double dd = b.uz[i] - b.uz[j];     // = z_i / ls - z_j / ls, or z_i / 1 - z_j / 1, as pairwise_kernel
+  double r2 = 0;
+  r2 += dd * dd;
+  if (b.mode == 1) {
+    k = dexp(-0.5 * r2) * b.s2;
+  } else {
+    const double lx = b.ul[i], lz = b.ul[j];
+    const double S = lx * lx + lz * lz;
+    const double C = dsqrt(2.0 * (lx * lz) / S);
+    k = 1.0 * C * dexp(-r2 / S);
+  }
+  if (i == j) k += b.jitter;
+  return k;
+}
+// the per-index inputs of a built prior's elements, staged in LDS (one division per index instead of two per element)
+__device__ inline void tp_stage(double* uz, double* ul, int mode, const double* Z, const double* ellZ, double ls,
+                                int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    uz[i] = mode == 1 ? Z[i] / ls : Z[i] / 1.0;
+    if (mode == 2) ul[i] = ellZ[i];
+  }
+  __syncthreads();
+}
 
 template <typename T, int NTPW>
 __device__ __attribute__((always_inline)) inline void chol2_potrf_role(T* Am, T* Xm, int n, int64_t lda, int64_t ldx, int32_t* info, int col_off,
@@ -892,9 +951,10 @@ __device__ inline void tri_decode_par(int tp, int par, int& ib, int& jb) {
   }
 }
 
-template <typename T, int NTPW, int NCTL = 2>
+template <typename T, int NTPW, int NCTL = 2, bool XPUB = false, bool BUILD = false>
 __device__ __attribute__((always_inline)) inline void chol3_trtri_role(T* Am, T* Xm, int n, int64_t lda,
-                                                                       int64_t ldx, int par, unsigned char* smem_raw) {
+                                                                       int64_t ldx, int par, unsigned char* smem_raw,
+                                                                       int nfin = 2, const TpBuild* bd = nullptr) {
   using acc_t = typename Mfma<T>::acc_t;
   const int nt = (n + 15) >> 4, NR = nt * 16;
   T* Ps = (T*)smem_raw + NR * CP;
@@ -924,6 +984,28 @@ __device__ __attribute__((always_inline)) inline void chol3_trtri_role(T* Am, T*
       }
     }
   }
+  // XPUB (the fused prior launch): X rows are stored write-through and, once drained, announced in xflag, so the
+  // launch's row workgroups can read them while the factorization runs
+  unsigned long long* xflag = ctl_xflag(Xm, n, par);
+  if (BUILD && bd->mode != 0) {
+    // a built prior: these workgroups wait for the first block column anyway, so they build block columns 1..3
+    // (par 0: 1 and 3, par 1: 2) into A write-through and announce each in bflag -- off the factor's serial chain
+    unsigned long long* bflag = ctl_bflag(Xm, n, par);
+    for (int c = 1 + par; c < 4 && c < nt; c += 2) {
+      const int ntc = nt - c;
+      for (int tl = w; tl < ntc; tl += RW) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gr = (c + tl) * 16 + Mfma<T>::row(lane, r), gc = c * 16 + (lane & 15);
+          if (gr < n && gc < n) bstore_sc1<T>(rAm, (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)), (T)tp_k22(*bd, gr, gc));
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) __hip_atomic_store(bflag, kFlagTag + (unsigned long long)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if constexpr (BUILD) TP_STAMP(bd->trace, 2);
   // strictly upper part of X is zero (rows of this parity; the two control words stay)
   for (int i = 2 * w + par; i < n; i += 2 * RW)
     for (int j = ((i >> 4) + 1) * 16 + lane; j < n; j += 64) {
@@ -972,7 +1054,13 @@ __device__ __attribute__((always_inline)) inline void chol3_trtri_role(T* Am, T*
       if (gr >= n || gc >= n) v = (gr == gc) ? (T)1 : (T)0;
       LiT[c * CP + r] = v;
     }
+    // (XPUB: the previous step's X rows had this step's poll and loads to drain)
+    if constexpr (XPUB) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
+    if constexpr (XPUB) {
+      if (t == 0 && kb > 0)
+        __hip_atomic_store(xflag, kFlagTag + (unsigned long long)kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     CHOL_STAMP1(kb, 1);
     // X[kb, jb] = L_kk^-1 R[kb, jb]   (jb <= kb of this parity)
 #pragma unroll
@@ -1011,17 +1099,30 @@ __device__ __attribute__((always_inline)) inline void chol3_trtri_role(T* Am, T*
     for (int idx = t; idx < ncol * 256; idx += RW * 64) {
       const int j = par + 2 * (idx >> 8), k = (idx >> 4) & 15, c = idx & 15;
       const int gr = kb * 16 + k, gc = j * 16 + c;
-      if (gr < n && gc < n) Xm[(int64_t)gr * ldx + gc] = Xrow[(j * 16 + k) * CP + c];
+      if (gr < n && gc < n) {
+        if constexpr (XPUB)
+          bstore_sc1<T>(rXm, (uint32_t)(((int64_t)gr * ldx + gc) * sizeof(T)), Xrow[(j * 16 + k) * CP + c]);
+        else
+          Xm[(int64_t)gr * ldx + gc] = Xrow[(j * 16 + k) * CP + c];
+      }
     }
     lds_barrier();
     CHOL_STAMP1(kb, 3);
   }
   CHOL_STAMPX(2);
+  if constexpr (BUILD) TP_STAMP(bd->trace, 3);
+  if constexpr (XPUB) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    if (t == 0) __hip_atomic_store(xflag, kFlagTag + (unsigned long long)nt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (t == 0) {
-    // the last consumer re-arms the progress word for the next launch and clears both words
+    // the last of the launch's `nfin` readers of this matrix's words re-arms the progress word for the next launch
+    // and clears the others
     const unsigned long long old = __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == kDoneTag + 1ull) {
+    if (old == kDoneTag + (unsigned long long)(nfin - 1)) {
       __hip_atomic_store(flag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if constexpr (XPUB || BUILD) tp_clear_words(Xm, n);
       __hip_atomic_store(done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -1066,8 +1167,9 @@ template <typename T> __device__ inline unsigned long long* ctl_hflag(T* Xm, int
 }
 
 template <typename T>
-__device__ __attribute__((always_inline)) inline bool poll_word(unsigned long long* word, int need, int nt) {
-  for (int spin = 0; spin < (1 << 26); ++spin) {
+__device__ __attribute__((always_inline)) inline bool poll_word(unsigned long long* word, int need, int nt,
+                                                                int max_spin = 1 << 26) {
+  for (int spin = 0; spin < max_spin; ++spin) {
     const unsigned long long f = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (f >= kFlagTag + (unsigned long long)need && f <= kFlagTag + (unsigned long long)nt) return true;
     __builtin_amdgcn_s_sleep(1);
@@ -1075,11 +1177,12 @@ __device__ __attribute__((always_inline)) inline bool poll_word(unsigned long lo
   return false;
 }
 
-template <typename T>
+template <typename T, bool BUILD = false>
 __device__ __attribute__((always_inline)) inline void chol7_factor_role(T* Am, T* Xm, int n, int64_t lda,
                                                                         int64_t ldx, int32_t* info, int col_off,
                                                                         int info_first, int mat,
-                                                                        unsigned char* smem_raw) {
+                                                                        unsigned char* smem_raw,
+                                                                        const TpBuild* bd = nullptr) {
   using acc_t = typename Mfma<T>::acc_t;
   const int nt = (n + 15) >> 4, NR = nt * 16;
   T* colbuf = (T*)smem_raw;            // NR x CP: block column k before its panel (local rows)
@@ -1094,7 +1197,9 @@ __device__ __attribute__((always_inline)) inline void chol7_factor_role(T* Am, T
   if (t == 0) __hip_atomic_store(hflag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   bool ok = true;
   acc_t acc[2];
-  // block column k's tiles (kb + w + RW u, kb): issue their loads (out-of-range ones read 0)
+  // block column k's tiles (kb + w + RW u, kb): issue their loads (out-of-range ones read 0).  BUILD (the fused
+  // prior launch): block columns 0..3, which no update workgroup has touched, are built here from the prior's
+  // inputs instead
   auto load_col = [&](int kb) {
     const int ntc = nt - kb;
 #pragma unroll
@@ -1109,7 +1214,25 @@ __device__ __attribute__((always_inline)) inline void chol7_factor_role(T* Am, T
     }
   };
   lds_barrier();
-  load_col(0);
+  bool built0 = false;
+  if constexpr (BUILD) {
+    // a built prior (the fused launch): block column 0 is built here; columns 1..3 by the inverse workgroups, which
+    // are idle until column 0 is published (read below after their bflag)
+    if (bd->mode != 0) {
+      built0 = true;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int tl = w + RW * u;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gr = tl * 16 + Mfma<T>::row(lane, r), gc = lane & 15;
+          acc[u][r] = (tl < nt && gr < n && gc < n) ? (T)tp_k22(*bd, gr, gc) : (T)0;
+        }
+      }
+    }
+  }
+  if (!built0) load_col(0);
+  if constexpr (BUILD) TP_STAMP(bd->trace, 2);
   int first_fail = 0;
   for (int kb = 0; kb < nt; ++kb) {
     const int nrow = NR - kb * 16, ntc = nt - kb;
@@ -1156,6 +1279,11 @@ __device__ __attribute__((always_inline)) inline void chol7_factor_role(T* Am, T
       if (kb + 1 >= 4) {
         bool seen = true;
         if (lane == 0) seen = poll_word<T>(hflag, kb - 2, nt);
+        ok &= seen;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      } else if (BUILD && bd->mode != 0) {
+        bool seen = true;
+        if (lane == 0) seen = poll_word<T>(ctl_bflag(Xm, n, (kb + 1) == 2 ? 1 : 0), kb + 1, nt);
         ok &= seen;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
@@ -1227,6 +1355,7 @@ __device__ __attribute__((always_inline)) inline void chol7_factor_role(T* Am, T
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_barrier();
+  if constexpr (BUILD) TP_STAMP(bd->trace, 3);
   if (t == 0) {
     __hip_atomic_store(flag, kFlagTag + (unsigned long long)nt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(hflag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // no reader left
@@ -1238,9 +1367,10 @@ __device__ __attribute__((always_inline)) inline void chol7_factor_role(T* Am, T
   if (lane == 0 && !ok) spin_gave_up(NMGP_STATUS_CHOL_SPIN);
 }
 
-template <typename T, int NTPW>
+template <typename T, int NTPW, bool BUILD = false>
 __device__ __attribute__((always_inline)) inline void chol7_update_role(T* Am, T* Xm, int n, int64_t lda,
-                                                                        unsigned char* smem_raw) {
+                                                                        unsigned char* smem_raw,
+                                                                        const TpBuild* bd = nullptr) {
   using acc_t = typename Mfma<T>::acc_t;
   const int nt = (n + 15) >> 4, NR = nt * 16;
   T* Ps = (T*)smem_raw;                // NR x CP: L[:, j] (local rows)
@@ -1266,13 +1396,19 @@ __device__ __attribute__((always_inline)) inline void chol7_update_role(T* Am, T
   }
 #define IB7(u) (tij[u] < 0 ? -1 : (tij[u] >> 8))
 #define JB7(u) (tij[u] < 0 ? -1 : (tij[u] & 255))
+  bool build = false;
+  if constexpr (BUILD) build = bd->mode != 0;     // the fused prior launch: the tiles are built, not read
 #pragma unroll
   for (int u = 0; u < NTPW; ++u) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int gr = IB7(u) * 16 + Mfma<T>::row(lane, r), gc = JB7(u) * 16 + (lane & 15);
       const bool in = IB7(u) >= 0 && gr < n && gc < n;
-      acc[u][r] = bload<T>(rAm, in ? (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)) : 0x80000000u);
+      if (build) {
+        if constexpr (BUILD) acc[u][r] = in ? (T)tp_k22(*bd, gr, gc) : (T)0;
+      } else {
+        acc[u][r] = bload<T>(rAm, in ? (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)) : 0x80000000u);
+      }
     }
   }
 #pragma unroll
@@ -1365,6 +1501,464 @@ __global__ __launch_bounds__(RW * 64) void chol_inv7_kernel(T* A, int n, int64_t
   } else {
     chol3_trtri_role<T, NTPW1, 3>(Am, Xm, n, lda, ldx, role - 2, smem_raw);
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fused prior launch (nmgp_chol_tp_f64, round 6).  The DSVI step's critical path ran
+//   RBF builders -> chol(v, t, L0, L1) -> v -> K_G22 builder -> chol(G) -> invG (T_G = K_G12 C_G^-T) ->
+//   projG (P_G = T_G C_G^-1) -> quad_W
+// with the t / L0 / L1 projections and the t-row on a side stream.  Here one launch per chol does all of it:
+//   - the four-role factorization of each matrix (chol_inv7_kernel's roles), its K22 + jitter I built by the
+//     factor and update workgroups (TpBuild) where it is a prior;
+//   - TPR-row workgroups per prior with minibatch products ("rows" workgroups, tp_rows_role), started in the same
+//     launch and fed by the factorization's own published data: block column kb of L and L_kk^-1 (the factor
+//     role's progress word) and block row kb of X = L^-1 (the inverse roles' xflag words, XPUB).  Each keeps
+//     R = its rows of K12 (built in registers, written out once) in MFMA accumulators and runs the right-looking
+//     triangular solve T = K12 L^-T one block column behind the factor: T(:, kb) = R(:, kb) L_kk^-T, then
+//     R(:, cb) -= T(:, kb) L(cb, kb)^T for cb > kb; and accumulates P = T X one block row behind the inverse
+//     workgroups: P(:, cb) += T(:, kb) X(kb, cb), cb <= kb.  rows 2 first forms the rows' t-row sample
+//     ell_X (dsvi_trow_kernel's arithmetic) and builds Gibbs K12 rows from it.
+// The launch ends (nearly) when the factorization does, and the step loses the builder, invG / projG launches and
+// their graph hand-offs.  Role workgroups come first in the grid (in-order dispatch per XCD), rows workgroups
+// only wait on them, never the reverse; the last of a matrix's readers re-arms its progress words.
+constexpr int TPR = 64;   // minibatch rows per rows workgroup
+// LDS below the staged per-index inputs: the roles' layout (chol_inv7_kernel's, with the third L buffer) or the row
+// workgroups' (NR CP + 16 CP + 4 TPR CP + 16 * 257 + TPR doubles), whichever is larger
+__host__ __device__ constexpr size_t chol_tp_roles_bytes(int n) {
+  return (size_t)((4 * (((n + 15) >> 4) * 16) * CP + 16 * CP) > ((((n + 15) >> 4) * 16) * CP + 16 * CP + 4 * TPR * CP +
+                                                                   16 * 257 + TPR)
+                      ? (4 * (((n + 15) >> 4) * 16) * CP + 16 * CP)
+                      : ((((n + 15) >> 4) * 16) * CP + 16 * CP + 4 * TPR * CP + 16 * 257 + TPR)) *
+         sizeof(double);
+}
+
+struct TpDev {
+  double* A;
+  double* X;
+  int32_t* info;
+  int64_t lda, strideA, ldx, strideX;
+  int n, batch, B, nct, ntp;
+  double jitter;
+  const double* Z;
+  const double* ellZ;
+  const double* x;
+  const double* Pt;
+  const double* Tt;
+  const double* v;
+  const double* zt;
+  const double* hyp_t;
+  double* ellX;
+  double* var_t;
+  int build[4], rows[4], tpm[4];
+  int dbg;   // PROBE ONLY (NMGP_TP_DBG): 1 factor role reads A instead of building, 2 update role reads A
+  const double* hyp[4];
+  double* K12[4];
+  double* Tm[4];
+  double* Pm[4];
+};
+
+__device__ __attribute__((always_inline)) inline void tp_rows_role(const TpDev& a, int m, int rt,
+                                                                   unsigned char* smem_raw) {
+  using acc_t = f64x4;
+  using MF = Mfma<double>;
+  const int n = a.n, nt = (n + 15) >> 4, NR = nt * 16, B = a.B;
+  constexpr int KP = 257;                // X-row pitch (n <= 256): compile-time, so LDS operand reads are one base
+                                         // register + immediate offsets
+  double* Ls = (double*)smem_raw;        // NR x CP: L[kb*16 + lr, kb*16 + c] (local rows)
+  double* Li = Ls + NR * CP;             // 16 x CP: L_kk^-1
+  double* Rs = Li + 16 * CP;             // TPR x CP: R(:, kb) (block column kb of the residual)
+  double* Tc = Rs + TPR * CP;            // 3 x TPR x CP: T(:, kb), triple-buffered (P uses step kb - 2's)
+  double* Xs = Tc + 3 * TPR * CP;        // 16 x KP: X[pk*16 + j, c], c <= pk*16 + j
+  double* rowv = Xs + 16 * KP;           // TPR: ell_X of the rows (rows 2)
+  double* Am = a.A + (int64_t)m * a.strideA;
+  double* Xm = a.X + (int64_t)m * a.strideX;
+  unsigned long long* flag = ctl_flag(Xm, n);
+  unsigned long long* done = ctl_done(Xm, n);
+  unsigned long long* xf0 = ctl_xflag(Xm, n, 0);
+  unsigned long long* xf1 = ctl_xflag(Xm, n, 1);
+  (void)xf0;
+  const __amdgpu_buffer_rsrc_t rAm = make_rsrc(Am, ((int64_t)(n - 1) * a.lda + n) * (int64_t)sizeof(double));
+  const __amdgpu_buffer_rsrc_t rXm = make_rsrc(Xm, ((int64_t)(n - 1) * a.ldx + n) * (int64_t)sizeof(double));
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int r0 = rt * TPR;
+  const int mode = a.rows[m];
+  double* K12 = a.K12[m];
+  double* Tg = a.Tm[m];
+  double* Pg = a.Pm[m];
+
+  // 1. rows 2: the t-row sample of each row (JGP_S, code/utils.py:226-235), dsvi_trow_kernel's arithmetic
+  if (mode == 2) {
+    const double s2t = dexp(a.hyp_t[0]);
+    for (int i = w; i < TPR; i += RW) {
+      const int r = r0 + i;
+      double lx = 1.0;
+      if (r < B) {
+        const double* Pr = a.Pt + (int64_t)r * n;
+        const double* Tr = a.Tt + (int64_t)r * n;
+        double mean = 0, q = 0;
+        for (int c = lane; c < n; c += 64) {
+          mean += Pr[c] * a.v[c];
+          const double tt = Tr[c];
+          q += (double)(tt * tt);
+        }
+        mean = wave_sum(mean);
+        q = wave_sum(q);
+        const double var = s2t - q;
+        const double tl = mean + a.zt[r] * dsqrt(var + a.jitter);
+        lx = dexp(tl);
+        if (lane == 0) {
+          a.ellX[r] = lx;
+          a.var_t[r] = var;
+        }
+      }
+      if (lane == 0) rowv[i] = lx;
+    }
+    __syncthreads();
+  }
+
+  // 2. R = this workgroup's rows of K12, built in the accumulator layout (pairwise_kernel's arithmetic) and
+  //    written out.  Wave w owns the tiles (rb = w & 3, cb = (w >> 2) + 2u), u < 8, of R and of P.
+  const int rbw = w & 3, cpar = w >> 2;
+  acc_t R[8], P[8];
+  double s2 = 1.0, ls = 1.0;
+  if (mode == 1) {
+    s2 = dexp(a.hyp[m][0]);
+    ls = dexp(a.hyp[m][1]);
+  }
+  double* uz = (double*)(smem_raw + chol_tp_roles_bytes(n));
+  double* ul = uz + 256;
+  tp_stage(uz, ul, mode, a.Z, a.ellZ, ls, n);
+  double xu[4];                      // x_i / ls (RBF) or x_i / 1 (Gibbs) of this lane's four rows
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = r0 + rbw * 16 + MF::row(lane, r);
+    xu[r] = row < B ? a.x[row] / ls : 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int cb = cpar + 2 * u;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = rbw * 16 + MF::row(lane, r), row = r0 + i, col = cb * 16 + (lane & 15);
+      double k = 0;
+      if (row < B && col < n) {
+        const double dd = xu[r] - uz[col];
+        double r2 = 0;
+        r2 += dd * dd;
+        if (mode == 1) {
+          k = dexp(-0.5 * r2) * s2;
+        } else {
+          const double lx = rowv[i], lz = ul[col];
+          const double S = lx * lx + lz * lz;
+          const double C = dsqrt(2.0 * (lx * lz) / S);
+          k = 1.0 * C * dexp(-r2 / S);
+        }
+        K12[(int64_t)row * n + col] = k;
+      }
+      R[u][r] = k;
+      P[u][r] = 0;
+    }
+  }
+
+  TP_STAMP((a.dbg & 16) != 0, 2);
+  // 3. one step per block column of the factorization.  Step kb: wait for L[:, kb] / L_kk^-1 (factor) and X row
+  //    block kb - 1 (both inverse workgroups: one poll loop reading all three words), issue their loads, and while
+  //    they are in flight add step kb - 2's P product (X row kb - 2 and T(:, kb - 2) are in LDS); then T(:, kb) and
+  //    the R update.  T is triple-buffered for that lag.
+  bool ok = true;
+  constexpr int PER = 256 * 16 / (RW * 64);   // elements per thread of a 256 x 16 block column / 16 x 256 block row
+  auto poll3 = [&](int nf, int nx) -> bool {  // flag >= nf and both X-row words >= nx (nx == 0: not needed)
+    for (int spin = 0; spin < (1 << 22); ++spin) {
+      const unsigned long long f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long x0 = nx ? __hip_atomic_load(xf0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+      const unsigned long long x1 = nx ? __hip_atomic_load(xf1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+      const unsigned long long lo = kFlagTag, hi = kFlagTag + (unsigned long long)nt;
+      const bool fok = nf == 0 || (f >= lo + (unsigned long long)nf && f <= hi);
+      const bool xok = nx == 0 || (x0 >= lo + (unsigned long long)nx && x0 <= hi && x1 >= lo + (unsigned long long)nx &&
+                                   x1 <= hi);
+      if (fok && xok) return true;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+  };
+  auto load_x_row = [&](int pk, double (&xv)[PER]) {   // X[pk*16 + j, c] for c <= pk*16 + j (lower)
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int idx = t + q * RW * 64, j = idx >> 8, c = idx & 255;
+      const int gr = pk * 16 + j;
+      const bool in = c < NR && gr < n && c < n && c <= gr;
+      xv[q] = bload_sc1<double>(rXm, in ? (uint32_t)(((int64_t)gr * a.ldx + c) * sizeof(double)) : 0x80000000u);
+    }
+  };
+  auto store_x_row = [&](const double (&xv)[PER], int pk) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int idx = t + q * RW * 64, j = idx >> 8, c = idx & 255;
+      if (c < (pk + 1) * 16) Xs[j * KP + c] = xv[q];
+    }
+  };
+  auto p_update = [&](int pk) {    // P(:, cb) += T(:, pk) X(pk, cb), cb <= pk
+    const double* Tp = Tc + (pk % 3) * TPR * CP;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int cb = cpar + 2 * u;
+      if (cb <= pk) {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const int kk = s2 * 4 + (lane >> 4);
+          P[u] = MF::mma(Tp[(rbw * 16 + (lane & 15)) * CP + kk], Xs[kk * KP + cb * 16 + (lane & 15)], P[u]);
+        }
+      }
+      // (one tile's operands in flight at a time: hoisting all tiles' LDS reads spilled the accumulators)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  for (int kb = 0; kb < nt; ++kb) {
+    const int nrow = NR - kb * 16;
+    // (bounded waits, and none after one gave up: a lost role costs wrong output and a status bit, not minutes)
+    if (t == 0 && ok) ok = poll3(kb + 1, kb);
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double lv[PER], xv[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int idx = t + q * RW * 64, lr = idx >> 4, c = idx & 15;
+      const int gr = kb * 16 + lr, gc = kb * 16 + c;
+      const uint32_t off =
+          (idx < nrow * 16 && gr < n && gc < n) ? (uint32_t)(((int64_t)gr * a.lda + gc) * sizeof(double)) : 0x80000000u;
+      lv[q] = bload_sc1<double>(rAm, off);
+    }
+    double li = 0;
+    if (t < 256) {
+      const int r = t >> 4, c = t & 15;
+      const int gr = kb * 16 + r, gc = kb * 16 + c;
+      const uint32_t off = (gr < n && gc < n) ? (uint32_t)(((int64_t)gr * a.ldx + gc) * sizeof(double)) : 0x80000000u;
+      li = bload_sc1<double>(rXm, off);
+    }
+    if (kb > 0) load_x_row(kb - 1, xv);
+    if (kb >= 2) p_update(kb - 2);      // under the loads
+    lds_barrier();                      // every wave is done reading the previous step's Rs / Ls / Li / Xs
+    if (t < 256) {
+      const int r = t >> 4, c = t & 15, gr = kb * 16 + r, gc = kb * 16 + c;
+      if (gr >= n || gc >= n) li = (gr == gc) ? 1.0 : 0.0;      // padded identity past n
+      Li[r * CP + c] = li;
+    }
+    // R(:, kb) to LDS (its owner waves)
+    if (cpar == (kb & 1)) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (u == (kb >> 1)) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Rs[(rbw * 16 + MF::row(lane, r)) * CP + (lane & 15)] = R[u][r];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int idx = t + q * RW * 64;
+      if (idx < nrow * 16) Ls[(idx >> 4) * CP + (idx & 15)] = lv[q];
+    }
+    if (kb > 0) store_x_row(xv, kb - 1);
+    lds_barrier();
+    // T(:, kb) = R(:, kb) L_kk^-T (waves 0..3, one row block each) -> LDS and out
+    double* Tk = Tc + (kb % 3) * TPR * CP;
+    if (w < 4) {
+      acc_t tacc = {0, 0, 0, 0};
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const int kk = s2 * 4 + (lane >> 4);
+        tacc = MF::mma(Rs[(w * 16 + (lane & 15)) * CP + kk], Li[(lane & 15) * CP + kk], tacc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = w * 16 + MF::row(lane, r), row = r0 + i, col = kb * 16 + (lane & 15);
+        Tk[i * CP + (lane & 15)] = tacc[r];
+        if (row < B && col < n) Tg[(int64_t)row * n + col] = tacc[r];
+      }
+    }
+    lds_barrier();
+    // R(:, cb) -= T(:, kb) L(cb, kb)^T, cb > kb
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int cb = cpar + 2 * u;
+      if (cb > kb && cb < nt) {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const int kk = s2 * 4 + (lane >> 4);
+          R[u] = MF::mma(-Tk[(rbw * 16 + (lane & 15)) * CP + kk], Ls[((cb - kb) * 16 + (lane & 15)) * CP + kk], R[u]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  TP_STAMP((a.dbg & 16) != 0, 3);
+  // the last two P products: X row nt - 2 is in LDS; X row nt - 1 once both inverse workgroups are done
+  if (nt >= 2) p_update(nt - 2);
+  if (t == 0 && ok) ok = poll3(0, nt);
+  TP_STAMP((a.dbg & 16) != 0, 4);
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  {
+    double xv[PER];
+    load_x_row(nt - 1, xv);
+    lds_barrier();
+    store_x_row(xv, nt - 1);
+  }
+  lds_barrier();
+  p_update(nt - 1);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int cb = cpar + 2 * u;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = r0 + rbw * 16 + MF::row(lane, r), col = cb * 16 + (lane & 15);
+      if (row < B && col < n) Pg[(int64_t)row * n + col] = P[u][r];
+    }
+  }
+  if (!ok && lane == 0) spin_gave_up(NMGP_STATUS_CHOL_SPIN);
+  __syncthreads();
+  if (t == 0) {
+    const int nfin = 2 + a.nct;
+    const unsigned long long old = __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == kDoneTag + (unsigned long long)(nfin - 1)) {
+      __hip_atomic_store(flag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tp_clear_words(Xm, n);
+      __hip_atomic_store(done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <int NTPW1, int NTPWU>
+__global__ __launch_bounds__(RW * 64) void chol_tp_kernel(TpDev a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int nroles = 4 * a.batch;
+  const bool tr = (a.dbg & 16) != 0;
+  TP_STAMP(tr, 0);
+  if ((int)blockIdx.x < nroles) {
+    const int mat = blockIdx.x / 4, role = blockIdx.x - 4 * mat;
+    double* Am = a.A + (int64_t)mat * a.strideA;
+    double* Xm = a.X + (int64_t)mat * a.strideX;
+    TpBuild bd;
+    bd.mode = a.build[mat];
+    bd.trace = (a.dbg & 16) != 0;
+    bd.jitter = a.jitter;
+    bd.s2 = 1.0;
+    double ls = 1.0;
+    if (bd.mode == 1) {
+      bd.s2 = dexp(a.hyp[mat][0]);
+      ls = dexp(a.hyp[mat][1]);
+    }
+    double* uz = (double*)(smem_raw + chol_tp_roles_bytes(a.n));
+    double* ul = uz + 256;
+    bd.uz = uz;
+    bd.ul = ul;
+    if (bd.mode != 0) tp_stage(uz, ul, bd.mode, a.Z, a.ellZ, ls, a.n);
+    // compile-time role variants: a matrix that is read (Sigma_v) runs chol_inv7_kernel's roles; a built prior the
+    // BUILD roles, whose inverse workgroups publish X rows (XPUB) when the matrix has row workgroups
+    if (bd.mode == 0) {
+      if (role == 0) {
+        if (threadIdx.x == 0) __hip_atomic_store(ctl_done(Xm, a.n), kDoneTag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        chol7_factor_role<double>(Am, Xm, a.n, a.lda, a.ldx, a.info, 0, 1, mat, smem_raw);
+      } else if (role == 1) {
+        chol7_update_role<double, NTPWU>(Am, Xm, a.n, a.lda, smem_raw);
+      } else {
+        chol3_trtri_role<double, NTPW1, 5>(Am, Xm, a.n, a.lda, a.ldx, role - 2, smem_raw);
+      }
+    } else {
+      TpBuild b0 = bd;
+      b0.mode = 0;
+      if (role == 0) {
+        if (threadIdx.x == 0) __hip_atomic_store(ctl_done(Xm, a.n), kDoneTag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        chol7_factor_role<double, true>(Am, Xm, a.n, a.lda, a.ldx, a.info, 0, 1, mat, smem_raw,
+                                        (a.dbg & 1) ? &b0 : &bd);
+      } else if (role == 1) {
+        chol7_update_role<double, NTPWU, true>(Am, Xm, a.n, a.lda, smem_raw, (a.dbg & 2) ? &b0 : &bd);
+      } else if (a.rows[mat]) {
+        chol3_trtri_role<double, NTPW1, 7, true, true>(Am, Xm, a.n, a.lda, a.ldx, role - 2, smem_raw, 2 + a.nct,
+                                                       (a.dbg & 1) ? &b0 : &bd);
+      } else {
+        chol3_trtri_role<double, NTPW1, 7, false, true>(Am, Xm, a.n, a.lda, a.ldx, role - 2, smem_raw, 2,
+                                                        (a.dbg & 1) ? &b0 : &bd);
+      }
+    }
+  } else {
+    const int c = blockIdx.x - nroles, k = c / a.nct;
+    tp_rows_role(a, a.tpm[k], c - k * a.nct, smem_raw);
+  }
+  TP_STAMP(tr, 1);
+}
+
+static size_t chol_tp_smem(int n) {
+  // the roles' layout (chol_inv7_kernel's, >= the row workgroups' NR CP + 16 CP + 4 TPR CP + 16 * 257 + TPR doubles),
+  // then the staged per-index inputs uz / ul (2 x 256 doubles)
+  return chol_tp_roles_bytes(n) + 2 * 256 * sizeof(double);
+}
+
+template <int NTPW1, int NTPWU>
+static void chol_tp_go(const TpDev& a, unsigned grid, size_t sm, hipStream_t s) {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    (void)hipFuncSetAttribute((const void*)chol_tp_kernel<NTPW1, NTPWU>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+  });
+  hipLaunchKernelGGL((chol_tp_kernel<NTPW1, NTPWU>), dim3(grid), dim3(RW * 64), sm, s, a);
+}
+
+static int chol_tp_launch(const nmgp_chol_tp_args* h, hipStream_t s) {
+  if (h == nullptr) return -1;
+  const nmgp_chol_tp_args& g = *h;
+  if (!g.A || !g.X || g.n < 128 || g.n > 256 || g.lda < g.n || g.ldx < g.n || g.batch < 1 || g.batch > 4 ||
+      g.B < 0 || g.B > 4096 || g.strideA < 0 || g.strideX < 0 || !g.info)
+    return -1;
+  TpDev a{};
+  a.A = g.A;
+  a.X = g.X;
+  a.info = g.info;
+  a.lda = g.lda;
+  a.strideA = g.strideA;
+  a.ldx = g.ldx;
+  a.strideX = g.strideX;
+  a.n = (int)g.n;
+  a.batch = (int)g.batch;
+  a.B = (int)g.B;
+  a.jitter = g.jitter;
+  a.Z = g.Z;
+  a.ellZ = g.ellZ;
+  a.x = g.x;
+  a.Pt = g.Pt;
+  a.Tt = g.Tt;
+  a.v = g.v;
+  a.zt = g.zt;
+  a.hyp_t = g.hyp_t;
+  a.ellX = g.ellX;
+  a.var_t = g.var_t;
+  for (int m = 0; m < a.batch; ++m) {
+    const nmgp_chol_tp_mat& mt = g.mats[m];
+    if (mt.build < 0 || mt.build > 2 || mt.rows < 0 || mt.rows > 2) return -1;
+    if (mt.build == 1 && (!mt.hyp || !g.Z)) return -1;
+    if (mt.build == 2 && (!g.Z || !g.ellZ)) return -1;
+    if (mt.rows && (!mt.K12 || !mt.T || !mt.P || !g.x || !g.Z)) return -1;
+    if (mt.rows == 1 && !mt.hyp) return -1;
+    if (mt.rows == 2 && (!g.Pt || !g.Tt || !g.v || !g.zt || !g.hyp_t || !g.ellX || !g.var_t || !g.ellZ)) return -1;
+    a.build[m] = mt.build;
+    a.rows[m] = g.B > 0 ? mt.rows : 0;
+    a.hyp[m] = mt.hyp;
+    a.K12[m] = mt.K12;
+    a.Tm[m] = mt.T;
+    a.Pm[m] = mt.P;
+    if (a.rows[m]) a.tpm[a.ntp++] = m;
+  }
+  a.nct = g.B > 0 ? (int)((g.B + TPR - 1) / TPR) : 0;
+  a.dbg = getenv("NMGP_TP_DBG") ? atoi(getenv("NMGP_TP_DBG")) : 0;
+  const unsigned grid = (unsigned)(4 * a.batch + a.ntp * a.nct);
+  const size_t sm = chol_tp_smem(a.n);
+  const int nt = (a.n + 15) >> 4, ntiles = nt * (nt + 1) / 2;
+  if (ntiles <= RW * 9)
+    chol_tp_go<5, 4>(a, grid, sm, s);
+  else
+    chol_tp_go<9, 10>(a, grid, sm, s);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
 }
 
 template <typename T, int NTPW>
@@ -1962,6 +2556,14 @@ NMGP_TU_STATUS_ACCESSOR(chol)
 }  // namespace nmgp
 
 extern "C" {
+int64_t nmgp_sizeof_chol_tp_args(void) { return (int64_t)sizeof(nmgp_chol_tp_args); }
+int nmgp_chol_tp_trace(uint64_t* out, int64_t n) {
+  if (!out || n < 0 || n > 8 * 512) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(nmgp::g_tp_trace), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? NMGP_OK
+             : NMGP_ERR_LAUNCH;
+}
+int nmgp_chol_tp_f64(const nmgp_chol_tp_args* args, hipStream_t s) { return nmgp::chol_tp_launch(args, s); }
 int nmgp_potrf_batched_f64(double* A, int64_t n, int64_t lda, int64_t sA, int64_t b, int32_t* info, hipStream_t s) {
   return nmgp::potrf_launch<double>(A, n, lda, sA, b, info, s);
 }

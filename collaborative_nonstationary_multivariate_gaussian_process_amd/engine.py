@@ -170,6 +170,12 @@ class DsviEngine:
         # per-factor offsets (BigBatch) instead of the grouped 64x64 tiles.  NMGP_BIG_SIDE=0 keeps them on the
         # grouped kernel: the only schedule switch left, for tests/test_gpu_engine.py's equivalence check
         self.big_side = self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0"
+        # round 6: fp64 engines of 128 <= M <= 256 run the GP priors as two fused launches (nmgp_chol_tp_f64): the
+        # RBF priors' K22 built, factored and inverted with K12 / T / P of their rows formed by the same launch, and
+        # likewise the Gibbs prior with its t-row sample -- no builder, invG / projG or t-row launches on the chain.
+        # NMGP_FUSE_TP=0 keeps the separate launches (the tests' equivalence switch)
+        self.fuse_tp = (self.dt == torch.float64 and 128 <= M <= 256 and B <= 4096
+                        and os.environ.get("NMGP_FUSE_TP", "0") != "0")
         # per-(output, factor) L-bar products of the grouped backward (bwd_lbar), summed by nmgp_lbar_reduce: D(D+1)/2
         # slots of M x M + M.  Only where the slots stay small (PM2.5: 15 slots, 7.9 MB); many outputs with few
         # rows each (HCP-like D = 50) keep one product per factor, whose k loop is then short anyway
@@ -387,7 +393,8 @@ class DsviEngine:
                             offs=(k * BM, (NF + k) * MM, k * BM), **rows_all)
         pproj = lambda k: g(self.P, self.T, self.Cinv, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), flags=L.B_LOWER,
                             offs=(k * BM, (NF + k) * MM, k * BM), **rows_all)
-        d5 += [tproj(k) for k in range(3)]
+        if not self.fuse_tp:
+            d5 += [tproj(k) for k in range(3)]
         if p64:
             d5 = []                       # prior inverses and T in fp64 (inv3_64)
         if not elbo_mode:
@@ -406,7 +413,7 @@ class DsviEngine:
                 p["xs_side"] = H.BigBatch(self.Cinv, th, self.Xs, slots, offs_f, slots, M, M, M, lda=M, ldb=M,
                                           b_kcontig=False, flags=L.A_LOWER | L.B_LOWER | L.OUT_TRIL)
         # F6: P_k = K12_k Ainv_k (k = t,0,1) ; Y_t, Y_0, Y_1
-        d6 = [pproj(k) for k in range(3)] if not p64 else []
+        d6 = [pproj(k) for k in range(3)] if not (p64 or self.fuse_tp) else []
         d6 += [g(self.Y, self.Ainv, th, M, 1, M, (M, 1, 0), (1, M, 0), (1, M), offs=(0, muv, D * M)),
                g(self.Y, self.Ainv, th, M, NPC, M, (M, 1, 0), (1, M, 0), (1, M), offs=(MM, muU, (D + 1) * M)),
                g(self.Y, self.Ainv, th, M, NPC, M, (M, 1, 0), (1, M, 0), (1, M),
@@ -431,10 +438,23 @@ class DsviEngine:
                 H.pairwise_desc(self.K12_64[3], self.x64, self.Z64, mode=L.GIBBS, ellX=self.ellX64,
                                 ellZ=self.ellZ64)], dev)
         p["invG"] = G([g(self.Ainv, self.Cinv, self.Cinv, M, M, M, (1, M, 0), (M, 1, 0), (M, 1),
-                         flags=L.A_UPPER | L.B_LOWER, offs=((NF + 3) * MM, (NF + 3) * MM, 3 * MM)), tproj(3)]) \
-            if not p64 else None
-        p["projG"] = G(([pproj(3)] if not p64 else []) +
+                         flags=L.A_UPPER | L.B_LOWER, offs=((NF + 3) * MM, (NF + 3) * MM, 3 * MM))] +
+                      ([] if self.fuse_tp else [tproj(3)])) if not p64 else None
+        p["projG"] = G(([pproj(3)] if not (p64 or self.fuse_tp) else []) +
                        [g(self.Y, self.Ainv, th, M, D, M, (M, 1, 0), (1, M, 0), (1, M), offs=(3 * MM, muW, 0))])
+        if self.fuse_tp:
+            # the two fused prior launches (hip_ops.CholTp): [v | t | L0 | L1] with the three RBF priors built and
+            # their K12 / T / P rows formed in the launch, then the Gibbs prior with the t-row and K_G12 rows
+            hyp_addr = lambda k: th.data_ptr() + (hyp + k) * th.element_size()
+            rbf = [dict(build=1, rows=1, hyp=hyp_addr(2 * k), K12=self.K12[k], T=self.T[k], P=self.P[k])
+                   for k in range(3)]
+            p["chol_tp_main"] = H.CholTp(self.Afac[FV], self.Cinv[FV], self.info[FV:], M, [dict()] + rbf,
+                                         jitter=self.jitter, Z=self.Z, x=self.x, B=B)
+            p["chol_tp_G"] = H.CholTp(self.Afac[NF + 3], self.Cinv[NF + 3], self.info[NF + 3:], M,
+                                      [dict(build=2, rows=2, K12=self.K12[3], T=self.T[3], P=self.P[3])],
+                                      jitter=self.jitter, Z=self.Z, ellZ=self.ellZ, x=self.x, B=B,
+                                      trow=dict(Pt=self.P[0], Tt=self.T[0], v=self.v, zt=self.noise[M:M + B],
+                                                hyp_t=hyp_addr(0), ellX=self.ellX, var_t=self.var_t))
         # F14: quadratic-form factors W = P L on the rows that use them
         d14 = []
         for d in range(D):
@@ -895,6 +915,9 @@ class DsviEngine:
             chol_main, chol_g = chol_prior(0, 3, v_too=True), chol_prior(3, 1)
         else:
             chol_main, chol_g = chol(FV, 4), chol(NF + 3, 1)
+        fuse = self.fuse_tp
+        if fuse:
+            chol_main, chol_g = p["chol_tp_main"], p["chol_tp_G"]
 
         kf0, kf1 = p["kl_range"]
         need_side = (not elbo_mode) or (with_kl and kf1 > kf0)
@@ -924,7 +947,8 @@ class DsviEngine:
         if self.p64:
             steps += [("conv_in", "convert", conv_in, "main"),
                       ("build_rbf64", "pairwise", pw64("build_rbf64"), "main")]
-        steps.append(("build_rbf", "pairwise", pw("build_rbf"), "main"))
+        if not fuse:
+            steps.append(("build_rbf", "pairwise", pw("build_rbf"), "main"))
         steps.append(("wait", "main", "syrk") if v_on_side else ("syrk", "gemm", gemm("syrk"), "main"))
         # forward chain: chol -> v -> K_G22 -> chol_G -> invG -> projG.  The t-prior projections, the
         # t-row (ell_X) and K_G12 run on the second side stream beside v / K_G22 / chol_G: they are
@@ -940,39 +964,55 @@ class DsviEngine:
             steps += [("inv3_64", "gemm", gemm("inv3_64"), "side2"),
                       ("proj3_64", "gemm", gemm("proj3_64"), "side2"),
                       ("conv3", "convert", round_back(0, 3), "side2")]
-        if p["inv3"] is not None:
-            steps.append(("inv3", "gemm", gemm("inv3"), "side2"))
-        steps += [
-            ("proj3", "gemm", gemm("proj3"), "side2"),
-            ("build_g22", "pairwise", (pw64 if self.p64 else pw)("build_g22"), "main"),
-            ("wait", "side2", "v"),
-            ("trow", "row", row(getattr(lib, "nmgp_dsvi_trow_" + self.sfx)), "side2"),
-        ]
-        if self.p64:
-            steps.append(("conv_ellX", "convert", widen(self.ellX, self.ellX64, self.B), "side2"))
-        steps.append(("build_g12", "pairwise", pw("build_g12"), "side2"))
-        if self.p64:
-            steps.append(("build_g12_64", "pairwise", pw64("build_g12_64"), "side2"))
-        steps.append(("sig", "side2", "g12"))
-        if not elbo_mode:
-            # the pair factors W_P = P_{0,1} L_ij need only the L0 / L1 projections: beside the Gibbs chain
-            steps += [("quad_P", "gemm", gemm("quad_P"), "side2"), ("sig", "side2", "quadP")]
-        steps += [
-            ("chol_G", "chol", chol_g, "main"),
-            ("wait", "main", "g12"),
-        ]
-        if self.p64:
-            steps += [("invG_64", "gemm", gemm("invG_64"), "main"),
-                      ("projG_64", "gemm", gemm("projG_64"), "main"),
-                      ("convG", "convert", round_back(3, 1), "main")]
+        if fuse:
+            # fused priors: T / P of t, L0, L1 came with their factorization; side2 runs the pair factors W_P first
+            # (recon waits for them), then the prior inverses and Y = A^-1 mu (KL and backward only); the Gibbs
+            # prior's launch on the main stream forms the t-row, K_G12, T_G and P_G itself
+            if not elbo_mode:
+                steps += [("quad_P", "gemm", gemm("quad_P"), "side2"), ("sig", "side2", "quadP")]
+            steps += [("inv3", "gemm", gemm("inv3"), "side2"), ("proj3", "gemm", gemm("proj3"), "side2"),
+                      ("chol_G", "chol", chol_g, "main"), ("sig", "main", "cholG")]
         else:
-            steps.append(("invG", "gemm", gemm("invG"), "main"))
-        steps.append(("projG", "gemm", gemm("projG"), "main"))
+            if p["inv3"] is not None:
+                steps.append(("inv3", "gemm", gemm("inv3"), "side2"))
+            steps += [
+                ("proj3", "gemm", gemm("proj3"), "side2"),
+                ("build_g22", "pairwise", (pw64 if self.p64 else pw)("build_g22"), "main"),
+                ("wait", "side2", "v"),
+                ("trow", "row", row(getattr(lib, "nmgp_dsvi_trow_" + self.sfx)), "side2"),
+            ]
+            if self.p64:
+                steps.append(("conv_ellX", "convert", widen(self.ellX, self.ellX64, self.B), "side2"))
+            steps.append(("build_g12", "pairwise", pw("build_g12"), "side2"))
+            if self.p64:
+                steps.append(("build_g12_64", "pairwise", pw64("build_g12_64"), "side2"))
+            steps.append(("sig", "side2", "g12"))
+            if not elbo_mode:
+                # the pair factors W_P = P_{0,1} L_ij need only the L0 / L1 projections: beside the Gibbs chain
+                steps += [("quad_P", "gemm", gemm("quad_P"), "side2"), ("sig", "side2", "quadP")]
+            steps += [
+                ("chol_G", "chol", chol_g, "main"),
+                ("wait", "main", "g12"),
+            ]
+            if self.p64:
+                steps += [("invG_64", "gemm", gemm("invG_64"), "main"),
+                          ("projG_64", "gemm", gemm("projG_64"), "main"),
+                          ("convG", "convert", round_back(3, 1), "main")]
+            else:
+                steps.append(("invG", "gemm", gemm("invG"), "main"))
+            steps.append(("projG", "gemm", gemm("projG"), "main"))
+        # fused: A_G^-1 and Y_G = A_G^-1 mu_W (KL_W, R_G) on side2 after the Gibbs launch, captured after the main
+        # stream's next launch so that the chain's child keeps the hardware queue
+        invG_side = [("wait", "side2", "cholG"), ("invG", "gemm", gemm("invG"), "side2"),
+                     ("projG", "gemm", gemm("projG"), "side2"), ("sig", "side2", "kl_in")] if fuse else []
         if elbo_mode:
             steps.append(("quad", "gemm", gemm("quad"), "main"))
+            steps += invG_side
             if need_side:
                 steps += [("sig", "side", "join"), ("wait", "main", "join")]
             if with_kl:
+                if fuse:
+                    steps.append(("wait", "main", "kl_in"))
                 steps.append(("kl", "row", row(getattr(lib, "nmgp_dsvi_kl_" + self.sfx)), "main"))
             steps += [("recon", "row", row(getattr(lib, "nmgp_dsvi_recon_" + self.sfx)), "main"),
                       ("finalize", "row", row(getattr(lib, "nmgp_dsvi_finalize_" + self.sfx)), "main")]
@@ -991,11 +1031,13 @@ class DsviEngine:
         # KL terms, prior-diagonal adjoints, the variational factors' KL L-bar (first writer of those
         # gradient rows -- bwd_lbar follows it on the same stream, so the accumulation order is fixed) and the
         # KL part of the prior adjoints Abar (the main stream waits for it before R_G is signalled)
-        steps.append(("sig", "main", "kl_in"))
+        if not fuse:
+            steps.append(("sig", "main", "kl_in"))
         if pre_planned:
             steps.append(("wait", "main", "plans"))
+        steps.append(("quad_W", "gemm", gemm("quad_W"), "main"))
+        steps += invG_side
         steps += [
-            ("quad_W", "gemm", gemm("quad_W"), "main"),
             ("wait", "side", "kl_in"),
             ("kl", "row", row(getattr(lib, "nmgp_dsvi_kl_" + self.sfx)), "side"),
             ("delta", "row", row(getattr(lib, "nmgp_dsvi_delta_" + self.sfx)), "side"),
@@ -1016,6 +1058,10 @@ class DsviEngine:
             ("sig", "main", "recon"),
             ("bwd_wG", "gemm", gemm("bwd_wG"), "main"),
             ("bwd_wGr", "row", pbar_reduce, "main"),
+        ]
+        if fuse:
+            steps.append(("wait", "main", "kl_in"))      # R_G = P-bar_G A_G^-1 (side2's invG, long done)
+        steps += [
             ("bwd_R", "gemm", gemm("bwd_R"), "main"),
             # L-bar / mu-bar gradient rows: after the KL L-bar (their first writer, same stream) and recon.
             ("wait", "side", "recon"),

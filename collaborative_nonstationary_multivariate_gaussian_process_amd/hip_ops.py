@@ -511,6 +511,47 @@ def chol_inv_(A, out=None, info=None, ws=None):
     return out, info
 
 
+def _ptr(t):
+    """Device address of a tensor (its data_ptr), an int address, or 0 for None."""
+    if t is None:
+        return 0
+    return int(t) if isinstance(t, int) else t.data_ptr()
+
+
+class CholTp:
+    """The fused GP-prior launch (nmgp_chol_tp_f64, fp64, 128 <= n <= 256): `batch` n x n slots of A (stride n*n,
+    from A's first element) factored in place with X <- L^-1 and info as chol_inv_, where mats[b] may
+      - build its K22 + jitter I in the launch ("build": 1 RBF from Z and hyp = (log s2, log ls) at that address,
+        2 Gibbs from Z and ellZ) instead of reading it from A, and
+      - form its minibatch products in the same launch ("rows": 1 RBF K12 rows from x, 2 the t-row sample -- ell_X,
+        var_t from trow = dict(Pt, Tt, v, zt, hyp_t, ellX, var_t) -- then Gibbs K12 rows): K12, T = K12 L^-T and
+        P = T L^-1 written to the (B, n) tensors mats[b]["K12" / "T" / "P"].
+    The argument struct is built once; a call is one launch (graph-capturable)."""
+
+    def __init__(self, A, X, info, n, mats, *, jitter=0.0, Z=None, ellZ=None, x=None, B=0, trow=None):
+        for t_, nm in ((A, "A"), (X, "X"), (info, "info")):
+            L.require_device(t_, nm)
+        assert A.dtype == torch.float64 and X.dtype == torch.float64 and 1 <= len(mats) <= 4
+        a = L.CholTpArgs()
+        a.A, a.n, a.lda, a.strideA = A.data_ptr(), n, n, n * n
+        a.X, a.ldx, a.strideX, a.batch = X.data_ptr(), n, n * n, len(mats)
+        a.info, a.jitter = info.data_ptr(), float(jitter)
+        a.Z, a.ellZ, a.x, a.B = _ptr(Z), _ptr(ellZ), _ptr(x), int(B)
+        tr = trow or {}
+        for k in ("Pt", "Tt", "v", "zt", "hyp_t", "ellX", "var_t"):
+            setattr(a, k, _ptr(tr.get(k)))
+        for b, m in enumerate(mats):
+            mt = a.mats[b]
+            mt.build, mt.rows = int(m.get("build", 0)), int(m.get("rows", 0))
+            mt.hyp, mt.K12, mt.T, mt.P = (_ptr(m.get(k)) for k in ("hyp", "K12", "T", "P"))
+        self.a = a
+        self._keep = (A, X, info, Z, ellZ, x, tr, mats)     # the struct holds raw addresses of these
+
+    def __call__(self, stream=None):
+        s = stream if stream is not None else L.stream_handle()
+        L.check(L.lib().nmgp_chol_tp_f64(ctypes.byref(self.a), s), "chol_tp")
+
+
 class BigBatch:
     """`batch` same-shape f32 products at per-problem element offsets on the 128x128 MFMA kernel
     (nmgp_gemm_big_offsets_epi_f32): C_b = alpha op(A_b) op(B_b) + beta C_b (+ diag_add on the diagonal)

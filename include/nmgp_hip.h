@@ -45,6 +45,7 @@ int64_t nmgp_sizeof_pairwise_desc(void);
 int64_t nmgp_sizeof_pairwise_bwd_desc(void);
 int64_t nmgp_sizeof_dsvi_args(void);
 int64_t nmgp_sizeof_pair_desc(void);
+int64_t nmgp_sizeof_chol_tp_args(void);
 
 /* ------------------------------------------------------------------ grouped GEMM (MFMA)
  * C(i,j) = alpha * sum_k op(A)(i,k) * s(k) * op(B)(k,j) + beta*C(i,j) + gamma*rs(i)*E(i,j)
@@ -173,6 +174,54 @@ int64_t nmgp_chol_inv_workspace_size_f32(int64_t n, int64_t batch);
 int nmgp_chol_inv_batched_ws_f32(float* A, int64_t n, int64_t lda, int64_t strideA, float* X, int64_t ldx,
                                  int64_t strideX, int64_t batch, int32_t* info, void* ws, int64_t ws_bytes,
                                  hipStream_t stream);
+
+/* Fused GP-prior launch (round 6): up to 4 prior matrices of one DSVI step factored and inverted as
+ * nmgp_chol_inv_batched_f64 does (A <- L, X <- L^-1, info), optionally
+ *   - with K22 + jitter I BUILT by the factor / update workgroups instead of read from A (build 1: RBF
+ *     s2 exp(-(z_i/ls - z_j/ls)^2 / 2) from Z and hyp = (log s2, log ls), code/utils.py:91-94; build 2:
+ *     Gibbs sqrt(2 l_i l_j / (l_i^2 + l_j^2)) exp(-(z_i - z_j)^2 / (l_i^2 + l_j^2)) from Z and ellZ,
+ *     code/utils.py:97-103), and
+ *   - with the prior's minibatch products formed by extra workgroups of the same launch while the
+ *     factorization runs (rows 1: K12 = RBF(x, Z) rows; rows 2: first the t-row sample of JGP_S --
+ *     ell_X = exp(P_t v + z_t sqrt(s2_t - ||T_t row||^2 + jitter)), code/utils.py:216-237 -- then
+ *     K12 = Gibbs(x, Z, ell_X, ellZ) rows): K12 (written out), T = K12 L^-T (right-looking, from the
+ *     published block columns of L) and P = T L^-1 = K12 (K22 + jitter I)^-1 (from the published rows
+ *     of X) -- the projections torch.solve forms in code/utils.py:117-120, 140-146, 228-232.
+ * 128 <= n <= 256, 1 <= batch <= 4, B <= 4096; every output of row stride n.  The mats with rows != 0
+ * need K12 / T / P; rows 2 needs Pt, Tt (B x n, the t prior's P and T), v, zt, hyp_t (log s2_t), ellX,
+ * var_t (B outputs) and ellZ.                                                                    */
+typedef struct nmgp_chol_tp_mat {
+  int32_t build;      /* 0: read A; 1: RBF K22; 2: Gibbs K22 (diagonal + jitter) */
+  int32_t rows;       /* 0: no minibatch products; 1: RBF K12 rows; 2: t-row + Gibbs K12 rows */
+  const double* hyp;  /* build / rows 1: (log sigma2, log lengthscale) */
+  double* K12;        /* B x n */
+  double* T;          /* B x n */
+  double* P;          /* B x n */
+} nmgp_chol_tp_mat;
+typedef struct nmgp_chol_tp_args {
+  double* A;
+  int64_t n, lda, strideA;
+  double* X;
+  int64_t ldx, strideX, batch;
+  int32_t* info;
+  double jitter;
+  const double* Z;     /* n inducing inputs */
+  const double* ellZ;  /* n Gibbs length scales (build 2 / rows 2) */
+  const double* x;     /* B minibatch inputs */
+  int64_t B;
+  const double* Pt;    /* rows 2: the t prior's P and T (B x n), the v sample (n), z_t (B), log s2_t */
+  const double* Tt;
+  const double* v;
+  const double* zt;
+  const double* hyp_t;
+  double* ellX;        /* rows 2 outputs (B) */
+  double* var_t;
+  nmgp_chol_tp_mat mats[4];
+} nmgp_chol_tp_args;
+int nmgp_chol_tp_f64(const nmgp_chol_tp_args* args, hipStream_t stream);
+/* diagnostics (synchronous): the launch's per-workgroup phase stamps, recorded when NMGP_TP_DBG has bit 16 set
+ * (8 x 64-bit wall-clock words per workgroup, tools/chol_tp_probe.py)                                  */
+int nmgp_chol_tp_trace(uint64_t* out, int64_t n);
 
 /* Single large SPD matrix (the M=4096 stress configuration, BASELINE.json configs[4]): blocked
  * right-looking Cholesky, A <- L in place (strictly upper part zeroed), info as potrf (first

@@ -543,3 +543,48 @@ def test_step_is_deterministic_run_to_run(case):
         outs.append((eng.out.clone().cpu(), grad.clone().cpu()))
     for o, gr in outs[1:]:
         assert torch.equal(o[:1], outs[0][0][:1]) and torch.equal(gr, outs[0][1])
+
+
+@pytest.mark.parametrize("sizes", [None, [120, 0, 95, 1, 64]])
+def test_fused_prior_launches_match_separate_launches(monkeypatch, sizes):
+    """Round 6: at M = 256 fp64 the engine runs the GP priors as two fused launches (nmgp_chol_tp_f64: builders,
+    factor + inverse, T = K12 L^-T, P = T L^-1 and the t-row in the launch).  Same step with NMGP_FUSE_TP=0 (the
+    separate builder / invG / projG / t-row launches): loss, every gradient and the projections agree to rounding
+    (T / P by substitution instead of explicit-inverse products), on the golden PM2.5 minibatch and a ragged one
+    with empty outputs (B = 280: a partial last row workgroup)."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.engine import DsviEngine
+    g = G.load("pm25_forward")
+    D, M = 5, 256
+    p = G.params(g, D=D, M=M)
+    theta = torch.cat([p[k].reshape(-1) for k in O.PARAM_NAMES]).to("cuda")
+    if sizes is None:
+        x, y, sz, noise = g["x"], g["y"], [int(s) for s in g["sizes"]], g["noise"]
+    else:
+        rng = np.random.default_rng(5)
+        sz = sizes
+        B = sum(sz)
+        x, y = np.sort(rng.random(B)), rng.standard_normal(B)
+        Q = D * (D + 1) // 2
+        noise = rng.standard_normal(M + B + Q * B)
+    B = sum(sz)
+    res = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("NMGP_FUSE_TP", fuse)
+        eng = DsviEngine(D, M, B, g["z"])
+        assert eng.fuse_tp == (fuse == "1")
+        grad = torch.zeros_like(theta)
+        eng.bind(theta, grad, frozen_mask=0, N=float(g["N"]))
+        eng.load_batch(x, y, sz, noise=noise)
+        eng.forward_backward()
+        torch.cuda.synchronize()
+        eng.check_info()
+        res[fuse] = (float(eng.out[0]), grad.clone(), eng.T.clone(), eng.P.clone(), eng.K12.clone(), eng.ellX.clone())
+    (l1, g1, T1, P1, K1, e1), (l0, g0, T0, P0, K0, e0) = res["1"], res["0"]
+    print(f"FUSED-TP sizes={sizes}: loss {abs(l1 - l0) / abs(l0):.2e} grad {_rel(g1, g0):.2e} T {_rel(T1, T0):.2e} "
+          f"P {_rel(P1, P0):.2e} K12 {_rel(K1, K0):.2e} ellX {_rel(e1, e0):.2e}")
+    # the separate launches' explicit-inverse products carry ~20x the fused substitution's error against exact
+    # triangular solves (tests/test_gpu_primitives.py::test_chol_tp_fused_priors_vs_torch: P 3e-9 vs 1.5e-10 at
+    # cond ~1e6); ell_X (P_t v) and K_G12 inherit that difference, the RBF K12 rows are the same arithmetic
+    assert abs(l1 - l0) / abs(l0) < 5e-11 and _rel(g1, g0) < 1e-8
+    assert _rel(K1[:3], K0[:3]) < 1e-14 and _rel(K1[3], K0[3]) < 1e-8 and _rel(e1, e0) < 1e-8
+    assert _rel(T1, T0) < 1e-8 and _rel(P1, P0) < 1e-7

@@ -712,6 +712,122 @@ def test_gemm_big_persistent_multi_item_walk(ops):
         assert rel(s_all[b].cpu()[lo], ref[lo]) < 2e-6 and torch.all(s_all[b].cpu()[~lo] == 5.0)
 
 
+def _rbf(a, b, s2, ls):
+    return s2 * torch.exp(-0.5 * (a[:, None] / ls - b[None, :] / ls) ** 2)
+
+
+def _gibbs(a, b, la, lb):
+    S = la[:, None] ** 2 + lb[None, :] ** 2
+    return torch.sqrt(2 * la[:, None] * lb[None, :] / S) * torch.exp(-(a[:, None] - b[None, :]) ** 2 / S)
+
+
+@pytest.mark.parametrize("n,B", [(256, 2000), (256, 1), (200, 130), (144, 64), (128, 63)])
+def test_chol_tp_fused_priors_vs_torch(ops, n, B):
+    """Round 6: nmgp_chol_tp_f64 -- [Sigma (read) | three RBF priors (built)] factored + inverted, the priors' K12 /
+    T = K12 L^-T / P = T L^-1 formed by the launch's row workgroups; then a Gibbs prior (built from ellZ) whose row
+    workgroups first draw the t-row ell_X.  Against fp64 torch on the same inputs, and T / P against the products of
+    the launch's own L^-1 (the unfused schedule's arithmetic, tight)."""
+    g = torch.Generator().manual_seed(n + B)
+    jit = 1e-4
+    Z = torch.linspace(0, 1, n, dtype=F64)
+    x = torch.rand(B, generator=g, dtype=F64)
+    hyp = torch.tensor([0.3, -1.2, -0.2, -0.9, 0.1, -1.5], dtype=F64)
+    S = torch.tril(0.1 * torch.randn(n, n, generator=g, dtype=F64))
+    A = torch.zeros(4, n, n, dtype=F64)
+    A[0] = S @ S.t() + jit * torch.eye(n, dtype=F64)
+    Ad, Xd = A.to(DEV), torch.zeros(4, n, n, dtype=F64, device=DEV)
+    info = torch.full((4,), 7, dtype=torch.int32, device=DEV)
+    K12, T, P = (torch.zeros(3, B, n, dtype=F64, device=DEV) for _ in range(3))
+    hd, Zd, xd = hyp.to(DEV), Z.to(DEV), x.to(DEV)
+    mats = [dict()] + [dict(build=1, rows=1, hyp=hd[2 * k:], K12=K12[k], T=T[k], P=P[k]) for k in range(3)]
+    ops.CholTp(Ad[0], Xd[0], info, n, mats, jitter=jit, Z=Zd, x=xd, B=B)()
+    torch.cuda.synchronize()
+    assert info.cpu().tolist() == [0, 0, 0, 0]
+    up = torch.triu(torch.ones(n, n, dtype=torch.bool), 1)
+    Lr = torch.linalg.cholesky(A[0])
+    assert rel(Ad[0], Lr) < 1e-12 and rel(Xd[0], torch.linalg.inv(Lr)) < 1e-9
+    for k in range(3):
+        s2, ls = float(torch.exp(hyp[2 * k])), float(torch.exp(hyp[2 * k + 1]))
+        K22 = _rbf(Z, Z, s2, ls) + jit * torch.eye(n, dtype=F64)
+        Kx = _rbf(x, Z, s2, ls)
+        Lk = torch.linalg.cholesky(K22)
+        L_, X_ = Ad[k + 1].cpu(), Xd[k + 1].cpu()
+        assert rel(L_, Lk) < 1e-11 and torch.all(L_[up] == 0) and torch.all(X_[up] == 0)
+        assert rel(K12[k], Kx) < 1e-14
+        _check_tp(T[k], P[k], Kx, Lk, X_, f"rbf{k}")
+    # the Gibbs prior: t-row (ell_X) and K_G12 rows in the launch
+    v = -1.5 + 0.3 * torch.randn(n, generator=g, dtype=F64)
+    ellZ = torch.exp(v)
+    Ptd = (0.02 * torch.randn(B, n, generator=g, dtype=F64)).to(DEV)
+    Ttd = (0.02 * torch.randn(B, n, generator=g, dtype=F64)).to(DEV)
+    zt = torch.randn(B, generator=g, dtype=F64)
+    ht = torch.tensor([0.2], dtype=F64)
+    AG, XG = torch.zeros(n, n, dtype=F64, device=DEV), torch.zeros(n, n, dtype=F64, device=DEV)
+    infoG = torch.full((1,), 7, dtype=torch.int32, device=DEV)
+    KG, TG, PG = (torch.zeros(B, n, dtype=F64, device=DEV) for _ in range(3))
+    ellX, var_t = torch.zeros(B, dtype=F64, device=DEV), torch.zeros(B, dtype=F64, device=DEV)
+    ops.CholTp(AG, XG, infoG, n, [dict(build=2, rows=2, K12=KG, T=TG, P=PG)], jitter=jit, Z=Zd, ellZ=ellZ.to(DEV),
+               x=xd, B=B, trow=dict(Pt=Ptd, Tt=Ttd, v=v.to(DEV), zt=zt.to(DEV), hyp_t=ht.to(DEV), ellX=ellX,
+                                    var_t=var_t))()
+    torch.cuda.synchronize()
+    assert int(infoG.item()) == 0
+    var = float(torch.exp(ht)) - (Ttd.cpu() ** 2).sum(1)
+    lx = torch.exp(Ptd.cpu() @ v + zt * torch.sqrt(var + jit))
+    assert rel(var_t, var) < 1e-14 and rel(ellX, lx) < 1e-13
+    K22 = _gibbs(Z, Z, ellZ, ellZ) + jit * torch.eye(n, dtype=F64)
+    Kx = _gibbs(x, Z, lx, ellZ)
+    LG = torch.linalg.cholesky(K22)
+    assert rel(AG, LG) < 1e-11 and rel(KG, Kx) < 1e-13
+    _check_tp(TG, PG, Kx, LG, XG.cpu(), "gibbs")
+    assert L_dev_status_clean()
+
+
+def _check_tp(T, P, Kx, Lk, X_, tag):
+    # T = Kx L^-T by substitution and P = T L^-1 against fp64 torch's triangular solves with torch's factor; the
+    # unfused schedule's explicit-inverse products (Kx X^T, Kx X^T X with this launch's X = L^-1) beside them: the
+    # fused launch must be at least about as accurate (both carry cond(K22) eps, ~1e6 eps here)
+    Tr = torch.linalg.solve_triangular(Lk, Kx.t(), upper=False).t()
+    Pr = torch.cholesky_solve(Kx.t(), Lk).t()
+    eT, eP = rel(T, Tr), rel(P, Pr)
+    xT, xP = rel(Kx @ X_.t(), Tr), rel(Kx @ X_.t() @ X_, Pr)
+    print(f"CHOL_TP {tag}: T err {eT:.2e} (explicit inverse {xT:.2e})  P err {eP:.2e} (explicit {xP:.2e})")
+    assert eT < max(3 * xT, 1e-13) and eP < max(3 * xP, 1e-12), (tag, eT, xT, eP, xP)
+    assert eT < 1e-9 and eP < 1e-6
+
+
+def L_dev_status_clean():
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L
+    return L.device_status(clear=True) == 0
+
+
+def test_chol_tp_not_pd_and_repeat(ops):
+    """A non-PD read matrix reports its column in info like chol_inv_, the built priors stay exact; the progress words
+    are re-armed, so the next launches on the same buffers (different B) agree bit for bit with a fresh one."""
+    n, jit = 256, 1e-4
+    Z = torch.linspace(0, 1, n, dtype=F64, device=DEV)
+    hyp = torch.tensor([0.0, -1.0], dtype=F64, device=DEV)
+    A = torch.zeros(2, n, n, dtype=F64, device=DEV)
+    A[0] = torch.eye(n, dtype=F64, device=DEV)
+    A[0, 100, 100] = -1.0
+    X = torch.zeros_like(A)
+    info = torch.zeros(2, dtype=torch.int32, device=DEV)
+    outs = []
+    for B in (500, 77, 500):
+        x = torch.linspace(0.01, 0.99, B, dtype=F64, device=DEV)
+        K12, T, P = (torch.zeros(B, n, dtype=F64, device=DEV) for _ in range(3))
+        A[0] = torch.eye(n, dtype=F64, device=DEV)
+        A[0, 100, 100] = -1.0
+        ops.CholTp(A[0], X[0], info, n, [dict(), dict(build=1, rows=1, hyp=hyp, K12=K12, T=T, P=P)], jitter=jit,
+                   Z=Z, x=x, B=B)()
+        torch.cuda.synchronize()
+        assert info.cpu().tolist() == [101, 0]
+        outs.append((A[1].clone(), X[1].clone(), T.clone(), P.clone()))
+    for a, b in zip(outs[0], outs[2]):
+        assert torch.equal(a, b)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])   # the prior: B-independent
+    assert L_dev_status_clean()
+
+
 def test_chol_inv_blocked_not_pd_reports_global_column(ops):
     A = _spd(400, 2, 9)
     bad = A.clone()
