@@ -73,7 +73,7 @@ class DsviArgs(ctypes.Structure):
 
 
 class CholTpMat(ctypes.Structure):
-    _fields_ = [("build", c_int), ("rows", c_int), ("hyp", c_vp), ("K12", c_vp), ("T", c_vp), ("P", c_vp)]
+    _fields_ = [("reserved", c_int), ("rows", c_int), ("hyp", c_vp), ("K12", c_vp), ("T", c_vp), ("P", c_vp)]
 
 
 class CholTpArgs(ctypes.Structure):
@@ -176,6 +176,8 @@ _SIGS = {
     "nmgp_kron_mv_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "nmgp_dsvi_hyper_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_hyper_f32": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_vg22_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
+    "nmgp_dsvi_vg22_f32": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_trow_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_trow_f32": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_dsvi_recon_f64": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),

@@ -597,16 +597,11 @@ template <typename T> __device__ inline unsigned long long* ctl_done(T* Xm, int 
 template <typename T> __device__ inline unsigned long long* ctl_xflag(T* Xm, int n, int par) {
   return (unsigned long long*)(Xm + (n - (4 + par) * kCtl<T>));
 }
-// ... and, for a built prior, the block columns 1..3 it built for the factor workgroup (par 0: 1 and 3, par 1: 2)
-template <typename T> __device__ inline unsigned long long* ctl_bflag(T* Xm, int n, int par) {
-  return (unsigned long long*)(Xm + (n - (6 + par) * kCtl<T>));
-}
 // the fused launch's extra words, cleared by the last of a matrix's readers
 template <typename T> __device__ inline void tp_clear_words(T* Xm, int n) {
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     __hip_atomic_store(ctl_xflag(Xm, n, q), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(ctl_bflag(Xm, n, q), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -619,30 +614,14 @@ template <typename T> __device__ inline void tp_clear_words(T* Xm, int n) {
 __device__ unsigned long long g_tp_trace[8 * 512];
 #define TP_STAMP(on, k) \
   if ((on) && threadIdx.x == 0 && blockIdx.x < 512) g_tp_trace[8 * blockIdx.x + (k)] = wall_clock64()
-struct TpBuild {
-  int mode;            // 0: read A, 1: RBF, 2: Gibbs
-  int trace;           // phase stamps (g_tp_trace)
-  double s2, jitter;
-  const double* uz;    // LDS: z_i / ls (RBF) or z_i (Gibbs), staged once per workgroup (tp_stage)
-  const double* ul;    // LDS: ell_Z (Gibbs)
-};
-__device__ inline double tp_k22(const TpBuild& b, int i, int j) {
-  double k;
-  const double dd = b.uz[i] - b.uz[j];     // = z_i / ls - z_j / ls, or z_i / 1 - z_j / 1, as pairwise_kernel
-  double r2 = 0;
-  r2 += dd * dd;
-  if (b.mode == 1) {
-    k = dexp(-0.5 * r2) * b.s2;
-  } else {
-    const double lx = b.ul[i], lz = b.ul[j];
-    const double S = lx * lx + lz * lz;
-    const double C = dsqrt(2.0 * (lx * lz) / S);
-    k = 1.0 * C * dexp(-r2 / S);
-  }
-  if (i == j) k += b.jitter;
-  return k;
+// Gibbs element from the squared distance and the two length scales: one division (1 / S) where pairwise_kernel
+// divides twice (<= 1 ulp apart); the exp / sqrt chains are long, so callers evaluate batches of independent
+// elements in straight-line code (no per-element branches) for the scheduler to interleave
+__device__ inline double tp_gibbs(double r2, double lx, double lz) {
+  const double iS = 1.0 / (lx * lx + lz * lz);
+  return dsqrt(2.0 * (lx * lz) * iS) * dexp(-r2 * iS);
 }
-// the per-index inputs of a built prior's elements, staged in LDS (one division per index instead of two per element)
+// the per-index inputs of the row workgroups' K12 elements, staged in LDS (one division per index, not per element)
 __device__ inline void tp_stage(double* uz, double* ul, int mode, const double* Z, const double* ellZ, double ls,
                                 int n) {
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
@@ -951,10 +930,10 @@ __device__ inline void tri_decode_par(int tp, int par, int& ib, int& jb) {
   }
 }
 
-template <typename T, int NTPW, int NCTL = 2, bool XPUB = false, bool BUILD = false>
+template <typename T, int NTPW, int NCTL = 2, bool XPUB = false>
 __device__ __attribute__((always_inline)) inline void chol3_trtri_role(T* Am, T* Xm, int n, int64_t lda,
                                                                        int64_t ldx, int par, unsigned char* smem_raw,
-                                                                       int nfin = 2, const TpBuild* bd = nullptr) {
+                                                                       int nfin = 2) {
   using acc_t = typename Mfma<T>::acc_t;
   const int nt = (n + 15) >> 4, NR = nt * 16;
   T* Ps = (T*)smem_raw + NR * CP;
@@ -987,25 +966,6 @@ __device__ __attribute__((always_inline)) inline void chol3_trtri_role(T* Am, T*
   // XPUB (the fused prior launch): X rows are stored write-through and, once drained, announced in xflag, so the
   // launch's row workgroups can read them while the factorization runs
   unsigned long long* xflag = ctl_xflag(Xm, n, par);
-  if (BUILD && bd->mode != 0) {
-    // a built prior: these workgroups wait for the first block column anyway, so they build block columns 1..3
-    // (par 0: 1 and 3, par 1: 2) into A write-through and announce each in bflag -- off the factor's serial chain
-    unsigned long long* bflag = ctl_bflag(Xm, n, par);
-    for (int c = 1 + par; c < 4 && c < nt; c += 2) {
-      const int ntc = nt - c;
-      for (int tl = w; tl < ntc; tl += RW) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int gr = (c + tl) * 16 + Mfma<T>::row(lane, r), gc = c * 16 + (lane & 15);
-          if (gr < n && gc < n) bstore_sc1<T>(rAm, (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)), (T)tp_k22(*bd, gr, gc));
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (t == 0) __hip_atomic_store(bflag, kFlagTag + (unsigned long long)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  if constexpr (BUILD) TP_STAMP(bd->trace, 2);
   // strictly upper part of X is zero (rows of this parity; the two control words stay)
   for (int i = 2 * w + par; i < n; i += 2 * RW)
     for (int j = ((i >> 4) + 1) * 16 + lane; j < n; j += 64) {
@@ -1110,7 +1070,6 @@ __device__ __attribute__((always_inline)) inline void chol3_trtri_role(T* Am, T*
     CHOL_STAMP1(kb, 3);
   }
   CHOL_STAMPX(2);
-  if constexpr (BUILD) TP_STAMP(bd->trace, 3);
   if constexpr (XPUB) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
@@ -1122,7 +1081,7 @@ __device__ __attribute__((always_inline)) inline void chol3_trtri_role(T* Am, T*
     const unsigned long long old = __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old == kDoneTag + (unsigned long long)(nfin - 1)) {
       __hip_atomic_store(flag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if constexpr (XPUB || BUILD) tp_clear_words(Xm, n);
+      if constexpr (XPUB) tp_clear_words(Xm, n);
       __hip_atomic_store(done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -1177,12 +1136,11 @@ __device__ __attribute__((always_inline)) inline bool poll_word(unsigned long lo
   return false;
 }
 
-template <typename T, bool BUILD = false>
+template <typename T>
 __device__ __attribute__((always_inline)) inline void chol7_factor_role(T* Am, T* Xm, int n, int64_t lda,
                                                                         int64_t ldx, int32_t* info, int col_off,
                                                                         int info_first, int mat,
-                                                                        unsigned char* smem_raw,
-                                                                        const TpBuild* bd = nullptr) {
+                                                                        unsigned char* smem_raw) {
   using acc_t = typename Mfma<T>::acc_t;
   const int nt = (n + 15) >> 4, NR = nt * 16;
   T* colbuf = (T*)smem_raw;            // NR x CP: block column k before its panel (local rows)
@@ -1197,9 +1155,7 @@ __device__ __attribute__((always_inline)) inline void chol7_factor_role(T* Am, T
   if (t == 0) __hip_atomic_store(hflag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   bool ok = true;
   acc_t acc[2];
-  // block column k's tiles (kb + w + RW u, kb): issue their loads (out-of-range ones read 0).  BUILD (the fused
-  // prior launch): block columns 0..3, which no update workgroup has touched, are built here from the prior's
-  // inputs instead
+  // block column k's tiles (kb + w + RW u, kb): issue their loads (out-of-range ones read 0)
   auto load_col = [&](int kb) {
     const int ntc = nt - kb;
 #pragma unroll
@@ -1214,25 +1170,7 @@ __device__ __attribute__((always_inline)) inline void chol7_factor_role(T* Am, T
     }
   };
   lds_barrier();
-  bool built0 = false;
-  if constexpr (BUILD) {
-    // a built prior (the fused launch): block column 0 is built here; columns 1..3 by the inverse workgroups, which
-    // are idle until column 0 is published (read below after their bflag)
-    if (bd->mode != 0) {
-      built0 = true;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int tl = w + RW * u;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int gr = tl * 16 + Mfma<T>::row(lane, r), gc = lane & 15;
-          acc[u][r] = (tl < nt && gr < n && gc < n) ? (T)tp_k22(*bd, gr, gc) : (T)0;
-        }
-      }
-    }
-  }
-  if (!built0) load_col(0);
-  if constexpr (BUILD) TP_STAMP(bd->trace, 2);
+  load_col(0);
   int first_fail = 0;
   for (int kb = 0; kb < nt; ++kb) {
     const int nrow = NR - kb * 16, ntc = nt - kb;
@@ -1279,11 +1217,6 @@ __device__ __attribute__((always_inline)) inline void chol7_factor_role(T* Am, T
       if (kb + 1 >= 4) {
         bool seen = true;
         if (lane == 0) seen = poll_word<T>(hflag, kb - 2, nt);
-        ok &= seen;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      } else if (BUILD && bd->mode != 0) {
-        bool seen = true;
-        if (lane == 0) seen = poll_word<T>(ctl_bflag(Xm, n, (kb + 1) == 2 ? 1 : 0), kb + 1, nt);
         ok &= seen;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
@@ -1355,7 +1288,6 @@ __device__ __attribute__((always_inline)) inline void chol7_factor_role(T* Am, T
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_barrier();
-  if constexpr (BUILD) TP_STAMP(bd->trace, 3);
   if (t == 0) {
     __hip_atomic_store(flag, kFlagTag + (unsigned long long)nt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(hflag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // no reader left
@@ -1367,10 +1299,9 @@ __device__ __attribute__((always_inline)) inline void chol7_factor_role(T* Am, T
   if (lane == 0 && !ok) spin_gave_up(NMGP_STATUS_CHOL_SPIN);
 }
 
-template <typename T, int NTPW, bool BUILD = false>
+template <typename T, int NTPW>
 __device__ __attribute__((always_inline)) inline void chol7_update_role(T* Am, T* Xm, int n, int64_t lda,
-                                                                        unsigned char* smem_raw,
-                                                                        const TpBuild* bd = nullptr) {
+                                                                        unsigned char* smem_raw) {
   using acc_t = typename Mfma<T>::acc_t;
   const int nt = (n + 15) >> 4, NR = nt * 16;
   T* Ps = (T*)smem_raw;                // NR x CP: L[:, j] (local rows)
@@ -1396,19 +1327,13 @@ __device__ __attribute__((always_inline)) inline void chol7_update_role(T* Am, T
   }
 #define IB7(u) (tij[u] < 0 ? -1 : (tij[u] >> 8))
 #define JB7(u) (tij[u] < 0 ? -1 : (tij[u] & 255))
-  bool build = false;
-  if constexpr (BUILD) build = bd->mode != 0;     // the fused prior launch: the tiles are built, not read
 #pragma unroll
   for (int u = 0; u < NTPW; ++u) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int gr = IB7(u) * 16 + Mfma<T>::row(lane, r), gc = JB7(u) * 16 + (lane & 15);
       const bool in = IB7(u) >= 0 && gr < n && gc < n;
-      if (build) {
-        if constexpr (BUILD) acc[u][r] = in ? (T)tp_k22(*bd, gr, gc) : (T)0;
-      } else {
-        acc[u][r] = bload<T>(rAm, in ? (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)) : 0x80000000u);
-      }
+      acc[u][r] = bload<T>(rAm, in ? (uint32_t)(((int64_t)gr * lda + gc) * sizeof(T)) : 0x80000000u);
     }
   }
 #pragma unroll
@@ -1507,21 +1432,24 @@ __global__ __launch_bounds__(RW * 64) void chol_inv7_kernel(T* A, int n, int64_t
 // Fused prior launch (nmgp_chol_tp_f64, round 6).  The DSVI step's critical path ran
 //   RBF builders -> chol(v, t, L0, L1) -> v -> K_G22 builder -> chol(G) -> invG (T_G = K_G12 C_G^-T) ->
 //   projG (P_G = T_G C_G^-1) -> quad_W
-// with the t / L0 / L1 projections and the t-row on a side stream.  Here one launch per chol does all of it:
-//   - the four-role factorization of each matrix (chol_inv7_kernel's roles), its K22 + jitter I built by the
-//     factor and update workgroups (TpBuild) where it is a prior;
-//   - TPR-row workgroups per prior with minibatch products ("rows" workgroups, tp_rows_role), started in the same
-//     launch and fed by the factorization's own published data: block column kb of L and L_kk^-1 (the factor
-//     role's progress word) and block row kb of X = L^-1 (the inverse roles' xflag words, XPUB).  Each keeps
-//     R = its rows of K12 (built in registers, written out once) in MFMA accumulators and runs the right-looking
-//     triangular solve T = K12 L^-T one block column behind the factor: T(:, kb) = R(:, kb) L_kk^-T, then
-//     R(:, cb) -= T(:, kb) L(cb, kb)^T for cb > kb; and accumulates P = T X one block row behind the inverse
-//     workgroups: P(:, cb) += T(:, kb) X(kb, cb), cb <= kb.  rows 2 first forms the rows' t-row sample
-//     ell_X (dsvi_trow_kernel's arithmetic) and builds Gibbs K12 rows from it.
-// The launch ends (nearly) when the factorization does, and the step loses the builder, invG / projG launches and
-// their graph hand-offs.  Role workgroups come first in the grid (in-order dispatch per XCD), rows workgroups
-// only wait on them, never the reverse; the last of a matrix's readers re-arms its progress words.
-constexpr int TPR = 64;   // minibatch rows per rows workgroup
+// with the t / L0 / L1 projections, the t-row and K_G12 on a side stream.  Here each chol launch carries, besides
+// the four-role factorization of each matrix (chol_inv7_kernel's roles), TPR-row workgroups per prior with
+// minibatch products ("rows" workgroups, tp_rows_role), fed by the factorization's own published data: block
+// column kb of L and L_kk^-1 (the factor role's progress word) and block row kb of X = L^-1 (the inverse roles'
+// xflag words, XPUB).  Each keeps R = its rows of K12 (built in registers, written out once) in MFMA accumulators
+// and runs the right-looking triangular solve T = K12 L^-T one block column behind the factor:
+// T(:, kb) = R(:, kb) L_kk^-T, then R(:, cb) -= T(:, kb) L(cb, kb)^T for cb > kb; and accumulates P = T X two
+// block rows behind the inverse workgroups: P(:, cb) += T(:, kb) X(kb, cb), cb <= kb.  rows 2 first forms the
+// rows' t-row sample ell_X (dsvi_trow_kernel's arithmetic) and builds Gibbs K12 rows from it.  (K22 is built
+// outside: fp64 exp / sqrt / division chains on the few role workgroups cost 9-20 us per launch, measured.)
+// The step loses the invG / projG products, the t-row and K12 builders and their graph hand-offs; T and P come out
+// more accurate than the explicit-inverse products (substitution).  Role workgroups come first in the grid
+// (in-order dispatch per XCD); rows workgroups only wait on them, never the reverse; the last of a matrix's
+// readers re-arms its progress words.
+constexpr int TPR = 32;             // minibatch rows per rows workgroup
+constexpr int RB = TPR / 16;        // its row blocks
+constexpr int CG = RW / RB;         // column groups of its waves (wave w: row block w % RB, columns w / RB + CG u)
+constexpr int NU = 16 / CG;         // R / P tiles per wave (n <= 256)
 // LDS below the staged per-index inputs: the roles' layout (chol_inv7_kernel's, with the third L buffer) or the row
 // workgroups' (NR CP + 16 CP + 4 TPR CP + 16 * 257 + TPR doubles), whichever is larger
 __host__ __device__ constexpr size_t chol_tp_roles_bytes(int n) {
@@ -1549,8 +1477,8 @@ struct TpDev {
   const double* hyp_t;
   double* ellX;
   double* var_t;
-  int build[4], rows[4], tpm[4];
-  int dbg;   // PROBE ONLY (NMGP_TP_DBG): 1 factor role reads A instead of building, 2 update role reads A
+  int rows[4], tpm[4];
+  int dbg;   // NMGP_TP_DBG bit 16: phase stamps (tools/chol_tp_probe.py)
   const double* hyp[4];
   double* K12[4];
   double* Tm[4];
@@ -1587,40 +1515,57 @@ __device__ __attribute__((always_inline)) inline void tp_rows_role(const TpDev& 
   double* Tg = a.Tm[m];
   double* Pg = a.Pm[m];
 
-  // 1. rows 2: the t-row sample of each row (JGP_S, code/utils.py:226-235), dsvi_trow_kernel's arithmetic
+  // 1. rows 2: the t-row sample of each row (JGP_S, code/utils.py:226-235), dsvi_trow_kernel's arithmetic; wave w
+  //    takes rows w, w + 8, ... with all of their loads in flight together
   if (mode == 2) {
     const double s2t = dexp(a.hyp_t[0]);
-    for (int i = w; i < TPR; i += RW) {
-      const int r = r0 + i;
-      double lx = 1.0;
-      if (r < B) {
-        const double* Pr = a.Pt + (int64_t)r * n;
-        const double* Tr = a.Tt + (int64_t)r * n;
-        double mean = 0, q = 0;
-        for (int c = lane; c < n; c += 64) {
-          mean += Pr[c] * a.v[c];
-          const double tt = Tr[c];
-          q += (double)(tt * tt);
+    constexpr int RPW = TPR / RW;          // rows per wave
+    constexpr int CPL = 256 / 64;          // columns per lane (n <= 256)
+    double pv[RPW][CPL], tv[RPW][CPL], vv[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) vv[c] = (lane + 64 * c < n) ? a.v[lane + 64 * c] : 0.0;
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const int r = min(r0 + w + RW * q, B - 1);
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const int col = min(lane + 64 * c, n - 1);
+        pv[q][c] = a.Pt[(int64_t)r * n + col];
+        tv[q][c] = a.Tt[(int64_t)r * n + col];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      double mean = 0, qq = 0;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        if (lane + 64 * c < n) {
+          mean += pv[q][c] * vv[c];
+          const double tt = tv[q][c];
+          qq += (double)(tt * tt);
         }
-        mean = wave_sum(mean);
-        q = wave_sum(q);
-        const double var = s2t - q;
-        const double tl = mean + a.zt[r] * dsqrt(var + a.jitter);
-        lx = dexp(tl);
-        if (lane == 0) {
+      }
+      mean = wave_sum(mean);
+      qq = wave_sum(qq);
+      const int i = w + RW * q, r = r0 + i;
+      const double var = s2t - qq;
+      const double lx = r < B ? dexp(mean + a.zt[r] * dsqrt(var + a.jitter)) : 1.0;
+      if (lane == 0) {
+        rowv[i] = lx;
+        if (r < B) {
           a.ellX[r] = lx;
           a.var_t[r] = var;
         }
       }
-      if (lane == 0) rowv[i] = lx;
     }
     __syncthreads();
   }
 
-  // 2. R = this workgroup's rows of K12, built in the accumulator layout (pairwise_kernel's arithmetic) and
-  //    written out.  Wave w owns the tiles (rb = w & 3, cb = (w >> 2) + 2u), u < 8, of R and of P.
-  const int rbw = w & 3, cpar = w >> 2;
-  acc_t R[8], P[8];
+  // 2. R = this workgroup's rows of K12, built in the accumulator layout (pairwise_kernel's arithmetic; Gibbs with
+  //    one division, tp_gibbs) and written out; straight-line, clamped indices, masked at the end.  Wave w owns the
+  //    tiles (rb = w % RB, cb = w / RB + CG u), u < NU, of R and of P.
+  const int rbw = w % RB, cgw = w / RB;
+  acc_t R[NU], P[NU];
   double s2 = 1.0, ls = 1.0;
   if (mode == 1) {
     s2 = dexp(a.hyp[m][0]);
@@ -1629,35 +1574,35 @@ __device__ __attribute__((always_inline)) inline void tp_rows_role(const TpDev& 
   double* uz = (double*)(smem_raw + chol_tp_roles_bytes(n));
   double* ul = uz + 256;
   tp_stage(uz, ul, mode, a.Z, a.ellZ, ls, n);
-  double xu[4];                      // x_i / ls (RBF) or x_i / 1 (Gibbs) of this lane's four rows
+  double xu[4], lxr[4];                 // x_i / ls (RBF) or x_i / 1 (Gibbs), ell_X of this lane's four rows
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int row = r0 + rbw * 16 + MF::row(lane, r);
-    xu[r] = row < B ? a.x[row] / ls : 0.0;
+    const int i = rbw * 16 + MF::row(lane, r);
+    xu[r] = a.x[min(r0 + i, B - 1)] / ls;
+    lxr[r] = mode == 2 ? rowv[i] : 1.0;
   }
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int cb = cpar + 2 * u;
+  for (int u = 0; u < NU; ++u) {
+    const int cb = cgw + CG * u;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int i = rbw * 16 + MF::row(lane, r), row = r0 + i, col = cb * 16 + (lane & 15);
-      double k = 0;
-      if (row < B && col < n) {
-        const double dd = xu[r] - uz[col];
-        double r2 = 0;
-        r2 += dd * dd;
-        if (mode == 1) {
-          k = dexp(-0.5 * r2) * s2;
-        } else {
-          const double lx = rowv[i], lz = ul[col];
-          const double S = lx * lx + lz * lz;
-          const double C = dsqrt(2.0 * (lx * lz) / S);
-          k = 1.0 * C * dexp(-r2 / S);
-        }
-        K12[(int64_t)row * n + col] = k;
-      }
-      R[u][r] = k;
+      const int col = min(cb * 16 + (lane & 15), n - 1);
+      const double dd = xu[r] - uz[col];
+      double r2 = 0;
+      r2 += dd * dd;
+      R[u][r] = mode == 1 ? dexp(-0.5 * r2) * s2 : tp_gibbs(r2, lxr[r], ul[col]);
       P[u][r] = 0;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int cb = cgw + CG * u;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = r0 + rbw * 16 + MF::row(lane, r), col = cb * 16 + (lane & 15);
+      const bool in = row < B && col < n;
+      R[u][r] = in ? R[u][r] : 0.0;
+      if (in) K12[(int64_t)row * n + col] = R[u][r];
     }
   }
 
@@ -1701,8 +1646,8 @@ __device__ __attribute__((always_inline)) inline void tp_rows_role(const TpDev& 
   auto p_update = [&](int pk) {    // P(:, cb) += T(:, pk) X(pk, cb), cb <= pk
     const double* Tp = Tc + (pk % 3) * TPR * CP;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int cb = cpar + 2 * u;
+    for (int u = 0; u < NU; ++u) {
+      const int cb = cgw + CG * u;
       if (cb <= pk) {
 #pragma unroll
         for (int s2 = 0; s2 < 4; ++s2) {
@@ -1745,10 +1690,10 @@ __device__ __attribute__((always_inline)) inline void tp_rows_role(const TpDev& 
       Li[r * CP + c] = li;
     }
     // R(:, kb) to LDS (its owner waves)
-    if (cpar == (kb & 1)) {
+    if (cgw == kb % CG) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (u == (kb >> 1)) {
+      for (int u = 0; u < NU; ++u)
+        if (u == kb / CG) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) Rs[(rbw * 16 + MF::row(lane, r)) * CP + (lane & 15)] = R[u][r];
         }
@@ -1760,9 +1705,9 @@ __device__ __attribute__((always_inline)) inline void tp_rows_role(const TpDev& 
     }
     if (kb > 0) store_x_row(xv, kb - 1);
     lds_barrier();
-    // T(:, kb) = R(:, kb) L_kk^-T (waves 0..3, one row block each) -> LDS and out
+    // T(:, kb) = R(:, kb) L_kk^-T (waves 0 .. RB-1, one row block each) -> LDS and out
     double* Tk = Tc + (kb % 3) * TPR * CP;
-    if (w < 4) {
+    if (w < RB) {
       acc_t tacc = {0, 0, 0, 0};
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2) {
@@ -1779,8 +1724,8 @@ __device__ __attribute__((always_inline)) inline void tp_rows_role(const TpDev& 
     lds_barrier();
     // R(:, cb) -= T(:, kb) L(cb, kb)^T, cb > kb
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int cb = cpar + 2 * u;
+    for (int u = 0; u < NU; ++u) {
+      const int cb = cgw + CG * u;
       if (cb > kb && cb < nt) {
 #pragma unroll
         for (int s2 = 0; s2 < 4; ++s2) {
@@ -1807,8 +1752,8 @@ __device__ __attribute__((always_inline)) inline void tp_rows_role(const TpDev& 
   lds_barrier();
   p_update(nt - 1);
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int cb = cpar + 2 * u;
+  for (int u = 0; u < NU; ++u) {
+    const int cb = cgw + CG * u;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = r0 + rbw * 16 + MF::row(lane, r), col = cb * 16 + (lane & 15);
@@ -1838,48 +1783,17 @@ __global__ __launch_bounds__(RW * 64) void chol_tp_kernel(TpDev a) {
     const int mat = blockIdx.x / 4, role = blockIdx.x - 4 * mat;
     double* Am = a.A + (int64_t)mat * a.strideA;
     double* Xm = a.X + (int64_t)mat * a.strideX;
-    TpBuild bd;
-    bd.mode = a.build[mat];
-    bd.trace = (a.dbg & 16) != 0;
-    bd.jitter = a.jitter;
-    bd.s2 = 1.0;
-    double ls = 1.0;
-    if (bd.mode == 1) {
-      bd.s2 = dexp(a.hyp[mat][0]);
-      ls = dexp(a.hyp[mat][1]);
-    }
-    double* uz = (double*)(smem_raw + chol_tp_roles_bytes(a.n));
-    double* ul = uz + 256;
-    bd.uz = uz;
-    bd.ul = ul;
-    if (bd.mode != 0) tp_stage(uz, ul, bd.mode, a.Z, a.ellZ, ls, a.n);
-    // compile-time role variants: a matrix that is read (Sigma_v) runs chol_inv7_kernel's roles; a built prior the
-    // BUILD roles, whose inverse workgroups publish X rows (XPUB) when the matrix has row workgroups
-    if (bd.mode == 0) {
-      if (role == 0) {
-        if (threadIdx.x == 0) __hip_atomic_store(ctl_done(Xm, a.n), kDoneTag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        chol7_factor_role<double>(Am, Xm, a.n, a.lda, a.ldx, a.info, 0, 1, mat, smem_raw);
-      } else if (role == 1) {
-        chol7_update_role<double, NTPWU>(Am, Xm, a.n, a.lda, smem_raw);
-      } else {
-        chol3_trtri_role<double, NTPW1, 5>(Am, Xm, a.n, a.lda, a.ldx, role - 2, smem_raw);
-      }
+    // a matrix without row workgroups runs chol_inv7_kernel's roles; with them, its inverse workgroups publish the
+    // X rows (XPUB) and count the row workgroups among the readers of its progress words
+    if (role == 0) {
+      if (threadIdx.x == 0) __hip_atomic_store(ctl_done(Xm, a.n), kDoneTag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      chol7_factor_role<double>(Am, Xm, a.n, a.lda, a.ldx, a.info, 0, 1, mat, smem_raw);
+    } else if (role == 1) {
+      chol7_update_role<double, NTPWU>(Am, Xm, a.n, a.lda, smem_raw);
+    } else if (a.rows[mat]) {
+      chol3_trtri_role<double, NTPW1, 5, true>(Am, Xm, a.n, a.lda, a.ldx, role - 2, smem_raw, 2 + a.nct);
     } else {
-      TpBuild b0 = bd;
-      b0.mode = 0;
-      if (role == 0) {
-        if (threadIdx.x == 0) __hip_atomic_store(ctl_done(Xm, a.n), kDoneTag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        chol7_factor_role<double, true>(Am, Xm, a.n, a.lda, a.ldx, a.info, 0, 1, mat, smem_raw,
-                                        (a.dbg & 1) ? &b0 : &bd);
-      } else if (role == 1) {
-        chol7_update_role<double, NTPWU, true>(Am, Xm, a.n, a.lda, smem_raw, (a.dbg & 2) ? &b0 : &bd);
-      } else if (a.rows[mat]) {
-        chol3_trtri_role<double, NTPW1, 7, true, true>(Am, Xm, a.n, a.lda, a.ldx, role - 2, smem_raw, 2 + a.nct,
-                                                       (a.dbg & 1) ? &b0 : &bd);
-      } else {
-        chol3_trtri_role<double, NTPW1, 7, false, true>(Am, Xm, a.n, a.lda, a.ldx, role - 2, smem_raw, 2,
-                                                        (a.dbg & 1) ? &b0 : &bd);
-      }
+      chol3_trtri_role<double, NTPW1, 5>(Am, Xm, a.n, a.lda, a.ldx, role - 2, smem_raw);
     }
   } else {
     const int c = blockIdx.x - nroles, k = c / a.nct;
@@ -1934,13 +1848,10 @@ static int chol_tp_launch(const nmgp_chol_tp_args* h, hipStream_t s) {
   a.var_t = g.var_t;
   for (int m = 0; m < a.batch; ++m) {
     const nmgp_chol_tp_mat& mt = g.mats[m];
-    if (mt.build < 0 || mt.build > 2 || mt.rows < 0 || mt.rows > 2) return -1;
-    if (mt.build == 1 && (!mt.hyp || !g.Z)) return -1;
-    if (mt.build == 2 && (!g.Z || !g.ellZ)) return -1;
+    if (mt.reserved != 0 || mt.rows < 0 || mt.rows > 2) return -1;
     if (mt.rows && (!mt.K12 || !mt.T || !mt.P || !g.x || !g.Z)) return -1;
     if (mt.rows == 1 && !mt.hyp) return -1;
     if (mt.rows == 2 && (!g.Pt || !g.Tt || !g.v || !g.zt || !g.hyp_t || !g.ellX || !g.var_t || !g.ellZ)) return -1;
-    a.build[m] = mt.build;
     a.rows[m] = g.B > 0 ? mt.rows : 0;
     a.hyp[m] = mt.hyp;
     a.K12[m] = mt.K12;

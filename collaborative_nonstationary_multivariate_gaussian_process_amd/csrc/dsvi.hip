@@ -145,6 +145,56 @@ __global__ __launch_bounds__(256) void dsvi_v_kernel(Args a) {
   }
 }
 
+// ------------------------------------------------------------------------------------ v + K_G22 (round 6)
+// The v sample and the Gibbs prior's K22 + jitter I in ONE wide launch (the fused-prior schedule, engine.py
+// fuse_tp): one workgroup per lower 16 x 16 tile (I, J) of K_G22 forms the v entries its rows and columns need --
+// dsvi_v_kernel's arithmetic per entry, v_c = mu_v[c] + sum_k L_v[c, k] z_v[k] (code/utils.py:226-227), ell_Z = exp(v)
+// -- then its 256 elements, one per thread, with pairwise_kernel's Gibbs arithmetic (code/utils.py:97-103).  The
+// diagonal tiles write v / ell_Z out.  Replaces the v launch + the 32-workgroup K_G22 builder (8 exp / sqrt /
+// division chains per thread) on the critical path.
+template <typename T>
+__global__ __launch_bounds__(256) void dsvi_vg22_kernel(Args a) {
+  __shared__ T vl[32];
+  const int M = a.M, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int I = (int)((sqrtf(8.0f * (float)blockIdx.x + 1.0f) - 1.0f) * 0.5f);
+  while ((I + 1) * (I + 2) / 2 <= (int)blockIdx.x) ++I;
+  while (I * (I + 1) / 2 > (int)blockIdx.x) --I;
+  const int J = (int)blockIdx.x - I * (I + 1) / 2;
+  const T* zv = (const T*)a.noise;
+  const T* Cv = (const T*)a.Afac + (int64_t)(a.NF - 1) * M * M;   // L of Sigma_v (factored in place)
+  // entries q < 16: rows I*16 + q; q >= 16: columns J*16 + q - 16 (I == J: the rows only)
+  const int nq = I == J ? 16 : 32;
+  for (int q = w; q < nq; q += 4) {
+    const int c = q < 16 ? I * 16 + q : J * 16 + q - 16;
+    T sacc = 0;
+    if (c < M)
+      for (int k = lane; k <= c; k += 64) sacc += Cv[(int64_t)c * M + k] * zv[k];
+    sacc = wave_sum(sacc);
+    if (lane == 0) {
+      const T v = c < M ? ((const T*)a.theta)[a.off_muv + c] + sacc : (T)0;
+      vl[q] = v;
+      if (I == J && c < M) {
+        ((T*)a.v)[c] = v;
+        ((T*)a.ellZ)[c] = dexp(v);
+      }
+    }
+  }
+  __syncthreads();
+  const int r = threadIdx.x >> 4, cc = threadIdx.x & 15;
+  const int i = I * 16 + r, j = J * 16 + cc;
+  if (i >= M || j >= M) return;
+  const T* Z = (const T*)a.Z;
+  const T lx = dexp(vl[r]), lz = dexp(vl[I == J ? cc : 16 + cc]);
+  T r2 = 0;
+  const T dd = Z[i] / (T)1 - Z[j] / (T)1;
+  r2 += dd * dd;
+  const T S = lx * lx + lz * lz;
+  const T C = dsqrt((T)2 * (lx * lz) / S);
+  T k = (T)1 * C * dexp(-r2 / S);
+  if (i == j) k += (T)a.jitter;
+  ((T*)a.Afac)[(int64_t)(a.NF + 3) * M * M + (int64_t)i * M + j] = k;
+}
+
 // ------------------------------------------------------------------------------------ t-row
 template <typename T>
 __global__ __launch_bounds__(256) void dsvi_trow_kernel(Args a) {
@@ -1304,6 +1354,13 @@ template <typename T> static int dsvi_hyper(const Args* a, hipStream_t s) {
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }
+template <typename T> static int dsvi_vg22(const Args* a, hipStream_t s) {
+  CHECK_ARGS(a);
+  const int nt = (a->M + 15) / 16;
+  hipLaunchKernelGGL(dsvi_vg22_kernel<T>, dim3((unsigned)(nt * (nt + 1) / 2)), dim3(256), 0, s, *a);
+  NMGP_CHECK_LAUNCH();
+  return NMGP_OK;
+}
 template <typename T> static int dsvi_trow(const Args* a, hipStream_t s) {
   CHECK_ARGS(a);
   hipLaunchKernelGGL(dsvi_trow_kernel<T>, dim3(blocks_rows(a->B)), dim3(256), 0, s, *a);
@@ -1417,6 +1474,7 @@ int nmgp_device_status(uint32_t* out, int clear) {
   int nmgp_dsvi_##name##_f64(const Args* a, hipStream_t s) { return nmgp::dsvi_##name<double>(a, s); } \
   int nmgp_dsvi_##name##_f32(const Args* a, hipStream_t s) { return nmgp::dsvi_##name<float>(a, s); }
 NMGP_DSVI_ENTRY(hyper)
+NMGP_DSVI_ENTRY(vg22)
 NMGP_DSVI_ENTRY(trow)
 NMGP_DSVI_ENTRY(recon)
 NMGP_DSVI_ENTRY(kl)

@@ -175,7 +175,7 @@ class DsviEngine:
         # likewise the Gibbs prior with its t-row sample -- no builder, invG / projG or t-row launches on the chain.
         # NMGP_FUSE_TP=0 keeps the separate launches (the tests' equivalence switch)
         self.fuse_tp = (self.dt == torch.float64 and 128 <= M <= 256 and B <= 4096
-                        and os.environ.get("NMGP_FUSE_TP", "0") != "0")
+                        and os.environ.get("NMGP_FUSE_TP", "1") != "0")
         # per-(output, factor) L-bar products of the grouped backward (bwd_lbar), summed by nmgp_lbar_reduce: D(D+1)/2
         # slots of M x M + M.  Only where the slots stay small (PM2.5: 15 slots, 7.9 MB); many outputs with few
         # rows each (HCP-like D = 50) keep one product per factor, whose k loop is then short anyway
@@ -443,18 +443,21 @@ class DsviEngine:
         p["projG"] = G(([pproj(3)] if not (p64 or self.fuse_tp) else []) +
                        [g(self.Y, self.Ainv, th, M, D, M, (M, 1, 0), (1, M, 0), (1, M), offs=(3 * MM, muW, 0))])
         if self.fuse_tp:
-            # the two fused prior launches (hip_ops.CholTp): [v | t | L0 | L1] with the three RBF priors built and
-            # their K12 / T / P rows formed in the launch, then the Gibbs prior with the t-row and K_G12 rows
+            # the two fused prior launches (hip_ops.CholTp): [v | t | L0 | L1] with the three RBF priors' K12 / T / P
+            # rows formed in the launch, then the Gibbs prior with the t-row and K_G12 rows.  The RBF priors' K22 +
+            # lam I (theta only) are built off the chain at the step's start (build_k22), K_G22 by the v launch
             hyp_addr = lambda k: th.data_ptr() + (hyp + k) * th.element_size()
-            rbf = [dict(build=1, rows=1, hyp=hyp_addr(2 * k), K12=self.K12[k], T=self.T[k], P=self.P[k])
-                   for k in range(3)]
+            rbf = [dict(rows=1, hyp=hyp_addr(2 * k), K12=self.K12[k], T=self.T[k], P=self.P[k]) for k in range(3)]
             p["chol_tp_main"] = H.CholTp(self.Afac[FV], self.Cinv[FV], self.info[FV:], M, [dict()] + rbf,
                                          jitter=self.jitter, Z=self.Z, x=self.x, B=B)
             p["chol_tp_G"] = H.CholTp(self.Afac[NF + 3], self.Cinv[NF + 3], self.info[NF + 3:], M,
-                                      [dict(build=2, rows=2, K12=self.K12[3], T=self.T[3], P=self.P[3])],
+                                      [dict(rows=2, K12=self.K12[3], T=self.T[3], P=self.P[3])],
                                       jitter=self.jitter, Z=self.Z, ellZ=self.ellZ, x=self.x, B=B,
                                       trow=dict(Pt=self.P[0], Tt=self.T[0], v=self.v, zt=self.noise[M:M + B],
                                                 hyp_t=hyp_addr(0), ellX=self.ellX, var_t=self.var_t))
+            p["build_k22"] = H.PairwiseGroup([
+                H.pairwise_desc(self.Afac[NF + k], self.Z, self.Z, mode=L.RBF, hyp=th, hyp_off=hoff, hyp_log=True,
+                                diag_add=self.jitter) for k, hoff in [(0, hyp + 0), (1, hyp + 2), (2, hyp + 4)]], dev)
         # F14: quadratic-form factors W = P L on the rows that use them
         d14 = []
         for d in range(D):
@@ -799,6 +802,7 @@ class DsviEngine:
         D, M, NF = self.D, self.M, self.NF
         MM = M * M
         FV = NF - 1
+        fuse = self.fuse_tp
         p = self._plan(elbo_mode)
         a = self._args(elbo_mode)
         self._keep_args = getattr(self, "_keep_args", {})
@@ -915,7 +919,6 @@ class DsviEngine:
             chol_main, chol_g = chol_prior(0, 3, v_too=True), chol_prior(3, 1)
         else:
             chol_main, chol_g = chol(FV, 4), chol(NF + 3, 1)
-        fuse = self.fuse_tp
         if fuse:
             chol_main, chol_g = p["chol_tp_main"], p["chol_tp_G"]
 
@@ -937,29 +940,43 @@ class DsviEngine:
         if need_side:
             steps += [("sig", "main", "fork"), ("wait", "side", "fork")]
             if v_on_side:
+                if fuse:      # the RBF priors' K22 (theta only) ahead of Sigma_v, beside the minibatch gather
+                    steps.append(("build_k22", "pairwise", pw("build_k22"), "side"))
                 steps += [("syrk", "gemm", gemm("syrk"), "side"), ("sig", "side", "syrk")]
             steps.append(("syrk_side", "gemm", gemm("syrk_side"), "side"))
             if pre_planned:
                 steps += [("plans", "gemm_plan", plans, "side"), ("sig", "side", "plans")]
-            steps.append(("chol_side", "chol", chol(kf0, kf1 - kf0), "side"))
+            side_fac = [("chol_side", "chol", chol(kf0, kf1 - kf0), "side")]
             if not elbo_mode:
-                steps.append(("xs_side", "gemm", gemm("xs_side"), "side"))
+                side_fac.append(("xs_side", "gemm", gemm("xs_side"), "side"))
+            side_after = fuse
+            if not side_after:
+                steps += side_fac
+                side_fac = []
         if self.p64:
             steps += [("conv_in", "convert", conv_in, "main"),
                       ("build_rbf64", "pairwise", pw64("build_rbf64"), "main")]
         if not fuse:
             steps.append(("build_rbf", "pairwise", pw("build_rbf"), "main"))
+        elif not v_on_side:
+            steps.append(("build_k22", "pairwise", pw("build_k22"), "main"))
         steps.append(("wait", "main", "syrk") if v_on_side else ("syrk", "gemm", gemm("syrk"), "main"))
         # forward chain: chol -> v -> K_G22 -> chol_G -> invG -> projG.  The t-prior projections, the
         # t-row (ell_X) and K_G12 run on the second side stream beside v / K_G22 / chol_G: they are
         # needed only from invG on (T_G = K_G12 C_G^-T)
+        side_fac = side_fac if need_side else []
         steps += [
             ("chol", "chol", chol_main, "main"),
             ("sig", "main", "chol"),
-            ("v", "row", row(getattr(lib, "nmgp_dsvi_hyper_" + self.sfx)), "main"),
-            ("sig", "main", "v"),
-            ("wait", "side2", "chol"),
         ]
+        steps += [
+            # fused: v and K_G22 + lam I in one wide launch (dsvi_vg22_kernel)
+            ("v", "row", row(getattr(lib, ("nmgp_dsvi_vg22_" if fuse else "nmgp_dsvi_hyper_") + self.sfx)), "main"),
+            ("sig", "main", "v"),
+        ]
+        if side_fac:        # the variational factors' batched factorization after the fused prior launch
+            steps += [("wait", "side", "chol")] + side_fac
+        steps.append(("wait", "side2", "chol"))
         if self.p64:
             steps += [("inv3_64", "gemm", gemm("inv3_64"), "side2"),
                       ("proj3_64", "gemm", gemm("proj3_64"), "side2"),
@@ -968,10 +985,10 @@ class DsviEngine:
             # fused priors: T / P of t, L0, L1 came with their factorization; side2 runs the pair factors W_P first
             # (recon waits for them), then the prior inverses and Y = A^-1 mu (KL and backward only); the Gibbs
             # prior's launch on the main stream forms the t-row, K_G12, T_G and P_G itself
-            if not elbo_mode:
-                steps += [("quad_P", "gemm", gemm("quad_P"), "side2"), ("sig", "side2", "quadP")]
-            steps += [("inv3", "gemm", gemm("inv3"), "side2"), ("proj3", "gemm", gemm("proj3"), "side2"),
-                      ("chol_G", "chol", chol_g, "main"), ("sig", "main", "cholG")]
+            qp = [("quad_P", "gemm", gemm("quad_P"), "side2"), ("sig", "side2", "quadP")] if not elbo_mode else []
+            i3 = [("inv3", "gemm", gemm("inv3"), "side2"), ("proj3", "gemm", gemm("proj3"), "side2")]
+            steps += i3 + qp
+            steps += [("chol_G", "chol", chol_g, "main"), ("sig", "main", "cholG")]
         else:
             if p["inv3"] is not None:
                 steps.append(("inv3", "gemm", gemm("inv3"), "side2"))
@@ -1021,7 +1038,7 @@ class DsviEngine:
                 # the RBF priors t, L0, L1 (builds, factors, inverses, projections P / T / Y), chol(Sigma_v)
                 # and the pair quadratic-form factors W_P; per sample only v, ell_X, the Gibbs prior and
                 # the latent-function factors W_G are recomputed (code/nmgp_dsvi.py:330-376)
-                skip = {"build_rbf", "syrk", "chol", "inv3", "proj3",
+                skip = {"build_rbf", "build_k22", "syrk", "chol", "inv3", "proj3",
                         "conv_in", "build_rbf64", "inv3_64", "proj3_64", "conv3"}
                 steps = [it for it in steps if not (len(it) == 4 and it[0] in skip)]
                 steps = [("quad_W",) + it[1:] if len(it) == 4 and it[0] == "quad" else it for it in steps]
@@ -1056,6 +1073,11 @@ class DsviEngine:
             ("wait", "main", "quadP"),
             ("recon", "row", row(getattr(lib, "nmgp_dsvi_recon_" + self.sfx)), "main"),
             ("sig", "main", "recon"),
+        ]
+        wp_first = fuse and p["bwd_wP"] is not None
+        if wp_first:
+            steps += [("wait", "side3", "recon"), ("bwd_wP", "gemm", gemm("bwd_wP"), "side3")]
+        steps += [
             ("bwd_wG", "gemm", gemm("bwd_wG"), "main"),
             ("bwd_wGr", "row", pbar_reduce, "main"),
         ]
@@ -1080,9 +1102,10 @@ class DsviEngine:
         # with the KL parts of A-bar_0/1 (kl_done, a one-way side -> side3 edge) -- the L0 / L1 prior adjoints
         # R_0/1 -> P^T R -> builder backward (hyper-parameter partials only; p64: P-bar_0/1, the KL parts of
         # A-bar_0/1 and the row coefficients c0 / c1 widened first)
-        steps.append(("wait", "side3", "recon"))
-        if p["bwd_wP"] is not None:
-            steps.append(("bwd_wP", "gemm", gemm("bwd_wP"), "side3"))
+        if not wp_first:
+            steps.append(("wait", "side3", "recon"))
+            if p["bwd_wP"] is not None:
+                steps.append(("bwd_wP", "gemm", gemm("bwd_wP"), "side3"))
         steps.append(("wait", "side3", "kl_done"))
         if self.p64:
             steps += [("wPbL", "convert", widen(self.Pbar, self.PbL64, 2 * BM, BM), "side3"),
@@ -1113,18 +1136,27 @@ class DsviEngine:
             ("tbwd", "row", row(getattr(lib, "nmgp_dsvi_tbwd_" + self.sfx)), "main"),
             ("sig", "main", "tb"),
             ("bwd_t1", "gemm", gemm("bwd_t1"), "main"),
-            ("wait", "side", "tb"),
-            ("bwd_vt", "gemm", gemm("bwd_vt"), "side"),      # (reads P_t and tbar only: beside the G-prior chain)
-            ("wait", "side", "g22"),
-            ("vbwd", "row", row(getattr(lib, "nmgp_dsvi_vbwd_" + self.sfx)), "side"),
-            ("bwd_v1", "gemm", gemm("bwd_v1"), "side"),
-            ("bwd_v2", "gemm", gemm("bwd_v2"), "side"),
-            ("mugrad", "row", row(getattr(lib, "nmgp_dsvi_mugrad_" + self.sfx)), "side"),
-            ("sig", "side", "v_done"),
-            ("bwd_t2", "gemm", gemm("bwd_t2"), "main"),
-            ("bwd_tbuild", "pairwise_bwd", (pw64 if self.p64 else pw)("bwd_tbuild"), "main"),
-            ("wait", "main", "v_done"),
-            ("wait", "main", "lbar_done"),
+        ]
+        vchain = [("bwd_vt", "gemm", gemm("bwd_vt"), None),      # (reads P_t and tbar only)
+                  ("vbwd", "row", row(getattr(lib, "nmgp_dsvi_vbwd_" + self.sfx)), None),
+                  ("bwd_v1", "gemm", gemm("bwd_v1"), None),
+                  ("bwd_v2", "gemm", gemm("bwd_v2"), None)]
+        mugrad = ("mugrad", "row", row(getattr(lib, "nmgp_dsvi_mugrad_" + self.sfx)), None)
+        if fuse:
+            # the v chain on side2 behind the K_G22 builder backward (its Gibbs partials; the KL L-bar -- first writer
+            # of the sqrt_v rows -- is done: side2 waited for R_G, which followed kl_done), not behind bwd_lbar on
+            # the side stream; the KL mean gradients (after bwd_lbar's mu products and vbwd's vbar) on main
+            steps += [("wait", "side2", "tb")] + [it[:3] + ("side2",) for it in vchain] + [("sig", "side2", "v_done")]
+            steps += [("bwd_t2", "gemm", gemm("bwd_t2"), "main"),
+                      ("bwd_tbuild", "pairwise_bwd", (pw64 if self.p64 else pw)("bwd_tbuild"), "main"),
+                      ("wait", "main", "v_done"), ("wait", "main", "lbar_done"), mugrad[:3] + ("main",)]
+        else:
+            steps += [("wait", "side", "tb"), vchain[0][:3] + ("side",), ("wait", "side", "g22")]
+            steps += [it[:3] + ("side",) for it in vchain[1:]] + [mugrad[:3] + ("side",), ("sig", "side", "v_done")]
+            steps += [("bwd_t2", "gemm", gemm("bwd_t2"), "main"),
+                      ("bwd_tbuild", "pairwise_bwd", (pw64 if self.p64 else pw)("bwd_tbuild"), "main"),
+                      ("wait", "main", "v_done"), ("wait", "main", "lbar_done")]
+        steps += [
             ("wait", "main", "L_done"),
             ("wait", "main", "g22"),          # (explicit join of side2; long done)
             ("finalize", "row", row(getattr(lib, "nmgp_dsvi_finalize_" + self.sfx)), "main"),

@@ -519,14 +519,12 @@ def _ptr(t):
 
 
 class CholTp:
-    """The fused GP-prior launch (nmgp_chol_tp_f64, fp64, 128 <= n <= 256): `batch` n x n slots of A (stride n*n,
-    from A's first element) factored in place with X <- L^-1 and info as chol_inv_, where mats[b] may
-      - build its K22 + jitter I in the launch ("build": 1 RBF from Z and hyp = (log s2, log ls) at that address,
-        2 Gibbs from Z and ellZ) instead of reading it from A, and
-      - form its minibatch products in the same launch ("rows": 1 RBF K12 rows from x, 2 the t-row sample -- ell_X,
-        var_t from trow = dict(Pt, Tt, v, zt, hyp_t, ellX, var_t) -- then Gibbs K12 rows): K12, T = K12 L^-T and
-        P = T L^-1 written to the (B, n) tensors mats[b]["K12" / "T" / "P"].
-    The argument struct is built once; a call is one launch (graph-capturable)."""
+    """The fused GP-prior launch (nmgp_chol_tp_f64, fp64, 128 <= n <= 256): `batch` n x n slots of A (K22 + jitter I,
+    stride n*n from A's first element) factored in place with X <- L^-1 and info as chol_inv_, where mats[b]["rows"]
+    != 0 also forms the minibatch products in the same launch (1: RBF K12 rows from x with hyp = (log s2, log ls) at
+    mats[b]["hyp"]; 2: the t-row sample -- ell_X, var_t from trow = dict(Pt, Tt, v, zt, hyp_t, ellX, var_t) -- then
+    Gibbs K12 rows with ellZ): K12, T = K12 L^-T and P = T L^-1 written to the (B, n) tensors mats[b]["K12" / "T" /
+    "P"].  The argument struct is built once; a call is one launch (graph-capturable)."""
 
     def __init__(self, A, X, info, n, mats, *, jitter=0.0, Z=None, ellZ=None, x=None, B=0, trow=None):
         for t_, nm in ((A, "A"), (X, "X"), (info, "info")):
@@ -542,7 +540,7 @@ class CholTp:
             setattr(a, k, _ptr(tr.get(k)))
         for b, m in enumerate(mats):
             mt = a.mats[b]
-            mt.build, mt.rows = int(m.get("build", 0)), int(m.get("rows", 0))
+            mt.reserved, mt.rows = 0, int(m.get("rows", 0))
             mt.hyp, mt.K12, mt.T, mt.P = (_ptr(m.get(k)) for k in ("hyp", "K12", "T", "P"))
         self.a = a
         self._keep = (A, X, info, Z, ellZ, x, tr, mats)     # the struct holds raw addresses of these

@@ -175,25 +175,21 @@ int nmgp_chol_inv_batched_ws_f32(float* A, int64_t n, int64_t lda, int64_t strid
                                  int64_t strideX, int64_t batch, int32_t* info, void* ws, int64_t ws_bytes,
                                  hipStream_t stream);
 
-/* Fused GP-prior launch (round 6): up to 4 prior matrices of one DSVI step factored and inverted as
- * nmgp_chol_inv_batched_f64 does (A <- L, X <- L^-1, info), optionally
- *   - with K22 + jitter I BUILT by the factor / update workgroups instead of read from A (build 1: RBF
- *     s2 exp(-(z_i/ls - z_j/ls)^2 / 2) from Z and hyp = (log s2, log ls), code/utils.py:91-94; build 2:
- *     Gibbs sqrt(2 l_i l_j / (l_i^2 + l_j^2)) exp(-(z_i - z_j)^2 / (l_i^2 + l_j^2)) from Z and ellZ,
- *     code/utils.py:97-103), and
- *   - with the prior's minibatch products formed by extra workgroups of the same launch while the
- *     factorization runs (rows 1: K12 = RBF(x, Z) rows; rows 2: first the t-row sample of JGP_S --
- *     ell_X = exp(P_t v + z_t sqrt(s2_t - ||T_t row||^2 + jitter)), code/utils.py:216-237 -- then
- *     K12 = Gibbs(x, Z, ell_X, ellZ) rows): K12 (written out), T = K12 L^-T (right-looking, from the
- *     published block columns of L) and P = T L^-1 = K12 (K22 + jitter I)^-1 (from the published rows
- *     of X) -- the projections torch.solve forms in code/utils.py:117-120, 140-146, 228-232.
- * 128 <= n <= 256, 1 <= batch <= 4, B <= 4096; every output of row stride n.  The mats with rows != 0
- * need K12 / T / P; rows 2 needs Pt, Tt (B x n, the t prior's P and T), v, zt, hyp_t (log s2_t), ellX,
- * var_t (B outputs) and ellZ.                                                                    */
+/* Fused GP-prior launch (round 6): up to 4 prior matrices of one DSVI step (A: K22 + jitter I, read) factored and
+ * inverted as nmgp_chol_inv_batched_f64 does (A <- L, X <- L^-1, info), where a matrix with rows != 0 also gets its
+ * minibatch products formed by extra workgroups of the same launch while the factorization runs (rows 1: K12 =
+ * RBF(x, Z) rows, s2 exp(-(x_i/ls - z_j/ls)^2 / 2) with hyp = (log s2, log ls), code/utils.py:91-94; rows 2: first
+ * the t-row sample of JGP_S -- ell_X = exp(P_t v + z_t sqrt(s2_t - ||T_t row||^2 + jitter)), code/utils.py:216-237
+ * -- then K12 = Gibbs(x, Z, ell_X, ellZ) rows, code/utils.py:97-103): K12 (written out), T = K12 L^-T (right-looking,
+ * from the published block columns of L) and P = T L^-1 = K12 (K22 + jitter I)^-1 (from the published rows of
+ * X) -- the projections torch.solve forms in code/utils.py:117-120, 140-146, 228-232.
+ * 128 <= n <= 256, 1 <= batch <= 4, B <= 4096; every output of row stride n.  The mats with rows != 0 need K12 /
+ * T / P, x and Z; rows 2 needs Pt, Tt (B x n, the t prior's P and T), v, zt, hyp_t (log s2_t), ellX, var_t (B
+ * outputs) and ellZ.                                                                                           */
 typedef struct nmgp_chol_tp_mat {
-  int32_t build;      /* 0: read A; 1: RBF K22; 2: Gibbs K22 (diagonal + jitter) */
+  int32_t reserved;   /* 0 */
   int32_t rows;       /* 0: no minibatch products; 1: RBF K12 rows; 2: t-row + Gibbs K12 rows */
-  const double* hyp;  /* build / rows 1: (log sigma2, log lengthscale) */
+  const double* hyp;  /* rows 1: (log sigma2, log lengthscale) */
   double* K12;        /* B x n */
   double* T;          /* B x n */
   double* P;          /* B x n */
@@ -206,7 +202,7 @@ typedef struct nmgp_chol_tp_args {
   int32_t* info;
   double jitter;
   const double* Z;     /* n inducing inputs */
-  const double* ellZ;  /* n Gibbs length scales (build 2 / rows 2) */
+  const double* ellZ;  /* n Gibbs length scales (rows 2) */
   const double* x;     /* B minibatch inputs */
   int64_t B;
   const double* Pt;    /* rows 2: the t prior's P and T (B x n), the v sample (n), z_t (B), log s2_t */
@@ -428,6 +424,7 @@ typedef struct nmgp_dsvi_args {
 } nmgp_dsvi_args;
 
 int nmgp_dsvi_hyper_f64(const nmgp_dsvi_args* a, hipStream_t s);      /* hyper values + v sample   */
+int nmgp_dsvi_vg22_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* v sample + K_G22 + jitter I (fused priors) */
 int nmgp_dsvi_trow_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* t-row forward             */
 int nmgp_dsvi_recon_f64(const nmgp_dsvi_args* a, hipStream_t s);      /* recon + per-row adjoints  */
 int nmgp_dsvi_kl_f64(const nmgp_dsvi_args* a, hipStream_t s);         /* KL per factor + e-vectors */
@@ -439,6 +436,7 @@ int nmgp_dsvi_mugrad_f64(const nmgp_dsvi_args* a, hipStream_t s);     /* KL mean
 int nmgp_dsvi_prefinal_f64(const nmgp_dsvi_args* a, hipStream_t s);   /* training step: recon + KL sums -> out[8..14] */
 /* fp32 twins (HCP / ECoG-shaped configurations): same arguments, every buffer float */
 int nmgp_dsvi_hyper_f32(const nmgp_dsvi_args* a, hipStream_t s);
+int nmgp_dsvi_vg22_f32(const nmgp_dsvi_args* a, hipStream_t s);
 int nmgp_dsvi_trow_f32(const nmgp_dsvi_args* a, hipStream_t s);
 int nmgp_dsvi_recon_f32(const nmgp_dsvi_args* a, hipStream_t s);
 int nmgp_dsvi_kl_f32(const nmgp_dsvi_args* a, hipStream_t s);

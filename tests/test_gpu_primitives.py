@@ -723,10 +723,10 @@ def _gibbs(a, b, la, lb):
 
 @pytest.mark.parametrize("n,B", [(256, 2000), (256, 1), (200, 130), (144, 64), (128, 63)])
 def test_chol_tp_fused_priors_vs_torch(ops, n, B):
-    """Round 6: nmgp_chol_tp_f64 -- [Sigma (read) | three RBF priors (built)] factored + inverted, the priors' K12 /
-    T = K12 L^-T / P = T L^-1 formed by the launch's row workgroups; then a Gibbs prior (built from ellZ) whose row
-    workgroups first draw the t-row ell_X.  Against fp64 torch on the same inputs, and T / P against the products of
-    the launch's own L^-1 (the unfused schedule's arithmetic, tight)."""
+    """Round 6: nmgp_chol_tp_f64 -- [Sigma | three RBF priors] factored + inverted, the priors' K12 / T = K12 L^-T /
+    P = T L^-1 formed by the launch's row workgroups; then a Gibbs prior whose row workgroups first draw the t-row
+    ell_X.  Against fp64 torch on the same inputs: L, K12, ell_X tight; T / P at least as accurate as the unfused
+    schedule's explicit-inverse products of the launch's own L^-1."""
     g = torch.Generator().manual_seed(n + B)
     jit = 1e-4
     Z = torch.linspace(0, 1, n, dtype=F64)
@@ -735,11 +735,13 @@ def test_chol_tp_fused_priors_vs_torch(ops, n, B):
     S = torch.tril(0.1 * torch.randn(n, n, generator=g, dtype=F64))
     A = torch.zeros(4, n, n, dtype=F64)
     A[0] = S @ S.t() + jit * torch.eye(n, dtype=F64)
+    for k in range(3):
+        A[k + 1] = _rbf(Z, Z, float(torch.exp(hyp[2 * k])), float(torch.exp(hyp[2 * k + 1]))) + jit * torch.eye(n, dtype=F64)
     Ad, Xd = A.to(DEV), torch.zeros(4, n, n, dtype=F64, device=DEV)
     info = torch.full((4,), 7, dtype=torch.int32, device=DEV)
     K12, T, P = (torch.zeros(3, B, n, dtype=F64, device=DEV) for _ in range(3))
     hd, Zd, xd = hyp.to(DEV), Z.to(DEV), x.to(DEV)
-    mats = [dict()] + [dict(build=1, rows=1, hyp=hd[2 * k:], K12=K12[k], T=T[k], P=P[k]) for k in range(3)]
+    mats = [dict()] + [dict(rows=1, hyp=hd[2 * k:], K12=K12[k], T=T[k], P=P[k]) for k in range(3)]
     ops.CholTp(Ad[0], Xd[0], info, n, mats, jitter=jit, Z=Zd, x=xd, B=B)()
     torch.cuda.synchronize()
     assert info.cpu().tolist() == [0, 0, 0, 0]
@@ -762,11 +764,12 @@ def test_chol_tp_fused_priors_vs_torch(ops, n, B):
     Ttd = (0.02 * torch.randn(B, n, generator=g, dtype=F64)).to(DEV)
     zt = torch.randn(B, generator=g, dtype=F64)
     ht = torch.tensor([0.2], dtype=F64)
-    AG, XG = torch.zeros(n, n, dtype=F64, device=DEV), torch.zeros(n, n, dtype=F64, device=DEV)
+    K22 = _gibbs(Z, Z, ellZ, ellZ) + jit * torch.eye(n, dtype=F64)
+    AG, XG = K22.to(DEV), torch.zeros(n, n, dtype=F64, device=DEV)
     infoG = torch.full((1,), 7, dtype=torch.int32, device=DEV)
     KG, TG, PG = (torch.zeros(B, n, dtype=F64, device=DEV) for _ in range(3))
     ellX, var_t = torch.zeros(B, dtype=F64, device=DEV), torch.zeros(B, dtype=F64, device=DEV)
-    ops.CholTp(AG, XG, infoG, n, [dict(build=2, rows=2, K12=KG, T=TG, P=PG)], jitter=jit, Z=Zd, ellZ=ellZ.to(DEV),
+    ops.CholTp(AG, XG, infoG, n, [dict(rows=2, K12=KG, T=TG, P=PG)], jitter=jit, Z=Zd, ellZ=ellZ.to(DEV),
                x=xd, B=B, trow=dict(Pt=Ptd, Tt=Ttd, v=v.to(DEV), zt=zt.to(DEV), hyp_t=ht.to(DEV), ellX=ellX,
                                     var_t=var_t))()
     torch.cuda.synchronize()
@@ -774,7 +777,6 @@ def test_chol_tp_fused_priors_vs_torch(ops, n, B):
     var = float(torch.exp(ht)) - (Ttd.cpu() ** 2).sum(1)
     lx = torch.exp(Ptd.cpu() @ v + zt * torch.sqrt(var + jit))
     assert rel(var_t, var) < 1e-14 and rel(ellX, lx) < 1e-13
-    K22 = _gibbs(Z, Z, ellZ, ellZ) + jit * torch.eye(n, dtype=F64)
     Kx = _gibbs(x, Z, lx, ellZ)
     LG = torch.linalg.cholesky(K22)
     assert rel(AG, LG) < 1e-11 and rel(KG, Kx) < 1e-13
@@ -801,14 +803,13 @@ def L_dev_status_clean():
 
 
 def test_chol_tp_not_pd_and_repeat(ops):
-    """A non-PD read matrix reports its column in info like chol_inv_, the built priors stay exact; the progress words
-    are re-armed, so the next launches on the same buffers (different B) agree bit for bit with a fresh one."""
+    """A non-PD matrix reports its column in info like chol_inv_ and leaves the other matrix of the launch exact; the
+    progress words are re-armed, so the next launches on the same buffers (different B) agree bit for bit."""
     n, jit = 256, 1e-4
     Z = torch.linspace(0, 1, n, dtype=F64, device=DEV)
     hyp = torch.tensor([0.0, -1.0], dtype=F64, device=DEV)
+    K22 = _rbf(Z.cpu(), Z.cpu(), 1.0, float(np.exp(-1.0))).to(DEV) + jit * torch.eye(n, dtype=F64, device=DEV)
     A = torch.zeros(2, n, n, dtype=F64, device=DEV)
-    A[0] = torch.eye(n, dtype=F64, device=DEV)
-    A[0, 100, 100] = -1.0
     X = torch.zeros_like(A)
     info = torch.zeros(2, dtype=torch.int32, device=DEV)
     outs = []
@@ -817,7 +818,8 @@ def test_chol_tp_not_pd_and_repeat(ops):
         K12, T, P = (torch.zeros(B, n, dtype=F64, device=DEV) for _ in range(3))
         A[0] = torch.eye(n, dtype=F64, device=DEV)
         A[0, 100, 100] = -1.0
-        ops.CholTp(A[0], X[0], info, n, [dict(), dict(build=1, rows=1, hyp=hyp, K12=K12, T=T, P=P)], jitter=jit,
+        A[1] = K22
+        ops.CholTp(A[0], X[0], info, n, [dict(), dict(rows=1, hyp=hyp, K12=K12, T=T, P=P)], jitter=jit,
                    Z=Z, x=x, B=B)()
         torch.cuda.synchronize()
         assert info.cpu().tolist() == [101, 0]

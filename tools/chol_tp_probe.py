@@ -1,7 +1,8 @@
 """Timing of the fused prior launch (nmgp_chol_tp_f64) alone on the GPU box, at the PM2.5 step's shapes (n = 256,
 B = 2000): the [v | t | L0 | L1]-shaped launch and the Gibbs launch, each with and without its row workgroups
-(rows = 0: factor + inverse only, K22 still built), graph-replayed (20 launches per graph, best of 5).  What the row
-workgroups add to a launch is the difference.  Usage: python tools/chol_tp_probe.py [B]"""
+(rows = 0: factor + inverse only), beside the plain four-role chol_inv_ on the same matrices; graph-replayed (20
+launches per graph, best of 5, the K22 restore copies timed alone and subtracted).  NMGP_TP_DBG=16: per-workgroup
+phase stamps of one launch instead.  Usage: python tools/chol_tp_probe.py [B]"""
 import json
 import os
 import sys
@@ -31,15 +32,41 @@ trow = dict(Pt=0.01 * torch.randn(B, n, generator=g, dtype=F, device=dev),
             var_t=torch.zeros(B, dtype=F, device=dev))
 
 
+def _prefill():
+    A0 = torch.zeros(4, n, n, dtype=F, device=dev)
+    for k in range(3):
+        ls = float(torch.exp(hyp[2 * k + 1]))
+        A0[k] = torch.exp(-0.5 * (Z[:, None] / ls - Z[None, :] / ls) ** 2) + 1e-4 * torch.eye(n, dtype=F, device=dev)
+    S = ellZ[:, None] ** 2 + ellZ[None, :] ** 2
+    A0[3] = torch.sqrt(2 * ellZ[:, None] * ellZ[None, :] / S) * torch.exp(-(Z[:, None] - Z[None, :]) ** 2 / S) \
+        + 1e-4 * torch.eye(n, dtype=F, device=dev)
+    return A0
+
+
+A0 = _prefill()
+A0m = A0[[0, 0, 1, 2]].clone()    # [Sigma-like | t | L0 | L1] slots
+
+
 def main_op(rows):
-    mats = [dict(build=1, rows=0, hyp=hyp[0:])] + [dict(build=1, rows=rows, hyp=hyp[2 * k:], K12=K12[k], T=T[k],
-                                                        P=P[k]) for k in range(1, 4)]
-    return H.CholTp(A[0], X[0], info, n, mats, jitter=1e-4, Z=Z, x=x, B=B)
+    # [Sigma-like | t | L0 | L1]: the K22 slots restored before each launch (its copy is timed separately)
+    mats = [dict()] + [dict(rows=rows, hyp=hyp[2 * k:], K12=K12[k], T=T[k], P=P[k]) for k in range(1, 4)]
+    op = H.CholTp(A[0], X[0], info, n, mats, jitter=1e-4, Z=Z, x=x, B=B)
+
+    def run():
+        A.copy_(A0m)
+        op()
+    return run
 
 
 def g_op(rows):
-    return H.CholTp(A[3], X[3], info[3:], n, [dict(build=2, rows=rows, K12=K12[3], T=T[3], P=P[3])], jitter=1e-4, Z=Z,
-                    ellZ=ellZ, x=x, B=B, trow=trow)
+    op = H.CholTp(A[3], X[3], info[3:], n, [dict(rows=rows, K12=K12[3], T=T[3], P=P[3])], jitter=1e-4, Z=Z,
+                  ellZ=ellZ, x=x, B=B, trow=trow)
+
+    def run():
+        A[3].copy_(A0[3])
+        op()
+    A[3].copy_(A0[3])
+    return run
 
 
 def time_op(op, reps=20):
@@ -65,32 +92,18 @@ def time_op(op, reps=20):
 
 
 def read_op():
-    # the plain four-role launch on the same matrices (K22 read from A, restored before each launch)
-    A0 = torch.zeros(4, n, n, dtype=F, device=dev)
-    for k in range(4):
-        ls = float(torch.exp(hyp[2 * k + 1]))
-        A0[k] = torch.exp(-0.5 * (Z[:, None] / ls - Z[None, :] / ls) ** 2) + 1e-4 * torch.eye(n, dtype=F, device=dev)
-    W = A0.clone()
+    # the plain four-role launch on the same four matrices (restored before each launch)
+    W = A0m.clone()
+    Wg = A0[3:].clone()
 
     def run():
-        W.copy_(A0)
+        W.copy_(A0m)
         H.chol_inv_(W, out=X, info=info)
-    return run, (lambda: W.copy_(A0))
 
-
-def main_prefilled(rows):
-    # the fused launch with every K22 already in A (restored before each launch): with NMGP_TP_DBG=1/2/3 the
-    # factor / update roles read it instead of building
-    A0 = torch.zeros(4, n, n, dtype=F, device=dev)
-    for k in range(4):
-        ls = float(torch.exp(hyp[2 * k + 1]))
-        A0[k] = torch.exp(-0.5 * (Z[:, None] / ls - Z[None, :] / ls) ** 2) + 1e-4 * torch.eye(n, dtype=F, device=dev)
-    op = main_op(rows)
-
-    def run():
-        A.copy_(A0)
-        op()
-    return run
+    def run_g():
+        Wg.copy_(A0[3:])
+        H.chol_inv_(Wg, out=X[3:], info=info[3:])
+    return run, (lambda: W.copy_(A0m)), run_g, (lambda: Wg.copy_(A0[3:]))
 
 
 def trace(op, nwg, label):
@@ -103,8 +116,6 @@ def trace(op, nwg, label):
         op()
     torch.cuda.synchronize()
     buf = np.zeros(8 * 512, dtype=np.uint64)
-    L.lib().nmgp_chol_tp_trace(ctypes.c_void_p(buf.ctypes.data), 0)
-    zero = np.zeros(8 * 512, dtype=np.uint64)
     op()
     torch.cuda.synchronize()
     L.lib().nmgp_chol_tp_trace(ctypes.c_void_p(buf.ctypes.data), buf.size)
@@ -116,18 +127,15 @@ def trace(op, nwg, label):
 
 
 if os.environ.get("NMGP_TP_DBG") == "16":
-    trace(main_op(1), 16 + 3 * ((B + 63) // 64), "main")
-    trace(g_op(2), 4 + (B + 63) // 64, "gibbs")
+    trace(main_op(1), 16 + 3 * ((B + 31) // 32), "main")
+    trace(g_op(2), 4 + (B + 31) // 32, "gibbs")
     sys.exit(0)
-if os.environ.get("NMGP_TP_DBG"):
-    dbg = int(os.environ["NMGP_TP_DBG"])
-    print(json.dumps({"dbg": dbg, "main_rows_prefilled_us": time_op(main_prefilled(1)) if not dbg & 4 else None,
-                      "main_no_rows_prefilled_us": time_op(main_prefilled(0))}))
-    sys.exit(0)
-rd, cp = read_op()
-rec = {"n": n, "B": B, "chol_inv7_4_us_incl_copy": time_op(rd), "copy_us": time_op(cp),
-       "main_rows_us": time_op(main_op(1)), "main_no_rows_us": time_op(main_op(0)),
-       "gibbs_rows_us": time_op(g_op(2)), "gibbs_no_rows_us": time_op(g_op(0))}
+rd, cp, rdg, cpg = read_op()
+rec = {"n": n, "B": B, "plain_4_us": round(time_op(rd) - time_op(cp), 2), "plain_1_us": round(time_op(rdg) - time_op(cpg), 2),
+       "fused_main_us": round(time_op(main_op(1)) - time_op(cp), 2),
+       "fused_main_no_rows_us": round(time_op(main_op(0)) - time_op(cp), 2),
+       "fused_gibbs_us": round(time_op(g_op(2)) - time_op(cpg), 2),
+       "fused_gibbs_no_rows_us": round(time_op(g_op(0)) - time_op(cpg), 2)}
 from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L  # noqa: E402
 rec["device_status"] = L.device_status(clear=True)
 print(json.dumps(rec))
