@@ -682,16 +682,15 @@ __global__ __launch_bounds__(256) void dsvi_vbwd_kernel(Args a) {
 // KL mean gradients A2^{-1} mu (Y) into the mu_W / mu_U gradient rows (live pairs j <= i only) and
 // mu_v += vbar + Y_t: one grid-strided element-wise pass, launched on the side stream after the last
 // writers of those rows (the mu-bar products of bwd_lbar and the v backward), off the main chain.
-template <typename T>
-__global__ __launch_bounds__(256) void dsvi_mugrad_kernel(Args a) {
+template <typename T> __device__ inline void mugrad_body(const Args& a, int64_t i0, int64_t stride) {
   const int D = a.D, M = a.M;
   T* __restrict__ gw = (T*)a.grad;
   const T* __restrict__ Y = (const T*)a.Y;
   const T* __restrict__ vbar = (const T*)a.vbar + M;   // completed by the v-backward kernel
   const int64_t DM = (int64_t)D * M, DDM = pair_cols(a) * M;
   const int64_t yu0 = (int64_t)(D + 1) * M, yu1 = yu0 + DDM;
-  const int64_t n = DM + M + DDM, stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+  const int64_t n = DM + M + DDM;
+  for (int64_t i = i0; i < n; i += stride) {
     if (i < DM) {
       if (a.n_wfac > 0) gw[a.off_muW + i] = gw[a.off_muW + i] + Y[i];
     } else if (i < DM + M) {
@@ -710,6 +709,10 @@ __global__ __launch_bounds__(256) void dsvi_mugrad_kernel(Args a) {
       if (pj <= pi) gw[a.off_muU + idx] = gw[a.off_muU + idx] + Y[(pi == pj ? yu1 : yu0) + idx];
     }
   }
+}
+template <typename T>
+__global__ __launch_bounds__(256) void dsvi_mugrad_kernel(Args a) {
+  mugrad_body<T>(a, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
 }
 
 // ------------------------------------------------------------------------------------ finalize
@@ -928,7 +931,9 @@ __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
     }
     for (int k = 0; k < 7; ++k) g[a.off_hyp + k] = (a.frozen_mask >> k & 1) ? (T)0 : gs[k];
   }
-  // (the KL mean gradients A2^{-1} mu and mu_v += vbar are added by dsvi_mugrad_kernel on the side stream)
+  // training step: the KL mean gradients A2^{-1} mu and mu_v += vbar (round 6: here, after every other writer of those
+  // rows -- bwd_lbar's mu products, nmgp_lbar_reduce, the v backward -- instead of a launch of their own)
+  if (!a.elbo_mode) mugrad_body<T>(a, threadIdx.x, blockDim.x);
 #ifdef NMGP_FIN_TRACE
   __syncthreads();
   if (threadIdx.x == 0) {

@@ -1141,18 +1141,18 @@ class DsviEngine:
                   ("vbwd", "row", row(getattr(lib, "nmgp_dsvi_vbwd_" + self.sfx)), None),
                   ("bwd_v1", "gemm", gemm("bwd_v1"), None),
                   ("bwd_v2", "gemm", gemm("bwd_v2"), None)]
-        mugrad = ("mugrad", "row", row(getattr(lib, "nmgp_dsvi_mugrad_" + self.sfx)), None)
+        # (the KL mean gradients -- after bwd_lbar's mu products and vbwd's vbar -- are added by finalize)
         if fuse:
             # the v chain on side2 behind the K_G22 builder backward (its Gibbs partials; the KL L-bar -- first writer
             # of the sqrt_v rows -- is done: side2 waited for R_G, which followed kl_done), not behind bwd_lbar on
-            # the side stream; the KL mean gradients (after bwd_lbar's mu products and vbwd's vbar) on main
+            # the side stream
             steps += [("wait", "side2", "tb")] + [it[:3] + ("side2",) for it in vchain] + [("sig", "side2", "v_done")]
             steps += [("bwd_t2", "gemm", gemm("bwd_t2"), "main"),
                       ("bwd_tbuild", "pairwise_bwd", (pw64 if self.p64 else pw)("bwd_tbuild"), "main"),
-                      ("wait", "main", "v_done"), ("wait", "main", "lbar_done"), mugrad[:3] + ("main",)]
+                      ("wait", "main", "v_done"), ("wait", "main", "lbar_done")]
         else:
             steps += [("wait", "side", "tb"), vchain[0][:3] + ("side",), ("wait", "side", "g22")]
-            steps += [it[:3] + ("side",) for it in vchain[1:]] + [mugrad[:3] + ("side",), ("sig", "side", "v_done")]
+            steps += [it[:3] + ("side",) for it in vchain[1:]] + [("sig", "side", "v_done")]
             steps += [("bwd_t2", "gemm", gemm("bwd_t2"), "main"),
                       ("bwd_tbuild", "pairwise_bwd", (pw64 if self.p64 else pw)("bwd_tbuild"), "main"),
                       ("wait", "main", "v_done"), ("wait", "main", "lbar_done")]

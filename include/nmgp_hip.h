@@ -432,7 +432,7 @@ int nmgp_dsvi_delta_f64(const nmgp_dsvi_args* a, hipStream_t s);      /* prior d
 int nmgp_dsvi_tbwd_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* t-row backward            */
 int nmgp_dsvi_vbwd_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* v backward -> Phi         */
 int nmgp_dsvi_finalize_f64(const nmgp_dsvi_args* a, hipStream_t s);   /* loss + scalar gradients   */
-int nmgp_dsvi_mugrad_f64(const nmgp_dsvi_args* a, hipStream_t s);     /* KL mean gradients of mu_W / mu_v / mu_U */
+int nmgp_dsvi_mugrad_f64(const nmgp_dsvi_args* a, hipStream_t s);     /* KL mean gradients of mu_W / mu_v / mu_U (training steps: part of finalize) */
 int nmgp_dsvi_prefinal_f64(const nmgp_dsvi_args* a, hipStream_t s);   /* training step: recon + KL sums -> out[8..14] */
 /* fp32 twins (HCP / ECoG-shaped configurations): same arguments, every buffer float */
 int nmgp_dsvi_hyper_f32(const nmgp_dsvi_args* a, hipStream_t s);

@@ -1228,6 +1228,22 @@ def test_hip_graph_external_event_node_fires_mid_replay(ops):
         y.fill_(1.0)
     comm = torch.cuda.Stream(device=DEV)
     torch.cuda.synchronize()
+    # HIP maps streams onto GPU_MAX_HW_QUEUES (4) hardware queues round-robin: once a process has created many
+    # streams (the whole suite), `comm` can share the graph stream's queue, and then nothing it holds can run before
+    # the replay ends.  Probe that first: a marker on `comm` must finish while a long GEMM on the replay stream is
+    # still running.
+    cur = torch.cuda.current_stream(DEV)          # the stream the graph is replayed on
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    e0.record(cur)
+    for _ in range(4):
+        ops.gemm_big(Ab, Ab, Cb, ws=ws)
+    e1.record(cur)
+    comm.wait_event(e0)
+    with torch.cuda.stream(comm):
+        e2.record(comm)
+    torch.cuda.synchronize()
+    if e0.elapsed_time(e2) > 0.5 * e0.elapsed_time(e1):
+        pytest.skip("the comm stream shares a hardware queue with another stream in this process")
     for rep in range(3):
         g.replay()
         ev.wait(comm)
