@@ -897,15 +897,25 @@ def main():
             return line
         # the dominant kernel by GPU time is the latency-oriented grouped GEMM (gemm_lat.hip) -- the
         # rocprofv3 kernel stats under profiles/ name it; the 64x64 tile kernel is reported beside it
-        roofline = with_iso("lat", "gemm_lat_kernel<double> (latency-oriented grouped MFMA f64 GEMM, 32x32 tiles)")
+        roofline = with_iso("lat", "gemm_lat_kernel<double> + gemm_lat_pipe_kernel<double> (latency-oriented grouped "
+                                   "MFMA f64 GEMM, 32x32 tiles; the persistent two-tiles-in-flight form on groups of "
+                                   "more than 512 tiles)")
         roofline["tile_kernel"] = with_iso("tile", "gemm_kernel<double> (grouped 64x64 MFMA f64 GEMM)")
         roofline["all_gemm"] = {"algorithmic_gflop_per_step": round(gemm_flops / 1e9, 4), "ms_per_step": round(gemm_ms, 4),
                                 "achieved": round(gemm_flops / (gemm_ms * 1e-3) / 1e12, 4), "launches_per_step": n_gemm}
         nchol = eng.NF + 4
         chol_ms = per_kind.get("chol", 0.0)   # serial (timed) run: the three fused factor+inverse launches
+        fuse_tp = bool(getattr(eng, "fuse_tp", False))
+        # fused prior launches (round 6): besides factor + inverse of the 4 priors, their row workgroups form
+        # T = K12 L^-T and P = T L^-1 (B M^2 flops each, triangular) for the 4 priors
+        chol_gflop = nchol * 2.0 * M ** 3 / 3.0 + (4 * 2.0 * B * M ** 2 if fuse_tp else 0.0)
         chol = {"matrices_per_step": nchol, "n": M, "ms_per_step": round(chol_ms, 4),
-                "kernel": "chol_inv7_kernel (factor + trailing-update + two inverse workgroups per matrix)",
-                "gflops": round(nchol * 2.0 * M ** 3 / 3.0 / (chol_ms * 1e-3) / 1e9, 2)}
+                "kernel": ("chol_tp_kernel (2 launches: factor + update + inverse roles of the 4 GP priors with row "
+                           "workgroups forming K12, T = K12 L^-T and P = T L^-1) + chol_inv7_kernel (variational "
+                           "factors)" if fuse_tp else
+                           "chol_inv7_kernel (factor + trailing-update + two inverse workgroups per matrix)"),
+                "algorithmic_gflop_per_step": round(chol_gflop / 1e9, 4),
+                "gflops": round(chol_gflop / (chol_ms * 1e-3) / 1e9, 2)}
         breakdown = {k: round(v, 4) for k, v in sorted(per_kind.items(), key=lambda kv: -kv[1])}
         breakdown_names = {k: round(v, 4) for k, v in sorted(per_name.items(), key=lambda kv: -kv[1])}
 
@@ -961,11 +971,12 @@ def main():
                     entry["mfma_busy"] = round(sum(r["mfma_util"] * r["avg_us"] * r["dispatches"] for r in rs) / w, 4)
                     entry["mfma_busy_source"] = msrc
 
-        attach(roofline, lambda n: "gemm_lat_kernel<double" in n)
+        attach(roofline, lambda n: "gemm_lat_kernel<double" in n or "gemm_lat_pipe_kernel<double" in n)
         attach(roofline["tile_kernel"], lambda n: n.startswith("void nmgp::gemm_kernel<double"))
         roofline["code_hash"] = CODE_HASH
         if chol is not None and mfj is not None:
-            rs = [r for r in mfj["rows"] if "chol_inv7_kernel" in r["kernel"] or "chol_inv3_kernel" in r["kernel"]]
+            rs = [r for r in mfj["rows"] if any(k in r["kernel"] for k in ("chol_inv7_kernel", "chol_inv3_kernel",
+                                                                          "chol_tp_kernel"))]
             w = sum(r["avg_us"] * r["dispatches"] for r in rs)
             if w:
                 chol["mfma_busy"] = round(sum(r["mfma_util"] * r["avg_us"] * r["dispatches"] for r in rs) / w, 4)

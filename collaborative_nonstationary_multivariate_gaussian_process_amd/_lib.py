@@ -132,6 +132,8 @@ _SIGS = {
     "nmgp_gemm_grouped_dyn_planned_f32": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
     "nmgp_gemm_grouped_lat_planned_f64": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
     "nmgp_gemm_grouped_lat_planned_f32": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
+    "nmgp_gemm_grouped_lat_pipe_f64": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
+    "nmgp_gemm_grouped_lat_pipe_f32": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
     "nmgp_gemm_f64": (c_int, [ctypes.POINTER(GemmDesc), c_vp, c_vp]),
     "nmgp_gemm_f32": (c_int, [ctypes.POINTER(GemmDesc), c_vp, c_vp]),
     "nmgp_potrf_batched_f64": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
@@ -158,6 +160,10 @@ _SIGS = {
     "nmgp_gemm_big_offsets_epi_f32": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_int, c_vp, c_i64, c_i64, c_int, c_int,
                                               c_int, c_int, c_dbl, c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
                                               c_i64, c_vp, c_vp, c_dbl, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "nmgp_gemm_big_offsets_seg_f32": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_int, c_vp, c_i64, c_i64, c_int, c_int,
+                                              c_int, c_int, c_dbl, c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
+                                              c_i64, c_vp, c_vp, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp,
+                                              c_vp]),
     "nmgp_pairwise_f64": (c_int, [c_vp, c_int, c_int, c_vp]),
     "nmgp_pairwise_f32": (c_int, [c_vp, c_int, c_int, c_vp]),
     "nmgp_pairwise_single_f64": (c_int, [ctypes.POINTER(PairwiseDesc), c_vp]),

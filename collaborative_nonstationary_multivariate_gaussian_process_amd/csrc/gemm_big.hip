@@ -58,6 +58,9 @@ struct BigGemmArgs {
   // per-problem k range from the minibatch segment table (offsets variants): problem b runs
   // k in [seg[kseg[b]], seg[kseg[b] + kspan[b]]) -- rows of the outputs it sums over
   const int32_t* seg; const int32_t* kseg; const int32_t* kspan;
+  // per-problem row range (offsets variants): problem b's rows are [seg[rseg[b]], seg[rseg[b] + rspan[b]]) of A, C
+  // (and E, RS) -- the rows of the outputs it serves; m is their upper bound (tiles past a problem's rows are skipped)
+  const int32_t* rseg; const int32_t* rspan;
   int koff;
   int ksplit;
   int streamk;              // 1: stream-K partition over a persistent grid (batch 1, uniform k)
@@ -112,8 +115,9 @@ __device__ inline void tile_krange(const BigGemmArgs& g, int K, int i0, int j0, 
 // 64 x 32, the tile's columns split over 4 wave columns (two workgroups per CU then hold 4 waves per SIMD: a CU
 // whose other workgroup is in its prologue / epilogue still has two waves per SIMD issuing MFMAs).
 template <bool AK, bool BK, int MODE, int AUX = 0, int NB = 2>
-__device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int koff, float* big_smem, int64_t bat,
-                                             int i0, int j0, int kend, int kt0, int kt1, f32x16 (&acc)[2][NB]) {
+__device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int koff, int M, int64_t roff, float* big_smem,
+                                             int64_t bat, int i0, int j0, int kend, int kt0, int kt1,
+                                             f32x16 (&acc)[2][NB]) {
   constexpr int NT = 512 / NB;                 // threads
   constexpr int NQ = 1024 / NT;                // 16-byte operand loads per thread and operand (4 or 2)
   const int t = threadIdx.x, lane = t & 63;
@@ -122,11 +126,12 @@ __device__ __forceinline__ void big_mainloop(const BigGemmArgs& g, int K, int ko
   const int wr8 = NB == 1 ? (w >> 2) : (w >> 1), wc8 = NB == 1 ? (w & 3) : (w & 1);
   const int fl = g.flags;
   const bool aLo = fl & NMGP_A_LOWER, aUp = fl & NMGP_A_UPPER, bUp = fl & NMGP_B_UPPER, bLo = fl & NMGP_B_LOWER;
-  const float* Ab = g.A + (MODE ? uniform64(g.offA[bat]) : bat * g.sAb) + (AK ? (int64_t)koff : (int64_t)koff * g.lda);
+  const float* Ab = g.A + (MODE ? uniform64(g.offA[bat]) : bat * g.sAb) + (AK ? (int64_t)koff : (int64_t)koff * g.lda) +
+                    (AK ? roff * g.lda : roff);
   const float* Bb = g.B + (MODE ? uniform64(g.offB[bat]) : bat * g.sBb) + (BK ? (int64_t)koff : (int64_t)koff * g.ldb);
   const __amdgpu_buffer_rsrc_t rA =
-      AK ? make_rsrc(Ab, ((int64_t)(g.m - 1) * g.lda + K) * 4)
-                  : make_rsrc(Ab, ((int64_t)(K - 1) * g.lda + g.m) * 4);
+      AK ? make_rsrc(Ab, ((int64_t)(M - 1) * g.lda + K) * 4)
+                  : make_rsrc(Ab, ((int64_t)(K - 1) * g.lda + M) * 4);
   const __amdgpu_buffer_rsrc_t rB =
       BK ? make_rsrc(Bb, ((int64_t)(g.n - 1) * g.ldb + K) * 4)
                   : make_rsrc(Bb, ((int64_t)(K - 1) * g.ldb + g.n) * 4);
@@ -400,8 +405,8 @@ __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S,
 // E must not alias C.  A is a template parameter so every accumulator index is a constant.
 template <int MODE, int A, int NB = 2>
 __device__ __forceinline__ void big_epi_half(const BigGemmArgs& g, float* Cb, __amdgpu_buffer_rsrc_t rCb,
-                                             __amdgpu_buffer_rsrc_t rEb, __amdgpu_buffer_rsrc_t rRS, int i0, int j0,
-                                             const f32x16 (&acc)[2][NB]) {
+                                             __amdgpu_buffer_rsrc_t rEb, __amdgpu_buffer_rsrc_t rRS, int M, int i0,
+                                             int j0, const f32x16 (&acc)[2][NB]) {
   constexpr bool EPI = MODE == 2;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -419,7 +424,7 @@ __device__ __forceinline__ void big_epi_half(const BigGemmArgs& g, float* Cb, __
     for (int r = 0; r < 16; ++r) {
       const int i = ib + (r & 3) + 8 * (r >> 2);
       // (elements that OUT_TRIL zeroes are not read: a third of C's traffic in the batched L-bar forms)
-      const bool ok = i < g.m && j < g.n && (!lower || j <= i) && !(tril && j > i);
+      const bool ok = i < M && j < g.n && (!lower || j <= i) && !(tril && j > i);
       cv[b][r] = ldc ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                            rCb, ok ? (uint32_t)(((int64_t)i * g.sCi + (int64_t)j * g.sCj) * 4) : 0x80000000u, 0, 0))
                      : 0.0f;
@@ -428,7 +433,7 @@ __device__ __forceinline__ void big_epi_half(const BigGemmArgs& g, float* Cb, __
         const float e = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
             rEb, oke ? (uint32_t)(((int64_t)i * g.sEi + (int64_t)j * g.sEj) * 4) : 0x80000000u, 0, 0));
         const float rv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-            rRS, i < g.m ? (uint32_t)(i * 4) : 0x80000000u, 0, 0));
+            rRS, i < M ? (uint32_t)(i * 4) : 0x80000000u, 0, 0));
         ev[b][r] = g.gamma * rv * e;
       } else {
         ev[b][r] = 0.0f;
@@ -443,7 +448,7 @@ __device__ __forceinline__ void big_epi_half(const BigGemmArgs& g, float* Cb, __
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int i = ib + (r & 3) + 8 * (r >> 2);
-      if (i < g.m && j < g.n && (!lower || j <= i)) {
+      if (i < M && j < g.n && (!lower || j <= i)) {
         float x = v[r];
         if constexpr (MODE == 1) {
           if (i == j) x += g.diag_add;
@@ -460,17 +465,15 @@ __device__ __forceinline__ void big_epi_half(const BigGemmArgs& g, float* Cb, __
 
 // C = alpha * acc + beta * C (+ diag_add, + the KL epilogue) on the stored part of the tile.
 template <int MODE, int NB = 2>
-__device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, int i0, int j0, f32x16 (&acc)[2][NB]) {
+__device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, float* Cb, const float* Eb, const float* rs, int M,
+                                             int i0, int j0, f32x16 (&acc)[2][NB]) {
   constexpr bool EPI = MODE == 2;
-  float* Cb = g.C + (MODE ? uniform64(g.offC[bat]) : bat * g.sCb);
-  const float* Eb = EPI ? g.E + (g.offE ? uniform64(g.offE[bat]) : 0) : nullptr;
-  const float* rs = EPI ? g.RS + (g.offRS ? uniform64(g.offRS[bat]) : 0) : nullptr;
-  const __amdgpu_buffer_rsrc_t rCb = make_rsrc(Cb, ((int64_t)(g.m - 1) * g.sCi + (int64_t)(g.n - 1) * g.sCj + 1) * 4);
+  const __amdgpu_buffer_rsrc_t rCb = make_rsrc(Cb, ((int64_t)(M - 1) * g.sCi + (int64_t)(g.n - 1) * g.sCj + 1) * 4);
   const __amdgpu_buffer_rsrc_t rEb =
-      make_rsrc(EPI ? Eb : Cb, EPI ? ((int64_t)(g.m - 1) * g.sEi + (int64_t)(g.n - 1) * g.sEj + 1) * 4 : 0);
-  const __amdgpu_buffer_rsrc_t rRS = make_rsrc(EPI ? rs : Cb, EPI ? (int64_t)g.m * 4 : 0);
-  big_epi_half<MODE, 0, NB>(g, Cb, rCb, rEb, rRS, i0, j0, acc);
-  big_epi_half<MODE, 1, NB>(g, Cb, rCb, rEb, rRS, i0, j0, acc);
+      make_rsrc(EPI ? Eb : Cb, EPI ? ((int64_t)(M - 1) * g.sEi + (int64_t)(g.n - 1) * g.sEj + 1) * 4 : 0);
+  const __amdgpu_buffer_rsrc_t rRS = make_rsrc(EPI ? rs : Cb, EPI ? (int64_t)M * 4 : 0);
+  big_epi_half<MODE, 0, NB>(g, Cb, rCb, rEb, rRS, M, i0, j0, acc);
+  big_epi_half<MODE, 1, NB>(g, Cb, rCb, rEb, rRS, M, i0, j0, acc);
 }
 
 // Row-vector epilogue through LDS (row-contiguous C, and E, 16-byte aligned): the accumulators (each lane holds 16
@@ -482,7 +485,7 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, int64_t bat, 
 constexpr int BCP = 136;   // LDS pitch of the C image (floats): lanes 32..63 of a column write land 32 banks over
 template <int MODE, int NB = 2>
 __device__ __forceinline__ void big_epilogue_rows(const BigGemmArgs& g, float* Cb, const float* Eb, const float* rs,
-                                                  int i0, int j0, const f32x16 (&acc)[2][NB], float* sm) {
+                                                  int M, int i0, int j0, const f32x16 (&acc)[2][NB], float* sm) {
   constexpr bool EPI = MODE == 2;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -498,7 +501,7 @@ __device__ __forceinline__ void big_epilogue_rows(const BigGemmArgs& g, float* C
   __syncthreads();
   // the scalar arguments the chunk loop uses, read once (left in the argument struct, several were spilled and
   // re-read from scratch per chunk)
-  const int gm = g.m, gn = g.n;
+  const int gm = M, gn = g.n;
   const int64_t sCi = g.sCi, sEi = EPI ? g.sEi : 0;
   const float alpha = g.alpha, beta = g.beta, dadd = g.diag_add, gamma = EPI ? g.gamma : 0.0f;
   const bool lower = g.flags & NMGP_OUT_LOWER;
@@ -628,6 +631,19 @@ __global__ __launch_bounds__(512 / NB, 4 / NB) void gemm_big_kernel(const BigGem
       koff = k0;
     }
   }
+  // this problem's rows (row-segment variants): read where needed rather than kept live across the main loop
+  auto rows_of = [&](int& M, int64_t& roff) {
+    M = g.m;
+    roff = 0;
+    if constexpr (MODE != 0) {
+      if (g.rseg != nullptr) {
+        const int s0 = uniform32(g.rseg[bat]);
+        const int r0 = uniform32(g.seg[s0]), r1 = uniform32(g.seg[s0 + uniform32(g.rspan[bat])]);
+        M = min(g.m, max(0, r1 - r0));
+        roff = r0;
+      }
+    }
+  };
 
   // One work segment per pass: a (tile, k-tile range).  Data-parallel / split-K grids run one
   // pass.  Stream-K (batch 1, every tile the same k range): workgroup w owns iterations
@@ -678,8 +694,15 @@ __global__ __launch_bounds__(512 / NB, 4 / NB) void gemm_big_kernel(const BigGem
     int tm, tn;
     tile_coords(g, tile, tm, tn);
     const int i0 = tm * BBM, j0 = tn * BBN;
+    int M;
+    int64_t roff;
+    rows_of(M, roff);
+    if (i0 >= M) {          // past this problem's rows (row-segment variants): nothing to compute or store
+      it += step;
+      continue;
+    }
     zero_acc(acc);
-    big_mainloop<AK, BK, MODE, 0, NB>(g, K, koff, big_smem, bat, i0, j0, kend, kt0, kt1, acc);
+    big_mainloop<AK, BK, MODE, 0, NB>(g, K, koff, M, roff, big_smem, bat, i0, j0, kend, kt0, kt1, acc);
     BIG_STAMP(2);
     bool store = true;
     if (nparts > 1) {
@@ -694,17 +717,18 @@ __global__ __launch_bounds__(512 / NB, 4 / NB) void gemm_big_kernel(const BigGem
     }
     BIG_STAMP(3);
     if (store) {
+      rows_of(M, roff);
       // row-vector epilogue when C (and E) rows are contiguous and 16-byte aligned (every engine product)
       constexpr bool EPI = MODE == 2;
-      float* Cb = g.C + (MODE ? uniform64(g.offC[bat]) : bat * g.sCb);
-      const float* Eb = EPI ? g.E + (g.offE ? uniform64(g.offE[bat]) : 0) : nullptr;
-      const float* rsb = EPI ? g.RS + (g.offRS ? uniform64(g.offRS[bat]) : 0) : nullptr;
+      float* Cb = g.C + (MODE ? uniform64(g.offC[bat]) : bat * g.sCb) + roff * g.sCi;
+      const float* Eb = EPI ? g.E + (g.offE ? uniform64(g.offE[bat]) : 0) + roff * g.sEi : nullptr;
+      const float* rsb = EPI ? g.RS + (g.offRS ? uniform64(g.offRS[bat]) : 0) + roff : nullptr;
       const bool rows = g.sCj == 1 && (g.sCi & 3) == 0 && (((uintptr_t)Cb) & 15) == 0 &&
                         (!EPI || (g.sEj == 1 && (g.sEi & 3) == 0 && (((uintptr_t)Eb) & 15) == 0));
       if (rows)
-        big_epilogue_rows<MODE>(g, Cb, Eb, rsb, i0, j0, acc, big_smem);
+        big_epilogue_rows<MODE>(g, Cb, Eb, rsb, M, i0, j0, acc, big_smem);
       else
-        big_epilogue<MODE>(g, bat, i0, j0, acc);
+        big_epilogue<MODE>(g, Cb, Eb, rsb, M, i0, j0, acc);
     }
     it += step;
   }
@@ -746,7 +770,7 @@ __global__ __launch_bounds__(256, 2) void potrf_step_kernel(PotrfStepArgs pa) {
   g.A = pa.P; g.lda = pa.lda; g.B = pa.X; g.ldb = 128; g.C = pa.P; g.sCi = pa.lda; g.sCj = 1;
   g.m = pa.n2; g.n = pa.nb; g.k = pa.nb; g.flags = NMGP_B_UPPER; g.alpha = 1.0f; g.beta = 0.0f;
   zero_acc(acc);
-  big_mainloop<true, true, 0>(g, g.k, 0, big_smem, 0, i0, 0, pa.nb, 0, pa.nb, acc);
+  big_mainloop<true, true, 0>(g, g.k, 0, g.m, 0, big_smem, 0, i0, 0, pa.nb, 0, pa.nb, acc);
   {
     const __amdgpu_buffer_rsrc_t rC = make_rsrc(pa.P, ((int64_t)(pa.n2 - 1) * pa.lda + pa.nb) * 4);
 #pragma unroll
@@ -784,7 +808,7 @@ __global__ __launch_bounds__(256, 2) void potrf_step_kernel(PotrfStepArgs pa) {
   g2.A = pa.P; g2.lda = pa.lda; g2.B = pa.P; g2.ldb = pa.lda; g2.C = pa.C; g2.sCi = pa.lda; g2.sCj = 1;
   g2.m = pa.n2; g2.n = pa.c1; g2.k = pa.nb; g2.flags = 0; g2.alpha = -1.0f; g2.beta = 1.0f;
   zero_acc(acc);
-  big_mainloop<true, true, 0, 16>(g2, g2.k, 0, big_smem, 0, i0, 0, pa.nb, 0, pa.nb, acc);
+  big_mainloop<true, true, 0, 16>(g2, g2.k, 0, g2.m, 0, big_smem, 0, i0, 0, pa.nb, 0, pa.nb, acc);
   if (t == 0) {
     const int old = __hip_atomic_fetch_add(pa.flag + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old == (int)gridDim.x - 1) {   // every reader is past its loads of L_0: re-arm for the next launch
@@ -792,7 +816,7 @@ __global__ __launch_bounds__(256, 2) void potrf_step_kernel(PotrfStepArgs pa) {
       __hip_atomic_store(pa.flag + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  big_epilogue<0>(g2, 0, i0, 0, acc);
+  big_epilogue<0>(g2, g2.C, nullptr, nullptr, g2.m, i0, 0, acc);
 }
 
 // Row-panel variant (the default): the step kernel above runs two dependent 128x128x128 products on each
@@ -974,6 +998,7 @@ struct BigEpi {
   const float* RS = nullptr; const int64_t* offRS = nullptr;
   float gamma = 0.0f;
   const int32_t* seg = nullptr; const int32_t* kseg = nullptr; const int32_t* kspan = nullptr;
+  const int32_t* rseg = nullptr; const int32_t* rspan = nullptr;
 };
 
 static int gemm_big_f32_ex(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C,
@@ -991,7 +1016,10 @@ static int gemm_big_f32_ex(const float* A, int64_t lda, const float* B, int64_t 
   g.E = ep.E; g.offE = ep.offE; g.sEi = ep.sEi; g.sEj = ep.sEj;
   g.RS = ep.RS; g.offRS = ep.offRS; g.gamma = ep.gamma;
   g.seg = ep.seg; g.kseg = ep.kseg; g.kspan = ep.kspan; g.koff = 0;
+  g.rseg = ep.rseg; g.rspan = ep.rspan;
   if (ep.kseg != nullptr && (offA == nullptr || ep.seg == nullptr || ep.kspan == nullptr)) return -1;
+  if (ep.rseg != nullptr && (offA == nullptr || ep.seg == nullptr || ep.rspan == nullptr || (flags & NMGP_OUT_LOWER)))
+    return -1;
   if ((flags & NMGP_EPI) && (ep.E == nullptr || ep.RS == nullptr)) return -1;
   {
     // 32-bit buffer offsets: every problem's operand, output and epilogue spans stay below 2 GiB
@@ -1120,13 +1148,13 @@ int nmgp_gemm_big_offsets_f32(const float* A, int64_t lda, const float* B, int64
   return nmgp::gemm_big_f32_ex(A, lda, B, ldb, b_kcontig, C, sCi, sCj, m, n, k, flags, (float)alpha, (float)beta, 0, 0,
                                0, offA, offB, offC, (float)diag_add, batch, ws, s);
 }
-int nmgp_gemm_big_offsets_epi_f32(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb,
-                                  int b_kcontig, float* C, int64_t sCi, int64_t sCj, int m, int n, int k, int flags,
-                                  double alpha, double beta, double diag_add, const int64_t* offA,
-                                  const int64_t* offB, const int64_t* offC, const float* E, const int64_t* offE,
-                                  int64_t sEi, int64_t sEj, const float* RS, const int64_t* offRS, double gamma,
-                                  const int32_t* seg, const int32_t* kseg, const int32_t* kspan, int batch,
-                                  void* ws, hipStream_t s) {
+static int big_offsets_impl(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb, int b_kcontig,
+                            float* C, int64_t sCi, int64_t sCj, int m, int n, int k, int flags, double alpha,
+                            double beta, double diag_add, const int64_t* offA, const int64_t* offB, const int64_t* offC,
+                            const float* E, const int64_t* offE, int64_t sEi, int64_t sEj, const float* RS,
+                            const int64_t* offRS, double gamma, const int32_t* seg, const int32_t* kseg,
+                            const int32_t* kspan, const int32_t* rseg, const int32_t* rspan, int batch, void* ws,
+                            hipStream_t s) {
   if (A == nullptr) return -1;
   if (B == nullptr) return -4;
   if (C == nullptr) return -7;
@@ -1145,8 +1173,33 @@ int nmgp_gemm_big_offsets_epi_f32(const float* A, int64_t lda, int a_kcontig, co
   ep.E = E; ep.offE = offE; ep.sEi = sEi; ep.sEj = sEj;
   ep.RS = RS; ep.offRS = offRS; ep.gamma = (float)gamma;
   if (kseg != nullptr && (seg == nullptr || kspan == nullptr)) return -26;
+  if (rseg != nullptr && (seg == nullptr || rspan == nullptr)) return -27;
+  if (rseg != nullptr && (flags & NMGP_OUT_LOWER)) return -13;
   ep.seg = seg; ep.kseg = kseg; ep.kspan = kspan;
+  ep.rseg = rseg; ep.rspan = rspan;
   return nmgp::gemm_big_f32_ex(A, lda, B, ldb, b_kcontig, C, sCi, sCj, m, n, k, flags, (float)alpha, (float)beta, 0, 0,
                                0, offA, offB, offC, (float)diag_add, batch, ws, s, ep);
+}
+int nmgp_gemm_big_offsets_epi_f32(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb,
+                                  int b_kcontig, float* C, int64_t sCi, int64_t sCj, int m, int n, int k, int flags,
+                                  double alpha, double beta, double diag_add, const int64_t* offA,
+                                  const int64_t* offB, const int64_t* offC, const float* E, const int64_t* offE,
+                                  int64_t sEi, int64_t sEj, const float* RS, const int64_t* offRS, double gamma,
+                                  const int32_t* seg, const int32_t* kseg, const int32_t* kspan, int batch,
+                                  void* ws, hipStream_t s) {
+  return big_offsets_impl(A, lda, a_kcontig, B, ldb, b_kcontig, C, sCi, sCj, m, n, k, flags, alpha, beta, diag_add,
+                          offA, offB, offC, E, offE, sEi, sEj, RS, offRS, gamma, seg, kseg, kspan, nullptr, nullptr,
+                          batch, ws, s);
+}
+int nmgp_gemm_big_offsets_seg_f32(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb,
+                                  int b_kcontig, float* C, int64_t sCi, int64_t sCj, int m, int n, int k, int flags,
+                                  double alpha, double beta, double diag_add, const int64_t* offA,
+                                  const int64_t* offB, const int64_t* offC, const float* E, const int64_t* offE,
+                                  int64_t sEi, int64_t sEj, const float* RS, const int64_t* offRS, double gamma,
+                                  const int32_t* seg, const int32_t* kseg, const int32_t* kspan, const int32_t* rseg,
+                                  const int32_t* rspan, int batch, void* ws, hipStream_t s) {
+  return big_offsets_impl(A, lda, a_kcontig, B, ldb, b_kcontig, C, sCi, sCj, m, n, k, flags, alpha, beta, diag_add,
+                          offA, offB, offC, E, offE, sEi, sEj, RS, offRS, gamma, seg, kseg, kspan, rseg, rspan, batch,
+                          ws, s);
 }
 }

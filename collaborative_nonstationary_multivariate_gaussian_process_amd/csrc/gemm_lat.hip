@@ -72,10 +72,22 @@ __device__ inline void loadv(T (&v)[NV], __amdgpu_buffer_rsrc_t r, uint32_t off,
   }
 }
 
+// One output tile (or COLPACK tile group) of a launch decoded from its descriptor: wave-uniform scalars plus this
+// wave's panel range.  (The operands' buffer resources are rebuilt from it where they are used: a resource carried
+// across the persistent kernel's loop becomes a loop phi the compiler places in VGPRs, and every load a waterfall.)
+struct LatJob {
+  int prob, tid, ks, ksplit, i0, m, K, flags;
+  int64_t r0, k0;
+  int jt[2], tnp[2];
+  bool pack, blkA, blkB, first_tile;
+  int kbA, kbB;
+  int pfirst, pstep, npan, j0, kbeg, kend;
+};
+
+// decode tile `tile` of the launch; false when it has no output (rows past the segment, masked-out tiles)
 template <typename T, int LW, int LKP>
-__device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_desc* __restrict__ descs,
-                                         const int32_t* __restrict__ dyn, T* red, int tile, bool first_tile) {
-  constexpr int NV = LKP / 4;   // k values per lane and operand block in one panel
+__device__ __forceinline__ bool lat_decode(const LatArgs& args, const nmgp_gemm_desc* __restrict__ descs,
+                                           const int32_t* __restrict__ dyn, int tile, bool first_tile, LatJob& J) {
   LAT_STAMP(0);
   int lo = 0, hi = args.nprob - 1;
   while (lo < hi) {
@@ -86,7 +98,7 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
   // wave-uniform problem index: the descriptor then comes in through scalar loads and the buffer
   // resources stay in SGPRs (a VGPR resource would turn every load into a readfirstlane loop)
   lo = __builtin_amdgcn_readfirstlane(lo);
-  const nmgp_gemm_desc d = descs[lo];
+  const nmgp_gemm_desc& d = descs[lo];
   tile -= dyn ? dyn[lo] : d.tile_start;
   LAT_STAMP(1);
   const int ksplit = d.ksplit > 1 ? d.ksplit : 1;
@@ -105,7 +117,7 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
     K = args.seg[d.k_seg + span] - (int)k0;
   }
   const int n = d.n, i0 = tm * LTM;
-  if (i0 >= m) return;
+  if (i0 >= m) return false;
   const int flags = d.flags;
   // The output tiles of this workgroup: one, or with NMGP_LAT_COLPACK (a B-triangular problem whose column
   // tiles have k ranges of 1..T panels) a group of up to two column tiles whose panels add up to <= LW:
@@ -162,102 +174,168 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
     tkend[q] = kend;
     tnp[q] = kend > kbeg ? (kend - kbeg + LKP - 1) / LKP : 0;
   }
-  if (jt[0] < 0 && jt[1] < 0) return;
-
-  const int t = threadIdx.x, lane = t & 63, li = lane & 15, g = lane >> 4;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  using acc_t = typename Mfma<T>::acc_t;
-  acc_t acc[2][2];
+  if (jt[0] < 0 && jt[1] < 0) return false;
+  J.prob = lo;
+  J.tid = tm * d.tiles_n + tn;
+  J.ks = ks;
+  J.ksplit = ksplit;
+  J.i0 = i0;
+  J.m = m;
+  J.K = K;
+  J.flags = flags;
+  J.r0 = r0;
+  J.k0 = k0;
+  J.pack = pack;
+  J.blkA = blkA;
+  J.blkB = blkB;
+  J.first_tile = first_tile;
+  J.kbA = kbA;
+  J.kbB = kbB;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) acc[q >> 1][q & 1] = acc_t{0, 0, 0, 0};
-
+  for (int q = 0; q < 2; ++q) {
+    J.jt[q] = jt[q];
+    J.tnp[q] = tnp[q];
+  }
   // this wave's tile (packed: the tile whose panel range holds panel w; otherwise tile 0, panels w, w+LW, ..)
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int myq = (pack && w >= tnp[0]) ? 1 : 0;
-  const int pfirst = pack ? (myq ? w - tnp[0] : w) : w;
-  const int pstep = pack ? 0x40000000 : LW;
-  const int npan = (pack && myq == 1 && jt[1] < 0) ? 0 : tnp[myq];
-  const int j0 = jt[myq] < 0 ? 0 : jt[myq] * LTN;
-  const int kbeg = tkbeg[myq], kend = tkend[myq];
-  if (pfirst < npan) {
-    constexpr int64_t sz = sizeof(T);
-    const int nkbA = blkA ? (K + kbA - 1) / kbA : 1, kinA = blkA ? kbA : K;
-    const int nkbB = blkB ? (K + kbB - 1) / kbB : 1, kinB = blkB ? kbB : K;
-    const char* baseA = (const char*)d.A + (r0 * d.sA_i + k0 * d.sA_k) * sz;
-    const char* baseB = (const char*)d.B + (k0 * d.sB_k) * sz;
-    const int64_t extA = ((int64_t)(m - 1) * d.sA_i + (int64_t)(kinA - 1) * d.sA_k + (int64_t)(nkbA - 1) * d.sA_kb + 1) * sz;
-    const int64_t extB = ((int64_t)(kinB - 1) * d.sB_k + (int64_t)(n - 1) * d.sB_j + (int64_t)(nkbB - 1) * d.sB_kb + 1) * sz;
-    const __amdgpu_buffer_rsrc_t rA = make_rsrc(baseA, extA);
-    const __amdgpu_buffer_rsrc_t rB = make_rsrc(baseB, extB);
+  J.pfirst = pack ? (myq ? w - tnp[0] : w) : w;
+  J.pstep = pack ? 0x40000000 : LW;
+  J.npan = (pack && myq == 1 && jt[1] < 0) ? 0 : tnp[myq];
+  J.j0 = jt[myq] < 0 ? 0 : jt[myq] * LTN;
+  J.kbeg = tkbeg[myq];
+  J.kend = tkend[myq];
+  return true;
+}
+
+// the operands' buffer resources of a decoded tile (every value readfirstlane'd: provably uniform, so they stay in
+// SGPRs)
+template <typename T>
+__device__ __forceinline__ void lat_rsrc(const LatJob& J, const nmgp_gemm_desc& d, __amdgpu_buffer_rsrc_t& rA,
+                                         __amdgpu_buffer_rsrc_t& rB) {
+  constexpr int64_t sz = sizeof(T);
+  const int m = uniform32(J.m), K = uniform32(J.K);
+  const int64_t r0 = uniform64(J.r0), k0 = uniform64(J.k0);
+  const bool blkA = uniform32(J.blkA), blkB = uniform32(J.blkB);
+  const int kbA = uniform32(J.kbA), kbB = uniform32(J.kbB);
+  const int nkbA = blkA ? (K + kbA - 1) / kbA : 1, kinA = blkA ? kbA : K;
+  const int nkbB = blkB ? (K + kbB - 1) / kbB : 1, kinB = blkB ? kbB : K;
+  const char* baseA = (const char*)d.A + (r0 * d.sA_i + k0 * d.sA_k) * sz;
+  const char* baseB = (const char*)d.B + (k0 * d.sB_k) * sz;
+  const int64_t extA = ((int64_t)(m - 1) * d.sA_i + (int64_t)(kinA - 1) * d.sA_k + (int64_t)(nkbA - 1) * d.sA_kb + 1) * sz;
+  const int64_t extB = ((int64_t)(kinB - 1) * d.sB_k + (int64_t)(d.n - 1) * d.sB_j + (int64_t)(nkbB - 1) * d.sB_kb + 1) * sz;
+  rA = make_rsrc(baseA, extA);
+  rB = make_rsrc(baseB, extB);
+}
+
+// this lane's operands of panel p (NV k values of two A rows and two B columns)
+template <typename T, int LW, int LKP>
+__device__ __forceinline__ void lat_load(const LatJob& J, const nmgp_gemm_desc& d, int p, __amdgpu_buffer_rsrc_t rA,
+                                         __amdgpu_buffer_rsrc_t rB, T (&a)[2][LKP / 4], T (&b)[2][LKP / 4]) {
+  constexpr int NV = LKP / 4;
+  constexpr int64_t sz = sizeof(T);
+  const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  const int kp = J.kbeg + p * LKP;
+  const int ba = kp / J.kbA, bb = kp / J.kbB;        // k-block of the panel (panels never straddle one)
+  const int kkA0 = kp - ba * (J.blkA ? J.kbA : 0), kkB0 = kp - bb * (J.blkB ? J.kbB : 0);   // block-local k
+  const int ka = kkA0 + NV * g, kbl = kkB0 + NV * g;   // this lane's first k (block-local)
+  const uint32_t stA = (uint32_t)(d.sA_k * sz), stB = (uint32_t)(d.sB_k * sz);
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi) {
+    const int64_t row = J.i0 + 16 * bi + li;
+    loadv<T, NV>(a[bi], rA, (uint32_t)((row * d.sA_i + (int64_t)ka * d.sA_k + (int64_t)ba * d.sA_kb) * sz), stA,
+                 d.sA_k == 1);
+  }
+#pragma unroll
+  for (int bj = 0; bj < 2; ++bj) {
+    const int64_t col = J.j0 + 16 * bj + li;
+    loadv<T, NV>(b[bj], rB, (uint32_t)(((int64_t)kbl * d.sB_k + col * d.sB_j + (int64_t)bb * d.sB_kb) * sz), stB,
+                 d.sB_k == 1);
+  }
+}
+
+// the first panel of a decoded tile (the one a persistent workgroup loads ahead)
+template <typename T, int LW, int LKP>
+__device__ __forceinline__ void lat_load_first(const LatJob& J, const nmgp_gemm_desc* __restrict__ descs,
+                                               T (&a)[2][LKP / 4], T (&b)[2][LKP / 4]) {
+  if (J.pfirst >= J.npan) return;
+  const nmgp_gemm_desc& d = descs[uniform32(J.prob)];
+  __amdgpu_buffer_rsrc_t rA, rB;
+  lat_rsrc<T>(J, d, rA, rB);
+  lat_load<T, LW, LKP>(J, d, J.pfirst, rA, rB, a, b);
+}
+
+// k scaling, element masks and the MFMAs of panel p
+template <typename T, int LW, int LKP>
+__device__ __forceinline__ void lat_mma(const LatJob& J, const nmgp_gemm_desc& d, int p, T (&a)[2][LKP / 4],
+                                        T (&b)[2][LKP / 4], typename Mfma<T>::acc_t (&acc)[2][2]) {
+  constexpr int NV = LKP / 4;
+  const bool first_tile = J.first_tile;
+  LAT_STAMP(2);
+  const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  const int flags = J.flags;
+  const int kp = J.kbeg + p * LKP;
+  const int ba = kp / J.kbA, bb = kp / J.kbB;
+  const int kkA0 = kp - ba * (J.blkA ? J.kbA : 0), kkB0 = kp - bb * (J.blkB ? J.kbB : 0);
+  const int ka = kkA0 + NV * g, kbl = kkB0 + NV * g;
+  if (flags & NMGP_KSCALE) {
     const GPtr<const T> ksc = (GPtr<const T>)d.kscale;
-    const bool aC = d.sA_k == 1, bC = d.sB_k == 1;
-    const uint32_t stA = (uint32_t)(d.sA_k * sz), stB = (uint32_t)(d.sB_k * sz);
-    const bool aLo = flags & NMGP_A_LOWER, aUp = flags & NMGP_A_UPPER;
-    const bool bLo = flags & NMGP_B_LOWER, bUp = flags & NMGP_B_UPPER;
-    for (int p = pfirst; p < npan; p += pstep) {
-      const int kp = kbeg + p * LKP;
-      const int ba = kp / kbA, bb = kp / kbB;        // k-block of the panel (panels never straddle one)
-      const int kkA0 = kp - ba * (blkA ? kbA : 0), kkB0 = kp - bb * (blkB ? kbB : 0);   // block-local k
-      const int ka = kkA0 + NV * g, kbl = kkB0 + NV * g;   // this lane's first k (block-local)
-      T a[2][NV], b[2][NV];
+    const int kg = kp + NV * g;
 #pragma unroll
-      for (int bi = 0; bi < 2; ++bi) {
-        const int64_t row = i0 + 16 * bi + li;
-        loadv<T, NV>(a[bi], rA, (uint32_t)((row * d.sA_i + (int64_t)ka * d.sA_k + (int64_t)ba * d.sA_kb) * sz), stA, aC);
-      }
+    for (int s = 0; s < NV; ++s) {
+      const T sc = ksc[J.k0 + min(kg + s, J.K - 1)];
+      b[0][s] *= sc;
+      b[1][s] *= sc;
+    }
+  }
+  const bool aLo = flags & NMGP_A_LOWER, aUp = flags & NMGP_A_UPPER;
+  const bool bLo = flags & NMGP_B_LOWER, bUp = flags & NMGP_B_UPPER;
+  const int i0 = J.i0, j0 = J.j0, kend = J.kend;
+  // element masks only on panels that need them (wave-uniform tests)
+  const bool tail = kp + LKP > kend;
+  const bool mA = tail || (aLo && kkA0 + LKP - 1 > i0) || (aUp && kkA0 < i0 + LTM - 1);
+  // (the k tail is masked in both operands: memory past kend inside an operand's extent may hold
+  // non-finite values, and 0 * inf would reach the sum)
+  const bool mB = tail || (bLo && j0 + LTN - 1 > kkB0) || (bUp && kkB0 + LKP - 1 > j0);
+  if (mA) {
 #pragma unroll
-      for (int bj = 0; bj < 2; ++bj) {
-        const int64_t col = j0 + 16 * bj + li;
-        loadv<T, NV>(b[bj], rB, (uint32_t)(((int64_t)kbl * d.sB_k + col * d.sB_j + (int64_t)bb * d.sB_kb) * sz), stB, bC);
-      }
-      LAT_STAMP(2);
-      if (flags & NMGP_KSCALE) {
-        const int kg = kp + NV * g;
-#pragma unroll
-        for (int s = 0; s < NV; ++s) {
-          const T sc = ksc[k0 + min(kg + s, K - 1)];
-          b[0][s] *= sc;
-          b[1][s] *= sc;
-        }
-      }
-      // element masks only on panels that need them (wave-uniform tests)
-      const bool tail = kp + LKP > kend;
-      const bool mA = tail || (aLo && kkA0 + LKP - 1 > i0) || (aUp && kkA0 < i0 + LTM - 1);
-      // (the k tail is masked in both operands: memory past kend inside an operand's extent may hold
-      // non-finite values, and 0 * inf would reach the sum)
-      const bool mB = tail || (bLo && j0 + LTN - 1 > kkB0) || (bUp && kkB0 + LKP - 1 > j0);
-      if (mA) {
-#pragma unroll
-        for (int bi = 0; bi < 2; ++bi) {
-          const int gi = i0 + 16 * bi + li;
-#pragma unroll
-          for (int s = 0; s < NV; ++s) {
-            const int kk = ka + s;
-            const bool ok = (kp + NV * g + s < kend) && !(aLo && kk > gi) && !(aUp && kk < gi);
-            a[bi][s] = keep_if(a[bi][s], ok);
-          }
-        }
-      }
-      if (mB) {
-#pragma unroll
-        for (int bj = 0; bj < 2; ++bj) {
-          const int gj = j0 + 16 * bj + li;
-#pragma unroll
-          for (int s = 0; s < NV; ++s) {
-            const int kk = kbl + s;
-            const bool ok = (kp + NV * g + s < kend) && !(bLo && gj > kk) && !(bUp && gj < kk);
-            b[bj][s] = keep_if(b[bj][s], ok);
-          }
-        }
-      }
+    for (int bi = 0; bi < 2; ++bi) {
+      const int gi = i0 + 16 * bi + li;
 #pragma unroll
       for (int s = 0; s < NV; ++s) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q >> 1][q & 1] = Mfma<T>::mma(a[q >> 1][s], b[q & 1][s], acc[q >> 1][q & 1]);
+        const int kk = ka + s;
+        const bool ok = (kp + NV * g + s < kend) && !(aLo && kk > gi) && !(aUp && kk < gi);
+        a[bi][s] = keep_if(a[bi][s], ok);
       }
     }
   }
+  if (mB) {
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj) {
+      const int gj = j0 + 16 * bj + li;
+#pragma unroll
+      for (int s = 0; s < NV; ++s) {
+        const int kk = kbl + s;
+        const bool ok = (kp + NV * g + s < kend) && !(bLo && gj > kk) && !(bUp && gj < kk);
+        b[bj][s] = keep_if(b[bj][s], ok);
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < NV; ++s) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q >> 1][q & 1] = Mfma<T>::mma(a[q >> 1][s], b[q & 1][s], acc[q >> 1][q & 1]);
+  }
+}
+
+// the waves' partial tiles summed through LDS in wave order, split-K hand-off, epilogue and store
+template <typename T, int LW, int LKP>
+__device__ __forceinline__ void lat_finish(const LatArgs& args, const LatJob& J, const nmgp_gemm_desc& d,
+                                           typename Mfma<T>::acc_t (&acc)[2][2], T* red) {
+  const bool first_tile = J.first_tile;
   LAT_STAMP(3);
-  // partial tiles of the waves -> LDS, summed in wave order per output tile
+  const int t = threadIdx.x, lane = t & 63, li = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
 #pragma unroll
@@ -267,13 +345,17 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
   lds_barrier();
   LAT_STAMP(4);
   constexpr int NE = (LTM * LTN) / (64 * LW);   // output values per thread and tile
-  const int ntl = (jt[1] >= 0) ? 2 : 1;
+  const bool pack = J.pack;
+  const int ksplit = J.ksplit, i0 = J.i0, m = J.m, flags = J.flags;
+  const int64_t r0 = J.r0;
+  const int ntl = (J.jt[1] >= 0) ? 2 : 1;
   for (int qt = 0; qt < ntl; ++qt) {
-    if (jt[qt] < 0) continue;
+    const int jtq = qt ? J.jt[1] : J.jt[0];      // (selects, not an indexed member: J stays in registers)
+    if (jtq < 0) continue;
     // waves holding this tile's partials: all (unpacked) or the tile's panel range (packed)
-    const int wb = pack ? (qt ? tnp[0] : 0) : 0;
-    const int we = pack ? (qt ? tnp[0] + tnp[1] : tnp[0]) : LW;
-    const int tj0 = jt[qt] * LTN;
+    const int wb = pack ? (qt ? J.tnp[0] : 0) : 0;
+    const int we = pack ? (qt ? J.tnp[0] + J.tnp[1] : J.tnp[0]) : LW;
+    const int tj0 = jtq * LTN;
     T vals[NE];
 #pragma unroll
     for (int q = 0; q < NE; ++q) {
@@ -287,17 +369,16 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
       // stores drained, bumps the tile's counter; the last arriver sums all partials in chunk order from
       // memory (sc1 loads bypass the stale L1) and runs the epilogue.  No waiting, so no co-residency
       // assumption; the last arriver re-arms the counter for the next launch.  (Never packed.)
-      const int tid = tm * d.tiles_n + tn;
-      T* wsb = (T*)d.ws + (int64_t)tid * ksplit * (LTM * LTN);
+      T* wsb = (T*)d.ws + (int64_t)J.tid * ksplit * (LTM * LTN);
       const __amdgpu_buffer_rsrc_t rws = make_rsrc(wsb, (int64_t)ksplit * (LTM * LTN) * (int64_t)sizeof(T));
 #pragma unroll
       for (int q = 0; q < NE; ++q)
-        bstore_sc1<T>(rws, (uint32_t)(((int64_t)ks * (LTM * LTN) + t + 64 * LW * q) * (int64_t)sizeof(T)), vals[q]);
+        bstore_sc1<T>(rws, (uint32_t)(((int64_t)J.ks * (LTM * LTN) + t + 64 * LW * q) * (int64_t)sizeof(T)), vals[q]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       int* s_last = (int*)red;          // the partial tiles in LDS are consumed (vals) -- reuse a word
       if (t == 0) {
-        int32_t* ctr = d.counters + tid;
+        int32_t* ctr = d.counters + J.tid;
         const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int last = old == ksplit - 1;
         if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -326,7 +407,7 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
       const int e = t + 64 * LW * q;
       const int gi = i0 + (e / LTN), gj = tj0 + (e % LTN);
       const T sum = vals[q];
-      if (gi >= m || gj >= n) continue;
+      if (gi >= m || gj >= d.n) continue;
       const bool upper = gj > gi;
       if (upper && (flags & NMGP_OUT_LOWER)) continue;
       const int64_t ci = (r0 + gi) * d.sC_i + (int64_t)gj * d.sC_j;
@@ -351,6 +432,29 @@ __device__ __forceinline__ void lat_tile(const LatArgs& args, const nmgp_gemm_de
   LAT_STAMP(6);
 }
 
+// a decoded tile whose first panel (p = J.pfirst) is in a / b: its MFMAs, the wave's further panels, the finish
+template <typename T, int LW, int LKP>
+__device__ __forceinline__ void lat_run(const LatArgs& args, const nmgp_gemm_desc* __restrict__ descs,
+                                        const LatJob& J, T (&a)[2][LKP / 4], T (&b)[2][LKP / 4], T* red) {
+  const nmgp_gemm_desc& d = descs[uniform32(J.prob)];
+  using acc_t = typename Mfma<T>::acc_t;
+  acc_t acc[2][2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q >> 1][q & 1] = acc_t{0, 0, 0, 0};
+  if (J.pfirst < J.npan) {
+    lat_mma<T, LW, LKP>(J, d, J.pfirst, a, b, acc);
+    if (J.pfirst + J.pstep < J.npan) {      // further rounds (loaded in place)
+      __amdgpu_buffer_rsrc_t rA, rB;
+      lat_rsrc<T>(J, d, rA, rB);
+      for (int p = J.pfirst + J.pstep; p < J.npan; p += J.pstep) {
+        lat_load<T, LW, LKP>(J, d, p, rA, rB, a, b);
+        lat_mma<T, LW, LKP>(J, d, p, a, b, acc);
+      }
+    }
+  }
+  lat_finish<T, LW, LKP>(args, J, d, acc, red);
+}
+
 template <typename T, int LW, int LKP, int OCC>
 __global__ __launch_bounds__(64 * LW, OCC) void gemm_lat_kernel(LatArgs args,
                                                                              const nmgp_gemm_desc* __restrict__ descs,
@@ -360,7 +464,59 @@ __global__ __launch_bounds__(64 * LW, OCC) void gemm_lat_kernel(LatArgs args,
   const int per = (total + 7) >> 3;   // tiles per XCD chunk
   for (int b = blockIdx.x; b < 8 * per; b += gridDim.x) {
     const int tile = (b & 7) * per + (b >> 3);
-    if (tile < total) lat_tile<T, LW, LKP>(args, descs, dyn, red, tile, b == (int)blockIdx.x);
+    LatJob J;
+    if (tile < total && lat_decode<T, LW, LKP>(args, descs, dyn, tile, b == (int)blockIdx.x, J)) {
+      T a[2][LKP / 4], bv[2][LKP / 4];
+      lat_load_first<T, LW, LKP>(J, descs, a, bv);
+      lat_run<T, LW, LKP>(args, descs, J, a, bv, red);
+    }
+    __syncthreads();
+  }
+}
+
+// the next tile with output in this workgroup's sequence b, b + gridDim.x, ... (b advanced past it)
+template <typename T, int LW, int LKP>
+__device__ __forceinline__ bool lat_next(const LatArgs& args, const nmgp_gemm_desc* __restrict__ descs,
+                                         const int32_t* __restrict__ dyn, int total, int per, int lim, int& b,
+                                         LatJob& J) {
+  for (; b < lim; b += gridDim.x) {
+    const int tile = (b & 7) * per + (b >> 3);
+    if (tile < total && lat_decode<T, LW, LKP>(args, descs, dyn, tile, b == (int)blockIdx.x, J)) {
+      b += gridDim.x;
+      return true;
+    }
+  }
+  return false;
+}
+
+// Persistent form for launches with more tiles than one round of workgroups (round 6): one
+// workgroup per CU walks its tiles (the same XCD-chunked order as gemm_lat_kernel) with two tiles in flight -- the
+// first panel of the next tile is loaded before the current tile's MFMAs and LDS reduction, so its global round
+// trip hides under them.  Each tile is computed exactly as gemm_lat_kernel computes it (same panels per wave, same
+// reduction order): results are bit-identical to the non-persistent launch.
+template <typename T, int LW, int LKP>
+__global__ __launch_bounds__(64 * LW, 1) void gemm_lat_pipe_kernel(LatArgs args,
+                                                                   const nmgp_gemm_desc* __restrict__ descs,
+                                                                   const int32_t* __restrict__ dyn) {
+  __shared__ T red[LW * LTM * LTN];
+  constexpr int NV = LKP / 4;
+  const int total = __builtin_amdgcn_readfirstlane(dyn ? dyn[args.nprob] : args.total);
+  const int per = (total + 7) >> 3;
+  const int lim = 8 * per;
+  int b = blockIdx.x;
+  LatJob J0, J1;
+  T a0[2][NV], b0[2][NV], a1[2][NV], b1[2][NV];
+  bool h0 = lat_next<T, LW, LKP>(args, descs, dyn, total, per, lim, b, J0);
+  if (h0) lat_load_first<T, LW, LKP>(J0, descs, a0, b0);
+  while (h0) {
+    const bool h1 = lat_next<T, LW, LKP>(args, descs, dyn, total, per, lim, b, J1);
+    if (h1) lat_load_first<T, LW, LKP>(J1, descs, a1, b1);
+    lat_run<T, LW, LKP>(args, descs, J0, a0, b0, red);
+    __syncthreads();
+    if (!h1) break;
+    h0 = lat_next<T, LW, LKP>(args, descs, dyn, total, per, lim, b, J0);
+    if (h0) lat_load_first<T, LW, LKP>(J0, descs, a0, b0);
+    lat_run<T, LW, LKP>(args, descs, J1, a1, b1, red);
     __syncthreads();
   }
 }
@@ -404,7 +560,7 @@ __global__ __launch_bounds__(256) void lat_plan_kernel(const nmgp_gemm_desc* __r
 
 template <typename T>
 int launch_lat(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles, const int32_t* d_seg, int32_t* d_plan,
-               int grid, hipStream_t s, bool planned = false) {
+               int grid, hipStream_t s, bool planned = false, bool pipe = false) {
   if (d_desc == nullptr) return -1;
   if (nprob <= 0) return -2;
   if (total_tiles < 0) return -3;
@@ -423,6 +579,22 @@ int launch_lat(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles, const i
     }
     a.dyn_start = d_plan;
     if (grid > 0) wgs = min(wgs, ((grid + 7) / 8) * 8);   // a multiple of 8 keeps each workgroup on one XCD chunk
+  }
+  if (pipe) {
+    // persistent: one workgroup per CU (the XCD chunking needs a multiple of 8), never more than the tiles
+    static int n_cu = 0;
+    if (n_cu == 0) {
+      int dev = 0, v = 0;
+      if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                  hipSuccess && v > 0)
+        n_cu = v;
+      else
+        n_cu = 256;
+    }
+    wgs = min(wgs, max(8, (n_cu / 8) * 8));
+    hipLaunchKernelGGL((gemm_lat_pipe_kernel<T, 8, 32>), dim3(wgs), dim3(512), 0, s, a, d_desc, a.dyn_start);
+    NMGP_CHECK_LAUNCH();
+    return NMGP_OK;
   }
   // 8 waves x 32-wide panels with registers capped at 128 so two workgroups share a CU (round 2: PM2.5 step +1%
   // over one workgroup per CU).  hip_ops.GemmGroup sizes split-K for 8 waves x 32.
@@ -459,5 +631,16 @@ int nmgp_gemm_grouped_lat_planned_f32(const nmgp_gemm_desc* d, int np, int tt, c
                                       int grid, hipStream_t s) {
   if (!plan) return -5;
   return nmgp::launch_lat<float>(d, np, tt, seg, plan, grid, s, true);
+}
+// persistent two-tiles-in-flight launches (same arguments; planned != 0: the device tile plan is already computed)
+int nmgp_gemm_grouped_lat_pipe_f64(const nmgp_gemm_desc* d, int np, int tt, const int32_t* seg, int32_t* plan,
+                                   int planned, hipStream_t s) {
+  if (planned && !plan) return -5;
+  return nmgp::launch_lat<double>(d, np, tt, seg, plan, 0, s, planned != 0, true);
+}
+int nmgp_gemm_grouped_lat_pipe_f32(const nmgp_gemm_desc* d, int np, int tt, const int32_t* seg, int32_t* plan,
+                                   int planned, hipStream_t s) {
+  if (planned && !plan) return -5;
+  return nmgp::launch_lat<float>(d, np, tt, seg, plan, 0, s, planned != 0, true);
 }
 }

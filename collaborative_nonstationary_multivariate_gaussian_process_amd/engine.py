@@ -165,11 +165,16 @@ class DsviEngine:
         n_out = (self.pair_range[1] - self.pair_range[0]) if self.pair_range is not None else D
         self.pair_stream = (self.Q > 0 and B <= 32 * max(1, n_out) and M % 4 == 0 and M <= 1024
                             and os.environ.get("NMGP_PAIR_STREAM", "1") != "0")
-        self.Zp = e(D, B, M) if self.pair_stream else None   # per-pair P-bar products W-hat_ij L_ij^T, slot j
+        self.big_side = self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0"
+        # round 6: with big_side the row-segmented B x M x M products (W = P L, P-bar = W-hat L^T) run on the 128x128
+        # kernel too; NMGP_BIG_ROWS=0 keeps them on the grouped kernel (A/B and equivalence switch)
+        self.big_rows = self.big_side and os.environ.get("NMGP_BIG_ROWS", "1") != "0"
+        # per-pair P-bar products W-hat_ij L_ij^T, slot j (pair kernels, or the 128x128 kernel at M >= 512)
+        self.Zp = e(D, B, M) if (self.pair_stream or (self.big_rows and self.Q > 0)) else None
         # HCP / ECoG shapes (fp32, M >= 512): the D+Q factor products run on the 128x128 f32 MFMA kernel at
         # per-factor offsets (BigBatch) instead of the grouped 64x64 tiles.  NMGP_BIG_SIDE=0 keeps them on the
-        # grouped kernel: the only schedule switch left, for tests/test_gpu_engine.py's equivalence check
-        self.big_side = self.dt == torch.float32 and M >= 512 and os.environ.get("NMGP_BIG_SIDE", "1") != "0"
+        # grouped kernel: the only schedule switch left, for tests/test_gpu_engine.py's equivalence check (set above,
+        # where the per-pair Z buffer is sized)
         # round 6: fp64 engines of 128 <= M <= 256 run the GP priors as two fused launches (nmgp_chol_tp_f64): the
         # RBF priors' K22 built, factored and inverted with K12 / T / P of their rows formed by the same launch, and
         # likewise the Gibbs prior with its t-row sample -- no builder, invG / projG or t-row launches on the chain.
@@ -486,6 +491,24 @@ class DsviEngine:
             # later Monte-Carlo samples of compute_ELBO: the pair factors W_P = P_{0,1} L_ij do not depend
             # on the sample (the L priors and Sigma_U are fixed within a call) -- only the D latent ones
             p["quad_W"] = G(d14[:D])
+        if self.big_rows:
+            # fp32 M >= 512 (HCP): the quadratic-form factors W = P L on the 128x128 f32 kernel at per-factor offsets,
+            # each problem's rows from the segment table (round 6: the grouped 64x64 kernel ran them at 21-28 TFLOP/s,
+            # profiles/r04h_hcp_gemm_groups.jsonl).  Same products as d14.
+            rsW = [(d, D - d) if not elbo_mode else (0, d + 1) for d in range(D)]
+            bq_w = self._big_rows(self.P, self.WG, [3 * BM] * D, [sW + d * MM for d in range(D)],
+                                  [d * BM for d in range(D)], rsW, L.B_LOWER, False)
+            p["quad_W"] = bq_w
+            bq_p = None
+            if pairs and not self.pair_stream:
+                sl = [((j, i) if not elbo_mode else (i, j)) for (i, j) in pairs]
+                bq_p = self._big_rows(self.P, self.WP, [(2 if i == j else 1) * BM for (i, j) in pairs],
+                                      [sU + pq(i, j) * MM for (i, j) in pairs], [s_ * BM for s_, _ in sl],
+                                      [(r, 1) for _, r in sl], L.B_LOWER, False)
+                if not elbo_mode:
+                    p["quad_P"] = bq_p
+            if elbo_mode:
+                p["quad"] = H.Seq([bq_w] + ([pair_quad] if self.pair_stream else [bq_p] if bq_p is not None else []))
         if elbo_mode:
             self._plans[key] = p
             return p
@@ -511,6 +534,19 @@ class DsviEngine:
         # profiles/r03za_kt_cap_ab.txt.)
         p["bwd_wG"] = G(d17G)
         p["bwd_wP"] = G(d17P) if d17P else None
+        if self.big_rows:
+            # fp32 M >= 512: Z_d = W-hat_d L_d^T (rows of outputs >= d) on the 128x128 kernel; the pair P-bar in the
+            # per-pair form Z_ij = W-hat_ij L_ij^T into slot j (rows of output i), summed onto P-bar_0 / P-bar_1 in
+            # j order by nmgp_pair_pbar_reduce (the k-blocked d17P products sum the same terms in one k loop)
+            p["bwd_wG"] = self._big_rows(self.WG, self.Zg, [d * BM for d in range(D)], [sW + d * MM for d in range(D)],
+                                         [d * BM for d in range(D)], [(d, D - d) for d in range(D)], L.B_UPPER, True)
+            if pairs and not self.pair_stream:
+                dot = self._big_rows(self.WP, self.Zp, [j * BM for (i, j) in pairs],
+                                     [sU + pq(i, j) * MM for (i, j) in pairs], [j * BM for (i, j) in pairs],
+                                     [(i, 1) for (i, j) in pairs], L.B_UPPER, True)
+                Zp_, Pb1_, Pb2_ = self.Zp, self.Pbar[1], self.Pbar[2]
+                p["bwd_wP"] = H.Seq([dot, lambda s_: H.pair_pbar_reduce(Zp_, BM, Pb1_, Pb2_, M, seg, D, i0, i1, B, M,
+                                                                        s_)])
         if self.pair_stream:
             # Z_ij = W-hat_ij L_ij^T into slot j (rows of output i), then P-bar_1 += Z_ii and P-bar_0 += Z_i0 + ...
             # + Z_i,i-1 in j order (csrc/pairs.hip pair_pbar_reduce)
@@ -1237,6 +1273,13 @@ class DsviEngine:
             self._elbo_sched = cache
         self._run(cache[key], stream, None)
         return self.out
+
+    def _big_rows(self, A, C, offA, offB, offC, rows, flags, b_kcontig):
+        """B x M x M products op(A) L on the 128x128 f32 kernel (BigBatch), L = theta at offB, problem b on the rows
+        [seg[r], seg[r + span]) of A and C, rows[b] = (r, span)."""
+        M = self.M
+        return H.BigBatch(A, self._theta, C, offA, offB, offC, self.B, M, M, lda=M, ldb=M, b_kcontig=b_kcontig,
+                          flags=flags, rseg=(self.seg, [r for r, _ in rows], [s_ for _, s_ in rows]))
 
     def gemm_groups(self):
         """(name, GemmGroup) of the training step, for FLOP accounting."""

@@ -103,6 +103,13 @@ _LAT_MODE = "auto"        # "0": never (the tests compare the two kernels), "for
 # AND long k: the P-bar / L-bar products over several latent blocks or the minibatch) stay on the
 # LDS-pipelined tile kernel (per-group A/B on the box: tools/gemm_group_probe.py)
 _LAT_MAX_ROUNDS = 2
+# persistent two-tiles-in-flight launches (gemm_lat_pipe_kernel) for latency-kernel groups with more tiles than one
+# round of workgroups (two 8-wave workgroups per CU): "auto", "0" (never), "force" (every latency-kernel group).
+# Off by default: measured on the PM2.5 step (round 6, gpurun_out r06l) it LOST -- one workgroup per CU (the second
+# operand buffer needs ~210 VGPRs) leaves 8 waves per CU where the one-tile kernel keeps 16, and the reduction /
+# epilogue phases then idle the matrix cores: bwd_wG 72 -> 135 us, bwd_lbar 100 -> 174 us, step 0.68 -> 0.83 ms
+_LAT_PIPE = os.environ.get("NMGP_LAT_PIPE", "0")
+LAT_ROUND_WGS = 512
 
 
 def _lat_split(descs, seg, target_wgs):
@@ -183,7 +190,7 @@ class GemmGroup:
         hold every CU slot while the critical chain's launches wait for them."""
         self.dtype = dtype
         self.seg = seg
-        self.lat = False
+        self.lat = self.pipe = False
         self._static_plan = False
         # the group owns copies: split-K, tile counts, workspaces and flags are set per group, so a descriptor
         # list shared by two groups (or reused by the caller) never carries one group's choices into another
@@ -302,6 +309,8 @@ class GemmGroup:
         self.descs = list(descs)
         raw = bytes(memoryview(arr).cast("B"))
         self.dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+        # more (expected) tiles than one round of workgroups: the persistent launch (bit-identical results)
+        self.pipe = _LAT_PIPE == "force" or (_LAT_PIPE == "auto" and expect > LAT_ROUND_WGS)
         self.plan, self.grid = None, 0
         if self.seg is not None and dyn_plan and any(d.row_seg >= 0 for d in descs):
             if dyn_plan == "force" or (t >= _DYN_MIN_TILES and expect < 0.5 * t):
@@ -329,8 +338,13 @@ class GemmGroup:
         segp = ctypes.c_void_p(self.seg.data_ptr()) if self.seg is not None else None
         pre = "_planned_" if ((planned or self._static_plan) and self.plan is not None) else "_"
         if self.lat:
-            fn = getattr(L.lib(), "nmgp_gemm_grouped_lat" + pre + _sfx(self.dtype))
             plan = ctypes.c_void_p(self.plan.data_ptr()) if self.plan is not None else None
+            if self.pipe:
+                fn = getattr(L.lib(), "nmgp_gemm_grouped_lat_pipe_" + _sfx(self.dtype))
+                L.check(fn(ctypes.c_void_p(self.dev.data_ptr()), self.n, self.total, segp, plan,
+                           1 if pre == "_planned_" else 0, s), "gemm_grouped_lat_pipe")
+                return
+            fn = getattr(L.lib(), "nmgp_gemm_grouped_lat" + pre + _sfx(self.dtype))
             L.check(fn(ctypes.c_void_p(self.dev.data_ptr()), self.n, self.total, segp, plan, self.grid, s),
                     "gemm_grouped_lat")
             return
@@ -555,11 +569,12 @@ class BigBatch:
     (nmgp_gemm_big_offsets_epi_f32): C_b = alpha op(A_b) op(B_b) + beta C_b (+ diag_add on the diagonal)
     (+ gamma rs_b(i) E_b(i, j) with `epi`).  op(A_b)(i, k) = A_b[i*lda + k] (a_kcontig) or
     A_b[k*lda + i]; op(B_b)(k, j) = B_b[j*ldb + k] (b_kcontig) or B_b[k*ldb + j]; X_b = X + offX[b].
-    epi = (E, offE, (sEi, sEj), RS, offRS, gamma).  Offsets are uploaded once; a call is one launch
-    (graph-capturable)."""
+    epi = (E, offE, (sEi, sEj), RS, offRS, gamma).  kseg / rseg = (seg, [segment index per problem], [segment span
+    per problem]): per-problem k range / row range (rows of A, C, E, RS; m bounds them) from the device segment table.
+    Offsets are uploaded once; a call is one launch (graph-capturable)."""
 
     def __init__(self, A, B, C, offA, offB, offC, m, n, k, *, lda, ldb, b_kcontig, a_kcontig=True, sC=None,
-                 flags=0, alpha=1.0, beta=0.0, diag_add=0.0, epi=None, kseg=None):
+                 flags=0, alpha=1.0, beta=0.0, diag_add=0.0, epi=None, kseg=None, rseg=None):
         for t_, nm in ((A, "A"), (B, "B"), (C, "C")):
             L.require_device(t_, nm)
             assert t_.dtype == torch.float32
@@ -583,6 +598,15 @@ class BigBatch:
             assert seg.dtype == torch.int32 and len(ks) == self.batch and len(sp) == self.batch
             i32 = lambda o: torch.tensor(list(o), dtype=torch.int32, device=dev)
             self.kseg = (seg, i32(ks), i32(sp))
+        self.rseg = None
+        if rseg is not None:
+            assert kseg is None, "BigBatch: row and k segments together are not supported"
+            assert not (flags & L.OUT_LOWER)
+            seg, rs_, sp = rseg
+            assert seg.dtype == torch.int32 and len(rs_) == self.batch and len(sp) == self.batch
+            i32 = lambda o: torch.tensor(list(o), dtype=torch.int32, device=dev)
+            self.rseg = (seg, i32(rs_), i32(sp))
+            self._rseg_host = (list(rs_), list(sp))
         self.args = (m, n, k, lda, a_kcontig, ldb, b_kcontig, sC if sC is not None else (n, 1), flags, alpha, beta,
                      diag_add)
 
@@ -591,6 +615,9 @@ class BigBatch:
         halves not counted; per-problem k from the host copy `seg` of the segment table with kseg)."""
         import types
         m, n, k, _, _, _, _, _, flags, _, _, _ = self.args
+        if self.rseg is not None:
+            return sum(desc_macs(types.SimpleNamespace(m=m, n=n, k=k, flags=flags, row_seg=a, k_seg=-1, seg_span=b,
+                                                       kbA=0), seg) for a, b in zip(*self._rseg_host))
         if self.kseg is None:
             return self.batch * desc_macs(types.SimpleNamespace(m=m, n=n, k=k, flags=flags, row_seg=-1, k_seg=-1,
                                                                 seg_span=0, kbA=0))
@@ -610,6 +637,14 @@ class BigBatch:
         else:
             ep = (None, None, 0, 0, None, None, 0.0)
         kp = tuple(vp(t_.data_ptr()) for t_ in self.kseg) if self.kseg is not None else (None, None, None)
+        if self.rseg is not None:
+            seg, rs_, sp = self.rseg
+            L.check(L.lib().nmgp_gemm_big_offsets_seg_f32(
+                vp(self.A.data_ptr()), lda, 1 if ak else 0, vp(self.B.data_ptr()), ldb, 1 if bk else 0,
+                vp(self.C.data_ptr()), sCi, sCj, m, n, k, flags, alpha, beta, dadd, vp(self.off[0].data_ptr()),
+                vp(self.off[1].data_ptr()), vp(self.off[2].data_ptr()), *ep, vp(seg.data_ptr()), None, None,
+                vp(rs_.data_ptr()), vp(sp.data_ptr()), self.batch, None, s), "gemm_big_offsets_seg")
+            return
         L.check(L.lib().nmgp_gemm_big_offsets_epi_f32(vp(self.A.data_ptr()), lda, 1 if ak else 0,
                                                       vp(self.B.data_ptr()), ldb, 1 if bk else 0,
                                                       vp(self.C.data_ptr()), sCi, sCj, m, n, k, flags, alpha, beta,
@@ -667,6 +702,10 @@ class Seq:
     def __call__(self, stream=None):
         for p_ in self.parts:
             p_(stream)
+
+    def macs(self, seg=None):
+        """Algorithmic multiply-adds of the parts that are products (reductions and other launches add none)."""
+        return sum(p_.macs(seg) for p_ in self.parts if hasattr(p_, "macs"))
 
 
 def potrf_blocked_(A, info=None, ws=None):

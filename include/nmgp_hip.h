@@ -137,6 +137,14 @@ int nmgp_gemm_grouped_lat_planned_f64(const nmgp_gemm_desc* d_desc, int nprob, i
                                       const int32_t* d_seg, int32_t* plan, int grid, hipStream_t stream);
 int nmgp_gemm_grouped_lat_planned_f32(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles,
                                       const int32_t* d_seg, int32_t* plan, int grid, hipStream_t stream);
+/* Persistent latency-kernel launch for groups with more tiles than one round of workgroups: one
+ * workgroup per CU walks its tiles with the next tile's first operand panel loaded under the
+ * current tile's MFMAs and reduction; results bit-identical to nmgp_gemm_grouped_lat_*.
+ * plan != NULL: device tile plan (planned != 0: already computed by nmgp_gemm_plan_lat).       */
+int nmgp_gemm_grouped_lat_pipe_f64(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles,
+                                   const int32_t* d_seg, int32_t* plan, int planned, hipStream_t stream);
+int nmgp_gemm_grouped_lat_pipe_f32(const nmgp_gemm_desc* d_desc, int nprob, int total_tiles,
+                                   const int32_t* d_seg, int32_t* plan, int planned, hipStream_t stream);
 /* one problem passed by value (host descriptor; tiles fields are filled internally)          */
 int nmgp_gemm_f64(const nmgp_gemm_desc* h_desc, const int32_t* d_seg, hipStream_t stream);
 int nmgp_gemm_f32(const nmgp_gemm_desc* h_desc, const int32_t* d_seg, hipStream_t stream);
@@ -285,6 +293,17 @@ int nmgp_gemm_big_offsets_epi_f32(const float* A, int64_t lda, int a_kcontig, co
                                   int64_t sEi, int64_t sEj, const float* RS, const int64_t* offRS, double gamma,
                                   const int32_t* seg, const int32_t* kseg, const int32_t* kspan, int batch,
                                   void* ws, hipStream_t stream);
+/* ... and with per-problem ROW ranges (rseg != NULL): problem b's rows are [seg[rseg[b]], seg[rseg[b] +
+ * rspan[b]]) of A, C (and E, RS), at most m -- the quadratic-form factors W = P L and the P-bar products
+ * W-hat L^T on the rows of the outputs each latent / pair factor serves (code/nmgp_dsvi.py:227-258), on the
+ * 128x128 kernel for the fp32 M >= 512 shapes.  Not with NMGP_OUT_LOWER.                                  */
+int nmgp_gemm_big_offsets_seg_f32(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb,
+                                  int b_kcontig, float* C, int64_t sCi, int64_t sCj, int m, int n, int k, int flags,
+                                  double alpha, double beta, double diag_add, const int64_t* offA,
+                                  const int64_t* offB, const int64_t* offC, const float* E, const int64_t* offE,
+                                  int64_t sEi, int64_t sEj, const float* RS, const int64_t* offRS, double gamma,
+                                  const int32_t* seg, const int32_t* kseg, const int32_t* kspan, const int32_t* rseg,
+                                  const int32_t* rspan, int batch, void* ws, hipStream_t stream);
 
 /* ------------------------------------------------------------------ pairwise kernel builder
  * mode RBF:   K = scale2 * exp(-0.5 * ||x/ls - z/ls||^2)          (code/utils.py:91-94)

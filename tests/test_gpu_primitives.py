@@ -181,13 +181,16 @@ def test_gemm_grouped_device_plan(ops, dt):
     assert rel(outs[1][0], ref) < tol and torch.equal(outs[0][0], outs[1][0])
 
 
+@pytest.mark.parametrize("pipe", ["0", "force"])
 @pytest.mark.parametrize("dt", [F64, torch.float32])
-def test_gemm_latency_kernel(ops, dt):
+def test_gemm_latency_kernel(ops, dt, pipe, monkeypatch):
     """gemm_lat.hip (32x32 tiles, k split over the waves, register-direct operands) on the descriptor
     features the DSVI step uses: triangular operands whose zero triangles hold inf, k-scaling, the
     rs(i) E epilogue, diagonal add, beta, OUT_LOWER / OUT_TRIL, transposed operands, k-blocked
-    operands (kb = 64), row / k segments, the device tile plan; repeat launches are bit-identical."""
+    operands (kb = 64), row / k segments, the device tile plan; repeat launches are bit-identical.
+    pipe="force": the persistent two-tiles-in-flight launch (one workgroup per CU walking several tiles)."""
     from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L
+    monkeypatch.setattr(ops, "_LAT_PIPE", pipe)
     g = torch.Generator().manual_seed(21)
     n, B, D, M = 100, 330, 3, 64
     S = torch.randn(n, n, generator=g, dtype=F64)
@@ -233,7 +236,7 @@ def test_gemm_latency_kernel(ops, dt):
             ops.gemm_desc(O4, Pd, Pd, M, M, 1500, (1, M, 0), (M, 1, 0), (M, 1), alpha=-1.0, beta=1.0),
         ]
         grp = ops.GemmGroup(descs, DEV, dt, seg=segd, kernel="lat", dyn_plan="force" if rep else False)
-        assert grp.lat and (grp.plan is not None) == bool(rep)
+        assert grp.lat and (grp.plan is not None) == bool(rep) and grp.pipe == (pipe == "force")
         assert max(d.ksplit for d in grp.descs) > 1
         grp()
         results.append([x.cpu() for x in (C1, C2, C3, O1, O2, O3, O4)])
@@ -253,6 +256,52 @@ def test_gemm_latency_kernel(ops, dt):
             assert torch.isfinite(a).all() and rel(a, r) < tol
     for a, b in zip(*results):          # static grid vs device plan: same tiles, same order of sums
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dt", [F64, torch.float32])
+def test_gemm_lat_persistent_walks_many_tiles(ops, dt, monkeypatch):
+    """The persistent latency launch (one workgroup per CU, the next tile's first panel loaded under the current
+    tile's MFMAs and reduction) over groups of thousands of tiles -- row segments with the device plan, a
+    B-triangular operand, a k range of several rounds (k = 600: 19 panels per 8 waves) and an odd tile count --
+    equals the one-tile-per-workgroup launch bit for bit, and the float64 reference."""
+    g = torch.Generator().manual_seed(5)
+    Bn, M, D, K2 = 6007, 256, 3, 600
+    W = torch.randn(D, Bn, M, generator=g, dtype=F64)
+    U = torch.randn(D, M, M, generator=g, dtype=F64)
+    A2 = torch.randn(1000, K2, generator=g, dtype=F64)
+    B2 = torch.randn(K2, 160, generator=g, dtype=F64)
+    seg = torch.tensor([0, 1800, 4100, Bn], dtype=torch.int32, device=DEV)
+    dv = lambda x: x.to(dt).to(DEV)
+    Wd, Ud, A2d, B2d = dv(W), dv(U), dv(A2), dv(B2)
+    out = {}
+    for pipe in ("0", "force"):
+        monkeypatch.setattr(ops, "_LAT_PIPE", pipe)
+        Z = torch.zeros(D, Bn, M, dtype=dt, device=DEV)
+        C2 = torch.zeros(1000, 160, dtype=dt, device=DEV)
+        descs = [ops.gemm_desc(Z, Wd, Ud, Bn, M, M, (M, 1, 0), (1, M, 0), (M, 1), flags=L_B_UPPER(),
+                               offs=(d * Bn * M, d * M * M, d * Bn * M), row_seg=d, seg_span=D - d) for d in range(D)]
+        grp = ops.GemmGroup(descs, DEV, dt, seg=seg, kernel="lat", dyn_plan="force")
+        grp2 = ops.GemmGroup([ops.gemm_desc(C2, A2d, B2d, 1000, 160, K2, (K2, 1, 0), (160, 1, 0), (160, 1))], DEV, dt,
+                             kernel="lat")
+        assert grp.pipe == grp2.pipe == (pipe == "force") and grp.total > 1024
+        grp()
+        grp2()
+        grp2()           # a second launch: split-K counters (if any) were re-armed
+        out[pipe] = (Z.cpu(), C2.cpu())
+    assert torch.equal(out["0"][0], out["force"][0]) and torch.equal(out["0"][1], out["force"][1])
+    Wc, Uc = W.to(dt).double(), U.to(dt).double()
+    ref = torch.zeros(D, Bn, M, dtype=F64)
+    for d in range(D):
+        r0 = int(seg[d])
+        ref[d, r0:] = Wc[d, r0:] @ torch.tril(Uc[d]).t()     # (B_UPPER over B(k, j) = U[j, k])
+    tol = 1e-13 if dt == F64 else 3e-6
+    assert rel(out["force"][0], ref) < tol
+    assert rel(out["force"][1], A2.to(dt).double() @ B2.to(dt).double()) < tol
+
+
+def L_B_UPPER():
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L
+    return L.B_UPPER
 
 
 def test_gemm_latency_kernel_dsvi_step(ops, monkeypatch):
@@ -655,6 +704,39 @@ def test_gemm_big_kseg_batch(ops):
         ref = torch.tril(C0[b].cpu().double() + P[k0:k1].cpu().double().t() @ W[w, k0:k1].cpu().double())
         got = C[b].cpu()
         assert rel(got, ref) < 2e-6 and torch.all(got[~lo] == 0)
+
+
+@pytest.mark.parametrize("bk", [False, True])
+def test_gemm_big_rseg_batch(ops, bk):
+    """Per-problem ROW ranges from a device segment table on the 128x128 kernel (the HCP-shaped quadratic-form
+    factors W_d = P[rows of outputs >= d] L_d and the P-bar products W-hat_d L_d^T): B_LOWER (bk False: B = L
+    k-strided) or B_UPPER over B(k, j) = L[j, k] (bk True), beta accumulate, an empty range and a range shorter
+    than one tile; rows outside every problem's range stay untouched."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd import _lib as L
+    g = torch.Generator().manual_seed(41)
+    Bn, M = 1000, 512
+    P = torch.randn(Bn, M, generator=g)
+    Lm = torch.tril(torch.randn(4, M, M, generator=g)) + torch.triu(torch.full((M, M), float("inf")), 1)
+    seg = torch.tensor([0, 300, 300, 350, 1000], dtype=torch.int32, device=DEV)   # segment 1 empty, 2 of 50 rows
+    probs = [(0, 4), (1, 1), (2, 2), (3, 1), (0, 1)]                             # (first segment, span)
+    C0 = torch.randn(len(probs), Bn, M, generator=g)
+    C = C0.clone().to(DEV)
+    flags = L.B_UPPER if bk else L.B_LOWER
+    op = ops.BigBatch(P.to(DEV), Lm.to(DEV), C, [0] * len(probs), [(b % 4) * M * M for b in range(len(probs))],
+                      [b * Bn * M for b in range(len(probs))], Bn, M, M, lda=M, ldb=M, b_kcontig=bk, flags=flags,
+                      beta=1.0, rseg=(seg, [s_ for (s_, _) in probs], [sp for (_, sp) in probs]))
+    op()
+    sc = seg.cpu().tolist()
+    Lc = torch.tril(torch.nan_to_num(Lm, posinf=0.0)).double()
+    for b, (s_, sp) in enumerate(probs):
+        r0, r1 = sc[s_], sc[s_ + sp]
+        ref = C0[b].double().clone()
+        Lb = Lc[b % 4]
+        ref[r0:r1] += P[r0:r1].double() @ (Lb.t() if bk else Lb)
+        got = C[b].cpu()
+        assert rel(got, ref) < 2e-6
+        assert torch.equal(got[:r0], C0[b][:r0]) and torch.equal(got[r1:], C0[b][r1:])
+    assert op.macs(seg.cpu()) == sum((sc[s_ + sp] - sc[s_]) * M * (M + 1) // 2 for (s_, sp) in probs)
 
 
 def test_gemm_big_persistent_multi_item_walk(ops):
