@@ -406,22 +406,26 @@ def train_roofline(eng, cfg):
     output halves and padding not counted; row / k segments of this minibatch), over the family's busy time
     per step (sum of its launch durations: concurrent streams overlap, so this is conservative)."""
     seg_host = eng.seg.cpu().numpy()
-    fams = {"gemm_big_kernel": [0.0, [], 0], "gemm_kernel<float": [0.0, [], 0]}
+    # family -> [GFLOP, group names, launches, algorithmic bytes] per step
+    fams = {"gemm_big_kernel": [0.0, [], 0, 0], "gemm_kernel<float": [0.0, [], 0, 0]}
     for nm, grp in eng.gemm_groups():
         parts = grp.parts if hasattr(grp, "parts") else [grp]
         for p_ in parts:
             if isinstance(p_, H_BigBatch()):
-                fams["gemm_big_kernel"][0] += 2.0 * p_.macs(seg_host) / 1e9
-                fams["gemm_big_kernel"][1].append(nm)
-                fams["gemm_big_kernel"][2] += 1
+                f = fams["gemm_big_kernel"]
             elif hasattr(p_, "macs") and not getattr(p_, "lat", False) and p_.dtype == torch.float32:
-                fams["gemm_kernel<float"][0] += 2.0 * p_.macs(seg_host) / 1e9
-                fams["gemm_kernel<float"][1].append(nm)
-                fams["gemm_kernel<float"][2] += 1
+                f = fams["gemm_kernel<float"]
+            else:
+                continue
+            f[0] += 2.0 * p_.macs(seg_host) / 1e9
+            f[1].append(nm)
+            f[2] += 1
+            f[3] += p_.algo_bytes(seg_host)
     from collaborative_nonstationary_multivariate_gaussian_process_amd import hip_ops as H
     kf0, kf1 = eng._plan(0)["kl_range"]
     if eng.M > 256:      # chol_side: recursive factor + inverse of the variational factors on gemm_big
         fams["gemm_big_kernel"][0] += (kf1 - kf0) * 2.0 * H.chol_inv_rec_macs(eng.M) / 1e9
+        fams["gemm_big_kernel"][3] += (kf1 - kf0) * H.chol_inv_rec_bytes(eng.M)
         fams["gemm_big_kernel"][1].append("chol_side (recursive factor + inverse GEMMs)")
     src, d, stale = matched_profile(f"r*_{cfg}_train_kernels.json")
     tsrc, td, tstale = matched_profile(f"r*_{cfg}_train_traffic.json")
@@ -435,23 +439,40 @@ def train_roofline(eng, cfg):
                     b_[1] += r["share_of_busy"]
                     b_[2] += r["launches_per_step"]
     lines = {}
-    for fam, (gf, names, n) in fams.items():
+    for fam, (gf, names, n, abytes) in fams.items():
         e = {"kernel": fam + ("> (grouped 64x64 MFMA f32 GEMM)" if fam.startswith("gemm_kernel")
                               else " (128x128 MFMA f32, batched factor products)"),
              "bound": "mfma", "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-             "algorithmic_gflop_per_step": round(gf, 3), "groups": sorted(set(names)), "traffic": None}
+             "algorithmic_gflop_per_step": round(gf, 3), "groups": sorted(set(names)), "traffic": None,
+             # each product's operands read once and its output written once (structural zeros not counted):
+             # hip_ops.desc_bytes / BigBatch.algo_bytes / chol_inv_rec_bytes
+             "algorithmic_bytes": int(abytes), "algorithmic_bytes_unit": "bytes/step"}
         if fam in busy:
             ms, share, launches = busy[fam]
             ach = gf / ms                                   # GFLOP / ms = TFLOP/s
-            e.update({"profile_ms_per_step": round(ms, 4), "profile_launches_per_step": launches,
-                      "profile_share_of_busy": round(share, 4), "achieved": round(ach, 3),
-                      "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "source": src, "stale": stale,
-                      "timing": "rocprofv3 --kernel-trace busy time of the family per graphed step"})
+            e.update({"profile_launches_per_step": launches, "source": src, "stale": stale,
+                      "in_graph_overlapped": {
+                          "ms_per_step": round(ms, 4), "share_of_busy": round(share, 4), "achieved": round(ach, 3),
+                          "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                          "timing": "rocprofv3 --kernel-trace busy time of the family per graphed step (streams "
+                                    "overlap: a launch's time includes waits for CUs other streams hold)"}})
+            e["achieved"], e["frac"] = e["in_graph_overlapped"]["achieved"], e["in_graph_overlapped"]["frac"]
+            e["timing"] = e["in_graph_overlapped"]["timing"]
         if tsrc is not None and fam in td.get("families", {}):
             # HBM traffic of the family per step from the FETCH / WRITE PMC passes (tools/train_pmc.sh)
-            tb = td["families"][fam]["traffic_bytes_per_step"]
+            tf_ = td["families"][fam]
+            tb = tf_["traffic_bytes_per_step"]
             e.update({"traffic": tb, "traffic_unit": "bytes/step (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
-                      "traffic_source": tsrc, "traffic_stale": tstale})
+                      "traffic_source": tsrc, "traffic_stale": tstale,
+                      "traffic_ratio": round(tb / abytes, 3) if abytes else None})
+            ser = tf_.get("serialised_ms_per_step")
+            if ser:
+                # the line's achieved / frac: the family's own kernel time, dispatches serialised by the PMC pass
+                ach = gf / ser
+                e.update({"serialised_ms_per_step": ser, "achieved": round(ach, 3),
+                          "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                          "timing": "rocprofv3 PMC (FETCH_SIZE) pass of the graphed step: the family's dispatch "
+                                    "durations, serialised by counter collection"})
             if fam in busy:
                 e["traffic_GBs_over_busy_time"] = round(tb / (busy[fam][0] * 1e-3) / 1e9, 1)
         lines[fam] = e

@@ -970,14 +970,15 @@ class DsviEngine:
         # a node's FIRST-created child keeps its hardware queue and every other child starts on another queue
         # behind a cross-queue barrier (10-20 us per hop in the r03 traces), so the critical-path child of each
         # fork is captured first (v after chol, quad_W after projG, bwd_R after bwd_wG, bwd_t1 after tbwd).
-        # Sigma_v: fp64 engines form it first on the side stream (one small launch beside the RBF builders);
-        # in fp32 its summation order shows through ell_Z = exp(v), so fp32 engines keep the grouped main launch
-        v_on_side = need_side and not elbo_mode and self.dt == torch.float64
+        # Sigma_v: fp64 engines without the fused priors form it first on the side stream (one small launch beside
+        # the RBF builders on main); in fp32 its summation order shows through ell_Z = exp(v), so fp32 engines keep
+        # the grouped main launch.  Fused priors: the RBF K22 and Sigma_v both on main, after the side stream's
+        # first launch (side keeps the hardware queue; on the side stream the fused launch waited for a cross-queue
+        # hand-off after them: 0.671 -> 0.667 ms A/B, profiles/r06q_head_main_after_fork_ab.txt)
+        v_on_side = need_side and not elbo_mode and self.dt == torch.float64 and not fuse
         if need_side:
             steps += [("sig", "main", "fork"), ("wait", "side", "fork")]
             if v_on_side:
-                if fuse:      # the RBF priors' K22 (theta only) ahead of Sigma_v, beside the minibatch gather
-                    steps.append(("build_k22", "pairwise", pw("build_k22"), "side"))
                 steps += [("syrk", "gemm", gemm("syrk"), "side"), ("sig", "side", "syrk")]
             steps.append(("syrk_side", "gemm", gemm("syrk_side"), "side"))
             if pre_planned:
@@ -994,7 +995,7 @@ class DsviEngine:
                       ("build_rbf64", "pairwise", pw64("build_rbf64"), "main")]
         if not fuse:
             steps.append(("build_rbf", "pairwise", pw("build_rbf"), "main"))
-        elif not v_on_side:
+        else:
             steps.append(("build_k22", "pairwise", pw("build_k22"), "main"))
         steps.append(("wait", "main", "syrk") if v_on_side else ("syrk", "gemm", gemm("syrk"), "main"))
         # forward chain: chol -> v -> K_G22 -> chol_G -> invG -> projG.  The t-prior projections, the

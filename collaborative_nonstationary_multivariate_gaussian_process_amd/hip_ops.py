@@ -320,6 +320,10 @@ class GemmGroup:
     def macs(self, seg=None):
         return sum(desc_macs(d, seg) for d in self.descs)
 
+    def algo_bytes(self, seg=None):
+        esz = 8 if self.dtype == _F64 else 4
+        return sum(desc_bytes(d, seg, esz, beta=d.beta, epi=bool(d.flags & L.EPI)) for d in self.descs)
+
     def plan_now(self, stream=None):
         """Enqueue only the device tile plan of a segment-sized group (e.g. right after the minibatch
         gather, on another stream); later calls with planned=True reuse it.  No-op for static groups."""
@@ -387,6 +391,32 @@ def desc_macs(d, seg=None):
     if f & (L.OUT_LOWER | L.OUT_TRIL):
         cnt = np.where(j <= i, cnt, 0)
     return int(cnt.sum()) * nblk
+
+
+def desc_bytes(d, seg=None, esz=4, beta=0.0, epi=False):
+    """Algorithmic HBM bytes of one problem: its operands read once (structurally zero triangles of triangular
+    operands not counted), C written once (the skipped upper half of OUT_LOWER / OUT_TRIL outputs not counted) and
+    read as well when beta != 0, the epilogue operand E read once; row / k ranges from the host segment table."""
+    span = d.seg_span if d.seg_span > 0 else 1
+    m = d.m if d.row_seg < 0 else int(seg[d.row_seg + span] - seg[d.row_seg])
+    K = d.k if d.k_seg < 0 else int(seg[d.k_seg + span] - seg[d.k_seg])
+    n = d.n
+    if m <= 0 or n <= 0:
+        return 0
+    f = d.flags
+    tri = lambda r, c: r * c - (min(r, c) * (min(r, c) - 1)) // 2 if r == c else r * c
+    a = tri(m, K) if f & (L.A_LOWER | L.A_UPPER) else m * K
+    b = tri(K, n) if f & (L.B_LOWER | L.B_UPPER) else K * n
+    c = (m * (m + 1)) // 2 if (f & (L.OUT_LOWER | L.OUT_TRIL)) and m == n else m * n
+    e = ((m * (m + 1)) // 2 if f & L.EPI_E_LOWER else m * n) if epi else 0
+    ab = (a + b) if K > 0 else 0
+    return esz * (ab + c * (2 if beta != 0.0 else 1) + e)
+
+
+def chol_inv_rec_bytes(n, esz=4):
+    """Algorithmic HBM bytes of one factor + inverse of an n x n SPD matrix: its lower triangle read once, L and
+    L^-1 (lower triangles) written once."""
+    return esz * 3 * (n * (n + 1)) // 2
 
 
 def chol_inv_rec_macs(n):
@@ -625,6 +655,20 @@ class BigBatch:
         return sum(desc_macs(types.SimpleNamespace(m=m, n=n, k=k, flags=flags, row_seg=-1, k_seg=a, seg_span=b,
                                                    kbA=0), seg) for a, b in zip(ks, sp))
 
+    def algo_bytes(self, seg=None):
+        """Algorithmic HBM bytes of the batch (desc_bytes per problem, row / k ranges from the host `seg`)."""
+        import types
+        m, n, k, _, _, _, _, _, flags, _, beta, _ = self.args
+        epi = self.epi is not None
+        ns = lambda **kw: types.SimpleNamespace(m=m, n=n, k=k, flags=flags, kbA=0, **kw)
+        if self.rseg is not None:
+            return sum(desc_bytes(ns(row_seg=a, k_seg=-1, seg_span=b), seg, 4, beta, epi)
+                       for a, b in zip(*self._rseg_host))
+        if self.kseg is None:
+            return self.batch * desc_bytes(ns(row_seg=-1, k_seg=-1, seg_span=0), None, 4, beta, epi)
+        ks, sp = self.kseg[1].tolist(), self.kseg[2].tolist()
+        return sum(desc_bytes(ns(row_seg=-1, k_seg=a, seg_span=b), seg, 4, beta, epi) for a, b in zip(ks, sp))
+
     def __call__(self, stream=None):
         if self.batch == 0:
             return
@@ -706,6 +750,9 @@ class Seq:
     def macs(self, seg=None):
         """Algorithmic multiply-adds of the parts that are products (reductions and other launches add none)."""
         return sum(p_.macs(seg) for p_ in self.parts if hasattr(p_, "macs"))
+
+    def algo_bytes(self, seg=None):
+        return sum(p_.algo_bytes(seg) for p_ in self.parts if hasattr(p_, "algo_bytes"))
 
 
 def potrf_blocked_(A, info=None, ws=None):
