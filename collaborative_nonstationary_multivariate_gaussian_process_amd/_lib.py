@@ -204,8 +204,6 @@ _SIGS = {
     "nmgp_dsvi_prefinal_f32": (c_int, [ctypes.POINTER(DsviArgs), c_vp]),
     "nmgp_adam_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_dbl, c_dbl, c_dbl, c_dbl, c_vp]),
     "nmgp_adam_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_dbl, c_dbl, c_dbl, c_dbl, c_vp]),
-    "nmgp_adam_step_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_dbl, c_dbl, c_dbl, c_dbl, c_vp]),
-    "nmgp_adam_step_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_dbl, c_dbl, c_dbl, c_dbl, c_vp]),
     "nmgp_adam_lower_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_vp, c_dbl, c_dbl, c_dbl,
                                     c_dbl, c_vp]),
     "nmgp_adam_lower_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_vp, c_dbl, c_dbl, c_dbl,

@@ -965,12 +965,9 @@ __device__ inline bool adam_elt(T& th, T gi, T& mi, T& vi, T lr, T b1, T b2, T e
 // corrections are computed once per workgroup (a double pow per element cost more than the memory
 // traffic at HCP's 670 M parameters).  Element arithmetic is unchanged, so results are bit-identical
 // to the scalar form.
-// arrive != nullptr (nmgp_adam_step_*): the last workgroup to finish also advances the step counter -- every
-// workgroup read it before it arrived -- instead of a one-thread launch after the update (round 6: the counter
-// launch sat between the step's Adam and the next step's first launch)
 template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void adam_kernel(T* th, const T* g, T* m, T* v, int64_t n, const int64_t* step,
-                                                   T lr, T b1, T b2, T eps, int64_t* step_inc, int32_t* arrive) {
+                                                   T lr, T b1, T b2, T eps) {
   __shared__ T s_bc[2];
   if (threadIdx.x == 0) {
     const double t = (double)(step[0] + 1);
@@ -1019,30 +1016,20 @@ __global__ __launch_bounds__(256) void adam_kernel(T* th, const T* g, T* m, T* v
       }
     }
   }
-  if (arrive != nullptr) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const int old = __hip_atomic_fetch_add(arrive, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (old == (int)gridDim.x - 1) {
-        __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        step_inc[0] = step[0] + 1;
-      }
-    }
-  }
 }
 
 template <typename T>
 static void adam_launch(T* th, const T* g, T* m, T* v, int64_t n, const int64_t* step, T lr, T b1, T b2, T eps,
-                        hipStream_t s, int64_t* step_inc = nullptr, int32_t* arrive = nullptr) {
+                        hipStream_t s) {
   const bool vec = ((((uintptr_t)th) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) == 0;
   const int64_t per = vec ? 16 / (int64_t)sizeof(T) : 1;
   const int64_t blocks = std::min<int64_t>((n / per + 255) / 256 + 1, 16384);
   if (vec)
     hipLaunchKernelGGL((adam_kernel<T, true>), dim3((unsigned)blocks), dim3(256), 0, s, th, g, m, v, n, step, lr, b1,
-                       b2, eps, step_inc, arrive);
+                       b2, eps);
   else
     hipLaunchKernelGGL((adam_kernel<T, false>), dim3((unsigned)blocks), dim3(256), 0, s, th, g, m, v, n, step, lr, b1,
-                       b2, eps, step_inc, arrive);
+                       b2, eps);
 }
 
 __global__ void counter_add_kernel(int64_t* c, int64_t inc) { c[0] += inc; }
@@ -1548,41 +1535,6 @@ int nmgp_adam_f32(float* th, const float* g, float* m, float* v, int64_t n, int6
   nmgp::adam_launch<float>(th, g, m, v, n, step, (float)lr, (float)b1, (float)b2, (float)eps, s);
   NMGP_CHECK_LAUNCH();
   hipLaunchKernelGGL(nmgp::counter_add_kernel, dim3(1), dim3(1), 0, s, step, (int64_t)1);
-  NMGP_CHECK_LAUNCH();
-  return NMGP_OK;
-}
-// One launch: the update and the step counter (arrive: an int32 arrival counter, 0 at rest and left 0)
-int nmgp_adam_step_f64(double* th, const double* g, double* m, double* v, int64_t n, int64_t* step, int32_t* arrive,
-                       double lr, double b1, double b2, double eps, hipStream_t s) {
-  if (!th) return -1;
-  if (!g) return -2;
-  if (!m) return -3;
-  if (!v) return -4;
-  if (!step) return -6;
-  if (!arrive) return -7;
-  if (n <= 0) {
-    hipLaunchKernelGGL(nmgp::counter_add_kernel, dim3(1), dim3(1), 0, s, step, (int64_t)1);
-    NMGP_CHECK_LAUNCH();
-    return NMGP_OK;
-  }
-  nmgp::adam_launch<double>(th, g, m, v, n, step, lr, b1, b2, eps, s, step, arrive);
-  NMGP_CHECK_LAUNCH();
-  return NMGP_OK;
-}
-int nmgp_adam_step_f32(float* th, const float* g, float* m, float* v, int64_t n, int64_t* step, int32_t* arrive,
-                       double lr, double b1, double b2, double eps, hipStream_t s) {
-  if (!th) return -1;
-  if (!g) return -2;
-  if (!m) return -3;
-  if (!v) return -4;
-  if (!step) return -6;
-  if (!arrive) return -7;
-  if (n <= 0) {
-    hipLaunchKernelGGL(nmgp::counter_add_kernel, dim3(1), dim3(1), 0, s, step, (int64_t)1);
-    NMGP_CHECK_LAUNCH();
-    return NMGP_OK;
-  }
-  nmgp::adam_launch<float>(th, g, m, v, n, step, (float)lr, (float)b1, (float)b2, (float)eps, s, step, arrive);
   NMGP_CHECK_LAUNCH();
   return NMGP_OK;
 }

@@ -1059,20 +1059,11 @@ class ExtEvent:
 
 
 # ------------------------------------------------------------------------------------ optimiser / rng
-def adam_(theta, grad, m, v, step, lr, betas=(0.9, 0.999), eps=1e-8, arrive=None):
-    """Adam on the flat vector; `step` (device int64) advanced by one.  arrive (device int32, 0): one launch, the
-    update's last workgroup advancing the counter (nmgp_adam_step_*)."""
-    vp = ctypes.c_void_p
-    args = (vp(theta.data_ptr()), vp(grad.data_ptr()), vp(m.data_ptr()), vp(v.data_ptr()), theta.numel(),
-            vp(step.data_ptr()))
-    tail = (float(lr), float(betas[0]), float(betas[1]), float(eps), L.stream_handle())
-    if arrive is not None:
-        assert arrive.dtype == torch.int32 and arrive.device == theta.device
-        fn = getattr(L.lib(), "nmgp_adam_step_" + _sfx(theta.dtype))
-        L.check(fn(*args, vp(arrive.data_ptr()), *tail), "adam_step")
-        return
+def adam_(theta, grad, m, v, step, lr, betas=(0.9, 0.999), eps=1e-8):
     fn = getattr(L.lib(), "nmgp_adam_" + _sfx(theta.dtype))
-    L.check(fn(*args, *tail), "adam")
+    L.check(fn(ctypes.c_void_p(theta.data_ptr()), ctypes.c_void_p(grad.data_ptr()), ctypes.c_void_p(m.data_ptr()),
+               ctypes.c_void_p(v.data_ptr()), theta.numel(), ctypes.c_void_p(step.data_ptr()), float(lr),
+               float(betas[0]), float(betas[1]), float(eps), L.stream_handle()), "adam")
 
 
 def adam_lower_(theta, grad, m, v, step, lr, tri, M, betas=(0.9, 0.999), eps=1e-8):

@@ -637,10 +637,7 @@ class DsviTrainer:
             H.adam_lower_(mdl._theta, mdl._grad, self.m, self.v, self.step_count, self.lr,
                           lower_block_ranges(mdl._offs), mdl.M, self.betas, self.eps)
         else:
-            if getattr(self, "_adam_arrive", None) is None:
-                self._adam_arrive = torch.zeros(1, dtype=torch.int32, device=mdl._theta.device)
-            H.adam_(mdl._theta, mdl._grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps,
-                    arrive=self._adam_arrive)
+            H.adam_(mdl._theta, mdl._grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps)
 
     def step(self, eng, noise=None):
         """One DSVI iteration on the batch already loaded in `eng`; returns the device loss scalar."""

@@ -468,17 +468,11 @@ int nmgp_dsvi_prefinal_f32(const nmgp_dsvi_args* a, hipStream_t s);
 
 /* ------------------------------------------------------------------ optimiser / RNG
  * torch.optim.Adam update (code/nmgp_dsvi.py:777,854) on a flat parameter vector; step is a
- * device counter (advanced by a one-thread launch after the update) so the call can be graph-replayed.  */
+ * device counter (incremented by the kernel's last block) so the call can be graph-replayed.  */
 int nmgp_adam_f64(double* theta, const double* grad, double* m, double* v, int64_t n,
                   int64_t* step, double lr, double beta1, double beta2, double eps, hipStream_t stream);
 int nmgp_adam_f32(float* theta, const float* grad, float* m, float* v, int64_t n,
                   int64_t* step, double lr, double beta1, double beta2, double eps, hipStream_t stream);
-/* The same in ONE launch: the update's last workgroup to finish advances `step` (arrive: a device int32 arrival
- * counter, 0 before the call and left 0; one per concurrently running update).                         */
-int nmgp_adam_step_f64(double* theta, const double* grad, double* m, double* v, int64_t n, int64_t* step,
-                       int32_t* arrive, double lr, double beta1, double beta2, double eps, hipStream_t stream);
-int nmgp_adam_step_f32(float* theta, const float* grad, float* m, float* v, int64_t n, int64_t* step,
-                       int32_t* arrive, double lr, double beta1, double beta2, double eps, hipStream_t stream);
 /* The same update where the ranges tri[2k] .. tri[2k] + tri[2k+1] M^2 of the vector are lower-triangular M x M
  * blocks (sqrt_W, sqrt_v, sqrt_U: their strictly upper triangles never receive a gradient, code/utils.py:68-72 --
  * torch's Adam leaves them unchanged): only the 16-byte vectors holding lower-triangle elements are read and

@@ -1121,28 +1121,22 @@ def test_lbar_reduce_adds_each_factors_output_products_in_order(ops, D, M, dt):
               L.stream_handle()) == -2
 
 
-@pytest.mark.parametrize("n,fused", [(1000, False), (1000, True), (3_000_001, True)])
-def test_adam_matches_torch(ops, n, fused):
-    # fused: one launch whose last workgroup advances the step counter (nmgp_adam_step_*); n = 3e6 + 1 runs the
-    # full 16384-workgroup grid with a scalar tail
+def test_adam_matches_torch(ops):
     g = torch.Generator().manual_seed(8)
-    p0 = torch.randn(n, generator=g, dtype=F64)
-    grads = [torch.randn(n, generator=g, dtype=F64) for _ in range(3)]
+    p0 = torch.randn(1000, generator=g, dtype=F64)
+    grads = [torch.randn(1000, generator=g, dtype=F64) for _ in range(3)]
     ref = p0.clone().requires_grad_()
     opt = torch.optim.Adam([ref], lr=0.01)
     th = p0.clone().to(DEV)
     m = torch.zeros_like(th)
     v = torch.zeros_like(th)
     step = torch.zeros(1, dtype=torch.int64, device=DEV)
-    arrive = torch.zeros(1, dtype=torch.int32, device=DEV) if fused else None
     for gr in grads:
         ref.grad = gr.clone()
         opt.step()
-        ops.adam_(th, gr.to(DEV), m, v, step, 0.01, arrive=arrive)
+        ops.adam_(th, gr.to(DEV), m, v, step, 0.01)
     assert rel(th, ref) < 1e-14
     assert int(step.cpu()) == 3
-    if fused:
-        assert int(arrive.cpu()) == 0
 
 
 def test_normal_rng(ops):
