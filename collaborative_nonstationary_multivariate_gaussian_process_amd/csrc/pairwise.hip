@@ -12,7 +12,10 @@
 
 namespace nmgp {
 
-constexpr int PR = 32, PC = 64;   // tile rows x cols
+constexpr int PR = 32, PC = 64;   // tile rows x cols (backward: its partial sums are per 32-row tile)
+// forward builders: 8-row tiles (two rows per wave) -- the M x M priors' K22 (256 x 256) were 96 workgroups of 32
+// rows, each wave computing and storing 8 rows in turn (round 6; include/nmgp_hip.h pairwise descriptors' `tiles`)
+constexpr int PRF = 8;
 
 struct PwArgs {
   const nmgp_pairwise_desc* descs;
@@ -98,6 +101,7 @@ __global__ __launch_bounds__(256) void pairwise_kernel(PwArgs args) {
   const int rt = tile / ctn, ct = tile - rt * ctn;
   const int j = ct * PC + (threadIdx.x & 63);
   if (j >= m) return;
+  constexpr int PR = PRF;
   T s2 = (T)d.scale2, ls = (T)d.length_scale;
   hyper_of((const T*)d.hyp, d.mode, d.flags, s2, ls);
   const T* X = (const T*)d.X;
@@ -157,11 +161,16 @@ __global__ __launch_bounds__(256) void pairwise_bwd_kernel(PwBwdArgs args) {
   const bool gibbs = d.mode == NMGP_GIBBS;
   const T lz = (gibbs && jok) ? ellZ[j] : (T)0;
   T s0 = 0, s1 = 0, gzacc = 0;
+  // the wave's PR/4 rows: every row's loads and arithmetic first (no store in between, so the loads of all rows
+  // are in flight together), then the per-row reductions of the Gibbs x-adjoints and their stores (round 6: the
+  // row loop with a store after each row's reduction ran one row's memory round trip at a time -- 29 us for the
+  // PM2.5 K_G12 backward, on the step's critical chain)
+  T gxs[PR / 4];
+#pragma unroll
   for (int e = 0; e < PR / 4; ++e) {
     const int i = rt * PR + w * (PR / 4) + e;
-    if (i >= n) break;   // wave-uniform
     T gx = 0;
-    if (jok) {
+    if (jok && i < n) {
       const int64_t idx = (int64_t)i * d.ld + j;
       T kb = Rb[idx];
       if (rc) kb -= rc[i] * Pm[idx];
@@ -183,9 +192,14 @@ __global__ __launch_bounds__(256) void pairwise_bwd_kernel(PwBwdArgs args) {
         gzacc += wv * ((T)0.5 / lz - lz / S + lz * r2s);
       }
     }
-    if (gibbs) {
-      gx = wave_sum(gx);
-      if (lane == 0) row_part[(int64_t)ct * n + i] = gx;
+    gxs[e] = gx;
+  }
+  if (gibbs) {
+#pragma unroll
+    for (int e = 0; e < PR / 4; ++e) {
+      const int i = rt * PR + w * (PR / 4) + e;
+      const T gx = wave_sum(gxs[e]);
+      if (lane == 0 && i < n) row_part[(int64_t)ct * n + i] = gx;
     }
   }
   if (gibbs) {
@@ -217,6 +231,7 @@ __global__ void colsum_kernel(const T* a, int64_t rows, int64_t cols, T beta, T*
 }
 
 static inline int pw_tiles(int n, int m) { return ((n + PR - 1) / PR) * ((m + PC - 1) / PC); }
+static inline int pw_tiles_fwd(int n, int m) { return ((n + PRF - 1) / PRF) * ((m + PC - 1) / PC); }
 
 template <typename T>
 static int pw_launch(const nmgp_pairwise_desc* dd, int nd, int tt, const nmgp_pairwise_desc* inl, hipStream_t s) {
@@ -258,14 +273,14 @@ int nmgp_pairwise_single_f64(const nmgp_pairwise_desc* h, hipStream_t s) {
   if (!h) return -1;
   nmgp_pairwise_desc d = *h;
   d.tile_start = 0;
-  d.tiles = nmgp::pw_tiles(d.n, d.m);
+  d.tiles = nmgp::pw_tiles_fwd(d.n, d.m);
   return nmgp::pw_launch<double>(nullptr, 1, d.tiles, &d, s);
 }
 int nmgp_pairwise_single_f32(const nmgp_pairwise_desc* h, hipStream_t s) {
   if (!h) return -1;
   nmgp_pairwise_desc d = *h;
   d.tile_start = 0;
-  d.tiles = nmgp::pw_tiles(d.n, d.m);
+  d.tiles = nmgp::pw_tiles_fwd(d.n, d.m);
   return nmgp::pw_launch<float>(nullptr, 1, d.tiles, &d, s);
 }
 int nmgp_pairwise_bwd_f64(const nmgp_pairwise_bwd_desc* d, int nd, int tt, hipStream_t s) {

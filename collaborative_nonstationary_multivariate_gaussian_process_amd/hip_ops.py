@@ -835,7 +835,7 @@ def pairwise_desc(K, X, Z, *, mode, dist=L.DIST_DIFF, scale2=1.0, length_scale=1
     d.n, d.m, d.p, d.mode, d.dist = n, m, p, mode, dist
     d.flags = L.HYP_LOG if hyp_log else 0
     d.scale2, d.length_scale, d.diag_add = float(scale2), float(length_scale), float(diag_add)
-    d.tiles = ((n + 31) // 32) * ((m + 63) // 64)
+    d.tiles = ((n + 7) // 8) * ((m + 63) // 64)   # csrc/pairwise.hip PRF x PC forward tiles
     return d
 
 

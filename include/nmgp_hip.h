@@ -324,7 +324,7 @@ typedef struct nmgp_pairwise_desc {
   int64_t ldk;
   int32_t n, m, p, mode, dist, flags;
   double scale2, length_scale, diag_add;
-  int32_t tiles, tile_start;
+  int32_t tiles, tile_start;   /* tiles = ceil(n/8) * ceil(m/64) (8-row x 64-column output tiles)           */
 } nmgp_pairwise_desc;
 
 int nmgp_pairwise_f64(const nmgp_pairwise_desc* d_desc, int ndesc, int total_tiles, hipStream_t stream);
