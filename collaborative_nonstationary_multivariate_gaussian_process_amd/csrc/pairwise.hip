@@ -7,15 +7,16 @@
 // once, the per-point inputs (x, z, ell) are read coalesced and stay in L1/L2.
 //
 // Backward: Kbar = Rbar - rowcoef(i) * Pm (the closed-form DSVI adjoint of K12 is R - c * P, see
-// DESIGN.md §4), reduced over 32-row x 64-column tiles into deterministic partial sums.
+// DESIGN.md §4), reduced over 8-row x 64-column tiles into deterministic partial sums.
 #include "common.hpp"
 
 namespace nmgp {
 
-constexpr int PR = 32, PC = 64;   // tile rows x cols (backward: its partial sums are per 32-row tile)
-// forward builders: 8-row tiles (two rows per wave) -- the M x M priors' K22 (256 x 256) were 96 workgroups of 32
-// rows, each wave computing and storing 8 rows in turn (round 6; include/nmgp_hip.h pairwise descriptors' `tiles`)
-constexpr int PRF = 8;
+// 8-row x 64-column tiles, two rows per wave (round 6: 32-row tiles left the M x M priors' K22 (256 x 256) at 96
+// workgroups and the K_G12 backward (2000 x 256) at 252, each wave working through 8 rows in turn; include/nmgp_hip.h
+// pairwise descriptors' `tiles`, the backward's partial sums are per 8-row tile)
+constexpr int PR = 8, PC = 64;
+constexpr int PRF = PR;
 
 struct PwArgs {
   const nmgp_pairwise_desc* descs;

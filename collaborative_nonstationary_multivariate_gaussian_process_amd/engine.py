@@ -199,8 +199,8 @@ class DsviEngine:
         self.red = e(4 * B + (B + 3) // 4)
         self.out = e(16)          # [0..4] loss / SELBO_R / KL_W / KL_v / KL_U, [8..14] training pre-sums
         self.n_ct = (M + 63) // 64
-        self.n_rt = (B + 31) // 32
-        self.n_rt22 = (M + 31) // 32
+        self.n_rt = H.bwd_tiles(B, M)[2]        # row tiles of the pairwise backward's column partials
+        self.n_rt22 = H.bwd_tiles(M, M)[2]
         self.gib_row = e(self.n_ct * B + self.n_ct * M)
         self.gib_col = e(self.n_rt * M + self.n_rt22 * M)
         tb = H.bwd_tiles(B, M)[0]

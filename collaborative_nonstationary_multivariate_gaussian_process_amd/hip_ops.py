@@ -889,7 +889,7 @@ def pairwise_bwd_desc(X, Z, K, Rbar, *, mode, ld, Pm=None, rowcoef=None, ellX=No
     d.n, d.m, d.p, d.mode = n, m, (X.shape[1] if X.dim() > 1 else 1), mode
     d.flags = L.HYP_LOG if hyp_log else 0
     d.scale2, d.length_scale = float(scale2), float(length_scale)
-    d.tiles = ((n + 31) // 32) * ((m + 63) // 64)
+    d.tiles = ((n + 7) // 8) * ((m + 63) // 64)   # csrc/pairwise.hip PR x PC backward tiles
     return d
 
 
@@ -913,7 +913,8 @@ class PairwiseBwdGroup:
 
 
 def bwd_tiles(n, m):
-    return ((n + 31) // 32) * ((m + 63) // 64), (m + 63) // 64, (n + 31) // 32
+    """(tiles, column tiles, row tiles) of a pairwise backward launch (csrc/pairwise.hip: 8 x 64 tiles)."""
+    return ((n + 7) // 8) * ((m + 63) // 64), (m + 63) // 64, (n + 7) // 8
 
 
 def colsum(a2d, out, beta=0.0):

@@ -337,7 +337,7 @@ int nmgp_pairwise_single_f32(const nmgp_pairwise_desc* h_desc, hipStream_t strea
  *   GIBBS: row_part[ct*n + i] = sum_j Kbar*K*dlogK/dlx_i over column tile ct,
  *          col_part[rt*m + j] = sum_i Kbar*K*dlogK/dlz_j over row tile rt,
  *          scal_part[t*2+0]  = sum Kbar*K
- * Tiles are 32 rows x 64 columns; partial sums are deterministic (no atomics).              */
+ * Tiles are 8 rows x 64 columns (tiles = ceil(n/8) * ceil(m/64)); partial sums are deterministic.   */
 typedef struct nmgp_pairwise_bwd_desc {
   const void* X; const void* Z; const void* ellX; const void* ellZ; const void* hyp;
   const void* K; const void* Rbar; const void* Pm; const void* rowcoef;
