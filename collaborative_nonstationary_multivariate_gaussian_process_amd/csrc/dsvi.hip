@@ -682,6 +682,10 @@ __global__ __launch_bounds__(256) void dsvi_vbwd_kernel(Args a) {
 // KL mean gradients A2^{-1} mu (Y) into the mu_W / mu_U gradient rows (live pairs j <= i only) and
 // mu_v += vbar + Y_t: one grid-strided element-wise pass, launched on the side stream after the last
 // writers of those rows (the mu-bar products of bwd_lbar and the v backward), off the main chain.
+// values the KL mean-gradient pass updates: mu_W (D M), mu_v (M), mu_U (pair columns x M)
+__device__ inline int64_t mugrad_count(const nmgp_dsvi_args& a) {
+  return (int64_t)a.D * a.M + a.M + pair_cols(a) * a.M;
+}
 template <typename T> __device__ inline void mugrad_body(const Args& a, int64_t i0, int64_t stride) {
   const int D = a.D, M = a.M;
   T* __restrict__ gw = (T*)a.grad;
@@ -932,8 +936,10 @@ __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
     for (int k = 0; k < 7; ++k) g[a.off_hyp + k] = (a.frozen_mask >> k & 1) ? (T)0 : gs[k];
   }
   // training step: the KL mean gradients A2^{-1} mu and mu_v += vbar (round 6: here, after every other writer of those
-  // rows -- bwd_lbar's mu products, nmgp_lbar_reduce, the v backward -- instead of a launch of their own)
-  if (!a.elbo_mode) mugrad_body<T>(a, threadIdx.x, blockDim.x);
+  // rows -- bwd_lbar's mu products, nmgp_lbar_reduce, the v backward -- instead of a launch of their own) when they
+  // are few (PM2.5: 5376 values); larger engines launch nmgp_dsvi_mugrad_* before finalize (one workgroup over
+  // ECoG's 8.5 M values took 6.6 ms)
+  if (!a.elbo_mode && mugrad_count(a) <= NMGP_MUGRAD_IN_FINALIZE_MAX) mugrad_body<T>(a, threadIdx.x, blockDim.x);
 #ifdef NMGP_FIN_TRACE
   __syncthreads();
   if (threadIdx.x == 0) {

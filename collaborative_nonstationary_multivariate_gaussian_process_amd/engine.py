@@ -22,6 +22,7 @@ from . import hip_ops as H
 F64 = torch.float64
 F32 = torch.float32
 JITTER = 1e-4   # code/utils.py:7
+MUGRAD_IN_FINALIZE_MAX = 65536     # include/nmgp_hip.h NMGP_MUGRAD_IN_FINALIZE_MAX
 
 
 def _sfx(dt):
@@ -1196,8 +1197,12 @@ class DsviEngine:
         steps += [
             ("wait", "main", "L_done"),
             ("wait", "main", "g22"),          # (explicit join of side2; long done)
-            ("finalize", "row", row(getattr(lib, "nmgp_dsvi_finalize_" + self.sfx)), "main"),
         ]
+        # the KL mean gradients: inside finalize for small engines, else their own launch first (include/nmgp_hip.h
+        # NMGP_MUGRAD_IN_FINALIZE_MAX; the same count as csrc/dsvi.hip mugrad_count)
+        if D * M + M + self.NPC * M > MUGRAD_IN_FINALIZE_MAX:
+            steps.append(("mugrad", "row", row(getattr(lib, "nmgp_dsvi_mugrad_" + self.sfx)), "main"))
+        steps.append(("finalize", "row", row(getattr(lib, "nmgp_dsvi_finalize_" + self.sfx)), "main"))
         return steps
 
     def _run(self, steps, stream, timer):

@@ -451,7 +451,11 @@ int nmgp_dsvi_delta_f64(const nmgp_dsvi_args* a, hipStream_t s);      /* prior d
 int nmgp_dsvi_tbwd_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* t-row backward            */
 int nmgp_dsvi_vbwd_f64(const nmgp_dsvi_args* a, hipStream_t s);       /* v backward -> Phi         */
 int nmgp_dsvi_finalize_f64(const nmgp_dsvi_args* a, hipStream_t s);   /* loss + scalar gradients   */
-int nmgp_dsvi_mugrad_f64(const nmgp_dsvi_args* a, hipStream_t s);     /* KL mean gradients of mu_W / mu_v / mu_U (training steps: part of finalize) */
+int nmgp_dsvi_mugrad_f64(const nmgp_dsvi_args* a, hipStream_t s);     /* KL mean gradients of mu_W / mu_v / mu_U */
+/* Training steps: nmgp_dsvi_finalize_* adds the KL mean gradients itself when D M + M + (pair columns) M is at most
+ * NMGP_MUGRAD_IN_FINALIZE_MAX; larger engines launch nmgp_dsvi_mugrad_* (after the L-bar and v backward, before
+ * finalize).                                                                                                   */
+#define NMGP_MUGRAD_IN_FINALIZE_MAX 65536
 int nmgp_dsvi_prefinal_f64(const nmgp_dsvi_args* a, hipStream_t s);   /* training step: recon + KL sums -> out[8..14] */
 /* fp32 twins (HCP / ECoG-shaped configurations): same arguments, every buffer float */
 int nmgp_dsvi_hyper_f32(const nmgp_dsvi_args* a, hipStream_t s);
