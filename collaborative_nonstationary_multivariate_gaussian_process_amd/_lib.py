@@ -80,7 +80,8 @@ class CholTpArgs(ctypes.Structure):
     _fields_ = [("A", c_vp), ("n", c_i64), ("lda", c_i64), ("strideA", c_i64), ("X", c_vp), ("ldx", c_i64),
                 ("strideX", c_i64), ("batch", c_i64), ("info", c_vp), ("jitter", c_dbl), ("Z", c_vp), ("ellZ", c_vp),
                 ("x", c_vp), ("B", c_i64), ("Pt", c_vp), ("Tt", c_vp), ("v", c_vp), ("zt", c_vp), ("hyp_t", c_vp),
-                ("ellX", c_vp), ("var_t", c_vp), ("mats", CholTpMat * 4)]
+                ("ellX", c_vp), ("var_t", c_vp), ("mats", CholTpMat * 4), ("vg_muv", c_vp), ("vg_z", c_vp),
+                ("vg_v", c_vp), ("vg_ellZ", c_vp), ("vg_K22", c_vp), ("vg_wgs", c_i64)]
 
 
 # flags (include/nmgp_hip.h)

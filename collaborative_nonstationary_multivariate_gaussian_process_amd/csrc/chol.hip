@@ -1483,7 +1483,97 @@ struct TpDev {
   double* K12[4];
   double* Tm[4];
   double* Pm[4];
+  // fused K_G22 workgroups (nvg > 0; matrix 0 is Sigma_v): v = mu_v + L_v z_v, ell_Z = exp(v), K_G22 + jitter I
+  int nvg;
+  const double* vg_muv;
+  const double* vg_z;
+  double* vg_v;
+  double* vg_ellZ;
+  double* vg_K22;
 };
+
+// The Gibbs prior's K22 inside the launch that factors Sigma_v (round 6), pipelined behind the factorization: row
+// block kb of v = mu_v + L_v z_v needs L_v's rows kb*16.., i.e. block columns 0..kb, so after matrix 0's factor role
+// has published block column kb, every one of the nvg workgroups forms v[kb*16 .. kb*16+15] (two entries per wave,
+// lanes over k: dsvi_vg22_kernel's sums) and then its share of the tiles (kb, J <= kb) of K_G22's lower 16 x 16 tiles
+// (two tiles per pass, one per 256 threads; dsvi_vg22_kernel's element arithmetic).  What is left after the last
+// column is one row block of tiles.  Workgroup 0 also writes v and ell_Z.  These workgroups are readers of matrix
+// 0's progress word: the last of them and of its two inverse workgroups re-arms it.
+__device__ __attribute__((always_inline)) inline void tp_vg_role(const TpDev& a, int g, unsigned char* smem_raw) {
+  const int n = a.n, nt = (n + 15) >> 4;
+  double* Xm = a.X;
+  unsigned long long* flag = ctl_flag(Xm, n);
+  unsigned long long* done = ctl_done(Xm, n);
+  const __amdgpu_buffer_rsrc_t rAm = make_rsrc(a.A, ((int64_t)(n - 1) * a.lda + n) * (int64_t)sizeof(double));
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  double* vl = (double*)smem_raw;                 // v (n)
+  int* s_ok = (int*)(vl + 256);
+  const int half = t >> 8, r = (t & 255) >> 4, cc = t & 15;
+  bool ok = true;
+  for (int kb = 0; kb < nt; ++kb) {
+    if (t == 0) {
+      int good = 0;
+      if (ok) {
+        for (int spin = 0; spin < (1 << 22); ++spin) {
+          const unsigned long long f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (f >= kFlagTag + (unsigned long long)(kb + 1) && f <= kFlagTag + (unsigned long long)nt) {
+            good = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      *s_ok = good;
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    ok = *s_ok != 0;
+    // v[kb*16 + e], e = w, w + RW (RW = 8 waves: two entries each)
+    for (int e = w; e < 16; e += RW) {
+      const int c = kb * 16 + e;
+      if (c < n) {
+        double s = 0;
+        for (int k = lane; k <= c; k += 64)
+          s += bload_sc1<double>(rAm, (uint32_t)(((int64_t)c * a.lda + k) * (int64_t)sizeof(double))) * a.vg_z[k];
+        s = wave_sum(s);
+        if (lane == 0) {
+          const double v = a.vg_muv[c] + s;
+          vl[c] = v;
+          if (g == 0) {
+            a.vg_v[c] = v;
+            a.vg_ellZ[c] = dexp(v);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // tiles (kb, J), J = 2 (g + nvg p) + half <= kb
+    for (int J = 2 * g + half; J <= kb; J += 2 * a.nvg) {
+      const int i = kb * 16 + r, j = J * 16 + cc;
+      if (i < n && j < n) {
+        const double lx = dexp(vl[i]), lz = dexp(vl[j]);
+        double r2 = 0;
+        const double dd = a.Z[i] / 1.0 - a.Z[j] / 1.0;
+        r2 += dd * dd;
+        const double S = lx * lx + lz * lz;
+        const double C = dsqrt(2.0 * (lx * lz) / S);
+        double k = 1.0 * C * dexp(-r2 / S);
+        if (i == j) k += a.jitter;
+        a.vg_K22[(int64_t)i * n + j] = k;
+      }
+    }
+  }
+  if (!ok && lane == 0) spin_gave_up(NMGP_STATUS_CHOL_SPIN);
+  __syncthreads();
+  if (t == 0) {
+    const unsigned long long old = __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == kDoneTag + (unsigned long long)(2 + a.nvg - 1)) {
+      __hip_atomic_store(flag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
 
 __device__ __attribute__((always_inline)) inline void tp_rows_role(const TpDev& a, int m, int rt,
                                                                    unsigned char* smem_raw) {
@@ -1793,11 +1883,15 @@ __global__ __launch_bounds__(RW * 64) void chol_tp_kernel(TpDev a) {
     } else if (a.rows[mat]) {
       chol3_trtri_role<double, NTPW1, 5, true>(Am, Xm, a.n, a.lda, a.ldx, role - 2, smem_raw, 2 + a.nct);
     } else {
-      chol3_trtri_role<double, NTPW1, 5>(Am, Xm, a.n, a.lda, a.ldx, role - 2, smem_raw);
+      // (matrix 0 with the fused K_G22 workgroups: they are readers of its progress word too)
+      chol3_trtri_role<double, NTPW1, 5>(Am, Xm, a.n, a.lda, a.ldx, role - 2, smem_raw, mat == 0 ? 2 + a.nvg : 2);
     }
-  } else {
+  } else if ((int)blockIdx.x < nroles + a.ntp * a.nct) {
     const int c = blockIdx.x - nroles, k = c / a.nct;
     tp_rows_role(a, a.tpm[k], c - k * a.nct, smem_raw);
+  } else {
+    // (after the row workgroups: dispatched last, they never take a CU a row workgroup is waiting for)
+    tp_vg_role(a, blockIdx.x - nroles - a.ntp * a.nct, smem_raw);
   }
   TP_STAMP(tr, 1);
 }
@@ -1861,7 +1955,17 @@ static int chol_tp_launch(const nmgp_chol_tp_args* h, hipStream_t s) {
   }
   a.nct = g.B > 0 ? (int)((g.B + TPR - 1) / TPR) : 0;
   a.dbg = getenv("NMGP_TP_DBG") ? atoi(getenv("NMGP_TP_DBG")) : 0;
-  const unsigned grid = (unsigned)(4 * a.batch + a.ntp * a.nct);
+  if (g.vg_wgs < 0 || g.vg_wgs > 64) return -1;
+  if (g.vg_wgs > 0) {
+    if (!g.vg_muv || !g.vg_z || !g.vg_v || !g.vg_ellZ || !g.vg_K22 || !g.Z || a.rows[0] != 0) return -1;
+    a.nvg = (int)g.vg_wgs;
+    a.vg_muv = g.vg_muv;
+    a.vg_z = g.vg_z;
+    a.vg_v = g.vg_v;
+    a.vg_ellZ = g.vg_ellZ;
+    a.vg_K22 = g.vg_K22;
+  }
+  const unsigned grid = (unsigned)(4 * a.batch + a.nvg + a.ntp * a.nct);
   const size_t sm = chol_tp_smem(a.n);
   const int nt = (a.n + 15) >> 4, ntiles = nt * (nt + 1) / 2;
   if (ntiles <= RW * 9)

@@ -182,6 +182,8 @@ class DsviEngine:
         # NMGP_FUSE_TP=0 keeps the separate launches (the tests' equivalence switch)
         self.fuse_tp = (self.dt == torch.float64 and 128 <= M <= 256 and B <= 4096
                         and os.environ.get("NMGP_FUSE_TP", "1") != "0")
+        # and the Gibbs prior's K22 from the first of them (NMGP_FUSE_VG=0: its own launch, dsvi_vg22)
+        self.fuse_vg = self.fuse_tp and os.environ.get("NMGP_FUSE_VG", "1") != "0"
         # per-(output, factor) L-bar products of the grouped backward (bwd_lbar), summed by nmgp_lbar_reduce: D(D+1)/2
         # slots of M x M + M.  Only where the slots stay small (PM2.5: 15 slots, 7.9 MB); many outputs with few
         # rows each (HCP-like D = 50) keep one product per factor, whose k loop is then short anyway
@@ -454,8 +456,14 @@ class DsviEngine:
             # lam I (theta only) are built off the chain at the step's start (build_k22), K_G22 by the v launch
             hyp_addr = lambda k: th.data_ptr() + (hyp + k) * th.element_size()
             rbf = [dict(rows=1, hyp=hyp_addr(2 * k), K12=self.K12[k], T=self.T[k], P=self.P[k]) for k in range(3)]
+            # training steps: K_G22 (and v, ell_Z) from extra workgroups of the same launch once L_v is factored
+            # (round 6; compute_ELBO keeps the v launch, which its cached samples rerun alone)
+            vg = None
+            if not elbo_mode and self.fuse_vg:
+                vg = dict(muv=th.data_ptr() + muv * th.element_size(), z=self.noise, v=self.v, ellZ=self.ellZ,
+                          K22=self.Afac[NF + 3], wgs=int(os.environ.get("NMGP_VG_WGS", "8")))
             p["chol_tp_main"] = H.CholTp(self.Afac[FV], self.Cinv[FV], self.info[FV:], M, [dict()] + rbf,
-                                         jitter=self.jitter, Z=self.Z, x=self.x, B=B)
+                                         jitter=self.jitter, Z=self.Z, x=self.x, B=B, vg=vg)
             p["chol_tp_G"] = H.CholTp(self.Afac[NF + 3], self.Cinv[NF + 3], self.info[NF + 3:], M,
                                       [dict(rows=2, K12=self.K12[3], T=self.T[3], P=self.P[3])],
                                       jitter=self.jitter, Z=self.Z, ellZ=self.ellZ, x=self.x, B=B,
@@ -1007,11 +1015,17 @@ class DsviEngine:
             ("chol", "chol", chol_main, "main"),
             ("sig", "main", "chol"),
         ]
-        steps += [
-            # fused: v and K_G22 + lam I in one wide launch (dsvi_vg22_kernel)
-            ("v", "row", row(getattr(lib, ("nmgp_dsvi_vg22_" if fuse else "nmgp_dsvi_hyper_") + self.sfx)), "main"),
-            ("sig", "main", "v"),
-        ]
+        vg_in_chol = fuse and self.fuse_vg and not elbo_mode
+        if not vg_in_chol:
+            steps += [
+                # fused: v and K_G22 + lam I in one wide launch (dsvi_vg22_kernel)
+                ("v", "row", row(getattr(lib, ("nmgp_dsvi_vg22_" if fuse else "nmgp_dsvi_hyper_") + self.sfx)), "main"),
+            ]
+        steps.append(("sig", "main", "v"))
+        if vg_in_chol:
+            # the Gibbs launch follows the first one directly: captured before the other streams' waits on it, so
+            # that it is the first launch's first child and keeps its hardware queue
+            steps += [("chol_G", "chol", chol_g, "main"), ("sig", "main", "cholG")]
         if side_fac:        # the variational factors' batched factorization after the fused prior launch
             steps += [("wait", "side", "chol")] + side_fac
         steps.append(("wait", "side2", "chol"))
@@ -1026,7 +1040,8 @@ class DsviEngine:
             qp = [("quad_P", "gemm", gemm("quad_P"), "side2"), ("sig", "side2", "quadP")] if not elbo_mode else []
             i3 = [("inv3", "gemm", gemm("inv3"), "side2"), ("proj3", "gemm", gemm("proj3"), "side2")]
             steps += i3 + qp
-            steps += [("chol_G", "chol", chol_g, "main"), ("sig", "main", "cholG")]
+            if not vg_in_chol:
+                steps += [("chol_G", "chol", chol_g, "main"), ("sig", "main", "cholG")]
         else:
             if p["inv3"] is not None:
                 steps.append(("inv3", "gemm", gemm("inv3"), "side2"))

@@ -570,7 +570,9 @@ class CholTp:
     Gibbs K12 rows with ellZ): K12, T = K12 L^-T and P = T L^-1 written to the (B, n) tensors mats[b]["K12" / "T" /
     "P"].  The argument struct is built once; a call is one launch (graph-capturable)."""
 
-    def __init__(self, A, X, info, n, mats, *, jitter=0.0, Z=None, ellZ=None, x=None, B=0, trow=None):
+    def __init__(self, A, X, info, n, mats, *, jitter=0.0, Z=None, ellZ=None, x=None, B=0, trow=None, vg=None):
+        """vg = dict(muv, z, v, ellZ, K22, wgs): mats[0] is Sigma_v, and `wgs` extra workgroups form v = muv + L_v z,
+        ellZ = exp(v) and the Gibbs prior's K22 + jitter I (n x n, lower 16 x 16 tiles) once L_v is factored."""
         for t_, nm in ((A, "A"), (X, "X"), (info, "info")):
             L.require_device(t_, nm)
         assert A.dtype == torch.float64 and X.dtype == torch.float64 and 1 <= len(mats) <= 4
@@ -586,8 +588,11 @@ class CholTp:
             mt = a.mats[b]
             mt.reserved, mt.rows = 0, int(m.get("rows", 0))
             mt.hyp, mt.K12, mt.T, mt.P = (_ptr(m.get(k)) for k in ("hyp", "K12", "T", "P"))
+        if vg is not None:
+            a.vg_muv, a.vg_z, a.vg_v, a.vg_ellZ, a.vg_K22 = (_ptr(vg[k]) for k in ("muv", "z", "v", "ellZ", "K22"))
+            a.vg_wgs = int(vg.get("wgs", 16))
         self.a = a
-        self._keep = (A, X, info, Z, ellZ, x, tr, mats)     # the struct holds raw addresses of these
+        self._keep = (A, X, info, Z, ellZ, x, tr, mats, vg)     # the struct holds raw addresses of these
 
     def __call__(self, stream=None):
         s = stream if stream is not None else L.stream_handle()

@@ -221,6 +221,16 @@ typedef struct nmgp_chol_tp_args {
   double* ellX;        /* rows 2 outputs (B) */
   double* var_t;
   nmgp_chol_tp_mat mats[4];
+  /* vg_wgs > 0 (round 6): mats[0] is Sigma_v (rows 0) and vg_wgs extra workgroups form, once L_v is factored,
+   * v = vg_muv + L_v vg_z -> vg_v, exp(v) -> vg_ellZ and the Gibbs prior's K22 + jitter I (lower 16 x 16 tiles,
+   * leading dimension n) -> vg_K22: nmgp_dsvi_vg22_*'s outputs from the same launch (code/utils.py:97-103,
+   * code/nmgp_dsvi.py:198-215).  0: off.                                                                 */
+  const double* vg_muv;
+  const double* vg_z;
+  double* vg_v;
+  double* vg_ellZ;
+  double* vg_K22;
+  int64_t vg_wgs;
 } nmgp_chol_tp_args;
 int nmgp_chol_tp_f64(const nmgp_chol_tp_args* args, hipStream_t stream);
 /* diagnostics (synchronous): the launch's per-workgroup phase stamps, recorded when NMGP_TP_DBG has bit 16 set

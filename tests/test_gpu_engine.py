@@ -588,3 +588,35 @@ def test_fused_prior_launches_match_separate_launches(monkeypatch, sizes):
     assert abs(l1 - l0) / abs(l0) < 5e-11 and _rel(g1, g0) < 1e-8
     assert _rel(K1[:3], K0[:3]) < 1e-14 and _rel(K1[3], K0[3]) < 1e-8 and _rel(e1, e0) < 1e-8
     assert _rel(T1, T0) < 1e-8 and _rel(P1, P0) < 1e-7
+
+
+def test_fused_gibbs_k22_matches_its_own_launch(monkeypatch):
+    """Round 6: the training step forms v, ell_Z and the Gibbs prior's K22 in extra workgroups of the fused prior launch
+    that factors Sigma_v (NMGP_FUSE_VG=1) instead of the dsvi_vg22 launch after it: the same sums in the same order,
+    so v, ell_Z, K_G22 (its lower triangle, before the Gibbs factorization overwrote it: read back as L L^T), the
+    loss and the gradient are bit-identical."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.engine import DsviEngine
+    g = G.load("pm25_forward")
+    D, M = 5, 256
+    p = G.params(g, D=D, M=M)
+    theta = torch.cat([p[k].reshape(-1) for k in O.PARAM_NAMES]).to("cuda")
+    x, y, sz, noise = g["x"], g["y"], [int(s) for s in g["sizes"]], g["noise"]
+    B = sum(sz)
+    res = {}
+    for vg in ("1", "0"):
+        monkeypatch.setenv("NMGP_FUSE_TP", "1")
+        monkeypatch.setenv("NMGP_FUSE_VG", vg)
+        eng = DsviEngine(D, M, B, g["z"])
+        assert eng.fuse_tp and eng.fuse_vg == (vg == "1")
+        grad = torch.zeros_like(theta)
+        eng.bind(theta, grad, frozen_mask=0, N=float(g["N"]))
+        eng.load_batch(x, y, sz, noise=noise)
+        for _ in range(2):                     # (a second step re-arms the launch's progress words)
+            eng.forward_backward()
+        torch.cuda.synchronize()
+        eng.check_info()
+        Lg = torch.tril(eng.Afac[eng.NF + 3].clone())
+        res[vg] = (eng.out[:1].clone(), grad.clone(), eng.v.clone(), eng.ellZ.clone(), Lg, eng.T.clone(),
+                   eng.P.clone())
+    for a, b in zip(res["1"], res["0"]):
+        assert torch.equal(a, b)
