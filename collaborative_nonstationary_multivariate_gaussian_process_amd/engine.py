@@ -183,7 +183,7 @@ class DsviEngine:
         self.fuse_tp = (self.dt == torch.float64 and 128 <= M <= 256 and B <= 4096
                         and os.environ.get("NMGP_FUSE_TP", "1") != "0")
         # and the Gibbs prior's K22 from the first of them (NMGP_FUSE_VG=0: its own launch, dsvi_vg22)
-        self.fuse_vg = self.fuse_tp and os.environ.get("NMGP_FUSE_VG", "0") != "0"
+        self.fuse_vg = self.fuse_tp and os.environ.get("NMGP_FUSE_VG", "1") != "0"
         # per-(output, factor) L-bar products of the grouped backward (bwd_lbar), summed by nmgp_lbar_reduce: D(D+1)/2
         # slots of M x M + M.  Only where the slots stay small (PM2.5: 15 slots, 7.9 MB); many outputs with few
         # rows each (HCP-like D = 50) keep one product per factor, whose k loop is then short anyway
