@@ -61,16 +61,25 @@ __device__ inline int prior_of(const nmgp_dsvi_args& a, int f) {
 
 // sum_{q < cnt} p[q * stride] in a fixed order with 8 loads in flight: written as a plain loop these
 // partial-sum reductions waited one L2 round trip per element (63 G12 column partials in the v backward)
+// 32 loads in flight per round (round 6: the pairwise backward's 8-row tiles made the G12 column partials 250 deep at
+// PM2.5, and 8 in flight left the v backward 32 round trips long); fixed summation order
 template <typename T> __device__ inline T strided_sum(const T* p, int cnt, int64_t stride) {
-  T acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int q = 0; q < cnt; q += 8) {
-    T v[8];
+  constexpr int U = 32;
+  T acc[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = (q + u < cnt) ? p[(int64_t)(q + u) * stride] : (T)0;
+  for (int u = 0; u < U; ++u) acc[u] = 0;
+  for (int q = 0; q < cnt; q += U) {
+    T v[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc[u] += v[u];
+    for (int u = 0; u < U; ++u) v[u] = (q + u < cnt) ? p[(int64_t)(q + u) * stride] : (T)0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] += v[u];
   }
-  return ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+#pragma unroll
+  for (int h = U / 2; h > 0; h >>= 1)
+#pragma unroll
+    for (int u = 0; u < h; ++u) acc[u] += acc[u + h];
+  return acc[0];
 }
 
 template <typename T> struct RowBuf {
