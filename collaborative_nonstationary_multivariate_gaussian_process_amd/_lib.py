@@ -150,6 +150,8 @@ _SIGS = {
     "nmgp_potrf_blocked_f64": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "nmgp_chol_inv_batched_ws_f32": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64,
                                              c_vp]),
+    "nmgp_chol_split_point": (c_i64, [c_i64]),
+    "nmgp_chol_blockinv_batched_f32": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "nmgp_syevj_workspace_size_f64": (c_i64, [c_i64]),
     "nmgp_syevj_batched_f64": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
                                        c_vp]),
@@ -165,6 +167,9 @@ _SIGS = {
                                               c_int, c_int, c_dbl, c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
                                               c_i64, c_vp, c_vp, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp,
                                               c_vp]),
+    "nmgp_gemm_big_offsets_dual_f32": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_int, c_vp, c_i64, c_i64, c_int,
+                                               c_int, c_int, c_int, c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
+                                               c_i64, c_vp, c_vp, c_dbl, c_vp, c_vp, c_i64, c_int, c_vp]),
     "nmgp_pairwise_f64": (c_int, [c_vp, c_int, c_int, c_vp]),
     "nmgp_pairwise_f32": (c_int, [c_vp, c_int, c_int, c_vp]),
     "nmgp_pairwise_single_f64": (c_int, [ctypes.POINTER(PairwiseDesc), c_vp]),

@@ -2264,11 +2264,17 @@ int potrf_strip_f32(const float* L, float* C, int64_t lda, int m, int c1, hipStr
 
 // f32 recursion (same algebra as chol_inv_rec below) with the products on the 128x128 MFMA kernel
 // of gemm_big.hip, split-K into `ws` where the tile grid would not fill the chip.
-static int chol_inv_rec_big(float* A, int n, int64_t lda, int64_t sA, float* X, int64_t ldx, int64_t sX,
-                            int64_t batch, int32_t* info, hipStream_t s, int col_off, void* ws) {
-  if (n <= 128) return chol_inv_small<float>(A, n, lda, sA, X, ldx, sX, batch, info, s, col_off, col_off == 0);
+static int chol_split_point(int n) {
   int n1 = ((n / 2 + 127) / 128) * 128;
-  if (n1 >= n) n1 = n - 128;
+  return n1 >= n ? n - 128 : n1;
+}
+// full = 0 (the top level of the KL L-bar solve form, nmgp_chol_blockinv_batched_f32): the factor and the inverses
+// X11, X22 of the split's two diagonal blocks only -- X21 = -X22 L21 X11 (two products) is not formed, X21 holds the
+// staged copy of A21 (scratch) and X12 is not touched
+static int chol_inv_rec_big(float* A, int n, int64_t lda, int64_t sA, float* X, int64_t ldx, int64_t sX,
+                            int64_t batch, int32_t* info, hipStream_t s, int col_off, void* ws, int full = 1) {
+  if (n <= 128) return chol_inv_small<float>(A, n, lda, sA, X, ldx, sX, batch, info, s, col_off, col_off == 0);
+  const int n1 = chol_split_point(n);
   const int n2 = n - n1, nb = (int)batch;
   int rc;
   float* A21 = A + (int64_t)n1 * lda;
@@ -2288,6 +2294,7 @@ static int chol_inv_rec_big(float* A, int n, int64_t lda, int64_t sA, float* X, 
     return rc;
   if ((rc = block_copy<float>(nullptr, 0, 0, A + n1, lda, sA, n1, n2, batch, s)) != NMGP_OK) return rc;   // L12 = 0
   if ((rc = chol_inv_rec_big(A22, n2, lda, sA, X22, ldx, sX, batch, info, s, col_off + n1, ws)) != NMGP_OK) return rc;
+  if (!full) return NMGP_OK;
   // T = L21 X11 (op(B)(k,j) = X11[k][j], lower) staged in X12;  X21 = -X22 T.  With n1 == n2 (every level of the
   // power-of-two shapes) T fits X12 row-major: coalesced stores, and the second product reads it k-row-wise (the
   // non-k-contiguous operand path stages as fast as the k-contiguous one).  Otherwise T is stored transposed.
@@ -2600,6 +2607,18 @@ int nmgp_chol_inv_batched_f64(double* A, int64_t n, int64_t lda, int64_t sA, dou
 int nmgp_chol_inv_batched_f32(float* A, int64_t n, int64_t lda, int64_t sA, float* X, int64_t ldx, int64_t sX,
                               int64_t b, int32_t* info, hipStream_t s) {
   return nmgp::chol_inv_launch<float>(A, n, lda, sA, X, ldx, sX, b, info, s);
+}
+int64_t nmgp_chol_split_point(int64_t n) { return n > 256 ? (int64_t)nmgp::chol_split_point((int)n) : 0; }
+int nmgp_chol_blockinv_batched_f32(float* A, int64_t n, int64_t lda, int64_t sA, float* X, int64_t ldx, int64_t sX,
+                                   int64_t b, int32_t* info, hipStream_t s) {
+  if (A == nullptr) return -1;
+  if (n <= 256) return -2;
+  if (lda < n) return -3;
+  if (X == nullptr) return -5;
+  if (ldx < n) return -6;
+  if (b < 0 || b > 65535) return -8;
+  if (b == 0) return NMGP_OK;
+  return nmgp::chol_inv_rec_big(A, (int)n, lda, sA, X, ldx, sX, b, info, s, 0, nullptr, 0);
 }
 int64_t nmgp_chol_inv_workspace_size_f32(int64_t n, int64_t batch) {
   return (n > 256 && batch > 0) ? (int64_t)nmgp::gemm_big_ws_bytes() : 0;

@@ -55,6 +55,9 @@ struct BigGemmArgs {
   const float* E; const int64_t* offE; int64_t sEi, sEj;
   const float* RS; const int64_t* offRS;
   float gamma;
+  // NMGP_EPI with D: the raw product acc(i, j) is also stored to D(i, j) = D[offD[b] + i * sDi + j] (the KL L-bar's
+  // solve form needs G21 = X22^T W21 itself besides the gradient rows it is added to)
+  float* D; const int64_t* offD; int64_t sDi;
   // per-problem k range from the minibatch segment table (offsets variants): problem b runs
   // k in [seg[kseg[b]], seg[kseg[b] + kspan[b]]) -- rows of the outputs it sums over
   const int32_t* seg; const int32_t* kseg; const int32_t* kspan;
@@ -404,7 +407,7 @@ __device__ __forceinline__ bool big_combine(const BigGemmArgs& g, int me, int S,
 // store before it (64 dependent round trips per tile in the KL L-bar product, the ECoG step's longest launch).
 // E must not alias C.  A is a template parameter so every accumulator index is a constant.
 template <int MODE, int A, int NB = 2>
-__device__ __forceinline__ void big_epi_half(const BigGemmArgs& g, float* Cb, __amdgpu_buffer_rsrc_t rCb,
+__device__ __forceinline__ void big_epi_half(const BigGemmArgs& g, float* Cb, float* Db, __amdgpu_buffer_rsrc_t rCb,
                                              __amdgpu_buffer_rsrc_t rEb, __amdgpu_buffer_rsrc_t rRS, int M, int i0,
                                              int j0, const f32x16 (&acc)[2][NB]) {
   constexpr bool EPI = MODE == 2;
@@ -458,6 +461,9 @@ __device__ __forceinline__ void big_epi_half(const BigGemmArgs& g, float* Cb, __
         }
         if (tril && j > i) x = 0.0f;
         Cb[(int64_t)i * g.sCi + (int64_t)j * g.sCj] = x;
+        if constexpr (EPI) {
+          if (Db != nullptr) Db[(int64_t)i * g.sDi + j] = acc[A][b][r];
+        }
       }
     }
   }
@@ -465,15 +471,15 @@ __device__ __forceinline__ void big_epi_half(const BigGemmArgs& g, float* Cb, __
 
 // C = alpha * acc + beta * C (+ diag_add, + the KL epilogue) on the stored part of the tile.
 template <int MODE, int NB = 2>
-__device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, float* Cb, const float* Eb, const float* rs, int M,
-                                             int i0, int j0, f32x16 (&acc)[2][NB]) {
+__device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, float* Cb, float* Db, const float* Eb,
+                                             const float* rs, int M, int i0, int j0, f32x16 (&acc)[2][NB]) {
   constexpr bool EPI = MODE == 2;
   const __amdgpu_buffer_rsrc_t rCb = make_rsrc(Cb, ((int64_t)(M - 1) * g.sCi + (int64_t)(g.n - 1) * g.sCj + 1) * 4);
   const __amdgpu_buffer_rsrc_t rEb =
       make_rsrc(EPI ? Eb : Cb, EPI ? ((int64_t)(M - 1) * g.sEi + (int64_t)(g.n - 1) * g.sEj + 1) * 4 : 0);
   const __amdgpu_buffer_rsrc_t rRS = make_rsrc(EPI ? rs : Cb, EPI ? (int64_t)M * 4 : 0);
-  big_epi_half<MODE, 0, NB>(g, Cb, rCb, rEb, rRS, M, i0, j0, acc);
-  big_epi_half<MODE, 1, NB>(g, Cb, rCb, rEb, rRS, M, i0, j0, acc);
+  big_epi_half<MODE, 0, NB>(g, Cb, Db, rCb, rEb, rRS, M, i0, j0, acc);
+  big_epi_half<MODE, 1, NB>(g, Cb, Db, rCb, rEb, rRS, M, i0, j0, acc);
 }
 
 // Row-vector epilogue through LDS (row-contiguous C, and E, 16-byte aligned): the accumulators (each lane holds 16
@@ -484,8 +490,9 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& g, float* Cb, co
 // tile.  Same arithmetic, element by element, as big_epi_half.
 constexpr int BCP = 136;   // LDS pitch of the C image (floats): lanes 32..63 of a column write land 32 banks over
 template <int MODE, int NB = 2>
-__device__ __forceinline__ void big_epilogue_rows(const BigGemmArgs& g, float* Cb, const float* Eb, const float* rs,
-                                                  int M, int i0, int j0, const f32x16 (&acc)[2][NB], float* sm) {
+__device__ __forceinline__ void big_epilogue_rows(const BigGemmArgs& g, float* Cb, float* Db, const float* Eb,
+                                                  const float* rs, int M, int i0, int j0, const f32x16 (&acc)[2][NB],
+                                                  float* sm) {
   constexpr bool EPI = MODE == 2;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -521,6 +528,10 @@ __device__ __forceinline__ void big_epilogue_rows(const BigGemmArgs& g, float* C
   const __amdgpu_buffer_rsrc_t rC = make_rsrc(Cb, ((int64_t)(gm - 1) * sCi + gn) * 4);
   const __amdgpu_buffer_rsrc_t rE = make_rsrc(EPI ? Eb : Cb, EPI ? ((int64_t)(gm - 1) * sEi + gn) * 4 : 0);
   const __amdgpu_buffer_rsrc_t rR = make_rsrc(EPI ? rs : Cb, EPI ? (int64_t)gm * 4 : 0);
+  const bool dst = EPI && Db != nullptr;
+  const int64_t sDi = EPI ? g.sDi : 0;
+  const __amdgpu_buffer_rsrc_t rD =
+      make_rsrc(dst ? (float*)uniform64((int64_t)Db) : Cb, dst ? ((int64_t)(gm - 1) * sDi + gn) * 4 : 0);
   constexpr uint32_t oob = 0x80000000u;
   // 16 chunks per thread in two halves of 8 (loads of a half in flight together)
 #pragma unroll
@@ -565,6 +576,18 @@ __device__ __forceinline__ void big_epilogue_rows(const BigGemmArgs& g, float* C
         x[e] = v;
       }
       const uint32_t off = (uint32_t)(((int64_t)i * sCi + j) * 4);
+      if (dst) {
+        // the raw product (D: no OUT_LOWER / OUT_TRIL masking -- the host allows D on full outputs only)
+        const uint32_t offd = (uint32_t)(((int64_t)i * sDi + j) * 4);
+        if (j + 3 < gn) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4g, av), rD, offd, 0, 0);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(((const float*)&av)[e]), rD,
+                                                  j + e < gn ? offd + 4 * e : oob, 0, 0);
+        }
+      }
       if (j + 3 < gn && !(lower && j + 3 > i)) {
         u32x4g v;
 #pragma unroll
@@ -723,12 +746,14 @@ __global__ __launch_bounds__(512 / NB, 4 / NB) void gemm_big_kernel(const BigGem
       float* Cb = g.C + (MODE ? uniform64(g.offC[bat]) : bat * g.sCb) + roff * g.sCi;
       const float* Eb = EPI ? g.E + (g.offE ? uniform64(g.offE[bat]) : 0) + roff * g.sEi : nullptr;
       const float* rsb = EPI ? g.RS + (g.offRS ? uniform64(g.offRS[bat]) : 0) + roff : nullptr;
+      float* Db = (EPI && g.D != nullptr) ? g.D + uniform64(g.offD[bat]) + roff * g.sDi : nullptr;
       const bool rows = g.sCj == 1 && (g.sCi & 3) == 0 && (((uintptr_t)Cb) & 15) == 0 &&
-                        (!EPI || (g.sEj == 1 && (g.sEi & 3) == 0 && (((uintptr_t)Eb) & 15) == 0));
+                        (!EPI || (g.sEj == 1 && (g.sEi & 3) == 0 && (((uintptr_t)Eb) & 15) == 0)) &&
+                        (Db == nullptr || ((g.sDi & 3) == 0 && (((uintptr_t)Db) & 15) == 0));
       if (rows)
-        big_epilogue_rows<MODE>(g, Cb, Eb, rsb, M, i0, j0, acc, big_smem);
+        big_epilogue_rows<MODE>(g, Cb, Db, Eb, rsb, M, i0, j0, acc, big_smem);
       else
-        big_epilogue<MODE>(g, Cb, Eb, rsb, M, i0, j0, acc);
+        big_epilogue<MODE>(g, Cb, Db, Eb, rsb, M, i0, j0, acc);
     }
     it += step;
   }
@@ -816,7 +841,7 @@ __global__ __launch_bounds__(256, 2) void potrf_step_kernel(PotrfStepArgs pa) {
       __hip_atomic_store(pa.flag + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  big_epilogue<0>(g2, g2.C, nullptr, nullptr, g2.m, i0, 0, acc);
+  big_epilogue<0>(g2, g2.C, nullptr, nullptr, nullptr, g2.m, i0, 0, acc);
 }
 
 // Row-panel variant (the default): the step kernel above runs two dependent 128x128x128 products on each
@@ -999,6 +1024,7 @@ struct BigEpi {
   float gamma = 0.0f;
   const int32_t* seg = nullptr; const int32_t* kseg = nullptr; const int32_t* kspan = nullptr;
   const int32_t* rseg = nullptr; const int32_t* rspan = nullptr;
+  float* D = nullptr; const int64_t* offD = nullptr; int64_t sDi = 0;
 };
 
 static int gemm_big_f32_ex(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C,
@@ -1017,6 +1043,10 @@ static int gemm_big_f32_ex(const float* A, int64_t lda, const float* B, int64_t 
   g.RS = ep.RS; g.offRS = ep.offRS; g.gamma = ep.gamma;
   g.seg = ep.seg; g.kseg = ep.kseg; g.kspan = ep.kspan; g.koff = 0;
   g.rseg = ep.rseg; g.rspan = ep.rspan;
+  g.D = ep.D; g.offD = ep.offD; g.sDi = ep.sDi;
+  if (ep.D != nullptr && (!(flags & NMGP_EPI) || ep.offD == nullptr || (flags & (NMGP_OUT_LOWER | NMGP_OUT_TRIL)) ||
+                          ep.sDi < n || (int64_t)(m - 1) * ep.sDi + n >= 0x7fffffffLL / 4))
+    return -1;
   if (ep.kseg != nullptr && (offA == nullptr || ep.seg == nullptr || ep.kspan == nullptr)) return -1;
   if (ep.rseg != nullptr && (offA == nullptr || ep.seg == nullptr || ep.rspan == nullptr || (flags & NMGP_OUT_LOWER)))
     return -1;
@@ -1078,8 +1108,12 @@ static int gemm_big_f32_ex(const float* A, int64_t lda, const float* B, int64_t 
   if (offs && (offB == nullptr || offC == nullptr)) return -1;
   if (!offs && (diag_add != 0.0f || (flags & NMGP_OUT_TRIL))) return -1;   // those live in the offsets variants
   if (epi) {
-    if (!offs || g.a_kcontig || g.b_kcontig) return -1;   // only the KL L-bar form (both operands transposed)
-    go(gemm_big_kernel<false, false, 2, 2>, 2);
+    // the KL L-bar forms: both operands transposed, or (the solve form's R = L21 - C21 W11) A k-contiguous
+    if (!offs || g.b_kcontig) return -1;
+    if (g.a_kcontig)
+      go(gemm_big_kernel<true, false, 2, 2>, 2);   // (8 waves: 88 bytes of scratch per lane)
+    else
+      go(gemm_big_kernel<false, false, 2, 2>, 2);
   } else if (offs) {
     if (g.a_kcontig && g.b_kcontig)
       go(gemm_big_kernel<true, true, 1, kBigNB>, kBigNB);
@@ -1154,7 +1188,7 @@ static int big_offsets_impl(const float* A, int64_t lda, int a_kcontig, const fl
                             const float* E, const int64_t* offE, int64_t sEi, int64_t sEj, const float* RS,
                             const int64_t* offRS, double gamma, const int32_t* seg, const int32_t* kseg,
                             const int32_t* kspan, const int32_t* rseg, const int32_t* rspan, int batch, void* ws,
-                            hipStream_t s) {
+                            hipStream_t s, float* D = nullptr, const int64_t* offD = nullptr, int64_t sDi = 0) {
   if (A == nullptr) return -1;
   if (B == nullptr) return -4;
   if (C == nullptr) return -7;
@@ -1177,6 +1211,7 @@ static int big_offsets_impl(const float* A, int64_t lda, int a_kcontig, const fl
   if (rseg != nullptr && (flags & NMGP_OUT_LOWER)) return -13;
   ep.seg = seg; ep.kseg = kseg; ep.kspan = kspan;
   ep.rseg = rseg; ep.rspan = rspan;
+  ep.D = D; ep.offD = offD; ep.sDi = sDi;
   return nmgp::gemm_big_f32_ex(A, lda, B, ldb, b_kcontig, C, sCi, sCj, m, n, k, flags, (float)alpha, (float)beta, 0, 0,
                                0, offA, offB, offC, (float)diag_add, batch, ws, s, ep);
 }
@@ -1201,5 +1236,19 @@ int nmgp_gemm_big_offsets_seg_f32(const float* A, int64_t lda, int a_kcontig, co
   return big_offsets_impl(A, lda, a_kcontig, B, ldb, b_kcontig, C, sCi, sCj, m, n, k, flags, alpha, beta, diag_add,
                           offA, offB, offC, E, offE, sEi, sEj, RS, offRS, gamma, seg, kseg, kspan, rseg, rspan, batch,
                           ws, s);
+}
+int nmgp_gemm_big_offsets_dual_f32(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb,
+                                   int b_kcontig, float* C, int64_t sCi, int64_t sCj, int m, int n, int k, int flags,
+                                   double alpha, double beta, const int64_t* offA, const int64_t* offB,
+                                   const int64_t* offC, const float* E, const int64_t* offE, int64_t sEi, int64_t sEj,
+                                   const float* RS, const int64_t* offRS, double gamma, float* D, const int64_t* offD,
+                                   int64_t sDi, int batch, hipStream_t s) {
+  if (!(flags & NMGP_EPI)) return -13;
+  if (D == nullptr) return -27;
+  if (offD == nullptr) return -28;
+  if (sDi < n) return -29;
+  return big_offsets_impl(A, lda, a_kcontig, B, ldb, b_kcontig, C, sCi, sCj, m, n, k, flags, alpha, beta, 0.0, offA,
+                          offB, offC, E, offE, sEi, sEj, RS, offRS, gamma, nullptr, nullptr, nullptr, nullptr, nullptr,
+                          batch, nullptr, s, D, offD, sDi);
 }
 }

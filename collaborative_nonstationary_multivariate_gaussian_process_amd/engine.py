@@ -170,6 +170,12 @@ class DsviEngine:
         # round 6: with big_side the row-segmented B x M x M products (W = P L, P-bar = W-hat L^T) run on the 128x128
         # kernel too; NMGP_BIG_ROWS=0 keeps them on the grouped kernel (A/B and equivalence switch)
         self.big_rows = self.big_side and os.environ.get("NMGP_BIG_ROWS", "1") != "0"
+        # round 6: the KL L-bar of the variational factors in the solve form, Sigma^-1 L = C^-T (C^-1 L) applied
+        # blockwise from the factor and the inverses of its two diagonal blocks (the recursion's top-level
+        # off-diagonal inverse block, two products, is not formed: nmgp_chol_blockinv_batched_f32).  NMGP_KL_SOLVE=0
+        # keeps the explicit-inverse form (A/B and equivalence switch)
+        self.kl_solve = (self.big_side and M > 256 and M % 128 == 0 and os.environ.get("NMGP_KL_SOLVE", "1") != "0")
+        self._ones = torch.ones(M, dtype=self.dt, device=self.dev) if self.kl_solve else None
         # per-pair P-bar products W-hat_ij L_ij^T, slot j (pair kernels, or the 128x128 kernel at M >= 512)
         self.Zp = e(D, B, M) if (self.pair_stream or (self.big_rows and self.Q > 0)) else None
         # HCP / ECoG shapes (fp32, M >= 512): the D+Q factor products run on the 128x128 f32 MFMA kernel at
@@ -420,6 +426,8 @@ class DsviEngine:
             if not elbo_mode:
                 p["xs_side"] = H.BigBatch(self.Cinv, th, self.Xs, slots, offs_f, slots, M, M, M, lda=M, ldb=M,
                                           b_kcontig=False, flags=L.A_LOWER | L.B_LOWER | L.OUT_TRIL)
+                if self.kl_solve and FV > 0:
+                    p["xs_side"] = self._kl_solve_xs(th, slots, offs_f)
         # F6: P_k = K12_k Ainv_k (k = t,0,1) ; Y_t, Y_0, Y_1
         d6 = [pproj(k) for k in range(3)] if not (p64 or self.fuse_tp) else []
         d6 += [g(self.Y, self.Ainv, th, M, 1, M, (M, 1, 0), (1, M, 0), (1, M), offs=(0, muv, D * M)),
@@ -652,6 +660,8 @@ class DsviEngine:
                                       flags=L.A_UPPER | L.B_LOWER | L.OUT_TRIL | L.EPI_E_LOWER, alpha=-1.0, beta=1.0,
                                       epi=(th, fac_off[:NFK], (M, 1), fb,
                                            [NF + 4 * M + prior_of[f] * M for f in range(NFK)], 1.0))
+            if self.kl_solve and FV > 0 and not elbo_mode:
+                p["kl_lbar"] = self._kl_solve_lbar(th, gr, fb, fac_off, prior_of, NFK)
         # B4: Abar_k -= 1/2 Y_k diag(sel_k) Y_k^T
         ybase = [D * M, (D + 1) * M, (D + 1 + NPC) * M, 0]
         ncol = [1, NPC, NPC, D]
@@ -920,12 +930,13 @@ class DsviEngine:
 
         chol_fn = getattr(lib, "nmgp_chol_inv_batched_" + self.sfx)
 
-        def chol(first, count):
-            # fused factor + inverse: Afac <- L (in place), Cinv <- L^{-1}
+        def chol(first, count, blockinv=False):
+            # fused factor + inverse: Afac <- L (in place), Cinv <- L^{-1} (blockinv: the inverses of the two
+            # diagonal blocks of the top-level split only -- the KL L-bar solve form)
             es = self.Afac.element_size()
-            return lambda s: L.check(chol_fn(vp(Af + first * MM * es), M, M, MM,
-                                                                   vp(Ci + first * MM * es), M, MM, count,
-                                                                   vp(info + first * 4), s), "chol_inv")
+            fn = lib.nmgp_chol_blockinv_batched_f32 if blockinv else chol_fn
+            return lambda s: L.check(fn(vp(Af + first * MM * es), M, M, MM, vp(Ci + first * MM * es), M, MM, count,
+                                        vp(info + first * 4), s), "chol_inv")
 
         if self.prior64:
             conv_up, conv_dn = lib.nmgp_convert_f32_to_f64, lib.nmgp_convert_f64_to_f32
@@ -992,7 +1003,7 @@ class DsviEngine:
             steps.append(("syrk_side", "gemm", gemm("syrk_side"), "side"))
             if pre_planned:
                 steps += [("plans", "gemm_plan", plans, "side"), ("sig", "side", "plans")]
-            side_fac = [("chol_side", "chol", chol(kf0, kf1 - kf0), "side")]
+            side_fac = [("chol_side", "chol", chol(kf0, kf1 - kf0, self.kl_solve and not elbo_mode), "side")]
             if not elbo_mode:
                 side_fac.append(("xs_side", "gemm", gemm("xs_side"), "side"))
             side_after = fuse
@@ -1294,6 +1305,67 @@ class DsviEngine:
             self._elbo_sched = cache
         self._run(cache[key], stream, None)
         return self.out
+
+    def _kl_solve_xs(self, th, slots, offs_f):
+        """W_f = C_f^-1 L_f of the variational factors f < FV from the factor C and the inverses X11, X22 of its two
+        diagonal blocks (nmgp_chol_blockinv_batched_f32; X21 is scratch): W11 = X11 L11, W22 = X22 L22,
+        R = L21 - C21 W11 (staged in X21), W21 = X22 R -- the forward substitution of the KL gradient's
+        Sigma_f^-1 L_f (code/utils.py:339-351 and its autograd) by blocks."""
+        M = self.M
+        n1 = int(L.lib().nmgp_chol_split_point(M))
+        n2 = M - n1
+        r1 = n1 * M
+        Ci, Xs, Af = self.Cinv, self.Xs, self.Afac
+        sh = lambda offs, d: [o + d for o in offs]
+        fl_tri = L.A_LOWER | L.B_LOWER | L.OUT_TRIL
+        if n1 == n2:
+            diag = [H.BigBatch(Ci, th, Xs, slots + sh(slots, r1 + n1), list(offs_f) + sh(offs_f, r1 + n1),
+                               slots + sh(slots, r1 + n1), n1, n1, n1, lda=M, ldb=M, b_kcontig=False, sC=(M, 1),
+                               flags=fl_tri)]
+        else:
+            diag = [H.BigBatch(Ci, th, Xs, sh(slots, d), sh(offs_f, d), sh(slots, d), nn, nn, nn, lda=M, ldb=M,
+                               b_kcontig=False, sC=(M, 1), flags=fl_tri) for d, nn in ((0, n1), (r1 + n1, n2))]
+        r = H.BigBatch(Af, Xs, Ci, sh(slots, r1), slots, sh(slots, r1), n2, n1, n1, lda=M, ldb=M, b_kcontig=False,
+                       sC=(M, 1), flags=L.B_LOWER, alpha=-1.0, beta=0.0,
+                       epi=(th, sh(offs_f, r1), (M, 1), self._ones, [0] * len(slots), 1.0))
+        w21 = H.BigBatch(Ci, Ci, Xs, sh(slots, r1 + n1), sh(slots, r1), sh(slots, r1), n2, n1, n2, lda=M, ldb=M,
+                         b_kcontig=False, sC=(M, 1), flags=L.A_LOWER)
+        return H.Seq(diag + [r, w21])
+
+    def _kl_solve_lbar(self, th, gr, fb, fac_off, prior_of, NFK):
+        """KL L-bar -Sigma_f^-1 L_f + diag(1/C2_ii^2) L_f (lower part) of the variational factors f < FV from W_f
+        (_kl_solve_xs): G21 = X22^T W21 (its raw value also kept in X21), G22 = X22^T W22, Y = W11 - C21^T G21 (in
+        W11's place, lower part), G11 = X11^T Y -- the backward substitution by blocks; Sigma_v (f = FV, factored
+        with its full inverse in the prior launch) keeps the explicit-inverse product."""
+        M, NF, FV = self.M, self.NF, self.NF - 1
+        n1 = int(L.lib().nmgp_chol_split_point(M))
+        n2 = M - n1
+        r1 = n1 * M
+        Ci, Xs, Af = self.Cinv, self.Xs, self.Afac
+        MM = M * M
+        slots = [f * MM for f in range(FV)]
+        fo = list(fac_off[:FV])
+        sh = lambda offs, d: [o + d for o in offs]
+        rs = [NF + 4 * M + prior_of[f] * M for f in range(FV)]
+        g21 = H.BigBatch(Ci, Xs, gr, sh(slots, r1 + n1), sh(slots, r1), sh(fo, r1), n2, n1, n2, lda=M, ldb=M,
+                         a_kcontig=False, b_kcontig=False, sC=(M, 1), flags=L.A_UPPER, alpha=-1.0, beta=1.0,
+                         epi=(th, sh(fo, r1), (M, 1), fb, sh(rs, n1), 1.0), dstore=(Ci, sh(slots, r1), M))
+        g22 = H.BigBatch(Ci, Xs, gr, sh(slots, r1 + n1), sh(slots, r1 + n1), sh(fo, r1 + n1), n2, n2, n2, lda=M,
+                         ldb=M, a_kcontig=False, b_kcontig=False, sC=(M, 1),
+                         flags=L.A_UPPER | L.B_LOWER | L.OUT_TRIL | L.EPI_E_LOWER, alpha=-1.0, beta=1.0,
+                         epi=(th, sh(fo, r1 + n1), (M, 1), fb, sh(rs, n1), 1.0))
+        y = H.BigBatch(Af, Ci, Xs, sh(slots, r1), sh(slots, r1), slots, n1, n1, n2, lda=M, ldb=M, a_kcontig=False,
+                       b_kcontig=False, sC=(M, 1), flags=L.OUT_TRIL, alpha=-1.0, beta=1.0)
+        g11 = H.BigBatch(Ci, Xs, gr, slots, slots, fo, n1, n1, n1, lda=M, ldb=M, a_kcontig=False, b_kcontig=False,
+                         sC=(M, 1), flags=L.A_UPPER | L.B_LOWER | L.OUT_TRIL | L.EPI_E_LOWER, alpha=-1.0, beta=1.0,
+                         epi=(th, fo, (M, 1), fb, rs, 1.0))
+        parts = [g21, g22, y, g11]
+        if NFK > FV:
+            parts.append(H.BigBatch(Ci, Xs, gr, [FV * MM], [FV * MM], [fac_off[FV]], M, M, M, lda=M, ldb=M,
+                                    a_kcontig=False, b_kcontig=False,
+                                    flags=L.A_UPPER | L.B_LOWER | L.OUT_TRIL | L.EPI_E_LOWER, alpha=-1.0, beta=1.0,
+                                    epi=(th, [fac_off[FV]], (M, 1), fb, [NF + 4 * M + prior_of[FV] * M], 1.0)))
+        return H.Seq(parts)
 
     def _big_rows(self, A, C, offA, offB, offC, rows, flags, b_kcontig):
         """B x M x M products op(A) L on the 128x128 f32 kernel (BigBatch), L = theta at offB, problem b on the rows

@@ -606,10 +606,11 @@ class BigBatch:
     A_b[k*lda + i]; op(B_b)(k, j) = B_b[j*ldb + k] (b_kcontig) or B_b[k*ldb + j]; X_b = X + offX[b].
     epi = (E, offE, (sEi, sEj), RS, offRS, gamma).  kseg / rseg = (seg, [segment index per problem], [segment span
     per problem]): per-problem k range / row range (rows of A, C, E, RS; m bounds them) from the device segment table.
+    dstore = (D, offD, sDi) (with epi, full outputs): the raw product is also stored to D + offD[b] (row stride sDi).
     Offsets are uploaded once; a call is one launch (graph-capturable)."""
 
     def __init__(self, A, B, C, offA, offB, offC, m, n, k, *, lda, ldb, b_kcontig, a_kcontig=True, sC=None,
-                 flags=0, alpha=1.0, beta=0.0, diag_add=0.0, epi=None, kseg=None, rseg=None):
+                 flags=0, alpha=1.0, beta=0.0, diag_add=0.0, epi=None, kseg=None, rseg=None, dstore=None):
         for t_, nm in ((A, "A"), (B, "B"), (C, "C")):
             L.require_device(t_, nm)
             assert t_.dtype == torch.float32
@@ -642,6 +643,13 @@ class BigBatch:
             i32 = lambda o: torch.tensor(list(o), dtype=torch.int32, device=dev)
             self.rseg = (seg, i32(rs_), i32(sp))
             self._rseg_host = (list(rs_), list(sp))
+        self.dstore = None
+        if dstore is not None:
+            D, offD, sDi = dstore
+            assert epi is not None and kseg is None and rseg is None and diag_add == 0.0
+            assert not (flags & (L.OUT_LOWER | L.OUT_TRIL)) and D.dtype == torch.float32 and len(offD) == self.batch
+            L.require_device(D, "D")
+            self.dstore = (D, i64(offD), int(sDi))
         self.args = (m, n, k, lda, a_kcontig, ldb, b_kcontig, sC if sC is not None else (n, 1), flags, alpha, beta,
                      diag_add)
 
@@ -670,7 +678,8 @@ class BigBatch:
             return sum(desc_bytes(ns(row_seg=a, k_seg=-1, seg_span=b), seg, 4, beta, epi)
                        for a, b in zip(*self._rseg_host))
         if self.kseg is None:
-            return self.batch * desc_bytes(ns(row_seg=-1, k_seg=-1, seg_span=0), None, 4, beta, epi)
+            extra = self.batch * m * n * 4 if self.dstore is not None else 0
+            return self.batch * desc_bytes(ns(row_seg=-1, k_seg=-1, seg_span=0), None, 4, beta, epi) + extra
         ks, sp = self.kseg[1].tolist(), self.kseg[2].tolist()
         return sum(desc_bytes(ns(row_seg=-1, k_seg=a, seg_span=b), seg, 4, beta, epi) for a, b in zip(ks, sp))
 
@@ -686,6 +695,14 @@ class BigBatch:
         else:
             ep = (None, None, 0, 0, None, None, 0.0)
         kp = tuple(vp(t_.data_ptr()) for t_ in self.kseg) if self.kseg is not None else (None, None, None)
+        if self.dstore is not None:
+            D, oD, sDi = self.dstore
+            L.check(L.lib().nmgp_gemm_big_offsets_dual_f32(
+                vp(self.A.data_ptr()), lda, 1 if ak else 0, vp(self.B.data_ptr()), ldb, 1 if bk else 0,
+                vp(self.C.data_ptr()), sCi, sCj, m, n, k, flags, alpha, beta, vp(self.off[0].data_ptr()),
+                vp(self.off[1].data_ptr()), vp(self.off[2].data_ptr()), *ep, vp(D.data_ptr()), vp(oD.data_ptr()), sDi,
+                self.batch, s), "gemm_big_offsets_dual")
+            return
         if self.rseg is not None:
             seg, rs_, sp = self.rseg
             L.check(L.lib().nmgp_gemm_big_offsets_seg_f32(

@@ -182,6 +182,14 @@ int64_t nmgp_chol_inv_workspace_size_f32(int64_t n, int64_t batch);
 int nmgp_chol_inv_batched_ws_f32(float* A, int64_t n, int64_t lda, int64_t strideA, float* X, int64_t ldx,
                                  int64_t strideX, int64_t batch, int32_t* info, void* ws, int64_t ws_bytes,
                                  hipStream_t stream);
+/* Round 6, the KL L-bar solve form (f32, n > 256): A <- L as above, but X holds only the inverses X11, X22 of the
+ * top-level split's two diagonal blocks (n1 = nmgp_chol_split_point(n) rows / columns, then n - n1): the off-diagonal
+ * block X21 = -X22 L21 X11 (two products of the recursion's top level) is not formed -- X's rows n1.. columns 0..n1-1
+ * are left as scratch and X12 is not written.  The caller applies L^-1 / L^-T blockwise (engine.py, kl_solve):
+ * Sigma^-1 L_f = L^-T (L^-1 L_f) for the KL gradient of code/utils.py:339-351 without forming L^-1.           */
+int64_t nmgp_chol_split_point(int64_t n);
+int nmgp_chol_blockinv_batched_f32(float* A, int64_t n, int64_t lda, int64_t strideA, float* X, int64_t ldx,
+                                   int64_t strideX, int64_t batch, int32_t* info, hipStream_t stream);
 
 /* Fused GP-prior launch (round 6): up to 4 prior matrices of one DSVI step (A: K22 + jitter I, read) factored and
  * inverted as nmgp_chol_inv_batched_f64 does (A <- L, X <- L^-1, info), where a matrix with rows != 0 also gets its
@@ -314,6 +322,16 @@ int nmgp_gemm_big_offsets_seg_f32(const float* A, int64_t lda, int a_kcontig, co
                                   int64_t sEi, int64_t sEj, const float* RS, const int64_t* offRS, double gamma,
                                   const int32_t* seg, const int32_t* kseg, const int32_t* kspan, const int32_t* rseg,
                                   const int32_t* rspan, int batch, void* ws, hipStream_t stream);
+/* NMGP_EPI product (offsets, no OUT_LOWER / OUT_TRIL, no split-K) that also stores the raw product
+ * acc(i, j) = sum_k op(A)(i,k) op(B)(k,j) to D_b(i, j) = D[offD[b] + i*sDi + j] (sDi >= n) besides
+ * C = alpha acc + beta C + gamma RS E: the KL L-bar solve form's G21 = X22^T W21, added to the gradient rows and
+ * needed again for G11 = X11^T (W11 - L21^T G21).  a_kcontig 0 or 1, b_kcontig 0.                       */
+int nmgp_gemm_big_offsets_dual_f32(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb,
+                                   int b_kcontig, float* C, int64_t sCi, int64_t sCj, int m, int n, int k, int flags,
+                                   double alpha, double beta, const int64_t* offA, const int64_t* offB,
+                                   const int64_t* offC, const float* E, const int64_t* offE, int64_t sEi, int64_t sEj,
+                                   const float* RS, const int64_t* offRS, double gamma, float* D, const int64_t* offD,
+                                   int64_t sDi, int batch, hipStream_t stream);
 
 /* ------------------------------------------------------------------ pairwise kernel builder
  * mode RBF:   K = scale2 * exp(-0.5 * ||x/ls - z/ls||^2)          (code/utils.py:91-94)

@@ -85,9 +85,12 @@ def _ecog_like_engine(dtype, packed):
     grad = torch.zeros_like(theta)
     eng.bind(theta, grad, frozen_mask=0, N=float(g["N"]))
     if dtype == torch.float32:
-        # the large-M fp32 path: per-factor offsets products on the 128x128 kernel
+        # the large-M fp32 path: per-factor offsets products on the 128x128 kernel (the KL L-bar in the solve form:
+        # a sequence of block products, each a BigBatch)
         plan = eng._plan(0)
-        assert isinstance(plan["syrk_side"], H.BigBatch) and isinstance(plan["kl_lbar"], H.BigBatch)
+        assert isinstance(plan["syrk_side"], H.BigBatch)
+        kl = plan["kl_lbar"]
+        assert isinstance(kl, H.BigBatch) or (eng.kl_solve and all(isinstance(q, H.BigBatch) for q in kl.parts))
     eng.load_batch(g["x"], g["y"], sizes, noise=g["noise"])
     eng.forward_backward()
     torch.cuda.synchronize()

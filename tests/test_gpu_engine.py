@@ -230,6 +230,41 @@ def test_fp32_big_side_products_match_grouped(monkeypatch):
     assert _rel(res[0][1], res[1][1]) < 1e-3
 
 
+@pytest.mark.parametrize("M", [512, 640])
+def test_kl_solve_form_matches_explicit_inverse(monkeypatch, M):
+    """The KL L-bar of the variational factors in the solve form (factor + diagonal-block inverses, W = C^-1 L and
+    C^-T W applied by blocks; nmgp_chol_blockinv_batched_f32 + the dual-store product) vs the explicit-inverse form
+    (NMGP_KL_SOLVE=0): same loss and gradients within fp32 rounding -- the variational factors' rows
+    (sqrt_W, sqrt_U) compared on their own.  M = 640 splits unevenly (384 + 256: the diagonal blocks in two
+    launches).  Reference: code/utils.py:339-351."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP
+    rng = np.random.default_rng(31)
+    D, n = 3, 200
+    X = [np.sort(rng.uniform(0, 1, n)).reshape(-1, 1) for _ in range(D)]
+    Y = [np.sin(6 * x + d) + 0.3 * rng.standard_normal(x.shape) for d, x in enumerate(X)]
+    res = []
+    for ks in ("1", "0"):
+        monkeypatch.setenv("NMGP_KL_SOLVE", ks)
+        model = NMGP(number_observations=D * n, dim_outputs=D, Z=np.linspace(0, 1, M), seed=23,
+                     device="cuda:0", noise="device", dtype=torch.float32, pair_layout="packed")
+        for k in ["length_scales_tildeell_log", "length_scales_L0_log", "length_scales_L1_log"]:
+            getattr(model, k).data.fill_(float(np.log(3.0 / M)))
+        loss = model(X, Y)
+        loss.backward()
+        torch.cuda.synchronize()
+        assert model.engine(D * n).kl_solve == (ks == "1")
+        g = {nm: p.grad.reshape(-1).double().cpu() for nm, p in model.named_parameters()}
+        res.append((float(loss), g))
+    (l1, g1), (l0, g0) = res
+    print(f"KL_SOLVE M={M}: loss rel {abs(l1 - l0) / abs(l0):.3e}  " +
+          "  ".join(f"{nm} {_rel(g1[nm], g0[nm]):.2e}" for nm in g0 if g0[nm].abs().max() > 0))
+    assert np.isfinite(l1)
+    assert l1 == pytest.approx(l0, rel=1e-5)
+    for nm in ("sqrt_W", "sqrt_U"):
+        assert _rel(g1[nm], g0[nm]) < 1e-4, nm
+    assert _rel(torch.cat(list(g1.values())), torch.cat(list(g0.values()))) < 1e-4
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 def test_pair_stream_products_match_grouped(monkeypatch, dtype):
     """Few rows per output (D = 16 outputs, 4 rows each on average, M = 512): the per-pair quadratic-form factors,
