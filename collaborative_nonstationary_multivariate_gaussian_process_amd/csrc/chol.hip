@@ -2269,8 +2269,9 @@ static int chol_split_point(int n) {
   return n1 >= n ? n - 128 : n1;
 }
 // full = 0 (the top level of the KL L-bar solve form, nmgp_chol_blockinv_batched_f32): the factor and the inverses
-// X11, X22 of the split's two diagonal blocks only -- X21 = -X22 L21 X11 (two products) is not formed, X21 holds the
-// staged copy of A21 (scratch) and X12 is not touched
+// X11, X22 of the split's two diagonal blocks only -- X21 = -X22 L21 X11 (two products) is not formed.  The factor's
+// off-diagonal block L21 is then written to X21 (its place in X is free) instead of A21: no staging copy of A21 and
+// no zeroing of A12 (the solve form reads neither; A21 keeps the input block as scratch)
 static int chol_inv_rec_big(float* A, int n, int64_t lda, int64_t sA, float* X, int64_t ldx, int64_t sX,
                             int64_t batch, int32_t* info, hipStream_t s, int col_off, void* ws, int full = 1) {
   if (n <= 128) return chol_inv_small<float>(A, n, lda, sA, X, ldx, sX, batch, info, s, col_off, col_off == 0);
@@ -2283,6 +2284,16 @@ static int chol_inv_rec_big(float* A, int n, int64_t lda, int64_t sA, float* X, 
   float* X22 = X21 + n1;
   float* X12 = X + n1;
   if ((rc = chol_inv_rec_big(A, n1, lda, sA, X, ldx, sX, batch, info, s, col_off, ws)) != NMGP_OK) return rc;
+  if (!full) {
+    // L21 = A21 X11^T into X21, A22 -= L21 L21^T from there, then the second diagonal block
+    if ((rc = gemm_big_f32(A21, lda, X, ldx, 1, X21, ldx, 1, n2, n1, n1, NMGP_B_UPPER, 1.f, 0.f, sA, sX, sX, nb, ws,
+                           s)) != NMGP_OK)
+      return rc;
+    if ((rc = gemm_big_f32(X21, ldx, X21, ldx, 1, A22, lda, 1, n2, n2, n1, NMGP_OUT_LOWER, -1.f, 1.f, sX, sX, sA, nb,
+                           ws, s)) != NMGP_OK)
+      return rc;
+    return chol_inv_rec_big(A22, n2, lda, sA, X22, ldx, sX, batch, info, s, col_off + n1, ws);
+  }
   if ((rc = block_copy<float>(A21, lda, sA, X21, ldx, sX, n2, n1, batch, s)) != NMGP_OK) return rc;
   // L21 = A21 X11^T      (op(B)(k,j) = X11[j][k], upper)
   if ((rc = gemm_big_f32(X21, ldx, X, ldx, 1, A21, lda, 1, n2, n1, n1, NMGP_B_UPPER, 1.f, 0.f, sX, sX, sA, nb, ws,
@@ -2294,7 +2305,6 @@ static int chol_inv_rec_big(float* A, int n, int64_t lda, int64_t sA, float* X, 
     return rc;
   if ((rc = block_copy<float>(nullptr, 0, 0, A + n1, lda, sA, n1, n2, batch, s)) != NMGP_OK) return rc;   // L12 = 0
   if ((rc = chol_inv_rec_big(A22, n2, lda, sA, X22, ldx, sX, batch, info, s, col_off + n1, ws)) != NMGP_OK) return rc;
-  if (!full) return NMGP_OK;
   // T = L21 X11 (op(B)(k,j) = X11[k][j], lower) staged in X12;  X21 = -X22 T.  With n1 == n2 (every level of the
   // power-of-two shapes) T fits X12 row-major: coalesced stores, and the second product reads it k-row-wise (the
   // non-k-contiguous operand path stages as fast as the k-contiguous one).  Otherwise T is stored transposed.

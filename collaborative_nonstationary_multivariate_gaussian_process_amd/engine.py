@@ -1159,7 +1159,9 @@ class DsviEngine:
             lbar_steps.append(("bwd_lbr", "row", lbar_reduce, "side"))
         lbar_steps.append(("sig", "side", "lbar_done"))
         # (bwd_lbar after R_G instead, so that it does not compete with the P-bar_G -> R_G chain for CUs: 1380 ->
-        # 1270 it/s, profiles/r04s_lbar_per_output_ab.txt)
+        # 1270 it/s, profiles/r04s_lbar_per_output_ab.txt.  Round 6, HCP / ECoG: bwd_lbar on the idle main stream
+        # before the KL L-bar, beside the factor chain: ECoG 0.2764 -> 0.2747 s, HCP 58.7 -> 57.4 it/s, not kept --
+        # profiles/r06zh_kl_solve_lbar_early_ab.txt)
         steps += lbar_steps
         BM = self.B * M
         # the pair P-bar_0/1 products start on the third side stream right after recon (beside bwd_wG), then --
@@ -1308,16 +1310,17 @@ class DsviEngine:
 
     def _kl_solve_xs(self, th, slots, offs_f):
         """W_f = C_f^-1 L_f of the variational factors f < FV from the factor C and the inverses X11, X22 of its two
-        diagonal blocks (nmgp_chol_blockinv_batched_f32; X21 is scratch): W11 = X11 L11, W22 = X22 L22,
-        R = L21 - C21 W11 (staged in X21), W21 = X22 R -- the forward substitution of the KL gradient's
-        Sigma_f^-1 L_f (code/utils.py:339-351 and its autograd) by blocks."""
+        diagonal blocks (nmgp_chol_blockinv_batched_f32: C21 in X21's place, A21 scratch): W11 = X11 L11,
+        W22 = X22 L22, R = L21 - C21 W11 (staged in A21), W21 = X22 R -- the forward substitution of the KL gradient's
+        Sigma_f^-1 L_f (code/utils.py:339-351 and its autograd) by blocks.  The triangular blocks are stored on
+        their lower tiles only (OUT_LOWER: the elements above a diagonal are never read -- B_LOWER masks them)."""
         M = self.M
         n1 = int(L.lib().nmgp_chol_split_point(M))
         n2 = M - n1
         r1 = n1 * M
         Ci, Xs, Af = self.Cinv, self.Xs, self.Afac
         sh = lambda offs, d: [o + d for o in offs]
-        fl_tri = L.A_LOWER | L.B_LOWER | L.OUT_TRIL
+        fl_tri = L.A_LOWER | L.B_LOWER | L.OUT_LOWER
         if n1 == n2:
             diag = [H.BigBatch(Ci, th, Xs, slots + sh(slots, r1 + n1), list(offs_f) + sh(offs_f, r1 + n1),
                                slots + sh(slots, r1 + n1), n1, n1, n1, lda=M, ldb=M, b_kcontig=False, sC=(M, 1),
@@ -1325,18 +1328,20 @@ class DsviEngine:
         else:
             diag = [H.BigBatch(Ci, th, Xs, sh(slots, d), sh(offs_f, d), sh(slots, d), nn, nn, nn, lda=M, ldb=M,
                                b_kcontig=False, sC=(M, 1), flags=fl_tri) for d, nn in ((0, n1), (r1 + n1, n2))]
-        r = H.BigBatch(Af, Xs, Ci, sh(slots, r1), slots, sh(slots, r1), n2, n1, n1, lda=M, ldb=M, b_kcontig=False,
+        r = H.BigBatch(Ci, Xs, Af, sh(slots, r1), slots, sh(slots, r1), n2, n1, n1, lda=M, ldb=M, b_kcontig=False,
                        sC=(M, 1), flags=L.B_LOWER, alpha=-1.0, beta=0.0,
                        epi=(th, sh(offs_f, r1), (M, 1), self._ones, [0] * len(slots), 1.0))
-        w21 = H.BigBatch(Ci, Ci, Xs, sh(slots, r1 + n1), sh(slots, r1), sh(slots, r1), n2, n1, n2, lda=M, ldb=M,
+        w21 = H.BigBatch(Ci, Af, Xs, sh(slots, r1 + n1), sh(slots, r1), sh(slots, r1), n2, n1, n2, lda=M, ldb=M,
                          b_kcontig=False, sC=(M, 1), flags=L.A_LOWER)
         return H.Seq(diag + [r, w21])
 
     def _kl_solve_lbar(self, th, gr, fb, fac_off, prior_of, NFK):
         """KL L-bar -Sigma_f^-1 L_f + diag(1/C2_ii^2) L_f (lower part) of the variational factors f < FV from W_f
-        (_kl_solve_xs): G21 = X22^T W21 (its raw value also kept in X21), G22 = X22^T W22, Y = W11 - C21^T G21 (in
+        (_kl_solve_xs): G21 = X22^T W21 (its raw value also kept in A21), G22 = X22^T W22, Y = W11 - C21^T G21 (in
         W11's place, lower part), G11 = X11^T Y -- the backward substitution by blocks; Sigma_v (f = FV, factored
-        with its full inverse in the prior launch) keeps the explicit-inverse product."""
+        with its full inverse in the prior launch) keeps the explicit-inverse product.  The triangular blocks' upper
+        parts are not stored (OUT_LOWER): those gradient elements stay as zeroed at the step's start (and bwd_lbar's
+        OUT_TRIL products store zeros there)."""
         M, NF, FV = self.M, self.NF, self.NF - 1
         n1 = int(L.lib().nmgp_chol_split_point(M))
         n2 = M - n1
@@ -1349,15 +1354,15 @@ class DsviEngine:
         rs = [NF + 4 * M + prior_of[f] * M for f in range(FV)]
         g21 = H.BigBatch(Ci, Xs, gr, sh(slots, r1 + n1), sh(slots, r1), sh(fo, r1), n2, n1, n2, lda=M, ldb=M,
                          a_kcontig=False, b_kcontig=False, sC=(M, 1), flags=L.A_UPPER, alpha=-1.0, beta=1.0,
-                         epi=(th, sh(fo, r1), (M, 1), fb, sh(rs, n1), 1.0), dstore=(Ci, sh(slots, r1), M))
+                         epi=(th, sh(fo, r1), (M, 1), fb, sh(rs, n1), 1.0), dstore=(Af, sh(slots, r1), M))
         g22 = H.BigBatch(Ci, Xs, gr, sh(slots, r1 + n1), sh(slots, r1 + n1), sh(fo, r1 + n1), n2, n2, n2, lda=M,
                          ldb=M, a_kcontig=False, b_kcontig=False, sC=(M, 1),
-                         flags=L.A_UPPER | L.B_LOWER | L.OUT_TRIL | L.EPI_E_LOWER, alpha=-1.0, beta=1.0,
+                         flags=L.A_UPPER | L.B_LOWER | L.OUT_LOWER | L.EPI_E_LOWER, alpha=-1.0, beta=1.0,
                          epi=(th, sh(fo, r1 + n1), (M, 1), fb, sh(rs, n1), 1.0))
-        y = H.BigBatch(Af, Ci, Xs, sh(slots, r1), sh(slots, r1), slots, n1, n1, n2, lda=M, ldb=M, a_kcontig=False,
-                       b_kcontig=False, sC=(M, 1), flags=L.OUT_TRIL, alpha=-1.0, beta=1.0)
+        y = H.BigBatch(Ci, Af, Xs, sh(slots, r1), sh(slots, r1), slots, n1, n1, n2, lda=M, ldb=M, a_kcontig=False,
+                       b_kcontig=False, sC=(M, 1), flags=L.OUT_LOWER, alpha=-1.0, beta=1.0)
         g11 = H.BigBatch(Ci, Xs, gr, slots, slots, fo, n1, n1, n1, lda=M, ldb=M, a_kcontig=False, b_kcontig=False,
-                         sC=(M, 1), flags=L.A_UPPER | L.B_LOWER | L.OUT_TRIL | L.EPI_E_LOWER, alpha=-1.0, beta=1.0,
+                         sC=(M, 1), flags=L.A_UPPER | L.B_LOWER | L.OUT_LOWER | L.EPI_E_LOWER, alpha=-1.0, beta=1.0,
                          epi=(th, fo, (M, 1), fb, rs, 1.0))
         parts = [g21, g22, y, g11]
         if NFK > FV:

@@ -184,8 +184,9 @@ int nmgp_chol_inv_batched_ws_f32(float* A, int64_t n, int64_t lda, int64_t strid
                                  hipStream_t stream);
 /* Round 6, the KL L-bar solve form (f32, n > 256): A <- L as above, but X holds only the inverses X11, X22 of the
  * top-level split's two diagonal blocks (n1 = nmgp_chol_split_point(n) rows / columns, then n - n1): the off-diagonal
- * block X21 = -X22 L21 X11 (two products of the recursion's top level) is not formed -- X's rows n1.. columns 0..n1-1
- * are left as scratch and X12 is not written.  The caller applies L^-1 / L^-T blockwise (engine.py, kl_solve):
+ * block X21 = -X22 L21 X11 (two products of the recursion's top level) is not formed, and the factor's off-diagonal
+ * block L21 is returned in X21's place (X rows n1.., columns 0..n1-1) -- A21 is left as scratch, A12 and X12 are not
+ * written (no staging copy, no zeroing).  The caller applies L^-1 / L^-T blockwise (engine.py, kl_solve):
  * Sigma^-1 L_f = L^-T (L^-1 L_f) for the KL gradient of code/utils.py:339-351 without forming L^-1.           */
 int64_t nmgp_chol_split_point(int64_t n);
 int nmgp_chol_blockinv_batched_f32(float* A, int64_t n, int64_t lda, int64_t strideA, float* X, int64_t ldx,
