@@ -111,6 +111,8 @@ _SIGS = {
     "nmgp_pair_dot_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp]),
     "nmgp_pair_rank_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp]),
     "nmgp_pair_rank_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp]),
+    "nmgp_pair_mv_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp]),
+    "nmgp_pair_mv_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp]),
     "nmgp_pair_pbar_reduce_f64": (c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int, c_int,
                                           c_vp]),
     "nmgp_pair_pbar_reduce_f32": (c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int, c_int,

@@ -511,9 +511,21 @@ __global__ __launch_bounds__(256) void dsvi_kl_kernel(Args a) {
   T ld1 = 0, ld2 = 0, t2 = 0, t3 = 0;
   T sq = 0;
   if (i < M) {
-    for (int c = q; c <= i; c += 16) {
-      const T x = S[(int64_t)i * M + c];
-      sq += x * x;
+    constexpr int V = 16 / (int)sizeof(T);
+    const T* Si = S + (int64_t)i * M;
+    if (M % V == 0 && (((uintptr_t)Si) & 15) == 0) {
+      // 16-byte loads (the ECoG KL reads 17.6 GB of lower triangles per step: 3.1 TB/s with single elements)
+      struct alignas(16) Vv { T e[V]; };
+      for (int c = V * q; c <= i; c += 16 * V) {
+        const Vv x = *(const Vv*)(Si + c);
+#pragma unroll
+        for (int e = 0; e < V; ++e) sq += (c + e <= i) ? x.e[e] * x.e[e] : (T)0;
+      }
+    } else {
+      for (int c = q; c <= i; c += 16) {
+        const T x = Si[c];
+        sq += x * x;
+      }
     }
   }
 #pragma unroll

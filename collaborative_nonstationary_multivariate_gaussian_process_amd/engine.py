@@ -599,15 +599,20 @@ class DsviEngine:
             if not self.pair_stream:
                 d17.append(g(gr, self.P, self.WP, M, M, B, (1, M, 0), (M, 1, 0), (M, 1), flags=L.OUT_TRIL, beta=1.0,
                              offs=(typ * BM, j * BM, sU + pq(i, j) * MM), k_seg=i))
-            d17.append(g(gr, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1), beta=1.0,
-                         offs=(typ * BM, (D + j) * B, muU + pq(i, j) * M), k_seg=i))
+                d17.append(g(gr, self.P, self.rowbuf, M, 1, B, (1, M, 0), (1, 1, 0), (1, 1), beta=1.0,
+                             offs=(typ * BM, (D + j) * B, muU + pq(i, j) * M), k_seg=i))
+        # pair mu-bar on the pair kernel (round 6): mu-bar_ij += P_typ[rows of i]^T c_j, one block per pair instead of
+        # M / 64 GEMM tiles with k ~ B / D
+        pair_mv = H.PairStream("mv", self.P, self.rowbuf, gr,
+                               [((2 if i == j else 1) * BM, (D + j) * B, muU + pq(i, j) * M, i) for (i, j) in pairs],
+                               seg, M) if self.pair_stream else None
         # pair L-bar on the pair kernel: G_ij(lower) += P_typ[rows of i]^T W-hat_ij (the KL L-bar, this block's
         # first writer on the same stream, already zeroed the strictly upper part: OUT_TRIL)
         pair_rank = H.PairStream("rank", self.P, gr, self.WP,
                                  [((2 if i == j else 1) * BM, sU + pq(i, j) * MM, j * BM, i) for (i, j) in pairs],
                                  seg, M) if self.pair_stream else None
         if not self.big_side:
-            p["bwd_lbar"] = G(d17) if pair_rank is None else H.Seq([G(d17), pair_rank])
+            p["bwd_lbar"] = G(d17) if pair_rank is None else H.Seq([G(d17), pair_rank, pair_mv])
         else:
             # the D + Q L-bar products P^T W (k over each factor's row segment) on the 128x128 kernel,
             # the M x 1 mu-bar products stay one grouped launch
@@ -620,7 +625,7 @@ class DsviEngine:
                 [sU + pq(i, j) * MM for (i, j) in pairs], M, M, B, lda=M, ldb=M, a_kcontig=False, b_kcontig=False,
                 flags=L.OUT_TRIL, beta=1.0, kseg=(seg, [i for (i, j) in pairs], [1] * len(pairs)))
             mu = G([dd for dd in d17 if dd.n == 1])
-            p["bwd_lbar"] = H.Seq([bw_w, bw_u, mu])
+            p["bwd_lbar"] = H.Seq([bw_w, bw_u, mu] + ([pair_mv] if pair_mv is not None else []))
         # B3: R_k = Pbar_k Ainv_k (G,0,1) ; Abar_k = Cinv^T diag(delta) Cinv ; KL L-bar
         d18 = [g(self.R, self.Pbar, self.Ainv, B, M, M, (M, 1, 0), (M, 1, 0), (M, 1), offs=(k * BM, k * MM, k * BM),
                  **rows_all) for k in (3, 1, 2)]

@@ -721,11 +721,12 @@ class BigBatch:
 
 class PairStream:
     """One launch of a pair-block streaming product (csrc/pairs.hip) over many problems, descriptors uploaded
-    once: kind "quad" C[r] = A[r] L, "dot" Z[r] = W[r] L^T, "rank" G(lower) += P^T W; problem p uses rows
+    once: kind "quad" C[r] = A[r] L, "dot" Z[r] = W[r] L^T, "rank" G(lower) += P^T W, "mv" c += A^T x (A = a, x = l,
+    c = c); problem p uses rows
     seg[s_p] .. seg[s_p + 1] - 1 and operands at the element offsets (a_off, l_off, c_off) of the bases
     (a, l, c).  Graph-capturable (no allocation per call)."""
 
-    FNS = {"quad": "nmgp_pair_quad_", "dot": "nmgp_pair_dot_", "rank": "nmgp_pair_rank_"}
+    FNS = {"quad": "nmgp_pair_quad_", "dot": "nmgp_pair_dot_", "rank": "nmgp_pair_rank_", "mv": "nmgp_pair_mv_"}
 
     def __init__(self, kind, a, l, c, probs, seg, M):
         assert kind in self.FNS

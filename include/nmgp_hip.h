@@ -544,6 +544,8 @@ int nmgp_pbar_reduce_f32(const float* Z, int64_t sZ, float* P, int64_t ldp, cons
  *   dot  : Z[r] = W[r] L^T            (W at a_off, L at l_off, Z at c_off)  -- their P-bar (autograd)
  *   rank : G[k][c] += sum_r P[r][k] W[r][c] for c <= k  (P at a_off, G at l_off, W at c_off; the strictly
  *          upper part of G is not touched)                                -- the pair's L-bar (autograd)
+ *   mv   : C[c] += sum_r A[r][c] x[r] over the problem's rows (A at a_off, x at l_off, C at c_off; any M)
+ *          -- the pair's mu-bar (autograd of mu_ij in W = mu + L eps), round 6
  *   pair_pbar_reduce: row r of output i (i0 <= i < i1): P1[r] += Z_i[r], P0[r] += Z_0[r] + ... + Z_{i-1}[r]
  *          in j order (Z_j at Z + j sZ) -- the L1 / L0 prior P-bars of code/nmgp_dsvi.py:227-237
  * M must be a multiple of 4 (f32) / 2 (f64); quad needs M <= 2048 (f32) / 3072 (f64), dot and rank M <= 1024.
@@ -565,6 +567,10 @@ int nmgp_pair_rank_f64(const double* P, double* G, const double* W, const nmgp_p
                        const int32_t* seg, int M, hipStream_t stream);
 int nmgp_pair_rank_f32(const float* P, float* G, const float* W, const nmgp_pair_desc* descs, int nprob,
                        const int32_t* seg, int M, hipStream_t stream);
+int nmgp_pair_mv_f64(const double* A, const double* x, double* C, const nmgp_pair_desc* descs, int nprob,
+                     const int32_t* seg, int M, hipStream_t stream);
+int nmgp_pair_mv_f32(const float* A, const float* x, float* C, const nmgp_pair_desc* descs, int nprob,
+                     const int32_t* seg, int M, hipStream_t stream);
 int nmgp_pair_pbar_reduce_f64(const double* Z, int64_t sZ, double* P0, double* P1, int64_t ldp, const int32_t* seg,
                               int D, int i0, int i1, int B, int M, hipStream_t stream);
 int nmgp_pair_pbar_reduce_f32(const float* Z, int64_t sZ, float* P0, float* P1, int64_t ldp, const int32_t* seg,
