@@ -2274,7 +2274,10 @@ static int chol_split_point(int n) {
 // no zeroing of A12 (the solve form reads neither; A21 keeps the input block as scratch)
 static int chol_inv_rec_big(float* A, int n, int64_t lda, int64_t sA, float* X, int64_t ldx, int64_t sX,
                             int64_t batch, int32_t* info, hipStream_t s, int col_off, void* ws, int full = 1) {
-  if (n <= 128) return chol_inv_small<float>(A, n, lda, sA, X, ldx, sX, batch, info, s, col_off, col_off == 0);
+  // leaves up to 256 wide on the fused register-resident kernels (round 6: ECoG 0.2734 -> 0.2707 s, HCP 59.5 -> 60.1
+  // it/s against 128-wide leaves, profiles/r06zj_rec_leaf_ab.txt); NMGP_REC_LEAF=128 keeps the deeper recursion
+  static const int leaf = [] { const char* e = getenv("NMGP_REC_LEAF"); return e && atoi(e) == 128 ? 128 : 256; }();
+  if (n <= leaf) return chol_inv_small<float>(A, n, lda, sA, X, ldx, sX, batch, info, s, col_off, col_off == 0);
   const int n1 = chol_split_point(n);
   const int n2 = n - n1, nb = (int)batch;
   int rc;

@@ -167,7 +167,7 @@ int nmgp_trtri_batched_f32(const float* L, int64_t n, int64_t ldl, int64_t strid
 /* Fused factor + inverse: A <- L = chol(A) in place (upper zeroed), X <- L^{-1}, info as potrf.
  * n <= 256 runs one register-resident kernel per matrix (the DSVI shapes: code/nmgp_dsvi.py:172-177
  * priors and variational covariances, whose inverses feed K12 K22^{-1} and the KL); larger n (HCP
- * M=512, ECoG M=1024, the M=4096 stress case) recurses on halves: 128-wide leaves use that kernel,
+ * M=512, ECoG M=1024, the M=4096 stress case) recurses on halves: leaves (up to 256 wide in f32, 128 in f64) use that kernel,
  * the panel / SYRK / inverse products are batched MFMA GEMMs of size ~n/2, n/4, ...  X's strictly
  * upper part is used as scratch and left zero.  batch <= 65535.                                */
 int nmgp_chol_inv_batched_f64(double* A, int64_t n, int64_t lda, int64_t strideA, double* X, int64_t ldx,
