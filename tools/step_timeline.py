@@ -1,5 +1,6 @@
-"""Print one graph-replayed DSVI step's kernel timeline from a rocprofv3 kernel-trace CSV (between the
-last two Adam kernels): kernel, queue, grid, start offset, duration.
+"""Print one graph-replayed DSVI step's kernel timeline from a rocprofv3 kernel-trace CSV (between the ends of
+the last steps' step-counter advances -- the last kernel of a training step): kernel, queue, grid, start offset,
+duration.
 usage: python tools/step_timeline.py <run_kernel_trace.csv> [min_us]"""
 import csv
 import sys
@@ -7,7 +8,7 @@ import sys
 r = list(csv.DictReader(open(sys.argv[1])))
 lim = float(sys.argv[2]) if len(sys.argv) > 2 else 0.0
 r.sort(key=lambda x: int(x['Start_Timestamp']))
-ad = [x for x in r if 'adam_kernel' in x['Kernel_Name']]
+ad = [x for x in r if 'counter_add_kernel' in x['Kernel_Name']]
 a0, a1 = int(ad[-3]['End_Timestamp']), int(ad[-2]['End_Timestamp'])
 print('step us', (a1 - a0) / 1e3)
 for x in r:
