@@ -78,8 +78,12 @@ def lower_block_ranges(offs):
     return sorted(out)
 
 
-# the triangular-block Adam from this M on (fewer, larger blocks: one dense launch is cheaper below)
-ADAM_LOWER_MIN_M = 512
+# the triangular-block Adam from this M on.  Round 6: nmgp_adam_lower is one launch over the whole flat vector
+# (csrc/dsvi.hip adam_flat_kernel), so the PM2.5 shape (M = 256) takes it too -- its sqrt blocks' upper halves are no
+# longer streamed (before: 512, below which the per-range launches cost more than the saved traffic).  Small toy
+# shapes keep the dense update, which also moves upper-triangle entries a synthetic gradient may carry;
+# NMGP_ADAM_LOWER_MIN_M overrides (A/B)
+ADAM_LOWER_MIN_M = int(os.environ.get("NMGP_ADAM_LOWER_MIN_M", "256"))
 
 
 def use_adam_lower(M, dtype, offs):
