@@ -189,11 +189,13 @@ def test_bench_refuses_gpus_world_mismatch():
 
 
 def test_adam_lower_gate_needs_vector_aligned_blocks():
-    """the triangular Adam only where M and every sqrt block offset are multiples of 16 / element size."""
+    """ADVICE r5: the triangular Adam only where M and every sqrt block offset are multiples of 16 / element size;
+    round 6: from M = 256 on (one launch over the flat vector), toy shapes below keep the dense update."""
     import torch
     from collaborative_nonstationary_multivariate_gaussian_process_amd.engine import param_layout, use_adam_lower
     for D, M, dt, want in [(2, 512, torch.float32, True), (2, 514, torch.float32, False),
                            (2, 513, torch.float64, False), (2, 1024, torch.float64, True),
-                           (2, 256, torch.float32, False)]:
+                           (2, 256, torch.float32, True), (5, 256, torch.float64, True), (2, 250, torch.float64, False),
+                           (2, 20, torch.float64, False)]:
         offs, _ = param_layout(D, M)
         assert use_adam_lower(M, dt, offs) is want, (D, M, dt)
