@@ -69,7 +69,7 @@ class DsviArgs(ctypes.Structure):
                 ("scal_off", c_i64 * 8), ("T", c_vp),
                 ("pair_q0", c_int), ("n_wfac", c_int), ("kl_v", c_int), ("pair_pad", c_int), ("T64", c_vp),
                 ("kl_f0", c_int), ("kl_f1", c_int), ("v64", c_vp), ("ellZ64", c_vp), ("K12_64", c_vp),
-                ("t64", c_vp), ("scal64", c_vp)]
+                ("t64", c_vp), ("scal64", c_vp), ("adam_step", c_vp)]
 
 
 class CholTpMat(ctypes.Structure):
@@ -214,6 +214,10 @@ _SIGS = {
     "nmgp_adam_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_dbl, c_dbl, c_dbl, c_dbl, c_vp]),
     "nmgp_adam_lower_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_vp, c_dbl, c_dbl, c_dbl,
                                     c_dbl, c_vp]),
+    "nmgp_adam_lower_advanced_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_vp, c_dbl, c_dbl,
+                                             c_dbl, c_dbl, c_vp]),
+    "nmgp_adam_lower_advanced_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_vp, c_dbl, c_dbl,
+                                             c_dbl, c_dbl, c_vp]),
     "nmgp_adam_lower_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_vp, c_dbl, c_dbl, c_dbl,
                                     c_dbl, c_vp]),
     "nmgp_normal_f64": (c_int, [c_vp, c_i64, c_u64, c_vp, c_i64, c_vp]),

@@ -961,6 +961,8 @@ __global__ __launch_bounds__(1024) void dsvi_finalize_kernel(Args a) {
   // are few (PM2.5: 5376 values); larger engines launch nmgp_dsvi_mugrad_* before finalize (one workgroup over
   // ECoG's 8.5 M values took 6.6 ms)
   if (!a.elbo_mode && mugrad_count(a) <= NMGP_MUGRAD_IN_FINALIZE_MAX) mugrad_body<T>(a, threadIdx.x, blockDim.x);
+  // the optimizer step counter of a captured training step (nmgp_adam_lower_advanced_* follows): no launch of its own
+  if (!a.elbo_mode && a.adam_step != nullptr && threadIdx.x == 0) a.adam_step[0] += 1;
 #ifdef NMGP_FIN_TRACE
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1125,10 +1127,10 @@ struct AdamTri {
 };
 template <typename T>
 __global__ __launch_bounds__(256) void adam_flat_kernel(T* th, const T* g, T* m, T* v, int64_t n, AdamTri tr, int M,
-                                                        const int64_t* step, T lr, T b1, T b2, T eps) {
+                                                        const int64_t* step, T lr, T b1, T b2, T eps, int sb) {
   __shared__ T s_bc[2];
   if (threadIdx.x == 0) {
-    const double t = (double)(step[0] + 1);
+    const double t = (double)(step[0] + sb);     // sb 0: the counter was already advanced for this step
     s_bc[0] = (T)(1.0 - pow((double)b1, t));
     s_bc[1] = (T)sqrt(1.0 - pow((double)b2, t));
   }
@@ -1178,13 +1180,13 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(T* th, const T* g, T* m,
 // the gaps, the triangular one on the ranges, then the step counter
 template <typename T>
 static int adam_lower(T* th, const T* g, T* m, T* v, int64_t n, const int64_t* tri, int ntri, int M, int64_t* step,
-                      T lr, T b1, T b2, T eps, hipStream_t s) {
+                      T lr, T b1, T b2, T eps, hipStream_t s, bool advanced = false) {
   if (ntri < 0 || (ntri > 0 && !tri)) return -6;
   if (M <= 0) return -8;
   constexpr int V = 16 / (int)sizeof(T);
   const bool aligned = ((((uintptr_t)th) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) == 0;
   static const bool flat = [] { const char* e = getenv("NMGP_ADAM_FLAT"); return !e || atoi(e) != 0; }();
-  if (flat && aligned && ntri <= 4 && M % V == 0) {
+  if ((flat || advanced) && aligned && ntri <= 4 && M % V == 0) {
     AdamTri tr{};
     tr.n = ntri;
     int64_t at = 0;
@@ -1200,13 +1202,15 @@ static int adam_lower(T* th, const T* g, T* m, T* v, int64_t n, const int64_t* t
     if (ok) {
       const int64_t blocks = std::min<int64_t>((n / V + 255) / 256 + 1, 32768);
       hipLaunchKernelGGL(adam_flat_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, s, th, g, m, v, n, tr, M, step, lr,
-                         b1, b2, eps);
+                         b1, b2, eps, advanced ? 0 : 1);
       NMGP_CHECK_LAUNCH();
+      if (advanced) return NMGP_OK;
       hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(1), 0, s, step, (int64_t)1);
       NMGP_CHECK_LAUNCH();
       return NMGP_OK;
     }
   }
+  if (advanced) return -12;   // (the advanced-counter form exists only as the single launch)
   int64_t at = 0;
   for (int k = 0; k < ntri; ++k) {
     const int64_t off = tri[2 * k], nb = tri[2 * k + 1];
@@ -1620,6 +1624,29 @@ int nmgp_adam_lower_f32(float* th, const float* g, float* m, float* v, int64_t n
   if (!step) return -9;
   if (n <= 0) return NMGP_OK;
   return nmgp::adam_lower<float>(th, g, m, v, n, tri, ntri, M, step, (float)lr, (float)b1, (float)b2, (float)eps, s);
+}
+int nmgp_adam_lower_advanced_f64(double* th, const double* g, double* m, double* v, int64_t n, const int64_t* tri,
+                                 int ntri, int M, const int64_t* step, double lr, double b1, double b2, double eps,
+                                 hipStream_t s) {
+  if (!th) return -1;
+  if (!g) return -2;
+  if (!m) return -3;
+  if (!v) return -4;
+  if (!step) return -9;
+  if (n <= 0) return NMGP_OK;
+  return nmgp::adam_lower<double>(th, g, m, v, n, tri, ntri, M, const_cast<int64_t*>(step), lr, b1, b2, eps, s, true);
+}
+int nmgp_adam_lower_advanced_f32(float* th, const float* g, float* m, float* v, int64_t n, const int64_t* tri, int ntri,
+                                 int M, const int64_t* step, double lr, double b1, double b2, double eps,
+                                 hipStream_t s) {
+  if (!th) return -1;
+  if (!g) return -2;
+  if (!m) return -3;
+  if (!v) return -4;
+  if (!step) return -9;
+  if (n <= 0) return NMGP_OK;
+  return nmgp::adam_lower<float>(th, g, m, v, n, tri, ntri, M, const_cast<int64_t*>(step), (float)lr, (float)b1,
+                                 (float)b2, (float)eps, s, true);
 }
 int nmgp_adam_f64(double* th, const double* g, double* m, double* v, int64_t n, int64_t* step, double lr,
                   double b1, double b2, double eps, hipStream_t s) {

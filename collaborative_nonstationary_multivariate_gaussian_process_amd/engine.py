@@ -829,6 +829,15 @@ class DsviEngine:
                                                                                         self.seg)), s),
                 "batch_gather")
 
+    def set_adam_step(self, step):
+        """Round 6: the training schedule's finalize launch advances `step` (an int64 device counter) at its end
+        (nmgp_dsvi_args.adam_step; None: off).  Set around a capture only (DsviTrainer.capture), after the warm-up
+        built the schedule: launches copy the argument struct when they are issued."""
+        ptr = None if step is None else ctypes.c_void_p(step.data_ptr())
+        for (elbo_mode, _), a in getattr(self, "_keep_args", {}).items():
+            if not elbo_mode:
+                a.adam_step = ptr
+
     def begin_step(self, seed, counter, stream=None):
         """Gather + device noise + noise-counter advance + gradient zeroing in one launch
         (nmgp_step_begin_*); the forward_backward that follows must not zero the gradient again."""

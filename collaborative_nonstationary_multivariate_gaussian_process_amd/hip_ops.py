@@ -1100,6 +1100,16 @@ def adam_lower_(theta, grad, m, v, step, lr, tri, M, betas=(0.9, 0.999), eps=1e-
                float(lr), float(betas[0]), float(betas[1]), float(eps), L.stream_handle()), "adam_lower")
 
 
+def adam_lower_advanced_(theta, grad, m, v, step, lr, tri, M, betas=(0.9, 0.999), eps=1e-8):
+    """adam_lower_ for a step counter already advanced for this step (by the finalize kernel: the engine's
+    adam_step); one launch, the counter untouched."""
+    fn = getattr(L.lib(), "nmgp_adam_lower_advanced_" + _sfx(theta.dtype))
+    arr = (ctypes.c_int64 * max(1, 2 * len(tri)))(*[int(x) for ab in tri for x in ab])
+    L.check(fn(ctypes.c_void_p(theta.data_ptr()), ctypes.c_void_p(grad.data_ptr()), ctypes.c_void_p(m.data_ptr()),
+               ctypes.c_void_p(v.data_ptr()), theta.numel(), arr, len(tri), int(M), ctypes.c_void_p(step.data_ptr()),
+               float(lr), float(betas[0]), float(betas[1]), float(eps), L.stream_handle()), "adam_lower_advanced")
+
+
 def normal_(out, seed, counter=None, offset=0):
     fn = getattr(L.lib(), "nmgp_normal_" + _sfx(out.dtype))
     L.check(fn(ctypes.c_void_p(out.data_ptr()), out.numel(), ctypes.c_uint64(seed),

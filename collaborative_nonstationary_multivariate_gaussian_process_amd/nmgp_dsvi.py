@@ -13,6 +13,7 @@ reproduces the reference sample for sample; ``noise="device"`` draws Philox norm
 (fast path, statistically equivalent, used by the benchmark).
 """
 import math
+import os
 import time
 
 import numpy as np
@@ -639,6 +640,10 @@ class DsviTrainer:
         else:
             H.adam_(mdl._theta, mdl._grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps)
 
+    # round 6: in the captured single-process step the finalize kernel advances the step counter and the update reads
+    # it (nmgp_adam_lower_advanced_*): one launch fewer at the step's tail; NMGP_FOLD_STEP=0 keeps the counter launch
+    FOLD_STEP = os.environ.get("NMGP_FOLD_STEP", "1") != "0"
+
     def step(self, eng, noise=None):
         """One DSVI iteration on the batch already loaded in `eng`; returns the device loss scalar."""
         loss = self.grad_step(eng, noise)
@@ -668,8 +673,19 @@ class DsviTrainer:
         for t, v in saved:
             t.copy_(v)
         g = H.HipGraph(mdl.device_)          # captured through the HIP runtime (nmgp_graph_*), not torch
+        fold = (include_update and self.FOLD_STEP and getattr(eng, "_dataset", None) is not None
+                and use_adam_lower(mdl.M, mdl._theta.dtype, mdl._offs) and len(lower_block_ranges(mdl._offs)) <= 4)
         with g.capture():
-            body(eng)
+            if fold:
+                eng.set_adam_step(self.step_count)
+                try:
+                    self.grad_step(eng)
+                finally:
+                    eng.set_adam_step(None)      # eager steps keep the counter launch of update()
+                H.adam_lower_advanced_(mdl._theta, mdl._grad, self.m, self.v, self.step_count, self.lr,
+                                       lower_block_ranges(mdl._offs), mdl.M, self.betas, self.eps)
+            else:
+                body(eng)
         self.graphs[id(eng)] = g
         return g
 

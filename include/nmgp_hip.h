@@ -469,6 +469,10 @@ typedef struct nmgp_dsvi_args {
   const void* K12_64;
   void* t64;
   void* scal64;
+  /* round 6: when non-NULL, the training step's finalize kernel advances this optimizer step counter by one at its
+     end (the captured step then runs nmgp_adam_lower_advanced_*, which reads the advanced counter: one launch fewer
+     at the step's tail).  NULL: untouched.                                                                      */
+  int64_t* adam_step;
 } nmgp_dsvi_args;
 
 int nmgp_dsvi_hyper_f64(const nmgp_dsvi_args* a, hipStream_t s);      /* hyper values + v sample   */
@@ -516,6 +520,16 @@ int nmgp_adam_lower_f64(double* theta, const double* grad, double* m, double* v,
                         hipStream_t stream);
 int nmgp_adam_lower_f32(float* theta, const float* grad, float* m, float* v, int64_t n, const int64_t* tri, int ntri,
                         int M, int64_t* step, double lr, double beta1, double beta2, double eps, hipStream_t stream);
+/* The same update for a step counter that was ALREADY advanced for this step (by the finalize kernel, adam_step
+ * above): the bias corrections use step[0] itself and the counter is not advanced again.  One launch; needs the
+ * aligned single-launch form (16-byte pointers, M and every range offset multiples of 16 / size, ntri <= 4), else
+ * -12.                                                                                                          */
+int nmgp_adam_lower_advanced_f64(double* theta, const double* grad, double* m, double* v, int64_t n,
+                                 const int64_t* tri, int ntri, int M, const int64_t* step, double lr, double beta1,
+                                 double beta2, double eps, hipStream_t stream);
+int nmgp_adam_lower_advanced_f32(float* theta, const float* grad, float* m, float* v, int64_t n, const int64_t* tri,
+                                 int ntri, int M, const int64_t* step, double lr, double beta1, double beta2,
+                                 double eps, hipStream_t stream);
 /* Counter-based Philox4x32-10 standard normals: out[i] = N(0,1) for stream (seed, *counter + i) */
 int nmgp_normal_f64(double* out, int64_t n, uint64_t seed, const int64_t* counter, int64_t offset,
                     hipStream_t stream);

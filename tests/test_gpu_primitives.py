@@ -1283,6 +1283,43 @@ def test_training_step_graph_is_captured_through_hip(ops):
     assert res[0][0] == res[1][0] and torch.equal(res[0][1], res[1][1])
 
 
+@pytest.mark.parametrize("dt,M", [(F64, 256), (torch.float32, 512)])
+def test_captured_step_folded_counter_matches_counter_launch(ops, monkeypatch, dt, M):
+    """The captured training step with the optimizer step counter advanced by the finalize kernel
+    (nmgp_dsvi_args.adam_step) and the update reading it (nmgp_adam_lower_advanced_*) equals the step with the
+    counter's own launch (DsviTrainer.FOLD_STEP = False) bit for bit after three replays: theta, m, v, and the
+    counter = 3 (M = 256 fp64: the fused prior schedule; fp32 M = 512).  Eager steps afterwards are unaffected
+    (the counter is advanced once per update, by update())."""
+    from collaborative_nonstationary_multivariate_gaussian_process_amd.nmgp_dsvi import NMGP, DsviTrainer
+    rng = np.random.default_rng(21)
+    D, B, nb = 3, 240, 2
+    res = []
+    for fold in (True, False):
+        monkeypatch.setattr(DsviTrainer, "FOLD_STEP", fold)
+        model = NMGP(number_observations=D * 400, dim_outputs=D, Z=np.linspace(0, 1, M), minibatch_size=B, seed=9,
+                     device=DEV, noise="device", dtype=dt)
+        tr = DsviTrainer(model, 0.01)
+        eng = model.engine(B)
+        g = np.random.default_rng(4)
+        Xb = torch.tensor(g.uniform(0, 1, (nb, B)), dtype=dt, device=DEV)
+        Yb = torch.tensor(g.standard_normal((nb, B)), dtype=dt, device=DEV)
+        ids = np.sort(g.integers(0, D, (nb, B)), axis=1)
+        Ib = torch.tensor(ids, dtype=torch.int32, device=DEV)
+        Sb = torch.tensor(np.stack([np.concatenate([[0], np.cumsum(np.bincount(r, minlength=D))]) for r in ids]),
+                          dtype=torch.int32, device=DEV)
+        eng.bind_dataset(Xb, Yb, Ib, Sb)
+        graph = tr.capture(eng, include_update=True)
+        for _ in range(3):
+            graph.replay()
+        torch.cuda.synchronize()
+        assert all(getattr(a, "adam_step", None) in (None, 0) for a in eng._keep_args.values())
+        res.append((model._theta.detach().cpu().clone(), tr.m.cpu().clone(), tr.v.cpu().clone(),
+                    int(tr.step_count.item())))
+    for a, b in zip(res[0][:3], res[1][:3]):
+        assert torch.equal(a, b)
+    assert res[0][3] == res[1][3] == 3
+
+
 def test_hip_graph_external_event_node_fires_mid_replay(ops):
     """nmgp_event_record_external inside a capture becomes an external event node: after the graph is
     launched, a stream OUTSIDE the graph that waits on the event runs as soon as that point of the replay is
