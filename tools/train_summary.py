@@ -27,7 +27,8 @@ def main():
     # first timed step to the end of the last Adam step-counter increment (the step's last launch; the Adam itself
     # is one or several launches, nmgp_adam / nmgp_adam_lower)
     begin = [x for x in rows if "step_begin_kernel" in x["Kernel_Name"]]
-    ctr = [x for x in rows if "counter_add_kernel" in x["Kernel_Name"]]
+    # (round 6: the captured step's counter is advanced by the finalize kernel -- the update is then the last launch)
+    ctr = [x for x in rows if "counter_add_kernel" in x["Kernel_Name"] or "adam" in x["Kernel_Name"]]
     t0, t1 = int(begin[-steps]["Start_Timestamp"]), int(ctr[-1]["End_Timestamp"])
     busy = collections.defaultdict(float)
     calls = collections.Counter()
