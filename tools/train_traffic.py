@@ -25,7 +25,8 @@ def window_sum(path, counter, steps, durations=None):
     rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
     rows.sort(key=lambda x: int(x["Start_Timestamp"]))
     begin = [x for x in rows if "step_begin_kernel" in x["Kernel_Name"]]
-    ctr = [x for x in rows if "counter_add_kernel" in x["Kernel_Name"]]
+    # (the step's last update launch: the folded captured step has no counter launch)
+    ctr = [x for x in rows if "counter_add_kernel" in x["Kernel_Name"] or "adam" in x["Kernel_Name"]]
     t0, t1 = int(begin[-steps]["Start_Timestamp"]), int(ctr[-1]["End_Timestamp"])
     acc = collections.defaultdict(float)
     for x in rows:
